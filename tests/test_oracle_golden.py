@@ -1,0 +1,81 @@
+"""Pin the CPU oracle against golden vectors produced by the reference itself.
+
+CPU-only.  Tolerances are fp32-restatement level (different op order inside
+ATen is allowed); post-step parameters use an absolute tolerance of 2*lr
+(Adam's first step is ~lr*sign(g), so elements with tiny
+gradients may flip sign), and pre-InstanceNorm biases are excluded from
+gradient-value checks (their exact gradient is zero; fp32 values are noise).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+from oracle import step as O
+
+SEEDS = dict(G=1, D=2, V=3)
+
+
+def build(fx):
+    H, W, B, noaa, noaaup = [int(v) for v in fx["meta"][:5]]
+    G = O.seeded_params(O.g_param_shapes(no_antialias=bool(noaa), no_antialias_up=bool(noaaup)),
+                        SEEDS["G"], bias_std=0.02)
+    D = O.seeded_params(O.d_param_shapes(), SEEDS["D"], bias_std=0.02)
+    V = O.seeded_params(O.vgg_param_shapes(), SEEDS["V"], kaiming=True)
+    return G, D, V, bool(noaa), bool(noaaup)
+
+
+def rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-12))
+
+
+@pytest.mark.parametrize("variant", ["s32", "s64", "s32_noaa", "s32_noaaup"])
+def test_oracle_step_matches_reference(variant):
+    torch.set_num_threads(4)
+    fx = load_golden(variant)
+    G, D, V, noaa, noaaup = build(fx)
+    ir, rgb = torch.from_numpy(fx["ir"]), torch.from_numpy(fx["rgb"])
+    optG, optD = O.AdamState(G), O.AdamState(D)
+    out = O.train_step(G, D, V, ir, rgb, optG, optD, no_antialias=noaa, no_antialias_up=noaaup)
+
+    assert rel(out["fake"], fx["fake"]) < 1e-5
+    assert rel(out["pred_real"], fx["pred_real"]) < 1e-5
+    assert rel(out["pred_fake"], fx["pred_fake"]) < 1e-5
+    assert rel(out["pred_fake_G"], fx["pred_fake_G"]) < 1e-4
+    for k in ("loss_D", "loss_G", "loss_G_GAN", "loss_G_L1", "loss_G_perc", "loss_G_TV", "loss_G_ssim"):
+        assert abs(float(out[k]) - fx["step1_" + k]) <= 1e-5 * max(1.0, abs(fx["step1_" + k])), k
+
+    pre_in = set(O.pre_in_bias_keys(list(G) + list(D)))
+    for tag, grads, params in (("gG", out["gradG"], G), ("gD", out["gradD"], D)):
+        for k, g in grads.items():
+            idx = fx[f"{tag}|{k}|idx"]
+            flat = g.reshape(-1).double().numpy()
+            post = params[k].reshape(-1).numpy()[idx]
+            assert np.max(np.abs(post - fx[f"{tag}|{k}|post"])) <= 2 * 2e-4 + 1e-6, k
+            if k in pre_in:
+                continue
+            scale = max(fx[f"{tag}|{k}|abs"] / flat.size, 1e-12)
+            assert np.max(np.abs(flat[idx] - fx[f"{tag}|{k}|val"])) <= 1e-3 * scale * 10 + 1e-6 * np.max(np.abs(flat)), k
+            assert abs(flat.sum() - fx[f"{tag}|{k}|sum"]) <= 1e-4 * fx[f"{tag}|{k}|abs"] + 1e-7, k
+
+    # second step on the same batch exercises Adam's running moments
+    out2 = O.train_step(G, D, V, ir, rgb, optG, optD, no_antialias=noaa, no_antialias_up=noaaup)
+    for k in ("loss_D", "loss_G"):
+        assert abs(float(out2[k]) - fx["step2_" + k]) <= 2e-4 * max(1.0, abs(fx["step2_" + k])), k
+
+
+def test_loss_probes():
+    fx = load_golden("s32")
+    ir, rgb = torch.from_numpy(fx["ir"]), torch.from_numpy(fx["rgb"])
+    V = O.seeded_params(O.vgg_param_shapes(), SEEDS["V"], kaiming=True)
+    assert rel(O.vgg_features(V, rgb)[:, :8].numpy(), fx["vgg_rgb"]) < 1e-5
+    assert abs(float(O.tv_loss(rgb)) - fx["tv_rgb"]) < 1e-6
+    assert abs(float(O.ssim_loss((rgb + 1) / 2, (ir.repeat(1, 3, 1, 1) + 1) / 2)) - fx["ssim_ir_rgb"]) < 1e-6
+
+
+def test_lr_lambda_schedule():
+    # ir:212-233: constant through epoch 40, linear to 0 at epoch 50
+    assert O.lr_lambda(0) == 1.0 and O.lr_lambda(39) == 1.0
+    assert abs(O.lr_lambda(40) - 0.9) < 1e-12 and abs(O.lr_lambda(44) - 0.5) < 1e-12
+    assert O.lr_lambda(49) == 0.0
