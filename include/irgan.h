@@ -1,0 +1,186 @@
+/*
+ * irgan.h -- C ABI of the MI355X (gfx950) kernels for the IR->RGB GAN train step.
+ *
+ * The reference (/root/reference/Code/ir_colorization.py, cited ir:LINE) has no
+ * FFI: its hot path (the train-step body ir:1636-1681) dispatches PyTorch ATen
+ * ops.  Each entry point below replaces the ATen work of one reference layer
+ * type; the Python host package (ir_colorization.py in the *_amd package)
+ * binds them with ctypes exactly as INTEGRATION.md shows.
+ *
+ * Conventions
+ *  - Activations are NHWC.  A tensor "slice" is (pointer, ld, off): pixel p,
+ *    channel c lives at ptr[p*ld + off + c], so torch.cat along channels
+ *    (ir:557, 564, 1639-1640) is free: producers write into channel slices.
+ *  - Conv weights are K-major "KRSC": w[cout][ky][kx][cin].
+ *  - dtype codes: IRGAN_F32 (exact-fp32 parity mode, f32 MFMA) or IRGAN_BF16
+ *    (bf16 MFMA, fp32 accumulate).  Bias / statistics / losses are fp32.
+ *  - All calls are asynchronous on the given HIP stream (hipStream_t passed as
+ *    void*), allocate nothing, and return 0 or a hipError_t / IRGAN_E* code.
+ *    The caller owns every buffer (PyTorch caching allocator on the host side).
+ */
+#ifndef IRGAN_H
+#define IRGAN_H
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* irgan_stream_t;
+
+enum { IRGAN_F32 = 0, IRGAN_BF16 = 1 };
+enum { IRGAN_PAD_ZERO = 0, IRGAN_PAD_REFLECT = 1 };
+/* forward activations (epilogues / IN apply) */
+enum { IRGAN_ACT_NONE = 0, IRGAN_ACT_RELU = 1, IRGAN_ACT_LRELU = 2, IRGAN_ACT_TANH = 3 };
+enum { IRGAN_OK = 0, IRGAN_EINVAL = 1001, IRGAN_EUNSUPPORTED = 1002 };
+
+/* Implicit-GEMM convolution descriptor.  Launch domain: N x Ho x Wo output
+ * positions (i, j); the input coordinate of tap (ty, tx) is
+ * (i*sy + ty + c0y, j*sx + tx + c0x), zero- or reflect-mapped into H x W; the
+ * result lands at output pixel (i*omy + ooy, j*omx + oox) of an N x OH x OW
+ * tensor.  A forward conv with stride s and padding p is sy=s, c0y=-p,
+ * omy=1, ooy=0.  Backward-data and ConvTranspose2d use the same descriptor on
+ * re-packed weights (irgan_weight_pack) and, for stride 2, one launch per
+ * output phase (omy=2, ooy=phase). */
+typedef struct irgan_conv_desc {
+    int32_t N, H, W, Cin, ldx, xoff;      /* input slice */
+    int32_t Ho, Wo, Cout, ldy, yoff;      /* launch domain + output slice */
+    int32_t OH, OW, omy, ooy, omx, oox;   /* output tensor + pixel mapping */
+    int32_t KH, KW, sy, sx, c0y, c0x;     /* taps / input mapping */
+    int32_t pad_mode;                     /* IRGAN_PAD_* */
+    int32_t act;                          /* IRGAN_ACT_* applied in the epilogue */
+    int32_t accumulate;                   /* 1: y += result (fp32 output only) */
+    int32_t dtype;                        /* input/weight dtype IRGAN_F32|IRGAN_BF16 */
+    int32_t out_dtype;                    /* output dtype */
+    int32_t mask_act;                     /* backward mask: 0 none, 1 relu, 2 lrelu(0.2) */
+    int32_t ldm, moff;                    /* mask slice (same pixel grid as output) */
+} irgan_conv_desc;
+
+/* y = act(conv(x, w) + bias) [* mask'(m)]   -- replaces nn.Conv2d forward
+ * (ir:460, 470, 478, 390, 411, 504, 521, 529, 600-629, vgg 664) and, on
+ * re-packed weights, conv backward-data and nn.ConvTranspose2d (ir:496, 513). */
+int irgan_conv_fwd(const irgan_conv_desc* d, const void* x, const void* w,
+                   const float* bias, void* y, const void* mask, irgan_stream_t s);
+
+/* dw[cout][ky][kx][cin] += sum_pixels dy * im2col(x)  (fp32 atomics, split-K
+ * over pixels) -- replaces the weight half of convolution_backward.  d is the
+ * FORWARD descriptor (x = forward input, dy = grad at the forward output with
+ * slice ldy/yoff); dw must be zeroed by the caller for a fresh gradient. */
+int irgan_conv_wgrad(const irgan_conv_desc* d, const void* x, const void* dy,
+                     float* dw, int32_t splitk, irgan_stream_t s);
+
+/* Weight re-pack: dst[co'][a][b][ci'] (dtype) from the fp32 KRSC master
+ * src[Cout][KH][KW][Cin].  transpose=0: plain cast (a=ky, b=kx, co'=co, ci'=ci).
+ * transpose=1: dst[ci][a][b][co] = src[co][tyr + s*(Ay-1-a)][txr + s*(Ax-1-b)][ci]
+ * (flip / phase selection for backward-data and transposed conv).  A
+ * ConvTranspose2d weight [Cin][Cout][K][K] is handed over as KRSC of its own. */
+int irgan_weight_pack(const float* src, void* dst, int32_t dtype, int32_t Cout, int32_t KH,
+                      int32_t KW, int32_t Cin, int32_t transpose, int32_t s, int32_t tyr,
+                      int32_t Ay, int32_t txr, int32_t Ax, irgan_stream_t st);
+
+/* ---- InstanceNorm (ir:154-165), per-(n,c) over H*W, eps 1e-5, no affine ---- */
+/* mr[n][c] = {mean, rstd}; work = 2*N*C doubles of scratch (zeroed inside). */
+int irgan_in_stats(const void* x, int32_t dtype, int32_t N, int32_t HW, int32_t C,
+                   int32_t ld, int32_t off, double* work, float* mr, irgan_stream_t s);
+/* y = act((x - mean) * rstd) [+ res];  optional xhat output ([P][C], dtype). */
+int irgan_in_apply(const void* x, int32_t dtype, int32_t N, int32_t HW, int32_t C, int32_t ldx,
+                   int32_t xoff, const float* mr, int32_t act, const void* res, int32_t ldr,
+                   int32_t roff, void* y, int32_t ldy, int32_t yoff, void* xhat, irgan_stream_t s);
+/* Backward of y = act(IN(x)) [+ res] given the PRE-norm input x and its
+ * (mean, rstd): xhat = (x - mean)*rstd, g = (dy [+ dy2]) * act'(xhat),
+ * red[n][c] = {mean g, mean g*xhat}.  work: 2*N*C doubles (zeroed inside). */
+int irgan_in_bwd_reduce(const void* dy, int32_t dy_dtype, int32_t lddy, int32_t dyoff,
+                        const void* dy2, int32_t dy2_dtype, int32_t lddy2, int32_t dy2off,
+                        const void* x, int32_t x_dtype, int32_t ldx, int32_t xoff, int32_t act,
+                        int32_t N, int32_t HW, int32_t C, const float* mr, double* work, float* red,
+                        irgan_stream_t s);
+/* dx = rstd*(g - mean(g) - xhat*mean(g*xhat)); also db[c] += sum dx (fp32 bias
+ * grad of the producing conv, caller zeroes) when db != NULL.  dx may alias dy. */
+int irgan_in_bwd_apply(const void* dy, int32_t dy_dtype, int32_t lddy, int32_t dyoff,
+                       const void* dy2, int32_t dy2_dtype, int32_t lddy2, int32_t dy2off,
+                       const void* x, int32_t x_dtype, int32_t ldx, int32_t xoff, int32_t act,
+                       int32_t N, int32_t HW, int32_t C, const float* mr, const float* red,
+                       void* dx, int32_t dx_dtype, int32_t lddx, int32_t dxoff, float* db,
+                       irgan_stream_t s);
+/* db[c] += sum over pixels of g[p][c] (bias gradient), g slice (dtype, ld, off). */
+int irgan_channel_sum(const void* g, int32_t dtype, int32_t P, int32_t C, int32_t ld,
+                      int32_t off, float* db, irgan_stream_t s);
+
+/* ---- resampling (ir:269-355, 1637-1640, vgg pooling) ---- */
+/* Downsample (ir:269-310): reflect pad 1 + binomial 3x3, stride 2. */
+int irgan_blur_down_fwd(const void* x, int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t C,
+                        int32_t ldx, int32_t xoff, void* y, int32_t ldy, int32_t yoff, irgan_stream_t s);
+int irgan_blur_down_bwd(const void* dy, int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t C,
+                        int32_t lddy, int32_t dyoff, void* dx, int32_t dx_dtype, int32_t lddx,
+                        int32_t dxoff, irgan_stream_t s);
+/* UpsampleAA (ir:313-355): bilinear x2 align_corners + reflect pad 1 + blur. H,W = input dims. */
+int irgan_upsample_fwd(const void* x, int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t C,
+                       int32_t ldx, int32_t xoff, void* y, int32_t ldy, int32_t yoff, irgan_stream_t s);
+/* work: N*2H*2W*C floats of scratch; accumulate: dx += result. */
+int irgan_upsample_bwd(const void* dy, int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t C,
+                       int32_t lddy, int32_t dyoff, float* work, void* dx, int32_t dx_dtype,
+                       int32_t lddx, int32_t dxoff, int32_t accumulate, irgan_stream_t s);
+/* reflect-pad backward: dx[q] = sum_{u: reflect(u-p)=q} dxpad[u]  (dxpad fp32, (H+2p)x(W+2p)) */
+int irgan_reflect_fold(const float* dxpad, int32_t N, int32_t H, int32_t W, int32_t C, int32_t p,
+                       void* dx, int32_t dx_dtype, int32_t lddx, int32_t dxoff, int32_t accumulate,
+                       irgan_stream_t s);
+/* 2x2 max pool (VGG features) forward / backward (first max wins, as ATen). */
+int irgan_maxpool_fwd(const void* x, int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t C,
+                      void* y, irgan_stream_t s);
+int irgan_maxpool_bwd(const void* x, const void* dy, int32_t dtype, int32_t N, int32_t H,
+                      int32_t W, int32_t C, void* dx, int32_t relu_mask, irgan_stream_t s);
+
+/* ---- layout / elementwise ---- */
+/* NCHW fp32 -> NHWC slice (dtype), optional affine y = x*scale[c] + shift[c]. */
+int irgan_nchw_to_nhwc(const float* x, int32_t N, int32_t C, int32_t H, int32_t W, void* y,
+                       int32_t dtype, int32_t ldy, int32_t yoff, const float* scale,
+                       const float* shift, irgan_stream_t s);
+/* NHWC slice (dtype) -> NCHW fp32, y = x*scale (+= when accumulate). */
+int irgan_nhwc_to_nchw(const void* x, int32_t dtype, int32_t ldx, int32_t xoff, int32_t N,
+                       int32_t C, int32_t H, int32_t W, float* y, float scale, int32_t accumulate,
+                       irgan_stream_t s);
+/* y[p][c] = a*x[p][c] (+ b*y) on slices; dtype conversion allowed. */
+int irgan_axpby(const void* x, int32_t xdtype, int32_t ldx, int32_t xoff, float a, void* y,
+                int32_t ydtype, int32_t ldy, int32_t yoff, float b, int32_t P, int32_t C,
+                irgan_stream_t s);
+/* y[p][c] = x[p][c]*scale[c] (+ shift[c]) (+ y when accumulate): VGG input
+ * normalisation (ir:679-682) and its backward. */
+int irgan_affine(const void* x, int32_t xdt, int32_t ldx, int32_t xoff, const float* scale,
+                 const float* shift, void* y, int32_t ydt, int32_t ldy, int32_t yoff,
+                 int32_t accumulate, int32_t P, int32_t C, irgan_stream_t s);
+/* dx = dy * act'(a): 1 relu (a>0), 2 lrelu (a>0 ? 1 : 0.2), 3 tanh (1 - a^2). */
+int irgan_act_bwd(const void* dy, int32_t dy_dtype, int32_t lddy, int32_t dyoff, const void* a,
+                  int32_t a_dtype, int32_t lda, int32_t aoff, int32_t act, void* dx,
+                  int32_t dx_dtype, int32_t lddx, int32_t dxoff, int32_t P, int32_t C,
+                  irgan_stream_t s);
+
+/* ---- losses (ir:1647-1679, 686-750) ; images NHWC fp32 (B,H,W,3) ---- */
+/* Hinge for D on a [real; fake] patch map (ir:1647-1649) and for G (ir:1662).
+ * mode 0: loss = 0.5*(mean relu(1-p[:n]) + mean relu(1+p[n:])), grad written;
+ * mode 1: loss = -mean p, grad = -scale/cnt. loss accumulated into *loss (fp64). */
+int irgan_hinge(const float* pred, int32_t n_half, int32_t mode, float scale, float* grad,
+                double* loss, irgan_stream_t s);
+/* Pixel / feature L1: loss += w*mean|a-b|; ga = w*sign(a-b)/cnt (dtype of ga). */
+int irgan_l1(const void* a, const void* b, int32_t dtype, int64_t count, float w, void* ga,
+             int32_t ga_dtype, int32_t accumulate, double* loss, irgan_stream_t s);
+/* TV (ir:686-694) on NHWC fp32 x: loss += w*tv(x), g += grad. */
+int irgan_tv(const float* x, int32_t N, int32_t H, int32_t W, int32_t C, float w, float* g,
+             double* loss, irgan_stream_t s);
+/* SSIM loss w*(1 - mean ssim((a+1)/2, (b+1)/2)) (ir:714-750, 1675-1677);
+ * grad wrt a accumulated into g.  work: 10*N*H*W*C floats of scratch. */
+int irgan_ssim(const float* a, const float* b, int32_t N, int32_t H, int32_t W, int32_t C, float w,
+               float* g, double* loss, float* work, irgan_stream_t s);
+
+/* ---- optimizer (torch.optim.Adam, ir:1601-1604) over a flat fp32 buffer ---- */
+/* step_size = lr/(1-beta1^t), bc2_sqrt = sqrt(1-beta2^t) (host, fp64 -> fp32). */
+int irgan_adam(float* p, const float* g, float* m, float* v, int64_t n, float step_size,
+               float beta1, float beta2, float bc2_sqrt, float eps, irgan_stream_t s);
+
+/* Version / capability probe (no GPU work). */
+int irgan_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IRGAN_H */

@@ -1,0 +1,306 @@
+// Loss kernels of the G/D objectives (ir:1647-1679) and the fused Adam update
+// (ir:1601-1604, 1651, 1681).  Images are NHWC fp32 (B, H, W, 3).  Every loss
+// is reduced per block in fp32 and across blocks with one fp64 atomic, and
+// writes its gradient in the same pass (no autograd tape).
+#include "common.h"
+
+namespace {
+
+constexpr int TPB = 256;
+
+IRGAN_HD void block_add(double* dst, float v) {
+    __shared__ float red[TPB / 64];
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) red[wid] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float t = 0.f;
+        for (int i = 0; i < TPB / 64; ++i) t += red[i];
+        atomicAdd(dst, (double)t);
+    }
+}
+
+IRGAN_HD float sgn(float x) { return x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f); }
+
+int nblocks(long total) { return (int)std::max<long>(1, std::min<long>((total + TPB - 1) / TPB, 8192)); }
+
+// mode 0: pred = [real (n) ; fake (n)] -> 0.5*(mean relu(1-r) + mean relu(1+f))   (ir:1647-1649)
+// mode 1: pred = fake (n) -> -mean(p) * scale                                    (ir:1662, x lambda_gan)
+__global__ __launch_bounds__(TPB) void hinge_kernel(const float* __restrict__ pred, int n, int mode, float scale,
+                                                    float* __restrict__ grad, double* __restrict__ loss) {
+    const long total = mode == 0 ? 2L * n : n;
+    float acc = 0.f;
+    const float inv = 1.f / (float)n;
+    for (long i = blockIdx.x * (long)TPB + threadIdx.x; i < total; i += (long)gridDim.x * TPB) {
+        const float p = pred[i];
+        if (mode == 0) {
+            if (i < n) {
+                const float t = 1.f - p;
+                acc += t > 0.f ? t : 0.f;
+                grad[i] = t > 0.f ? -0.5f * inv * scale : 0.f;
+            } else {
+                const float t = 1.f + p;
+                acc += t > 0.f ? t : 0.f;
+                grad[i] = t > 0.f ? 0.5f * inv * scale : 0.f;
+            }
+        } else {
+            acc += p;
+            grad[i] = -scale * inv;
+        }
+    }
+    block_add(loss, mode == 0 ? 0.5f * acc * inv * scale : -acc * inv * scale);
+}
+
+template <typename T, typename G>
+__global__ __launch_bounds__(TPB) void l1_kernel(const T* __restrict__ a, const T* __restrict__ b, long count, float w,
+                                                 G* __restrict__ ga, int accumulate, double* __restrict__ loss) {
+    float acc = 0.f;
+    const float inv = w / (float)count;
+    for (long i = blockIdx.x * (long)TPB + threadIdx.x; i < count; i += (long)gridDim.x * TPB) {
+        const float d = to_f<T>(a[i]) - to_f<T>(b[i]);
+        acc += fabsf(d);
+        if (ga) {
+            float gv = sgn(d) * inv;
+            if (accumulate) gv += to_f<G>(ga[i]);
+            ga[i] = from_f<G>(gv);
+        }
+    }
+    block_add(loss, acc * inv);
+}
+
+// TV (ir:686-694): mean|x[h+1]-x[h]| + mean|x[w+1]-x[w]| over N*C*(H-1)*W and N*C*H*(W-1)
+__global__ __launch_bounds__(TPB) void tv_kernel(const float* __restrict__ x, int H, int W, int C, float w,
+                                                 float* __restrict__ g, double* __restrict__ loss, long total,
+                                                 float inv_v, float inv_h) {
+    float acc = 0.f;
+    for (long idx = blockIdx.x * (long)TPB + threadIdx.x; idx < total; idx += (long)gridDim.x * TPB) {
+        long t = idx / C;
+        const int xw = (int)(t % W); t /= W;
+        const int yh = (int)(t % H);
+        const float v = x[idx];
+        float gv = 0.f;
+        if (yh + 1 < H) {
+            const float d = x[idx + (long)W * C] - v;
+            acc += fabsf(d) * inv_v;
+            gv -= sgn(d) * inv_v;
+        }
+        if (yh > 0) gv += sgn(v - x[idx - (long)W * C]) * inv_v;
+        if (xw + 1 < W) {
+            const float d = x[idx + C] - v;
+            acc += fabsf(d) * inv_h;
+            gv -= sgn(d) * inv_h;
+        }
+        if (xw > 0) gv += sgn(v - x[idx - C]) * inv_h;
+        g[idx] += w * gv;
+    }
+    block_add(loss, w * acc);
+}
+
+struct Win11 {
+    float g[11];
+};
+
+// SSIM (ir:714-750) on a' = (a+1)/2, b' = (b+1)/2 with the separable 11-tap
+// Gaussian (sigma 1.5) and zero padding 5.  Planar fp32 work maps of size S.
+__global__ __launch_bounds__(TPB) void ssim_h5_kernel(const float* __restrict__ a, const float* __restrict__ b, int W,
+                                                      int C, Win11 win, float* __restrict__ out, long S) {
+    for (long idx = blockIdx.x * (long)TPB + threadIdx.x; idx < S; idx += (long)gridDim.x * TPB) {
+        const int xw = (int)((idx / C) % W);
+        float m1 = 0.f, m2 = 0.f, e11 = 0.f, e22 = 0.f, e12 = 0.f;
+#pragma unroll
+        for (int k = 0; k < 11; ++k) {
+            const int xx = xw + k - 5;
+            if (xx < 0 || xx >= W) continue;
+            const long j = idx + (long)(k - 5) * C;
+            const float p = (a[j] + 1.f) * 0.5f, q = (b[j] + 1.f) * 0.5f, gk = win.g[k];
+            m1 += gk * p;
+            m2 += gk * q;
+            e11 += gk * p * p;
+            e22 += gk * q * q;
+            e12 += gk * p * q;
+        }
+        out[idx] = m1;
+        out[S + idx] = m2;
+        out[2 * S + idx] = e11;
+        out[3 * S + idx] = e22;
+        out[4 * S + idx] = e12;
+    }
+}
+
+template <int NM>
+__global__ __launch_bounds__(TPB) void ssim_v_kernel(const float* __restrict__ in, int H, int W, int C, Win11 win,
+                                                     float* __restrict__ out, long S) {
+    for (long idx = blockIdx.x * (long)TPB + threadIdx.x; idx < S; idx += (long)gridDim.x * TPB) {
+        const int yh = (int)((idx / ((long)C * W)) % H);
+        float acc[NM];
+#pragma unroll
+        for (int m = 0; m < NM; ++m) acc[m] = 0.f;
+#pragma unroll
+        for (int k = 0; k < 11; ++k) {
+            const int yy = yh + k - 5;
+            if (yy < 0 || yy >= H) continue;
+            const long j = idx + (long)(k - 5) * W * C;
+#pragma unroll
+            for (int m = 0; m < NM; ++m) acc[m] += win.g[k] * in[m * S + j];
+        }
+#pragma unroll
+        for (int m = 0; m < NM; ++m) out[m * S + idx] = acc[m];
+    }
+}
+
+template <int NM>
+__global__ __launch_bounds__(TPB) void ssim_h_kernel(const float* __restrict__ in, int W, int C, Win11 win,
+                                                     float* __restrict__ out, long S) {
+    for (long idx = blockIdx.x * (long)TPB + threadIdx.x; idx < S; idx += (long)gridDim.x * TPB) {
+        const int xw = (int)((idx / C) % W);
+        float acc[NM];
+#pragma unroll
+        for (int m = 0; m < NM; ++m) acc[m] = 0.f;
+#pragma unroll
+        for (int k = 0; k < 11; ++k) {
+            const int xx = xw + k - 5;
+            if (xx < 0 || xx >= W) continue;
+            const long j = idx + (long)(k - 5) * C;
+#pragma unroll
+            for (int m = 0; m < NM; ++m) acc[m] += win.g[k] * in[m * S + j];
+        }
+#pragma unroll
+        for (int m = 0; m < NM; ++m) out[m * S + idx] = acc[m];
+    }
+}
+
+// SSIM map, loss and dL/d{mu1, e11, e12} (ir:738-750)
+__global__ __launch_bounds__(TPB) void ssim_map_kernel(const float* __restrict__ mom, float w, float* __restrict__ d3,
+                                                       double* __restrict__ loss, long S) {
+    const float C1 = 0.01f * 0.01f, C2 = 0.03f * 0.03f;
+    const float dLdS = -w / (float)S;
+    float acc = 0.f;
+    for (long idx = blockIdx.x * (long)TPB + threadIdx.x; idx < S; idx += (long)gridDim.x * TPB) {
+        const float mu1 = mom[idx], mu2 = mom[S + idx], e11 = mom[2 * S + idx], e22 = mom[3 * S + idx],
+                    e12 = mom[4 * S + idx];
+        const float m11 = mu1 * mu1, m22 = mu2 * mu2, m12 = mu1 * mu2;
+        const float s11 = e11 - m11, s22 = e22 - m22, s12 = e12 - m12;
+        const float A1 = 2.f * m12 + C1, A2 = 2.f * s12 + C2;
+        const float B1 = m11 + m22 + C1, B2 = s11 + s22 + C2;
+        const float den = B1 * B2;
+        const float Sv = (A1 * A2) / den;
+        acc += 1.f - Sv;
+        // dS/dmu1 = (2 mu2 A2 - 2 mu2 A1)/den - S*2 mu1/B1 + S*2 mu1/B2
+        const float dmu1 = (2.f * mu2 * (A2 - A1)) / den - Sv * 2.f * mu1 / B1 + Sv * 2.f * mu1 / B2;
+        const float de11 = -Sv / B2;
+        const float de12 = 2.f * A1 / den;
+        d3[idx] = dLdS * dmu1;
+        d3[S + idx] = dLdS * de11;
+        d3[2 * S + idx] = dLdS * de12;
+    }
+    block_add(loss, w * acc / (float)S);
+}
+
+__global__ __launch_bounds__(TPB) void ssim_grad_kernel(const float* __restrict__ bd3, const float* __restrict__ a,
+                                                        const float* __restrict__ b, float* __restrict__ g, long S) {
+    for (long idx = blockIdx.x * (long)TPB + threadIdx.x; idx < S; idx += (long)gridDim.x * TPB) {
+        const float p = (a[idx] + 1.f) * 0.5f, q = (b[idx] + 1.f) * 0.5f;
+        const float gp = bd3[idx] + 2.f * p * bd3[S + idx] + q * bd3[2 * S + idx];
+        g[idx] += 0.5f * gp;  // d a'/d a = 1/2
+    }
+}
+
+__global__ __launch_bounds__(TPB) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v, long n,
+                                                   float step_size, float b1, float b2, float bc2s, float eps) {
+    const float w1 = 1.f - b1, w2 = 1.f - b2;
+    for (long i = blockIdx.x * (long)TPB + threadIdx.x; i < n; i += (long)gridDim.x * TPB) {
+        const float gi = g[i];
+        float mi = m[i];
+        // torch lerp: weight < 0.5 ? m + w*(g-m) : g - (g-m)*(1-w)
+        mi = (w1 < 0.5f) ? mi + w1 * (gi - mi) : gi - (gi - mi) * (1.f - w1);
+        float vi = v[i] * b2 + w2 * gi * gi;
+        const float denom = sqrtf(vi) / bc2s + eps;
+        p[i] = p[i] + (-step_size) * (mi / denom);
+        m[i] = mi;
+        v[i] = vi;
+    }
+}
+
+Win11 gauss11() {
+    // ir:699-703 in fp32: coords = arange(11) - 5, exp(-c^2 / (2*1.5^2)), normalised
+    Win11 w;
+    float s = 0.f;
+    for (int k = 0; k < 11; ++k) {
+        float c = (float)k - 5.0f;
+        w.g[k] = expf(-(c * c) / (2.f * 1.5f * 1.5f));
+        s += w.g[k];
+    }
+    for (int k = 0; k < 11; ++k) w.g[k] /= s;
+    return w;
+}
+
+}  // namespace
+
+extern "C" int irgan_hinge(const float* pred, int32_t n_half, int32_t mode, float scale, float* grad, double* loss,
+                           irgan_stream_t s) {
+    long total = mode == 0 ? 2L * n_half : n_half;
+    hinge_kernel<<<nblocks(total), TPB, 0, (hipStream_t)s>>>(pred, n_half, mode, scale, grad, loss);
+    IRGAN_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int irgan_l1(const void* a, const void* b, int32_t dtype, int64_t count, float w, void* ga,
+                        int32_t ga_dtype, int32_t accumulate, double* loss, irgan_stream_t s) {
+    hipStream_t st = (hipStream_t)s;
+    int nb = nblocks(count);
+    if (dtype == IRGAN_F32) {
+        if (ga_dtype == IRGAN_BF16)
+            l1_kernel<float, bf16_t><<<nb, TPB, 0, st>>>((const float*)a, (const float*)b, count, w, (bf16_t*)ga,
+                                                         accumulate, loss);
+        else
+            l1_kernel<float, float><<<nb, TPB, 0, st>>>((const float*)a, (const float*)b, count, w, (float*)ga,
+                                                        accumulate, loss);
+    } else {
+        if (ga_dtype == IRGAN_BF16)
+            l1_kernel<bf16_t, bf16_t><<<nb, TPB, 0, st>>>((const bf16_t*)a, (const bf16_t*)b, count, w, (bf16_t*)ga,
+                                                          accumulate, loss);
+        else
+            l1_kernel<bf16_t, float><<<nb, TPB, 0, st>>>((const bf16_t*)a, (const bf16_t*)b, count, w, (float*)ga,
+                                                         accumulate, loss);
+    }
+    IRGAN_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int irgan_tv(const float* x, int32_t N, int32_t H, int32_t W, int32_t C, float w, float* g, double* loss,
+                        irgan_stream_t s) {
+    long total = (long)N * H * W * C;
+    float inv_v = H > 1 ? 1.f / (float)((long)N * C * (H - 1) * W) : 0.f;
+    float inv_h = W > 1 ? 1.f / (float)((long)N * C * H * (W - 1)) : 0.f;
+    tv_kernel<<<nblocks(total), TPB, 0, (hipStream_t)s>>>(x, H, W, C, w, g, loss, total, inv_v, inv_h);
+    IRGAN_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int irgan_ssim(const float* a, const float* b, int32_t N, int32_t H, int32_t W, int32_t C, float w,
+                          float* g, double* loss, float* work, irgan_stream_t s) {
+    hipStream_t st = (hipStream_t)s;
+    const long S = (long)N * H * W * C;
+    const Win11 win = gauss11();
+    float* w0 = work;          // 5 maps
+    float* w1 = work + 5 * S;  // 5 maps
+    const int nb = nblocks(S);
+    ssim_h5_kernel<<<nb, TPB, 0, st>>>(a, b, W, C, win, w0, S);
+    ssim_v_kernel<5><<<nb, TPB, 0, st>>>(w0, H, W, C, win, w1, S);
+    ssim_map_kernel<<<nb, TPB, 0, st>>>(w1, w, w0, loss, S);
+    ssim_h_kernel<3><<<nb, TPB, 0, st>>>(w0, W, C, win, w1, S);
+    ssim_v_kernel<3><<<nb, TPB, 0, st>>>(w1, H, W, C, win, w0, S);
+    ssim_grad_kernel<<<nb, TPB, 0, st>>>(w0, a, b, g, S);
+    IRGAN_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int irgan_adam(float* p, const float* g, float* m, float* v, int64_t n, float step_size, float beta1,
+                          float beta2, float bc2_sqrt, float eps, irgan_stream_t s) {
+    if (n <= 0) return 0;
+    adam_kernel<<<nblocks(n), TPB, 0, (hipStream_t)s>>>(p, g, m, v, n, step_size, beta1, beta2, bc2_sqrt, eps);
+    IRGAN_LAUNCH_CHECK();
+    return 0;
+}

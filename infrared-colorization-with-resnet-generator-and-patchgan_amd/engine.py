@@ -1,0 +1,651 @@
+"""The fused GAN train step on HIP kernels (the product hot path).
+
+One ``GANStep.step(ir, rgb)`` = the reference's inner-loop body
+(ir:1636-1681) in its minimal form: one G forward reused (detached) for the D
+step; D forward/backward on the batched [real; fake] pair; D Adam; D forward on
+fake with the updated D; hinge + L1 + VGG-perceptual + TV + SSIM losses with
+their gradients written directly; G backward; G Adam.  No autograd tape: every
+backward is an explicit HIP kernel sequence over activations kept in static
+NHWC buffers (capturable in a HIP graph).
+
+Parameters live in flat fp32 buffers (one per network) whose per-key slices are
+KRSC conv weights; the reference's OIHW ``state_dict`` tensors are permuted
+*views* of those slices (``ParamStore.oihw``), so checkpoints load/save in the
+reference layout while the kernels and the single-launch Adam read the flat
+buffer.  Data-parallel: each rank owns a batch shard and all-reduces the flat
+gradient buffers (RCCL) before each Adam.
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+
+import torch
+
+from . import ops
+from .ops import (ACT_LRELU, ACT_NONE, ACT_RELU, ACT_TANH, BF16, F32, PAD_REFLECT, PAD_ZERO, ConvSpec, Feat,
+                  PackedConv)
+
+IMAGENET_MEAN = (0.485, 0.456, 0.406)   # ir:672
+IMAGENET_STD = (0.229, 0.224, 0.225)    # ir:673
+
+
+# ----------------------------------------------------------------------------
+# parameter layout (reference state_dict keys / OIHW shapes / order)
+# ----------------------------------------------------------------------------
+
+def g_param_shapes(input_nc=1, output_nc=3, ngf=64, n_blocks=9, no_antialias=False, no_antialias_up=False):
+    """ResnetUNetGenerator state_dict layout (ir:443-531), buffers included."""
+    s = OrderedDict()
+    s["inc.1.weight"] = (ngf, input_nc, 7, 7); s["inc.1.bias"] = (ngf,)
+    s["down1.0.weight"] = (2 * ngf, ngf, 3, 3); s["down1.0.bias"] = (2 * ngf,)
+    if not no_antialias:
+        s["down1_down.filt"] = (2 * ngf, 1, 3, 3)
+    s["down2.0.weight"] = (4 * ngf, 2 * ngf, 3, 3); s["down2.0.bias"] = (4 * ngf,)
+    if not no_antialias:
+        s["down2_down.filt"] = (4 * ngf, 1, 3, 3)
+    for b in range(n_blocks):
+        for c in (1, 5):
+            s[f"resblocks.{b}.conv_block.{c}.weight"] = (4 * ngf, 4 * ngf, 3, 3)
+            s[f"resblocks.{b}.conv_block.{c}.bias"] = (4 * ngf,)
+    for name, ch, cat in (("up1", 4 * ngf, 6 * ngf), ("up2", 2 * ngf, 3 * ngf)):
+        if no_antialias_up:
+            s[f"{name}_up.weight"] = (ch, ch, 3, 3); s[f"{name}_up.bias"] = (ch,)
+        else:
+            s[f"{name}_up.filt"] = (ch, 1, 3, 3)
+        s[f"{name}_conv.0.weight"] = (ch // 2, cat, 3, 3); s[f"{name}_conv.0.bias"] = (ch // 2,)
+    s["outc.1.weight"] = (output_nc, ngf, 7, 7); s["outc.1.bias"] = (output_nc,)
+    return s
+
+
+def d_param_shapes(input_nc=4, ndf=64):
+    """NLayerDiscriminator(n_layers=3) layout (ir:585-632)."""
+    s = OrderedDict()
+    chans = [input_nc, ndf, 2 * ndf, 4 * ndf, 8 * ndf, 1]
+    for i, idx in enumerate((0, 2, 5, 8, 11)):
+        s[f"model.{idx}.weight"] = (chans[i + 1], chans[i], 4, 4)
+        s[f"model.{idx}.bias"] = (chans[i + 1],)
+    return s
+
+
+VGG_CONVS = ((0, 3, 64), (2, 64, 64), (5, 64, 128), (7, 128, 128), (10, 128, 256), (12, 256, 256), (14, 256, 256))
+
+
+def vgg_param_shapes():
+    s = OrderedDict()
+    for i, ci, co in VGG_CONVS:
+        s[f"{i}.weight"] = (co, ci, 3, 3); s[f"{i}.bias"] = (co,)
+    return s
+
+
+class ParamStore:
+    """Flat fp32 parameter / gradient / Adam-moment buffers for one network."""
+
+    def __init__(self, shapes: "OrderedDict[str, tuple]", device, with_grad=True, with_adam=True):
+        self.shapes = OrderedDict((k, tuple(v)) for k, v in shapes.items() if not k.endswith(".filt"))
+        self.offsets, off = {}, 0
+        for k, shp in self.shapes.items():
+            self.offsets[k] = off
+            off += math.prod(shp)
+            off = (off + 63) // 64 * 64  # 256-byte aligned slices
+        self.numel = off
+        self.device = device
+        self.flat = torch.zeros(off, device=device)
+        self.grad = torch.zeros(off, device=device) if with_grad else None
+        self.m = torch.zeros(off, device=device) if with_adam else None
+        self.v = torch.zeros(off, device=device) if with_adam else None
+        self.step_count = 0
+
+    def krsc(self, k, buf=None):
+        buf = self.flat if buf is None else buf
+        o = self.offsets[k]
+        return buf[o:o + math.prod(self.shapes[k])]
+
+    def oihw(self, k, buf=None):
+        """The reference-layout view: OIHW shape over KRSC storage."""
+        shp = self.shapes[k]
+        t = self.krsc(k, buf)
+        if len(shp) == 4:
+            O, I, KH, KW = shp
+            return t.view(O, KH, KW, I).permute(0, 3, 1, 2)
+        return t.view(shp)
+
+    @torch.no_grad()
+    def load(self, state: dict, strict=False):
+        """Copy OIHW tensors (reference checkpoint / state_dict) into the store."""
+        missing = []
+        for k in self.shapes:
+            if k not in state:
+                missing.append(k)
+                continue
+            src = state[k]
+            dst = self.oihw(k)
+            if tuple(src.shape) != tuple(dst.shape):
+                raise RuntimeError(f"size mismatch for {k}: copying {tuple(src.shape)} into {tuple(dst.shape)}")
+            dst.copy_(src.to(self.device, torch.float32))
+        if strict and missing:
+            raise RuntimeError(f"missing keys {missing}")
+        return missing
+
+    def state(self, buf=None):
+        return OrderedDict((k, self.oihw(k, buf)) for k in self.shapes)
+
+    def zero_grad(self):
+        self.grad.zero_()
+
+    def adam_step(self, lr, b1=0.5, b2=0.999, eps=1e-8):
+        self.step_count += 1
+        ops.adam(self.flat, self.grad, self.m, self.v, self.step_count, lr, b1, b2, eps)
+
+
+def _pc(store: ParamStore, key: str, spec: ConvSpec, dtype, need_dgrad=True, bias=True):
+    return PackedConv(spec, store.krsc(key + ".weight"), store.krsc(key + ".bias") if bias else None, dtype,
+                      need_dgrad=need_dgrad)
+
+
+class Buffers:
+    """Static device buffers keyed by name (allocated once per shape)."""
+
+    def __init__(self, device):
+        self.device, self.d = device, {}
+
+    def get(self, name, shape, dtype):
+        t = self.d.get(name)
+        if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype:
+            t = torch.empty(shape, dtype=dtype, device=self.device)
+            self.d[name] = t
+        return t
+
+    def flat(self, name, numel, dtype=torch.float32):
+        t = self.d.get(name)
+        if t is None or t.numel() < numel or t.dtype != dtype:
+            t = torch.empty(numel, dtype=dtype, device=self.device)
+            self.d[name] = t
+        return t
+
+
+class INLayer:
+    """Per-layer InstanceNorm statistics kept from forward to backward."""
+
+    def __init__(self):
+        self.mr = None
+
+    def fwd(self, bufs: Buffers, name: str, x: Feat, y: Feat, act, res: Feat = None, xhat=None):
+        N, C = x.N, x.C
+        work = bufs.flat("in_work", 2 * N * C, torch.float64)
+        self.mr = bufs.get("mr_" + name, (N * C * 2,), torch.float32)
+        ops.in_stats(x, work, self.mr)
+        ops.in_apply(x, self.mr, y, act=act, res=res, xhat=xhat)
+
+    def bwd(self, bufs: Buffers, dy: Feat, z: Feat, act, dx: Feat, db=None, dy2: Feat = None):
+        """z: the PRE-norm input kept from forward; act: the activation after IN."""
+        N, C = z.N, z.C
+        work = bufs.flat("in_work", 2 * N * C, torch.float64)
+        red = bufs.flat("in_red", 2 * N * C)
+        ops.in_backward(dy, z, act, self.mr, work, red, dx, db=db, dy2=dy2)
+
+
+# ----------------------------------------------------------------------------
+# generator  (ir:425-569)
+# ----------------------------------------------------------------------------
+
+class GeneratorEngine:
+    def __init__(self, store: ParamStore, dtype=BF16, ngf=64, input_nc=1, output_nc=3, n_blocks=9,
+                 no_antialias=False, no_antialias_up=False):
+        self.store, self.dtype, self.ngf = store, dtype, ngf
+        self.input_nc, self.output_nc, self.n_blocks = input_nc, output_nc, n_blocks
+        self.no_aa, self.no_aa_up = no_antialias, no_antialias_up
+        self.tdt = ops.TORCH_DT[dtype]
+        c0, c1, c2 = ngf, 2 * ngf, 4 * ngf
+        sd = 2 if no_antialias else 1
+        S = store
+        self.inc = _pc(S, "inc.1", ConvSpec(input_nc, c0, 7, 1, 3, PAD_REFLECT), dtype, need_dgrad=False)
+        self.down1 = _pc(S, "down1.0", ConvSpec(c0, c1, 3, sd, 1, PAD_ZERO), dtype)
+        self.down2 = _pc(S, "down2.0", ConvSpec(c1, c2, 3, sd, 1, PAD_ZERO), dtype)
+        self.res = [(_pc(S, f"resblocks.{b}.conv_block.1", ConvSpec(c2, c2, 3, 1, 1, PAD_REFLECT), dtype),
+                     _pc(S, f"resblocks.{b}.conv_block.5", ConvSpec(c2, c2, 3, 1, 1, PAD_REFLECT), dtype))
+                    for b in range(n_blocks)]
+        if no_antialias_up:
+            # ConvTranspose2d(C, C, 3, s2, p1, op1) == backward-data of conv(3, s2, p1)
+            self.up1_up = _pc(S, "up1_up", ConvSpec(c2, c2, 3, 2, 1, PAD_ZERO), dtype)
+            self.up2_up = _pc(S, "up2_up", ConvSpec(c1, c1, 3, 2, 1, PAD_ZERO), dtype)
+        self.up1 = _pc(S, "up1_conv.0", ConvSpec(c2 + c1, c1, 3, 1, 1, PAD_ZERO), dtype)
+        self.up2 = _pc(S, "up2_conv.0", ConvSpec(c1 + c0, c0, 3, 1, 1, PAD_ZERO), dtype)
+        self.outc = _pc(S, "outc.1", ConvSpec(c0, output_nc, 7, 1, 3, PAD_REFLECT), dtype)
+        self.packs = [self.inc, self.down1, self.down2, self.up1, self.up2, self.outc] + \
+            [p for pr in self.res for p in pr] + ([self.up1_up, self.up2_up] if no_antialias_up else [])
+        n_in = 5 + 2 * n_blocks
+        self.norms = {k: INLayer() for k in ["inc", "down1", "down2", "up1", "up2"] +
+                      [f"r{b}_{i}" for b in range(n_blocks) for i in (1, 2)]}
+        assert len(self.norms) == n_in
+        self.bufs = Buffers(store.device)
+        self.shape = None
+
+    def pack(self):
+        for p in self.packs:
+            p.pack()
+
+    # -- shapes
+    def _dims(self, H, W):
+        H1, W1 = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        H2, W2 = (H1 - 1) // 2 + 1, (W1 - 1) // 2 + 1
+        return H1, W1, H2, W2
+
+    def forward(self, ir_nchw: torch.Tensor, keep=True) -> torch.Tensor:
+        """ir (B, input_nc, H, W) fp32 in [-1,1] -> fake NHWC fp32 (B, H, W, 3)."""
+        B, _, H, W = ir_nchw.shape
+        if H % 4 or W % 4:
+            raise NotImplementedError("the HIP generator path needs H, W divisible by 4 "
+                                      "(the reference's odd-size resize fallback ir:555-556 is not ported)")
+        g, T = self.bufs, self.tdt
+        c0, c1, c2 = self.ngf, 2 * self.ngf, 4 * self.ngf
+        H1, W1, H2, W2 = self._dims(H, W)
+        self.shape = (B, H, W)
+        ir_t = Feat(g.get("ir", (B, H, W, self.input_nc), T))
+        ops.nchw_to_nhwc(ir_nchw.contiguous(), ir_t)
+        cat2 = g.get("cat2", (B, H, W, c1 + c0), T)       # [up2 out | x0]
+        cat1 = g.get("cat1", (B, H1, W1, c2 + c1), T)     # [up1 out | x1]
+        x0 = Feat(cat2, c1, c0)
+        x1 = Feat(cat1, c2, c1)
+        # inc: reflect-pad 3, conv7x7, IN, ReLU  (ir:458-463)
+        z0 = Feat(g.get("z0", (B, H, W, c0), T))
+        ops.conv_fwd(self.inc, ir_t, z0)
+        self.norms["inc"].fwd(g, "inc", z0, x0, ACT_RELU)
+        # down1 (+ blur-down)  (ir:469-474)
+        if self.no_aa:
+            z1 = Feat(g.get("z1", (B, H1, W1, c1), T))
+            ops.conv_fwd(self.down1, x0, z1)
+            self.norms["down1"].fwd(g, "down1", z1, x1, ACT_RELU)
+        else:
+            z1 = Feat(g.get("z1", (B, H, W, c1), T))
+            a1 = Feat(g.get("a1", (B, H, W, c1), T))
+            ops.conv_fwd(self.down1, x0, z1)
+            self.norms["down1"].fwd(g, "down1", z1, a1, ACT_RELU)
+            ops.blur_down(a1, x1)
+        # down2 (+ blur-down)  (ir:477-482)
+        h = Feat(g.get("h0", (B, H2, W2, c2), T))
+        if self.no_aa:
+            z2 = Feat(g.get("z2", (B, H2, W2, c2), T))
+            ops.conv_fwd(self.down2, x1, z2)
+            self.norms["down2"].fwd(g, "down2", z2, h, ACT_RELU)
+        else:
+            z2 = Feat(g.get("z2", (B, H1, W1, c2), T))
+            a2 = Feat(g.get("a2", (B, H1, W1, c2), T))
+            ops.conv_fwd(self.down2, x1, z2)
+            self.norms["down2"].fwd(g, "down2", z2, a2, ACT_RELU)
+            ops.blur_down(a2, h)
+        # 9 ResnetBlocks  (ir:362-418, 485-490)
+        for b, (p1, p2) in enumerate(self.res):
+            r1 = Feat(g.get(f"r1_{b}", (B, H2, W2, c2), T))
+            t = Feat(g.get(f"t{b}", (B, H2, W2, c2), T))
+            ops.conv_fwd(p1, h, r1)
+            self.norms[f"r{b}_1"].fwd(g, f"r{b}_1", r1, t, ACT_RELU)
+            r2 = Feat(g.get(f"r2_{b}", (B, H2, W2, c2), T))
+            ops.conv_fwd(p2, t, r2)
+            hn = Feat(g.get(f"h{b + 1}", (B, H2, W2, c2), T))
+            self.norms[f"r{b}_2"].fwd(g, f"r{b}_2", r2, hn, ACT_NONE, res=h)
+            h = hn
+        # up1 -> cat with x1 -> conv/IN/ReLU  (ir:554-558)
+        y1 = Feat(cat1, 0, c2)
+        if self.no_aa_up:
+            ops.conv_dgrad(self.up1_up, h, y1, bias=True)
+        else:
+            ops.upsample(h, y1)
+        z3 = Feat(g.get("z3", (B, H1, W1, c1), T))
+        a3 = Feat(g.get("a3", (B, H1, W1, c1), T))
+        ops.conv_fwd(self.up1, Feat(cat1), z3)
+        self.norms["up1"].fwd(g, "up1", z3, a3, ACT_RELU)
+        # up2 -> cat with x0 -> conv/IN/ReLU  (ir:561-565)
+        y2 = Feat(cat2, 0, c1)
+        if self.no_aa_up:
+            ops.conv_dgrad(self.up2_up, a3, y2, bias=True)
+        else:
+            ops.upsample(a3, y2)
+        z4 = Feat(g.get("z4", (B, H, W, c0), T))
+        a4 = Feat(g.get("a4", (B, H, W, c0), T))
+        ops.conv_fwd(self.up2, Feat(cat2), z4)
+        self.norms["up2"].fwd(g, "up2", z4, a4, ACT_RELU)
+        # outc: reflect-pad 3, conv7x7 (+bias), tanh  (ir:527-531)
+        fake = g.get("fake", (B, H, W, self.output_nc), torch.float32)
+        ops.conv_fwd(self.outc, a4, Feat(fake), act=ACT_TANH)
+        return fake
+
+    def backward(self, dfake: torch.Tensor):
+        """dfake: dL/dfake, NHWC fp32 (B,H,W,3).  Accumulates into store.grad."""
+        B, H, W = self.shape
+        g, T, S, dt = self.bufs, self.tdt, self.store, self.dtype
+        c0, c1, c2 = self.ngf, 2 * self.ngf, 4 * self.ngf
+        H1, W1, H2, W2 = self._dims(H, W)
+        G = S.grad
+        cat1, cat2 = Feat(g.d["cat1"]), Feat(g.d["cat2"])
+        x0, x1 = cat2.sl(c1, c0), cat1.sl(c2, c1)
+        padbuf = g.flat("dpad", max(B * (H + 6) * (W + 6) * c0, B * (H2 + 2) * (W2 + 2) * c2))
+
+        def wg(pc, key, x, dy):
+            ops.conv_wgrad(pc.spec, x, dy, S.krsc(key + ".weight", G), dt)
+
+        # outc: tanh' then conv backward
+        fake = Feat(g.d["fake"])
+        dzo = Feat(g.get("dz_out", (B, H, W, self.output_nc), T))
+        ops.act_bwd(Feat(dfake), fake, ACT_TANH, dzo)
+        a4 = Feat(g.d["a4"])
+        wg(self.outc, "outc.1", a4, dzo)
+        ops.channel_sum(dzo, S.krsc("outc.1.bias", G))
+        da4 = Feat(g.get("da4", (B, H, W, c0), T))
+        ops.conv_dgrad(self.outc, dzo, da4, pad_buf=padbuf)
+        # up2_conv
+        self.norms["up2"].bwd(g, da4, Feat(g.d["z4"]), ACT_RELU, da4, db=S.krsc("up2_conv.0.bias", G))
+        wg(self.up2, "up2_conv.0", cat2, da4)
+        dcat2 = Feat(g.get("dcat2", (B, H, W, c1 + c0), T))
+        ops.conv_dgrad(self.up2, da4, dcat2)
+        # up2_up
+        a3 = Feat(g.d["a3"])
+        da3 = Feat(g.get("da3", (B, H1, W1, c1), T))
+        dy2 = dcat2.sl(0, c1)
+        if self.no_aa_up:
+            ops.channel_sum(dy2, S.krsc("up2_up.bias", G))
+            wg(self.up2_up, "up2_up", dy2, a3)
+            ops.conv_fwd(self.up2_up, dy2, da3, bias=False)
+        else:
+            ops.upsample_bwd(dy2, da3, g.flat("up_work", B * H * W * c1))
+        # up1_conv
+        self.norms["up1"].bwd(g, da3, Feat(g.d["z3"]), ACT_RELU, da3, db=S.krsc("up1_conv.0.bias", G))
+        wg(self.up1, "up1_conv.0", cat1, da3)
+        dcat1 = Feat(g.get("dcat1", (B, H1, W1, c2 + c1), T))
+        ops.conv_dgrad(self.up1, da3, dcat1)
+        # up1_up
+        h9 = Feat(g.d[f"h{self.n_blocks}"])
+        dh = Feat(g.get("dh", (B, H2, W2, c2), T))
+        dy1 = dcat1.sl(0, c2)
+        if self.no_aa_up:
+            ops.channel_sum(dy1, S.krsc("up1_up.bias", G))
+            wg(self.up1_up, "up1_up", dy1, h9)
+            ops.conv_fwd(self.up1_up, dy1, dh, bias=False)
+        else:
+            ops.upsample_bwd(dy1, dh, g.flat("up_work", B * H * W * c1))
+        # resblocks, reversed: dh holds d h_{b+1}; becomes d h_b in place
+        dt_ = Feat(g.get("dtmp", (B, H2, W2, c2), T))
+        for b in reversed(range(self.n_blocks)):
+            p1, p2 = self.res[b]
+            key = f"resblocks.{b}.conv_block."
+            t, hb = Feat(g.d[f"t{b}"]), Feat(g.d[f"h{b}"])
+            r1, r2 = Feat(g.d[f"r1_{b}"]), Feat(g.d[f"r2_{b}"])
+            self.norms[f"r{b}_2"].bwd(g, dh, r2, ACT_NONE, dt_, db=S.krsc(key + "5.bias", G))
+            wg(p2, key + "5", t, dt_)
+            dr = Feat(g.get("dtmp2", (B, H2, W2, c2), T))
+            ops.conv_dgrad(p2, dt_, dr, pad_buf=padbuf)
+            self.norms[f"r{b}_1"].bwd(g, dr, r1, ACT_RELU, dr, db=S.krsc(key + "1.bias", G))
+            wg(p1, key + "1", hb, dr)
+            ops.conv_dgrad(p1, dr, dh, accumulate=True, pad_buf=padbuf)
+        # down2 (+ blur-down)
+        z2 = Feat(g.d["z2"])
+        if self.no_aa:
+            self.norms["down2"].bwd(g, dh, z2, ACT_RELU, dh, db=S.krsc("down2.0.bias", G))
+            dz2 = dh
+        else:
+            dz2 = Feat(g.get("da2", (B, H1, W1, c2), T))
+            ops.blur_down_bwd(dh, dz2)
+            self.norms["down2"].bwd(g, dz2, z2, ACT_RELU, dz2, db=S.krsc("down2.0.bias", G))
+        wg(self.down2, "down2.0", x1, dz2)
+        dx1 = dcat1.sl(c2, c1)
+        ops.conv_dgrad(self.down2, dz2, dx1, accumulate=True)  # x1 feeds down2 and the up1 concat
+        # down1 (+ blur-down)
+        z1 = Feat(g.d["z1"])
+        if self.no_aa:
+            dz1 = Feat(g.get("da1", (B, H1, W1, c1), T))
+            self.norms["down1"].bwd(g, dx1, z1, ACT_RELU, dz1, db=S.krsc("down1.0.bias", G))
+        else:
+            dz1 = Feat(g.get("da1", (B, H, W, c1), T))
+            ops.blur_down_bwd(dx1, dz1)
+            self.norms["down1"].bwd(g, dz1, z1, ACT_RELU, dz1, db=S.krsc("down1.0.bias", G))
+        wg(self.down1, "down1.0", x0, dz1)
+        dx0 = dcat2.sl(c1, c0)
+        ops.conv_dgrad(self.down1, dz1, dx0, accumulate=True)
+        # inc
+        self.norms["inc"].bwd(g, dx0, Feat(g.d["z0"]), ACT_RELU, dx0, db=S.krsc("inc.1.bias", G))
+        wg(self.inc, "inc.1", Feat(g.d["ir"]), dx0)
+
+
+# ----------------------------------------------------------------------------
+# discriminator  (ir:576-635)
+# ----------------------------------------------------------------------------
+
+class DiscriminatorEngine:
+    LAYERS = (("model.0", 2, False), ("model.2", 2, True), ("model.5", 2, True), ("model.8", 1, True),
+              ("model.11", 1, False))
+
+    def __init__(self, store: ParamStore, dtype=BF16, input_nc=4, ndf=64):
+        self.store, self.dtype, self.tdt = store, dtype, ops.TORCH_DT[dtype]
+        chans = [input_nc, ndf, 2 * ndf, 4 * ndf, 8 * ndf, 1]
+        self.chans = chans
+        self.packs = [_pc(store, k, ConvSpec(chans[i], chans[i + 1], 4, s, 1, PAD_ZERO), dtype)
+                      for i, (k, s, _) in enumerate(self.LAYERS)]
+        self.norms = [INLayer() if n else None for (_, _, n) in self.LAYERS]
+        self.bufs = Buffers(store.device)
+
+    def pack(self):
+        for p in self.packs:
+            p.pack()
+
+    def forward(self, din: Feat, tag="") -> torch.Tensor:
+        """din: NHWC (NB, H, W, 4) compute-dtype -> patch logits (NB, h, w, 1) fp32."""
+        g, T = self.bufs, self.tdt
+        x = din
+        self.acts = [din]
+        self.pre = {}
+        for i, pc in enumerate(self.packs):
+            Ho, Wo = pc.spec.out_hw(x.H, x.W)
+            last = i == len(self.packs) - 1
+            y = Feat(g.get(f"{tag}e{i}", (x.N, Ho, Wo, pc.spec.cout), torch.float32 if last else T))
+            if i == 0:
+                ops.conv_fwd(pc, x, y, act=ACT_LRELU)
+            elif last:
+                ops.conv_fwd(pc, x, y)
+            else:
+                z = Feat(g.get(f"{tag}z{i}", (x.N, Ho, Wo, pc.spec.cout), T))
+                ops.conv_fwd(pc, x, z)
+                self.norms[i].fwd(g, f"{tag}n{i}", z, y, ACT_LRELU)
+                self.pre[i] = z
+            self.acts.append(y)
+            x = y
+        return x.t
+
+    def backward(self, dout: torch.Tensor, want_wgrad=True, want_dinput=False, tag=""):
+        """dout: dL/dlogits fp32 (same shape as forward output).  Weight grads
+        accumulate into store.grad; returns d input (fp32 NHWC) if asked."""
+        g, T, S = self.bufs, self.tdt, self.store
+        G = S.grad
+        n = len(self.packs)
+        dy = Feat(g.get(f"{tag}dout_t", tuple(dout.shape), T))
+        ops.axpby(Feat(dout), 1.0, dy)
+        for i in reversed(range(n)):
+            pc, key = self.packs[i], self.LAYERS[i][0]
+            x = self.acts[i]
+            if i == n - 1:
+                if want_wgrad:
+                    ops.channel_sum(Feat(dout), S.krsc(key + ".bias", G))
+            elif self.norms[i] is not None:
+                self.norms[i].bwd(g, dy, self.pre[i], ACT_LRELU, dy,
+                                  db=S.krsc(key + ".bias", G) if want_wgrad else None)
+            elif want_wgrad:  # layer 0: LReLU mask already folded into dy by the layer-1 dgrad
+                ops.channel_sum(dy, S.krsc(key + ".bias", G))
+            if want_wgrad:
+                ops.conv_wgrad(pc.spec, x, dy, S.krsc(key + ".weight", G), self.dtype)
+            if i == 0:
+                if not want_dinput:
+                    return None
+                dx = Feat(g.get(f"{tag}dinput", (x.N, x.H, x.W, x.C), torch.float32))
+                ops.conv_dgrad(pc, dy, dx)
+                return dx
+            dx = Feat(g.get(f"{tag}d{i}", (x.N, x.H, x.W, x.C), T))
+            if i == 1:  # previous activation is LReLU without IN: fold its derivative in the epilogue
+                ops.conv_dgrad(pc, dy, dx, mask=x, mask_act=2)
+            else:
+                ops.conv_dgrad(pc, dy, dx)
+            dy = dx
+        return None
+
+
+# ----------------------------------------------------------------------------
+# VGG-16 features[:16] perceptual extractor  (ir:642-683), frozen
+# ----------------------------------------------------------------------------
+
+class VGGEngine:
+    def __init__(self, store: ParamStore, dtype=BF16):
+        self.store, self.dtype, self.tdt = store, dtype, ops.TORCH_DT[dtype]
+        self.packs = [_pc(store, str(i), ConvSpec(ci, co, 3, 1, 1, PAD_ZERO), dtype) for i, ci, co in VGG_CONVS]
+        dev = store.device
+        std = torch.tensor(IMAGENET_STD)
+        mean = torch.tensor(IMAGENET_MEAN)
+        # ((x+1)/2 - mean)/std  ==  x * (0.5/std) + (0.5 - mean)/std
+        self.scale = (0.5 / std).float().to(dev)
+        self.shift = ((0.5 - mean) / std).float().to(dev)
+        self.bufs = Buffers(dev)
+
+    def pack(self):
+        for p in self.packs:
+            p.pack()
+
+    def forward(self, vin: Feat) -> Feat:
+        g, T = self.bufs, self.tdt
+        x = vin
+        self.acts = [vin]
+        for j, pc in enumerate(self.packs):
+            y = Feat(g.get(f"v{j}", (x.N, x.H, x.W, pc.spec.cout), T))
+            ops.conv_fwd(pc, x, y, act=ACT_RELU)
+            self.acts.append(y)
+            x = y
+            if j in (1, 3):
+                p = Feat(g.get(f"p{j}", (x.N, x.H // 2, x.W // 2, x.C), T))
+                ops.maxpool(x, p)
+                self.acts.append(p)
+                x = p
+        return x
+
+    def backward_input(self, dfeat: Feat, nb: int) -> Feat:
+        """d(input) for the first nb images (frozen weights: backward-data only).
+        dfeat = dL/d(relu3_3 output) for those images."""
+        g, T = self.bufs, self.tdt
+        acts = [a.batch(0, nb) for a in self.acts]
+        # acts: [vin, v0, v1, p1, v2, v3, p3, v4, v5, v6]
+        out_of = {0: 1, 1: 2, 2: 4, 3: 5, 4: 7, 5: 8, 6: 9}     # conv j output index in acts
+        in_of = {0: 0, 1: 1, 2: 3, 3: 4, 4: 6, 5: 7, 6: 8}      # conv j input index in acts
+        dz = Feat(g.get("dz6", tuple(dfeat.t.shape), T))
+        ops.act_bwd(dfeat, acts[out_of[6]], ACT_RELU, dz)
+        for j in reversed(range(len(self.packs))):
+            pc = self.packs[j]
+            xin = acts[in_of[j]]
+            if j == 0:
+                dvin = Feat(g.get("dvin", (nb, xin.H, xin.W, xin.C), torch.float32))
+                ops.conv_dgrad(pc, dz, dvin)
+                return dvin
+            prev = in_of[j]
+            if prev in (3, 6):  # input is a pool output: dgrad -> maxpool bwd (+relu') of the pool input
+                dp = Feat(g.get(f"dp{j}", (nb, xin.H, xin.W, xin.C), T))
+                ops.conv_dgrad(pc, dz, dp)
+                src = acts[prev - 1]
+                dzn = Feat(g.get(f"dz{j - 1}", (nb, src.H, src.W, src.C), T))
+                ops.maxpool_bwd(src, dp, dzn, relu_mask=True)
+            else:  # input is a ReLU output: fold relu' into the dgrad epilogue
+                dzn = Feat(g.get(f"dz{j - 1}", (nb, xin.H, xin.W, xin.C), T))
+                ops.conv_dgrad(pc, dz, dzn, mask=xin, mask_act=1)
+            dz = dzn
+        return None
+
+
+# ----------------------------------------------------------------------------
+# the train step
+# ----------------------------------------------------------------------------
+
+class GANStep:
+    """Buffers, engines and the fused step for one rank.
+
+    Loss slots (fp64, device): 0 loss_D, 1 lambda_gan*GAN, 2 L1*l, 3 perc*l, 4 TV*l, 5 SSIM*l.
+    """
+
+    def __init__(self, G: ParamStore, D: ParamStore, V: ParamStore, cfg, dtype=BF16, process_group=None,
+                 gen: GeneratorEngine = None, dis: DiscriminatorEngine = None, vgg: VGGEngine = None):
+        self.G, self.D, self.V, self.cfg, self.dtype = G, D, V, cfg, dtype
+        self.tdt = ops.TORCH_DT[dtype]
+        self.gen = gen or GeneratorEngine(G, dtype, ngf=cfg.ngf, input_nc=cfg.input_nc, output_nc=cfg.output_nc,
+                                          no_antialias=cfg.no_antialias, no_antialias_up=cfg.no_antialias_up)
+        self.dis = dis or DiscriminatorEngine(D, dtype, input_nc=cfg.input_nc + cfg.output_nc)
+        self.vgg = vgg or VGGEngine(V, dtype)
+        self.bufs = Buffers(G.device)
+        self.losses = torch.zeros(8, dtype=torch.float64, device=G.device)
+        self.pg = process_group
+        self.lr_scale = 1.0
+        self.vgg.pack()
+        self.gen.pack()
+        self.dis.pack()
+
+    def _allreduce(self, t):
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.AVG, group=self.pg)
+
+    def _din(self, ir_t: Feat, img: torch.Tensor, out: Feat):
+        """cat([ir, img], 1) (ir:1639-1640) written straight into the NHWC D input."""
+        ops.axpby(ir_t, 1.0, out.sl(0, ir_t.C))
+        ops.axpby(Feat(img), 1.0, out.sl(ir_t.C, img.shape[3]))
+
+    def step(self, ir: torch.Tensor, rgb: torch.Tensor):
+        """One train step on NCHW fp32 device tensors; returns the loss vector (device)."""
+        cfg, b, T = self.cfg, self.bufs, self.tdt
+        B, _, H, W = ir.shape
+        cin, cout = cfg.input_nc, cfg.output_nc
+        self.losses.zero_()
+        L = self.losses
+        # ---- G forward once (ir:1638 / 1657 compute the same image)
+        fake = self.gen.forward(ir)
+        ir_t = Feat(self.gen.bufs.d["ir"])
+        rgb_h = b.get("rgb_nhwc", (B, H, W, cout), torch.float32)
+        ops.nchw_to_nhwc(rgb.contiguous(), Feat(rgb_h))
+        # ---- D step on [real; fake] as one 2B batch (ir:1636-1651)
+        self.D.zero_grad()
+        din = Feat(b.get("din2", (2 * B, H, W, cin + cout), T))
+        self._din(ir_t, rgb_h, din.batch(0, B))
+        self._din(ir_t, fake, din.batch(B, B))
+        pred = self.dis.forward(din, tag="d")
+        dpred = b.get("dpred", tuple(pred.shape), torch.float32)
+        ops.hinge(pred, pred[:B].numel(), 0, 1.0, dpred, L[0:1])
+        self.dis.backward(dpred, want_wgrad=True, want_dinput=False, tag="d")
+        self._allreduce(self.D.grad)
+        self.D.adam_step(cfg.lr_D * self.lr_scale, cfg.beta1, cfg.beta2)
+        self.dis.pack()
+        # ---- G step (ir:1656-1681)
+        self.G.zero_grad()
+        dfake = b.get("dfake", (B, H, W, cout), torch.float32)
+        dfake.zero_()
+        dinf = Feat(b.get("din1", (B, H, W, cin + cout), T))
+        self._din(ir_t, fake, dinf)
+        predg = self.dis.forward(dinf, tag="g")
+        dpg = b.get("dpredg", tuple(predg.shape), torch.float32)
+        ops.hinge(predg, predg.numel(), 1, cfg.lambda_gan, dpg, L[1:2])
+        dd = self.dis.backward(dpg, want_wgrad=False, want_dinput=True, tag="g")
+        ops.axpby(dd.sl(cin, cout), 1.0, Feat(dfake), 1.0)
+        ops.l1(fake, rgb_h, cfg.lambda_L1, dfake, L[2:3], accumulate=True)
+        # perceptual: VGG on [fake; rgb] as one 2B batch (ir:1667-1669)
+        vin = Feat(b.get("vin", (2 * B, H, W, cout), T))
+        ops.affine(Feat(fake), self.vgg.scale, self.vgg.shift, vin.batch(0, B))
+        ops.affine(Feat(rgb_h), self.vgg.scale, self.vgg.shift, vin.batch(B, B))
+        feat = self.vgg.forward(vin)
+        dfeat = b.get("dfeat", (B, feat.H, feat.W, feat.C), T)
+        ops.l1(feat.t[:B], feat.t[B:], cfg.lambda_perc, dfeat, L[3:4])
+        dv = self.vgg.backward_input(Feat(dfeat), B)
+        ops.affine(dv, self.vgg.scale, None, Feat(dfake), accumulate=True)
+        ops.tv(Feat(fake), cfg.lambda_tv, dfake, L[4:5])
+        ssim_work = b.flat("ssim_work", 10 * fake.numel())
+        ops.ssim(Feat(fake), Feat(rgb_h), cfg.lambda_ssim, dfake, L[5:6], ssim_work)
+        self.gen.backward(dfake)
+        self._allreduce(self.G.grad)
+        self.G.adam_step(cfg.lr_G * self.lr_scale, cfg.beta1, cfg.beta2)
+        self.gen.pack()
+        return L
+
+    @staticmethod
+    def loss_dict(L: torch.Tensor, cfg) -> dict:
+        v = L.tolist()
+        gan = v[1] / cfg.lambda_gan if cfg.lambda_gan else 0.0
+        return dict(loss_D=v[0], loss_G=v[1] + v[2] + v[3] + v[4] + v[5], loss_G_GAN=gan, loss_G_L1=v[2],
+                    loss_G_perc=v[3], loss_G_TV=v[4], loss_G_ssim=v[5])

@@ -1,0 +1,302 @@
+"""Thin typed wrappers over the C ABI (include/irgan.h) on device tensors.
+
+Activations are NHWC ``Feat`` slices (tensor, channel offset, channel count);
+torch is used for device memory and the current HIP stream only.  Every
+function here launches hand-written HIP kernels from libirgan.so.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+
+from . import _lib
+from ._lib import ACT_LRELU, ACT_NONE, ACT_RELU, ACT_TANH, BF16, F32, PAD_REFLECT, PAD_ZERO  # noqa: F401
+
+TORCH_DT = {F32: torch.float32, BF16: torch.bfloat16}
+
+
+def dt_code(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return F32
+    if t.dtype == torch.bfloat16:
+        return BF16
+    raise TypeError(f"unsupported dtype {t.dtype}")
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def P(t):
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+class Feat:
+    """NHWC channel slice: element (p, c) at t.view(-1)[p*ld + off + c]."""
+    __slots__ = ("t", "off", "C")
+
+    def __init__(self, t: torch.Tensor, off: int = 0, C: int | None = None):
+        assert t.dim() == 4 and t.is_contiguous()
+        self.t, self.off = t, off
+        self.C = t.shape[3] - off if C is None else C
+
+    N = property(lambda s: s.t.shape[0])
+    H = property(lambda s: s.t.shape[1])
+    W = property(lambda s: s.t.shape[2])
+    ld = property(lambda s: s.t.shape[3])
+    dt = property(lambda s: dt_code(s.t))
+    P = property(lambda s: s.t.shape[0] * s.t.shape[1] * s.t.shape[2])
+
+    @property
+    def ptr(self):
+        return ctypes.c_void_p(self.t.data_ptr())
+
+    def sl(self, off, C):
+        return Feat(self.t, self.off + off, C)
+
+    def batch(self, b0, nb):
+        return Feat(self.t[b0:b0 + nb], self.off, self.C)
+
+
+# ----------------------------------------------------------------------------
+# convolution
+# ----------------------------------------------------------------------------
+
+class ConvSpec:
+    """A conv layer's geometry.  For nn.ConvTranspose2d the spec describes the
+    conv it transposes (cout = ConvT in-channels, cin = ConvT out-channels)."""
+
+    def __init__(self, cin, cout, k, stride=1, pad=0, mode=PAD_ZERO):
+        self.cin, self.cout, self.k, self.stride, self.pad, self.mode = cin, cout, k, stride, pad, mode
+
+    def out_hw(self, H, W):
+        p, k, s = self.pad, self.k, self.stride
+        return (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+
+    def phases(self, reflect_padded=False):
+        """backward-data phase decomposition per axis: (phase, tap residue, taps, c0)."""
+        k, s = self.k, self.stride
+        p = 0 if reflect_padded else self.pad
+        out = []
+        for ph in range(s):
+            tr = (ph + p) % s
+            A = max(0, -(-(k - tr) // s))
+            base = (ph + p - tr) // s
+            out.append((ph, tr, A, base - A + 1))
+        return out
+
+
+def _desc(**kw):
+    d = _lib.ConvDesc()
+    for k, v in kw.items():
+        setattr(d, k, int(v))
+    return d
+
+
+def weight_pack(master: torch.Tensor, dst: torch.Tensor, cout, kh, kw, cin, transpose=0, s=1, tyr=0, ay=0,
+                txr=0, ax=0):
+    _lib.call("irgan_weight_pack", P(master), P(dst), dt_code(dst), cout, kh, kw, cin, transpose, s, tyr, ay, txr,
+              ax, stream())
+
+
+class PackedConv:
+    """Per-layer packed weights: forward (cast) and backward-data (flipped /
+    per-phase) images in the compute dtype, refreshed after each optimizer step."""
+
+    def __init__(self, spec: ConvSpec, master: torch.Tensor, bias: torch.Tensor | None, dtype: int,
+                 need_dgrad=True, reflect_dgrad=None):
+        self.spec, self.master, self.bias, self.dtype = spec, master, bias, dtype
+        dev = master.device
+        tdt = TORCH_DT[dtype]
+        k = spec.k
+        self.fwd = master if dtype == F32 else torch.empty(master.numel(), dtype=tdt, device=dev)
+        self.reflect = spec.mode == PAD_REFLECT if reflect_dgrad is None else reflect_dgrad
+        self.dg = []
+        if need_dgrad:
+            for (py, tyr, ay, c0y) in spec.phases(self.reflect):
+                for (px, txr, ax, c0x) in spec.phases(self.reflect):
+                    buf = torch.empty(spec.cin * ay * ax * spec.cout, dtype=tdt, device=dev)
+                    self.dg.append(((py, tyr, ay, c0y), (px, txr, ax, c0x), buf))
+
+    def pack(self):
+        s = self.spec
+        if self.dtype != F32:
+            weight_pack(self.master, self.fwd, s.cout, s.k, s.k, s.cin)
+        for (py, tyr, ay, _), (px, txr, ax, _), buf in self.dg:
+            weight_pack(self.master, buf, s.cout, s.k, s.k, s.cin, 1, s.stride, tyr, ay, txr, ax)
+
+
+def conv_fwd(pc: PackedConv, x: Feat, y: Feat, act=ACT_NONE, bias=True, accumulate=False, mask: Feat = None,
+             mask_act=0):
+    s = pc.spec
+    Ho, Wo = s.out_hw(x.H, x.W)
+    assert (y.H, y.W, y.C) == (Ho, Wo, s.cout) and x.C == s.cin and y.N == x.N, "conv_fwd shape mismatch"
+    d = _desc(N=x.N, H=x.H, W=x.W, Cin=s.cin, ldx=x.ld, xoff=x.off, Ho=Ho, Wo=Wo, Cout=s.cout, ldy=y.ld,
+              yoff=y.off, OH=Ho, OW=Wo, omy=1, ooy=0, omx=1, oox=0, KH=s.k, KW=s.k, sy=s.stride, sx=s.stride,
+              c0y=-s.pad, c0x=-s.pad, pad_mode=s.mode, act=act, accumulate=int(accumulate), dtype=pc.dtype,
+              out_dtype=y.dt, mask_act=mask_act, ldm=mask.ld if mask else 0, moff=mask.off if mask else 0)
+    assert x.dt == pc.dtype
+    _lib.call("irgan_conv_fwd", ctypes.byref(d), x.ptr, P(pc.fwd), P(pc.bias if bias else None), y.ptr,
+              mask.ptr if mask else None, stream())
+
+
+def conv_dgrad(pc: PackedConv, dy: Feat, dx: Feat, accumulate=False, mask: Feat = None, mask_act=0,
+               pad_buf: torch.Tensor = None, bias=False):
+    """dx = d(conv)/dx^T dy.  Reflect-padded layers go through an fp32
+    (H+2p)x(W+2p) buffer and the reflect fold; stride-2 layers launch per phase."""
+    s = pc.spec
+    assert dy.C == s.cout and dx.C == s.cin and dy.dt == pc.dtype
+    if pc.reflect:
+        p = s.pad
+        Hp, Wp = dx.H + 2 * p, dx.W + 2 * p
+        assert pad_buf is not None and pad_buf.numel() >= dx.N * Hp * Wp * s.cin
+        tgt = Feat(pad_buf[:dx.N * Hp * Wp * s.cin].view(dx.N, Hp, Wp, s.cin))
+        (_, _, ay, c0y), (_, _, ax, c0x), buf = pc.dg[0]
+        d = _desc(N=dy.N, H=dy.H, W=dy.W, Cin=s.cout, ldx=dy.ld, xoff=dy.off, Ho=Hp, Wo=Wp, Cout=s.cin,
+                  ldy=tgt.ld, yoff=0, OH=Hp, OW=Wp, omy=1, ooy=0, omx=1, oox=0, KH=ay, KW=ax, sy=1, sx=1,
+                  c0y=c0y, c0x=c0x, pad_mode=PAD_ZERO, act=0, accumulate=0, dtype=pc.dtype, out_dtype=F32,
+                  mask_act=0, ldm=0, moff=0)
+        _lib.call("irgan_conv_fwd", ctypes.byref(d), dy.ptr, P(buf), None, tgt.ptr, None, stream())
+        assert mask is None
+        _lib.call("irgan_reflect_fold", tgt.ptr, dx.N, dx.H, dx.W, s.cin, p, dx.ptr, dx.dt, dx.ld, dx.off,
+                  int(accumulate), stream())
+        return
+    st = s.stride
+    for (py, _, ay, c0y), (px, _, ax, c0x), buf in pc.dg:
+        Ho, Wo = -(-(dx.H - py) // st), -(-(dx.W - px) // st)
+        if Ho <= 0 or Wo <= 0:
+            continue
+        assert ay > 0 and ax > 0
+        d = _desc(N=dy.N, H=dy.H, W=dy.W, Cin=s.cout, ldx=dy.ld, xoff=dy.off, Ho=Ho, Wo=Wo, Cout=s.cin,
+                  ldy=dx.ld, yoff=dx.off, OH=dx.H, OW=dx.W, omy=st, ooy=py, omx=st, oox=px, KH=ay, KW=ax, sy=1,
+                  sx=1, c0y=c0y, c0x=c0x, pad_mode=PAD_ZERO, act=0, accumulate=int(accumulate), dtype=pc.dtype,
+                  out_dtype=dx.dt, mask_act=mask_act, ldm=mask.ld if mask else 0, moff=mask.off if mask else 0)
+        _lib.call("irgan_conv_fwd", ctypes.byref(d), dy.ptr, P(buf), P(pc.bias if bias else None), dx.ptr,
+                  mask.ptr if mask else None, stream())
+
+
+def conv_wgrad(spec: ConvSpec, x: Feat, dy: Feat, dw: torch.Tensor, dtype: int, splitk=0):
+    """dw (fp32 KRSC view, accumulated) += weight gradient of conv(x) given dy."""
+    Ho, Wo = spec.out_hw(x.H, x.W)
+    assert (dy.H, dy.W, dy.C) == (Ho, Wo, spec.cout) and x.C == spec.cin
+    assert x.dt == dtype and dy.dt == dtype and dw.dtype == torch.float32
+    d = _desc(N=x.N, H=x.H, W=x.W, Cin=spec.cin, ldx=x.ld, xoff=x.off, Ho=Ho, Wo=Wo, Cout=spec.cout, ldy=dy.ld,
+              yoff=dy.off, OH=Ho, OW=Wo, omy=1, ooy=0, omx=1, oox=0, KH=spec.k, KW=spec.k, sy=spec.stride,
+              sx=spec.stride, c0y=-spec.pad, c0x=-spec.pad, pad_mode=spec.mode, act=0, accumulate=1, dtype=dtype,
+              out_dtype=F32, mask_act=0, ldm=0, moff=0)
+    _lib.call("irgan_conv_wgrad", ctypes.byref(d), x.ptr, dy.ptr, P(dw), splitk, stream())
+
+
+# ----------------------------------------------------------------------------
+# instance norm / reductions
+# ----------------------------------------------------------------------------
+
+def in_stats(x: Feat, work: torch.Tensor, mr: torch.Tensor):
+    _lib.call("irgan_in_stats", x.ptr, x.dt, x.N, x.H * x.W, x.C, x.ld, x.off, P(work), P(mr), stream())
+
+
+def in_apply(x: Feat, mr, y: Feat, act=ACT_NONE, res: Feat = None, xhat: torch.Tensor = None):
+    assert x.dt == y.dt
+    _lib.call("irgan_in_apply", x.ptr, x.dt, x.N, x.H * x.W, x.C, x.ld, x.off, P(mr), act,
+              res.ptr if res else None, res.ld if res else 0, res.off if res else 0, y.ptr, y.ld, y.off, P(xhat),
+              stream())
+
+
+def in_backward(dy: Feat, x: Feat, act: int, mr, work, red, dx: Feat, db=None, dy2: Feat = None):
+    """dx = backward of act(IN(x)) applied to (dy [+ dy2]); x = PRE-norm input."""
+    N, HW, C = x.N, x.H * x.W, x.C
+    d2 = (dy2.ptr, dy2.dt, dy2.ld, dy2.off) if dy2 is not None else (None, 0, 0, 0)
+    _lib.call("irgan_in_bwd_reduce", dy.ptr, dy.dt, dy.ld, dy.off, *d2, x.ptr, x.dt, x.ld, x.off, act, N, HW, C,
+              P(mr), P(work), P(red), stream())
+    _lib.call("irgan_in_bwd_apply", dy.ptr, dy.dt, dy.ld, dy.off, *d2, x.ptr, x.dt, x.ld, x.off, act, N, HW, C,
+              P(mr), P(red), dx.ptr, dx.dt, dx.ld, dx.off, P(db), stream())
+
+
+def channel_sum(g: Feat, db: torch.Tensor):
+    _lib.call("irgan_channel_sum", g.ptr, g.dt, g.P, g.C, g.ld, g.off, P(db), stream())
+
+
+# ----------------------------------------------------------------------------
+# resampling / elementwise
+# ----------------------------------------------------------------------------
+
+def blur_down(x: Feat, y: Feat):
+    _lib.call("irgan_blur_down_fwd", x.ptr, x.dt, x.N, x.H, x.W, x.C, x.ld, x.off, y.ptr, y.ld, y.off, stream())
+
+
+def blur_down_bwd(dy: Feat, dx: Feat):
+    _lib.call("irgan_blur_down_bwd", dy.ptr, dy.dt, dx.N, dx.H, dx.W, dx.C, dy.ld, dy.off, dx.ptr, dx.dt, dx.ld,
+              dx.off, stream())
+
+
+def upsample(x: Feat, y: Feat):
+    _lib.call("irgan_upsample_fwd", x.ptr, x.dt, x.N, x.H, x.W, x.C, x.ld, x.off, y.ptr, y.ld, y.off, stream())
+
+
+def upsample_bwd(dy: Feat, dx: Feat, work: torch.Tensor, accumulate=False):
+    _lib.call("irgan_upsample_bwd", dy.ptr, dy.dt, dx.N, dx.H, dx.W, dx.C, dy.ld, dy.off, P(work), dx.ptr, dx.dt,
+              dx.ld, dx.off, int(accumulate), stream())
+
+
+def maxpool(x: Feat, y: Feat):
+    assert x.off == 0 and x.C == x.ld and y.off == 0
+    _lib.call("irgan_maxpool_fwd", x.ptr, x.dt, x.N, x.H, x.W, x.C, y.ptr, stream())
+
+
+def maxpool_bwd(x: Feat, dy: Feat, dx: Feat, relu_mask=True):
+    _lib.call("irgan_maxpool_bwd", x.ptr, dy.ptr, x.dt, x.N, x.H, x.W, x.C, dx.ptr, int(relu_mask), stream())
+
+
+def nchw_to_nhwc(x: torch.Tensor, y: Feat, scale=None, shift=None):
+    N, C, H, W = x.shape
+    _lib.call("irgan_nchw_to_nhwc", P(x), N, C, H, W, y.ptr, y.dt, y.ld, y.off, P(scale), P(shift), stream())
+
+
+def nhwc_to_nchw(x: Feat, y: torch.Tensor, scale=1.0, accumulate=False):
+    _lib.call("irgan_nhwc_to_nchw", x.ptr, x.dt, x.ld, x.off, x.N, x.C, x.H, x.W, P(y), ctypes.c_float(scale),
+              int(accumulate), stream())
+
+
+def axpby(x: Feat, a: float, y: Feat, b: float = 0.0):
+    _lib.call("irgan_axpby", x.ptr, x.dt, x.ld, x.off, ctypes.c_float(a), y.ptr, y.dt, y.ld, y.off,
+              ctypes.c_float(b), x.P, x.C, stream())
+
+
+def affine(x: Feat, scale, shift, y: Feat, accumulate=False):
+    _lib.call("irgan_affine", x.ptr, x.dt, x.ld, x.off, P(scale), P(shift), y.ptr, y.dt, y.ld, y.off,
+              int(accumulate), x.P, x.C, stream())
+
+
+def act_bwd(dy: Feat, a: Feat, act: int, dx: Feat):
+    _lib.call("irgan_act_bwd", dy.ptr, dy.dt, dy.ld, dy.off, a.ptr, a.dt, a.ld, a.off, act, dx.ptr, dx.dt, dx.ld,
+              dx.off, dy.P, dy.C, stream())
+
+
+# ----------------------------------------------------------------------------
+# losses / optimizer
+# ----------------------------------------------------------------------------
+
+def hinge(pred: torch.Tensor, n_half: int, mode: int, scale: float, grad: torch.Tensor, loss: torch.Tensor):
+    _lib.call("irgan_hinge", P(pred), n_half, mode, ctypes.c_float(scale), P(grad), P(loss), stream())
+
+
+def l1(a: torch.Tensor, b: torch.Tensor, w: float, ga: torch.Tensor, loss: torch.Tensor, accumulate=False):
+    _lib.call("irgan_l1", P(a), P(b), dt_code(a), a.numel(), ctypes.c_float(w), P(ga),
+              dt_code(ga) if ga is not None else 0, int(accumulate), P(loss), stream())
+
+
+def tv(x: Feat, w: float, g: torch.Tensor, loss: torch.Tensor):
+    _lib.call("irgan_tv", x.ptr, x.N, x.H, x.W, x.C, ctypes.c_float(w), P(g), P(loss), stream())
+
+
+def ssim(a: Feat, b: Feat, w: float, g: torch.Tensor, loss: torch.Tensor, work: torch.Tensor):
+    _lib.call("irgan_ssim", a.ptr, b.ptr, a.N, a.H, a.W, a.C, ctypes.c_float(w), P(g), P(loss), P(work), stream())
+
+
+def adam(p, g, m, v, step: int, lr: float, b1: float, b2: float, eps: float):
+    bc1 = 1 - b1 ** step
+    bc2 = 1 - b2 ** step
+    _lib.call("irgan_adam", P(p), P(g), P(m), P(v), p.numel(), ctypes.c_float(lr / bc1), ctypes.c_float(b1),
+              ctypes.c_float(b2), ctypes.c_float(math.sqrt(bc2)), ctypes.c_float(eps), stream())

@@ -1,0 +1,231 @@
+"""Per-kernel numerics on the MI355X: every HIP kernel vs a plain PyTorch fp32
+CPU reference of the same op (fp32 mode: ~1e-5 rel; bf16 mode: bf16-level
+tolerance stated per test).  Calls go through the C ABI (libirgan.so)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import pkg
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def ops():
+    m = pkg()
+    return m.ops
+
+
+def nhwc(x):  # NCHW cpu -> NHWC device
+    return x.permute(0, 2, 3, 1).contiguous().to(DEV)
+
+
+def nchw(x):
+    return x.float().cpu().permute(0, 3, 1, 2).contiguous()
+
+
+def relerr(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-12))
+
+
+def ref_conv(x, w, b, k, s, p, mode):
+    if mode == 1:
+        x = F.pad(x, (p, p, p, p), mode="reflect")
+        p = 0
+    return F.conv2d(x, w, b, stride=s, padding=p)
+
+
+CONV_CASES = [
+    # cin, cout, k, s, p, mode, H
+    (64, 128, 3, 1, 1, 0, 16),
+    (256, 256, 3, 1, 1, 1, 8),
+    (1, 64, 7, 1, 3, 1, 16),
+    (64, 3, 7, 1, 3, 1, 16),
+    (4, 64, 4, 2, 1, 0, 32),
+    (64, 128, 4, 2, 1, 0, 16),
+    (256, 512, 4, 1, 1, 0, 6),
+    (512, 1, 4, 1, 1, 0, 5),
+    (3, 64, 3, 1, 1, 0, 16),
+    (64, 128, 3, 2, 1, 0, 16),
+    (192, 64, 3, 1, 1, 0, 8),
+]
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_dgrad_wgrad(ops, case, dtype):
+    cin, cout, k, s, p, mode, H = case
+    torch.manual_seed(0)
+    N = 2
+    x = torch.randn(N, cin, H, H)
+    w = torch.randn(cout, cin, k, k) * (1.0 / (cin * k * k) ** 0.5)
+    b = torch.randn(cout) * 0.1
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    y_ref = ref_conv(xr, wr, b, k, s, p, mode)
+    gy = torch.randn_like(y_ref)
+    y_ref.backward(gy)
+
+    code = ops.F32 if dtype == "f32" else ops.BF16
+    tdt = torch.float32 if dtype == "f32" else torch.bfloat16
+    tol = 2e-5 if dtype == "f32" else 3e-2
+    spec = ops.ConvSpec(cin, cout, k, s, p, mode)
+    master = w.permute(0, 2, 3, 1).contiguous().reshape(-1).to(DEV)
+    pc = ops.PackedConv(spec, master, b.to(DEV), code)
+    pc.pack()
+    # forward into a channel slice of a wider tensor (exercises ld/off)
+    xd = nhwc(x).to(tdt)
+    Ho, Wo = y_ref.shape[2:]
+    ybuf = torch.zeros(N, Ho, Wo, cout + 8, device=DEV, dtype=torch.float32)
+    ops.conv_fwd(pc, ops.Feat(xd), ops.Feat(ybuf, 8, cout))
+    assert relerr(nchw(ybuf[..., 8:]), y_ref.detach()) < tol
+    # backward-data
+    gyd = nhwc(gy).to(tdt)
+    dx = torch.zeros(N, H, H, cin, device=DEV, dtype=torch.float32)
+    pad = torch.empty(N * (H + 2 * p) ** 2 * cin, device=DEV) if mode == 1 else None
+    ops.conv_dgrad(pc, ops.Feat(gyd), ops.Feat(dx), pad_buf=pad)
+    assert relerr(nchw(dx), xr.grad) < tol
+    # backward-weight
+    dw = torch.zeros(cout * k * k * cin, device=DEV)
+    ops.conv_wgrad(spec, ops.Feat(xd), ops.Feat(gyd), dw, code)
+    dw = dw.view(cout, k, k, cin).permute(0, 3, 1, 2).cpu()
+    assert relerr(dw, wr.grad) < (2e-5 if dtype == "f32" else 3e-2)
+
+
+def test_conv_act_and_mask(ops):
+    torch.manual_seed(1)
+    x = torch.randn(2, 64, 8, 8)
+    w = torch.randn(64, 64, 3, 3) * 0.05
+    b = torch.randn(64) * 0.1
+    m = torch.randn(2, 64, 8, 8)
+    spec = ops.ConvSpec(64, 64, 3, 1, 1, 0)
+    pc = ops.PackedConv(spec, w.permute(0, 2, 3, 1).contiguous().reshape(-1).to(DEV), b.to(DEV), ops.F32)
+    pc.pack()
+    for act, fn in ((ops.ACT_RELU, F.relu), (ops.ACT_LRELU, lambda t: F.leaky_relu(t, 0.2)), (ops.ACT_TANH, torch.tanh)):
+        y = torch.empty(2, 8, 8, 64, device=DEV)
+        ops.conv_fwd(pc, ops.Feat(nhwc(x)), ops.Feat(y), act=act)
+        assert relerr(nchw(y), fn(F.conv2d(x, w, b, padding=1))) < 2e-5
+    y = torch.empty(2, 8, 8, 64, device=DEV)
+    ops.conv_fwd(pc, ops.Feat(nhwc(x)), ops.Feat(y), mask=ops.Feat(nhwc(m)), mask_act=2)
+    ref = F.conv2d(x, w, b, padding=1) * torch.where(m > 0, 1.0, 0.2)
+    assert relerr(nchw(y), ref) < 2e-5
+
+
+@pytest.mark.parametrize("act", [0, 1, 2])
+def test_instance_norm_fwd_bwd(ops, act):
+    torch.manual_seed(2)
+    N, C, H = 2, 96, 12
+    x = (torch.randn(N, C, H, H) * 3 + 1).requires_grad_(True)
+    res = torch.randn(N, C, H, H)
+    xh = F.instance_norm(x, eps=1e-5)
+    y = {0: xh, 1: F.relu(xh), 2: F.leaky_relu(xh, 0.2)}[act]
+    if act == 0:
+        y = y + res
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    xd = nhwc(x.detach())
+    work = torch.empty(2 * N * C, dtype=torch.float64, device=DEV)
+    mr = torch.empty(2 * N * C, device=DEV)
+    red = torch.empty(2 * N * C, device=DEV)
+    ops.in_stats(ops.Feat(xd), work, mr)
+    yd = torch.empty_like(xd)
+    xhat = torch.empty_like(xd) if act == 0 else None
+    ops.in_apply(ops.Feat(xd), mr, ops.Feat(yd), act=act, res=ops.Feat(nhwc(res)) if act == 0 else None, xhat=xhat)
+    assert relerr(nchw(yd), y.detach()) < 1e-5
+    dx = torch.empty_like(xd)
+    db = torch.zeros(C, device=DEV)
+    ops.in_backward(ops.Feat(nhwc(gy)), ops.Feat(xd), act, mr, work, red, ops.Feat(dx), db=db)
+    assert relerr(nchw(dx), x.grad) < 1e-4
+    assert float(db.abs().max()) < 1e-3  # sum of an IN input-grad is ~0
+
+
+def test_blur_down_upsample_fold_pool(ops):
+    torch.manual_seed(3)
+    from oracle import step as O
+    C = 16
+    filt = O.binomial_filter(3)[None, None].repeat(C, 1, 1, 1)
+    for H in (8, 9, 16):
+        x = torch.randn(2, C, H, H, requires_grad=True)
+        y = O.blur_down(x, filt)
+        g = torch.randn_like(y)
+        y.backward(g)
+        yd = torch.empty(2, y.shape[2], y.shape[3], C, device=DEV)
+        ops.blur_down(ops.Feat(nhwc(x.detach())), ops.Feat(yd))
+        assert relerr(nchw(yd), y.detach()) < 1e-5
+        dx = torch.empty(2, H, H, C, device=DEV)
+        ops.blur_down_bwd(ops.Feat(nhwc(g)), ops.Feat(dx))
+        assert relerr(nchw(dx), x.grad) < 1e-5
+    for H in (4, 8, 7):
+        x = torch.randn(2, C, H, H, requires_grad=True)
+        y = O.up_aa(x, filt)
+        g = torch.randn_like(y)
+        y.backward(g)
+        yd = torch.empty(2, 2 * H, 2 * H, C, device=DEV)
+        ops.upsample(ops.Feat(nhwc(x.detach())), ops.Feat(yd))
+        assert relerr(nchw(yd), y.detach()) < 1e-5
+        dx = torch.zeros(2, H, H, C, device=DEV)
+        work = torch.empty(2 * 4 * H * H * C, device=DEV)
+        ops.upsample_bwd(ops.Feat(nhwc(g)), ops.Feat(dx), work)
+        assert relerr(nchw(dx), x.grad) < 1e-5
+    x = torch.randn(2, C, 8, 8, requires_grad=True)
+    y = F.max_pool2d(F.relu(x), 2)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xr = nhwc(F.relu(x.detach()))
+    yd = torch.empty(2, 4, 4, C, device=DEV)
+    ops.maxpool(ops.Feat(xr), ops.Feat(yd))
+    assert relerr(nchw(yd), y.detach()) < 1e-6
+    dx = torch.empty_like(xr)
+    ops.maxpool_bwd(ops.Feat(xr), ops.Feat(nhwc(g)), ops.Feat(dx))
+    assert relerr(nchw(dx), x.grad) < 1e-6
+
+
+def test_losses(ops):
+    torch.manual_seed(4)
+    from oracle import step as O
+    N, H = 2, 24
+    a = (torch.rand(N, 3, H, H) * 2 - 1).requires_grad_(True)
+    b = torch.rand(N, 3, H, H) * 2 - 1
+    ad, bd = nhwc(a.detach()), nhwc(b)
+    loss = torch.zeros(8, dtype=torch.float64, device=DEV)
+    g = torch.zeros_like(ad)
+    ops.l1(ad, bd, 30.0, g, loss[0:1], accumulate=True)
+    ops.tv(ops.Feat(ad), 1e-4, g, loss[1:2])
+    work = torch.empty(10 * ad.numel(), device=DEV)
+    ops.ssim(ops.Feat(ad), ops.Feat(bd), 2.0, g, loss[2:3], work)
+    l_l1 = (a - b).abs().mean() * 30
+    l_tv = O.tv_loss(a) * 1e-4
+    l_ss = O.ssim_loss((a + 1) / 2, (b + 1) / 2) * 2.0
+    (l_l1 + l_tv + l_ss).backward()
+    lc = loss.cpu()
+    assert abs(lc[0] - l_l1.item()) < 1e-5 * l_l1.item()
+    assert abs(lc[1] - l_tv.item()) < 1e-5 * l_tv.item()
+    assert abs(lc[2] - l_ss.item()) < 1e-5 * max(l_ss.item(), 1e-3)
+    assert relerr(nchw(g), a.grad) < 1e-4
+    # hinge
+    p = torch.randn(2 * 50)
+    pd = p.to(DEV)
+    gp = torch.empty_like(pd)
+    ops.hinge(pd, 50, 0, 1.0, gp, loss[3:4])
+    pr = p.clone().requires_grad_(True)
+    ld = 0.5 * (F.relu(1 - pr[:50]).mean() + F.relu(1 + pr[50:]).mean())
+    ld.backward()
+    assert abs(loss[3].item() - ld.item()) < 1e-6
+    assert relerr(gp.cpu(), pr.grad) < 1e-6
+
+
+def test_adam_matches_torch(ops):
+    torch.manual_seed(5)
+    p = torch.randn(1000)
+    grads = [torch.randn(1000) for _ in range(3)]
+    pt = p.clone().requires_grad_(True)
+    opt = torch.optim.Adam([pt], lr=2e-4, betas=(0.5, 0.999))
+    pd, m, v = p.to(DEV), torch.zeros(1000, device=DEV), torch.zeros(1000, device=DEV)
+    for i, gr in enumerate(grads):
+        pt.grad = gr.clone()
+        opt.step()
+        ops.adam(pd, gr.to(DEV), m, v, i + 1, 2e-4, 0.5, 0.999, 1e-8)
+    assert float((pd.cpu() - pt.detach()).abs().max()) < 5e-7  # a few fp32 ulps of |p|~2

@@ -1,0 +1,177 @@
+"""Step-level parity on the MI355X: the fused HIP train step vs the reference's
+golden vectors (tests/golden, produced by executing the reference) and vs the
+CPU oracle on the same seeded inputs.
+
+Tolerances (north star: 1e-3 rel fp32):
+  fp32 mode  - outputs / losses <= 1e-4 rel; D weight grads <= 1e-3 rel;
+               post-step params within 2*lr abs (Adam's first step is ~lr*sign(g);
+               pre-IN biases excluded, their exact gradient is 0 -- SURVEY.md s.4).
+               G weight grads are measured against the reference run in fp64
+               (the exact answer): the perceptual L1 (sign of VGG feature
+               differences) and ReLU masks make them discontinuous, and the
+               reference's OWN fp32 run is off by up to ~2e-2 max-rel on some
+               tensors (recorded per tensor as err32 in the fixtures).  On the
+               smooth objective (s32_smooth: GAN + SSIM only) the HIP path must
+               be within max(1e-3, 3*err32) max-rel of fp64 per tensor; with the
+               full objective within max(5e-3, 3*err32) sampled max-rel and
+               max(2e-3, 3*err32l2) relative L2 of fp64.
+  bf16 mode  - losses <= 3e-2 rel, G output <= 5e-2 abs (bf16 operands, fp32 acc).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden, pkg
+from oracle import step as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+LOSS_KEYS = ("loss_D", "loss_G", "loss_G_GAN", "loss_G_L1", "loss_G_perc", "loss_G_TV", "loss_G_ssim")
+
+
+LAMBDA_ORDER = ("lambda_L1", "lambda_perc", "lambda_tv", "lambda_ssim", "lambda_gan")
+
+
+def make_trainer(fx, dtype):
+    irc = pkg()
+    H, W, B, noaa, noaaup = [int(v) for v in fx["meta"][:5]]
+    cfg = irc.Config()
+    cfg.device = DEV
+    cfg.compute_dtype = dtype
+    for k, v in zip(LAMBDA_ORDER, fx["lambdas"]):
+        setattr(cfg, k, float(v))
+    cfg.no_antialias, cfg.no_antialias_up = bool(noaa), bool(noaaup)
+    tr = irc.GANTrainer(cfg)
+    tr.netG.store.load(O.seeded_params(O.g_param_shapes(no_antialias=bool(noaa), no_antialias_up=bool(noaaup)),
+                                       1, bias_std=0.02), strict=True)
+    tr.netD.store.load(O.seeded_params(O.d_param_shapes(), 2, bias_std=0.02), strict=True)
+    tr.vgg.store.load(O.seeded_params(O.vgg_param_shapes(), 3, kaiming=True), strict=True)
+    for m in (tr.netG, tr.netD, tr.vgg):
+        m.repack()
+    return tr, cfg
+
+
+def digest_check(store, fx, tag, pre_in, tol):
+    """Sampled grads vs the fp64 reference, within max(tol, 3*err32[k])."""
+    for k in store.shapes:
+        g = store.oihw(k, store.grad).reshape(-1).double().cpu().numpy()
+        idx = fx[f"{tag}|{k}|idx"]
+        post = store.oihw(k).reshape(-1).cpu().numpy()[idx]
+        assert np.max(np.abs(post - fx[f"{tag}|{k}|post"])) <= 2 * 2e-4 + 1e-6, f"post-step {k}"
+        if k in pre_in:
+            continue
+        scale = max(np.max(np.abs(g)), 1e-12)
+        err = np.max(np.abs(g[idx] - fx[f"{tag}|{k}|val64"])) / scale
+        lim = max(tol, 3 * float(fx[f"{tag}|{k}|err32"]))
+        assert err <= lim, f"grad {k}: {err} > {lim}"
+
+
+@pytest.mark.parametrize("variant", ["s32", "s64", "s32_noaa", "s32_noaaup", "s32_smooth"])
+def test_step_fp32_matches_reference_golden(variant):
+    fx = load_golden(variant)
+    tr, cfg = make_trainer(fx, "fp32")
+    ir, rgb = torch.from_numpy(fx["ir"]).to(DEV), torch.from_numpy(fx["rgb"]).to(DEV)
+    L = tr.step(ir, rgb)
+    d = tr.losses(L)
+    for k in LOSS_KEYS:
+        ref = fx["step1_" + k]
+        assert abs(d[k] - ref) <= 1e-4 * max(1.0, abs(ref)), (k, d[k], ref)
+    fake = tr.netG.engine.bufs.d["fake"].permute(0, 3, 1, 2).cpu().numpy()
+    assert np.max(np.abs(fake - fx["fake"])) <= 1e-4
+    pred = tr.netD.engine.bufs.d["de4"].permute(0, 3, 1, 2).cpu().numpy()
+    B = fx["ir"].shape[0]
+    scale = max(np.max(np.abs(fx["pred_real"])), 1e-6)
+    assert np.max(np.abs(pred[:B] - fx["pred_real"])) <= 1e-4 * max(1, scale)
+    assert np.max(np.abs(pred[B:] - fx["pred_fake"])) <= 1e-4 * max(1, scale)
+    pre_in = set(O.pre_in_bias_keys(list(tr.netG.store.shapes) + list(tr.netD.store.shapes)))
+    digest_check(tr.netD.store, fx, "gD", pre_in, 1e-3)
+    digest_check(tr.netG.store, fx, "gG", pre_in, 1e-3 if variant.endswith("smooth") else 5e-3)
+    L2 = tr.step(ir, rgb)
+    d2 = tr.losses(L2)
+    for k in ("loss_D", "loss_G"):
+        ref = fx["step2_" + k]
+        assert abs(d2[k] - ref) <= 1e-3 * max(1.0, abs(ref)), (k, d2[k], ref)
+
+
+def test_step_bf16_close_to_reference():
+    fx = load_golden("s64")
+    tr, cfg = make_trainer(fx, "bf16")
+    ir, rgb = torch.from_numpy(fx["ir"]).to(DEV), torch.from_numpy(fx["rgb"]).to(DEV)
+    d = tr.losses(tr.step(ir, rgb))
+    for k in ("loss_D", "loss_G", "loss_G_L1", "loss_G_perc", "loss_G_ssim"):
+        ref = fx["step1_" + k]
+        assert abs(d[k] - ref) <= 3e-2 * max(1.0, abs(ref)), (k, d[k], ref)
+    fake = tr.netG.engine.bufs.d["fake"].permute(0, 3, 1, 2).cpu().numpy()
+    err = np.abs(fake - fx["fake"])
+    assert err.mean() <= 1e-2 and err.max() <= 0.15, (err.mean(), err.max())
+
+
+def _oracle(dtype, ir, rgb, lam):
+    G = {k: v.to(dtype).clone() for k, v in O.seeded_params(O.g_param_shapes(), 1, bias_std=0.02).items()}
+    D = {k: v.to(dtype).clone() for k, v in O.seeded_params(O.d_param_shapes(), 2, bias_std=0.02).items()}
+    V = {k: v.to(dtype).clone() for k, v in O.seeded_params(O.vgg_param_shapes(), 3, kaiming=True).items()}
+    return O.train_step(G, D, V, ir.to(dtype), rgb.to(dtype), O.AdamState(G), O.AdamState(D), lam=lam)
+
+
+@pytest.mark.parametrize("seed,smooth", [(11, True), (12, True), (11, False), (12, False)])
+def test_step_fp32_vs_oracle_full_tensors(seed, smooth):
+    """Full-tensor comparison against the CPU oracle (fp32 and fp64) on fresh seeded batches."""
+    fx = load_golden("s32_smooth" if smooth else "s32")
+    lam = dict(zip(LAMBDA_ORDER, (float(v) for v in fx["lambdas"])))
+    tr, cfg = make_trainer(fx, "fp32")
+    g = torch.Generator().manual_seed(seed)
+    ir = torch.rand(2, 1, 32, 32, generator=g) * 2 - 1
+    rgb = torch.rand(2, 3, 32, 32, generator=g) * 2 - 1
+    o32, o64 = _oracle(torch.float32, ir, rgb, lam), _oracle(torch.float64, ir, rgb, lam)
+    d = tr.losses(tr.step(ir.to(DEV), rgb.to(DEV)))
+    for k in LOSS_KEYS:
+        assert abs(d[k] - float(o64[k])) <= 1e-4 * max(1.0, abs(float(o64[k]))), k
+    pre_in = set(O.pre_in_bias_keys(list(o64["gradG"]) + list(o64["gradD"])))
+    for store, tag in ((tr.netG.store, "gradG"), (tr.netD.store, "gradD")):
+        for k, g64 in o64[tag].items():
+            if k in pre_in:
+                continue
+            got = store.oihw(k, store.grad).cpu().double()
+            if smooth or tag == "gradD":
+                den = g64.abs().max().clamp_min(1e-30)
+                err32 = float((o32[tag][k].double() - g64).abs().max() / den)
+                err = float((got - g64).abs().max() / den)
+                assert err <= max(1e-3, 3 * err32), (k, err, err32)
+            else:
+                den = g64.norm().clamp_min(1e-30)
+                err32 = float((o32[tag][k].double() - g64).norm() / den)
+                err = float((got - g64).norm() / den)
+                assert err <= max(2e-3, 3 * err32), (k, err, err32)
+
+
+def test_generator_module_api_and_checkpoint_layout(tmp_path):
+    """nn.Module API: state_dict keys/shapes as the reference, load/save round trip,
+    forward on the HIP kernels with autograd."""
+    irc = pkg()
+    cfg = irc.Config()
+    cfg.device = DEV
+    cfg.compute_dtype = "fp32"
+    model = irc.IRColorizationModel(cfg)
+    sd = model.netG.state_dict()
+    shapes = O.g_param_shapes()
+    assert list(sd.keys()) == list(shapes.keys())
+    assert all(tuple(sd[k].shape) == tuple(v) for k, v in shapes.items())
+    G = O.seeded_params(shapes, 1, bias_std=0.02)
+    path = tmp_path / "netG.pth"
+    torch.save(G, path)
+    model.load_weights(str(path))
+    x = torch.from_numpy(load_golden("s32")["ir"]).to(DEV)
+    y = model(x)
+    ref = O.g_forward(G, x.cpu())
+    assert float((y.cpu() - ref).abs().max()) < 1e-4
+    # autograd through the HIP backward
+    xg = x.clone().requires_grad_(False)
+    out, _ = model.netG(xg)
+    out.square().mean().backward()
+    Gr = {k: v.clone().requires_grad_(not k.endswith(".filt")) for k, v in G.items()}
+    O.g_forward(Gr, x.cpu()).square().mean().backward()
+    for k, p in model.netG.named_parameters():
+        if k in O.PRE_IN_BIAS_G:
+            continue
+        err = float((p.grad.cpu() - Gr[k].grad).abs().max() / Gr[k].grad.abs().max().clamp_min(1e-12))
+        assert err < 1e-3, (k, err)

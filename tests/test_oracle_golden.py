@@ -30,14 +30,22 @@ def rel(a, b):
     return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-12))
 
 
-@pytest.mark.parametrize("variant", ["s32", "s64", "s32_noaa", "s32_noaaup"])
+LAMBDA_ORDER = ("lambda_L1", "lambda_perc", "lambda_tv", "lambda_ssim", "lambda_gan")
+
+
+def lambdas(fx):
+    return dict(zip(LAMBDA_ORDER, (float(v) for v in fx["lambdas"])))
+
+
+@pytest.mark.parametrize("variant", ["s32", "s64", "s32_noaa", "s32_noaaup", "s32_smooth"])
 def test_oracle_step_matches_reference(variant):
     torch.set_num_threads(4)
     fx = load_golden(variant)
     G, D, V, noaa, noaaup = build(fx)
     ir, rgb = torch.from_numpy(fx["ir"]), torch.from_numpy(fx["rgb"])
     optG, optD = O.AdamState(G), O.AdamState(D)
-    out = O.train_step(G, D, V, ir, rgb, optG, optD, no_antialias=noaa, no_antialias_up=noaaup)
+    lam = lambdas(fx)
+    out = O.train_step(G, D, V, ir, rgb, optG, optD, lam=lam, no_antialias=noaa, no_antialias_up=noaaup)
 
     assert rel(out["fake"], fx["fake"]) < 1e-5
     assert rel(out["pred_real"], fx["pred_real"]) < 1e-5
@@ -60,7 +68,7 @@ def test_oracle_step_matches_reference(variant):
             assert abs(flat.sum() - fx[f"{tag}|{k}|sum"]) <= 1e-4 * fx[f"{tag}|{k}|abs"] + 1e-7, k
 
     # second step on the same batch exercises Adam's running moments
-    out2 = O.train_step(G, D, V, ir, rgb, optG, optD, no_antialias=noaa, no_antialias_up=noaaup)
+    out2 = O.train_step(G, D, V, ir, rgb, optG, optD, lam=lam, no_antialias=noaa, no_antialias_up=noaaup)
     for k in ("loss_D", "loss_G"):
         assert abs(float(out2[k]) - fx["step2_" + k]) <= 2e-4 * max(1.0, abs(fx["step2_" + k])), k
 
