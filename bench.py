@@ -1,0 +1,172 @@
+"""GAN train-step throughput on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--size 256] [--batch 16]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
+
+A step = the fused HIP train step (G forward, D fwd/bwd on [real; fake], D
+Adam, D fwd/bwd on fake, VGG/L1/TV/SSIM losses, G backward, G Adam) on one
+synthetic 256x256 batch of 16 IR/RGB pairs per GPU, bf16 operands with fp32
+accumulation, random-init weights of the reference architecture.  Weak scaling:
+every rank trains on its own 16-pair shard and all-reduces grads (RCCL).
+
+Prints ONE JSON line (rank 0) with the metric, a live roofline for the dominant
+conv kernel (HIP events around its launches) and the CPU-oracle baseline.
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+PKG = "infrared-colorization-with-resnet-generator-and-patchgan_amd"
+
+METRIC = "GAN train-step img/s (G+D fwd/bwd) at 256×256, 1/2/4/8 MI355X"
+MIN_GFLOP_PER_IMG_256 = 534.85   # minimal-step algorithmic FLOPs per image at 256^2
+BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+FP32_MFMA_PEAK_TFLOPS = 157.3
+
+
+def min_gflop_per_img(H, W):
+    # conv FLOPs scale with pixel count (the architecture is fully convolutional)
+    return MIN_GFLOP_PER_IMG_256 * (H * W) / (256 * 256)
+
+
+def cpu_baseline(H, W, batch=1, budget_s=20.0):
+    """The CPU oracle (fp32 PyTorch-CPU restatement of ir:1636-1681) on host cores."""
+    import torch
+    from oracle import step as O
+    threads = min(os.cpu_count() or 1, 16)
+    torch.set_num_threads(threads)
+    G = O.seeded_params(O.g_param_shapes(), 0)
+    D = O.seeded_params(O.d_param_shapes(), 1)
+    V = O.seeded_params(O.vgg_param_shapes(), 3, kaiming=True)
+    g = torch.Generator().manual_seed(7)
+    ir = torch.rand(batch, 1, H, W, generator=g) * 2 - 1
+    rgb = torch.rand(batch, 3, H, W, generator=g) * 2 - 1
+    oG, oD = O.AdamState(G), O.AdamState(D)
+    O.train_step(G, D, V, ir, rgb, oG, oD)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        O.train_step(G, D, V, ir, rgb, oG, oD)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or n >= 20:
+            break
+    return {"value": round(n * batch / el, 4), "unit": "img/s", "cores": threads, "kind": "port",
+            "sample": f"{n} oracle steps of batch {batch} at {H}x{W} fp32 after 1 warm-up ({el:.1f}s, "
+                      f"torch CPU threads={threads}, {os.cpu_count()} host CPUs)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--batch", type=int, default=16, help="per-GPU batch")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    irc = importlib.import_module(PKG)
+    ops = irc.ops
+
+    H = W = args.size
+    B = args.batch
+    cfg = irc.Config()
+    cfg.device = f"cuda:{local}"
+    cfg.compute_dtype = args.dtype
+    cfg.batch_size = B
+    cfg.img_size = H
+    tr = irc.GANTrainer(cfg)
+    # random-init weights of the reference architecture (seeded; identical on every rank)
+    tr.netG.store.load(irc.seeded_state(irc.g_param_shapes(), 0), strict=True)
+    tr.netD.store.load(irc.seeded_state(irc.d_param_shapes(), 1), strict=True)
+    for m in (tr.netG, tr.netD, tr.vgg):
+        m.repack()
+    g = torch.Generator().manual_seed(7 + rank)
+    ir = (torch.rand(B, 1, H, W, generator=g) * 2 - 1).cuda()
+    rgb = (torch.rand(B, 3, H, W, generator=g) * 2 - 1).cuda()
+
+    # dominant kernel for the live roofline: the resblock 3x3 conv (256->256 @ H/4)
+    res_tags = [ops.conv_tag(k, ops.ConvSpec(256, 256, 3, 1, 1, 1), (H // 4, W // 4))
+                for k in ("fwd", "dgrad", "wgrad")]
+    for _ in range(args.warmup):
+        tr.step(ir, rgb)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ops.TIMER.tags = set(res_tags)
+    ops.TIMER.enabled = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        L = tr.step(ir, rgb)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    ops.TIMER.enabled = False
+    if world > 1:
+        t = torch.tensor([el], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t)
+    timing = ops.TIMER.summary()
+    losses = tr.losses(L)
+
+    if rank == 0:
+        imgs = B * world * args.steps
+        value = imgs / el
+        ms = el / args.steps * 1e3
+        # roofline of the dominant kernel family: algorithmic FLOPs per launch / mean launch time
+        res_flop = 2.0 * B * (H // 4) * (W // 4) * 256 * 256 * 9
+        peak = BF16_DENSE_PEAK_TFLOPS if args.dtype == "bf16" else FP32_MFMA_PEAK_TFLOPS
+        kern = {}
+        for tg in res_tags:
+            if tg in timing:
+                n, mean_ms = timing[tg]
+                kern[tg] = {"launches": n, "mean_ms": round(mean_ms, 4),
+                            "tflops": round(res_flop / (mean_ms * 1e-3) / 1e12, 2)}
+        dom = max(kern, key=lambda k: kern[k]["launches"] * kern[k]["mean_ms"]) if kern else None
+        achieved = kern[dom]["tflops"] if dom else None
+        step_tflops = value * min_gflop_per_img(H, W) / 1e3 / world
+        out = {
+            "metric": METRIC, "value": round(value, 3), "unit": "img/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (U(-1,1) IR/RGB pairs, seeded; random-init weights)",
+            "config": {"workload": f"GAN train step {H}x{W}, batch {B}/GPU (BASELINE configs[1]"
+                                   f"{' / [2]' if world > 1 else ''})", "global_batch": B * world,
+                       "img_size": H, "parallelism": f"dp{world}",
+                       "min_gflop_per_img": round(min_gflop_per_img(H, W), 2),
+                       "step_tflops_per_gpu": round(step_tflops, 2),
+                       "step_frac_of_bf16_peak": round(step_tflops / BF16_DENSE_PEAK_TFLOPS, 4)},
+            "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                         "frac": round(achieved / peak, 4) if achieved else None, "traffic": None,
+                         "flop_per_launch": res_flop, "per_kernel": kern},
+            "losses": {k: round(v, 5) for k, v in losses.items()},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(H, W, 1, args.cpu_budget)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -107,24 +107,23 @@ int irgan_in_bwd_apply(const void* dy, int32_t dy_dtype, int32_t lddy, int32_t d
 int irgan_channel_sum(const void* g, int32_t dtype, int32_t P, int32_t C, int32_t ld,
                       int32_t off, float* db, irgan_stream_t s);
 
-/* ---- resampling (ir:269-355, 1637-1640, vgg pooling) ---- */
-/* Downsample (ir:269-310): reflect pad 1 + binomial 3x3, stride 2. */
-int irgan_blur_down_fwd(const void* x, int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t C,
-                        int32_t ldx, int32_t xoff, void* y, int32_t ldy, int32_t yoff, irgan_stream_t s);
-int irgan_blur_down_bwd(const void* dy, int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t C,
-                        int32_t lddy, int32_t dyoff, void* dx, int32_t dx_dtype, int32_t lddx,
-                        int32_t dxoff, irgan_stream_t s);
-/* UpsampleAA (ir:313-355): bilinear x2 align_corners + reflect pad 1 + blur. H,W = input dims. */
-int irgan_upsample_fwd(const void* x, int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t C,
-                       int32_t ldx, int32_t xoff, void* y, int32_t ldy, int32_t yoff, irgan_stream_t s);
-/* work: N*2H*2W*C floats of scratch; accumulate: dx += result. */
-int irgan_upsample_bwd(const void* dy, int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t C,
-                       int32_t lddy, int32_t dyoff, float* work, void* dx, int32_t dx_dtype,
-                       int32_t lddx, int32_t dxoff, int32_t accumulate, irgan_stream_t s);
-/* reflect-pad backward: dx[q] = sum_{u: reflect(u-p)=q} dxpad[u]  (dxpad fp32, (H+2p)x(W+2p)) */
-int irgan_reflect_fold(const float* dxpad, int32_t N, int32_t H, int32_t W, int32_t C, int32_t p,
-                       void* dx, int32_t dx_dtype, int32_t lddx, int32_t dxoff, int32_t accumulate,
-                       irgan_stream_t s);
+/* ---- resampling (ir:269-355 and reflection-pad backward) ---- */
+/* Per-axis tables of a separable resampling map (host only, no GPU work).
+ * kind 0: Downsample = reflect pad 1 + [1,2,1]/4 taps, stride 2 (ir:269-310);
+ * kind 1: UpsampleAA = bilinear x2 (align_corners) + reflect pad 1 + blur (ir:313-355);
+ * kind 2: nn.ReflectionPad2d(p).  transpose=1 gives the adjoint (rows = the
+ * forward map's input coordinates).  Fills idx/w [rows][tmax] and returns rows,
+ * or a negative IRGAN_E* code. */
+int irgan_resample_table(int32_t kind, int32_t n_in, int32_t p, int32_t transpose, int32_t* idx,
+                         float* w, int32_t tmax, int32_t rows_cap);
+/* out = (Wy (x) Wx) in on NHWC slices, tables from irgan_resample_table (device
+ * copies); accumulate: out += result.  Downsample / UpsampleAA forward and
+ * backward, and the reflect-pad fold, are all this one launch. */
+int irgan_sep_resample(const void* in, int32_t in_dtype, int32_t N, int32_t Hin, int32_t Win,
+                       int32_t C, int32_t ldi, int32_t offi, void* out, int32_t out_dtype,
+                       int32_t Hout, int32_t Wout, int32_t ldo, int32_t offo, const int32_t* ty,
+                       const float* wy, const int32_t* tx, const float* wx, int32_t T,
+                       int32_t accumulate, irgan_stream_t s);
 /* 2x2 max pool (VGG features) forward / backward (first max wins, as ATen). */
 int irgan_maxpool_fwd(const void* x, int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t C,
                       void* y, irgan_stream_t s);

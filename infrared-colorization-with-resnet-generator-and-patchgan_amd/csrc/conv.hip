@@ -161,6 +161,14 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const irgan_conv_desc d, 
         if (kt + 1 < nk) load_tile(kt + 1);
         const char* A = smem + cur * (BM + BN) * ROWB;
         const char* B = A + BM * ROWB;
+        // fp32 parity mode: blocked summation (one fresh partial per K-tile) keeps the
+        // fp32 error at O(32 + K/32) ulps instead of a K-long FMA chain
+        f32x4 part[MI][NJ];
+        constexpr bool BLOCKED = sizeof(T) == 4;
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) part[i][j] = BLOCKED ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][j];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             uint4 af[MI], bfr[NJ];
@@ -172,8 +180,12 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const irgan_conv_desc d, 
 #pragma unroll
             for (int i = 0; i < MI; ++i)
 #pragma unroll
-                for (int j = 0; j < NJ; ++j) mma16(acc[i][j], af[i], bfr[j], (const T*)nullptr);
+                for (int j = 0; j < NJ; ++j) mma16(part[i][j], af[i], bfr[j], (const T*)nullptr);
         }
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) acc[i][j] = BLOCKED ? acc[i][j] + part[i][j] : part[i][j];
         if (kt + 1 < nk) store_tile(cur ^ 1);
         __syncthreads();
     }
@@ -380,6 +392,12 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const irgan_conv_desc d
         if (kt + 1 < nk) load_tile(pb + (long)(kt + 1) * BKP);
         const char* A = smem + cur * (BM + BN) * ROWB;
         const char* B = A + BM * ROWB;
+        f32x4 part[MI][NJ];
+        constexpr bool BLOCKED = sizeof(T) == 4;  // see conv_fwd_kernel
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) part[i][j] = BLOCKED ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][j];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             uint4 af[MI], bfr[NJ];
@@ -391,8 +409,12 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const irgan_conv_desc d
 #pragma unroll
             for (int i = 0; i < MI; ++i)
 #pragma unroll
-                for (int j = 0; j < NJ; ++j) mma16(acc[i][j], af[i], bfr[j], (const T*)nullptr);
+                for (int j = 0; j < NJ; ++j) mma16(part[i][j], af[i], bfr[j], (const T*)nullptr);
         }
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) acc[i][j] = BLOCKED ? acc[i][j] + part[i][j] : part[i][j];
         if (kt + 1 < nk) store_tile(cur ^ 1);
         __syncthreads();
     }

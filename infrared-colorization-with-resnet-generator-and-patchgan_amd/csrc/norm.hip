@@ -3,23 +3,55 @@
 // running stats) + the fused ReLU / LeakyReLU(0.2) / residual add of ir:392,
 // 417-418, 601-624 and their autograd backward.
 //
-// Statistics are accumulated per block in fp32 and across blocks in fp64
-// atomics (one add per (n, c) per block), then finalised to fp32 (mean, rstd)
-// or (mean g, mean g*xhat) by a second tiny launch.
+// HBM-bound: every thread owns 8 consecutive channels (one 16-byte bf16 load /
+// two 16-byte fp32 loads per pixel) and walks rows with 4 loads in flight; a
+// block covers a run of rows of one image, reduces its partial sums through
+// LDS and issues one fp64 atomic per (n, c).  A finalize launch turns the fp64
+// sums into fp32 (mean, rstd) or (mean g, mean g*xhat).
 #include "common.h"
 
 namespace {
 
 constexpr int TPB = 256;
+constexpr int V = 8;  // channels per thread
 
-// thread -> (channel, row lane) layout for a C-wide NHWC row block
-struct RowLayout {
-    int cpt, rpar;  // channels covered per pass, rows processed in parallel
-    __device__ RowLayout(int C) {
-        cpt = C < TPB ? C : TPB;
-        rpar = TPB / cpt;
+IRGAN_HD void ld8(const void* p, int dt, long i, float* o) {
+    if (dt == IRGAN_BF16) {
+        const uint4 u = *(const uint4*)((const bf16_t*)p + i);
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            o[2 * k] = __uint_as_float(w[k] << 16);
+            o[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+        }
+    } else {
+        const float4 a = *(const float4*)((const float*)p + i), b = *(const float4*)((const float*)p + i + 4);
+        o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
     }
-};
+}
+IRGAN_HD void st8(void* p, int dt, long i, const float* v) {
+    if (dt == IRGAN_BF16) {
+        uint4 u;
+        u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        u.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+        u.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+        *(uint4*)((bf16_t*)p + i) = u;
+    } else {
+        *(float4*)((float*)p + i) = make_float4(v[0], v[1], v[2], v[3]);
+        *(float4*)((float*)p + i + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    }
+}
+template <int VW>
+IRGAN_HD void ldv_(const void* p, int dt, long i, float* o) {
+    if constexpr (VW == 8) ld8(p, dt, i, o);
+    else o[0] = ldv(p, dt, i);
+}
+template <int VW>
+IRGAN_HD void stv_(void* p, int dt, long i, const float* v) {
+    if constexpr (VW == 8) st8(p, dt, i, v);
+    else stv(p, dt, i, v[0]);
+}
 
 // derivative of the activation that followed the norm, at xhat
 IRGAN_HD float act_grad(float xh, int act) {
@@ -28,60 +60,112 @@ IRGAN_HD float act_grad(float xh, int act) {
     return 1.f;
 }
 
-// generic per-(n,c) two-moment reduction; MODE 0: (x, x^2); MODE 1: (g, g*xhat)
-template <int MODE>
-__global__ __launch_bounds__(TPB) void reduce2_kernel(const void* __restrict__ x, int xdt, int ldx, int xoff,
-                                                      const void* __restrict__ dy2, int d2dt, int ld2, int off2,
-                                                      const void* __restrict__ a, int adt, int lda, int aoff,
-                                                      int act, const float* __restrict__ mr, int HW, int C,
-                                                      int rows_per_block, double* __restrict__ work) {
-    __shared__ float s0[TPB], s1[TPB];
+struct Slice {
+    const void* p;
+    int dt, ld, off;
+};
+
+// block layout: CL lanes per row (VW channels each), RP rows in parallel
+struct Lay {
+    int CL, RP, cl, rl;
+    __device__ Lay(int C, int VW) {
+        CL = (C + VW - 1) / VW;
+        if (CL > TPB) CL = TPB;
+        RP = TPB / CL;
+        cl = threadIdx.x % CL;
+        rl = threadIdx.x / CL;
+    }
+};
+
+// MODE 0: (sum x, sum x^2); MODE 1: (sum g, sum g*xhat), g = (dy+dy2)*act'(xhat),
+// xhat = (x-mean)*rstd;  MODE 2: MODE-1 pass that also writes dx and sums dx (db);
+// MODE 3: plain channel sum of x into db (bias gradients)
+template <int MODE, int VW>
+__global__ __launch_bounds__(TPB) void rows_kernel(Slice X, Slice DY, Slice DY2, int act, const float* __restrict__ mr,
+                                                   const float* __restrict__ red, void* __restrict__ dx, int dxdt,
+                                                   int lddx, int dxoff, int HW, int C, int rows_per_block,
+                                                   double* __restrict__ work, float* __restrict__ db) {
+    __shared__ float s0[TPB * VW], s1[TPB * VW];
     const int n = blockIdx.y;
     const int r0 = blockIdx.x * rows_per_block;
     const int r1 = min(HW, r0 + rows_per_block);
-    RowLayout L(C);
-    const int tid = threadIdx.x;
-    const int cl = tid % L.cpt, rl = tid / L.cpt;
-    const bool active = rl < L.rpar;
-    for (int cbase = 0; cbase < C; cbase += L.cpt) {
-        const int c = cbase + cl;
-        float acc0 = 0.f, acc1 = 0.f;
-        if (active && c < C) {
-            float2 st = make_float2(0.f, 0.f);
-            if (MODE == 1) st = ((const float2*)mr)[(long)n * C + c];
-            for (int r = r0 + rl; r < r1; r += L.rpar) {
-                const long p = (long)n * HW + r;
-                float v = ldv(x, xdt, p * ldx + xoff + c);
-                if (MODE == 0) {
-                    acc0 += v;
-                    acc1 += v * v;
-                } else {
-                    if (dy2) v += ldv(dy2, d2dt, p * ld2 + off2 + c);
-                    const float xh = (ldv(a, adt, p * lda + aoff + c) - st.x) * st.y;
-                    const float g = v * act_grad(xh, act);
-                    acc0 += g;
-                    acc1 += g * xh;
+    Lay L(C, VW);
+    const bool active = L.rl < L.RP;
+    for (int cb = 0; cb < C; cb += L.CL * VW) {
+        const int c = cb + L.cl * VW;
+        const bool on = active && c < C;
+        float a0[VW], a1[VW], mean[VW], rstd[VW], mg[VW], mgx[VW];
+#pragma unroll
+        for (int k = 0; k < VW; ++k) { a0[k] = 0.f; a1[k] = 0.f; }
+        if (on && MODE >= 1) {
+#pragma unroll
+            for (int k = 0; k < VW; ++k) {
+                const float2 st = ((const float2*)mr)[(long)n * C + c + k];
+                mean[k] = st.x; rstd[k] = st.y;
+                if (MODE == 2) {
+                    const float2 rd = ((const float2*)red)[(long)n * C + c + k];
+                    mg[k] = rd.x; mgx[k] = rd.y;
                 }
             }
         }
-        s0[tid] = acc0;
-        s1[tid] = acc1;
-        __syncthreads();
-        if (active && rl == 0 && c < C) {
-            float t0 = 0.f, t1 = 0.f;
-            for (int k = 0; k < L.rpar; ++k) {
-                t0 += s0[cl + k * L.cpt];
-                t1 += s1[cl + k * L.cpt];
+        if (on) {
+#pragma unroll 4
+            for (int r = r0 + L.rl; r < r1; r += L.RP) {
+                const long p = (long)n * HW + r;
+                float xv[VW];
+                ldv_<VW>(X.p, X.dt, p * X.ld + X.off + c, xv);
+                if (MODE == 0 || MODE == 3) {
+#pragma unroll
+                    for (int k = 0; k < VW; ++k) { a0[k] += xv[k]; a1[k] += xv[k] * xv[k]; }
+                } else {
+                    float gv[VW], g2[VW];
+                    ldv_<VW>(DY.p, DY.dt, p * DY.ld + DY.off + c, gv);
+                    if (DY2.p) {
+                        ldv_<VW>(DY2.p, DY2.dt, p * DY2.ld + DY2.off + c, g2);
+#pragma unroll
+                        for (int k = 0; k < VW; ++k) gv[k] += g2[k];
+                    }
+                    float o[VW];
+#pragma unroll
+                    for (int k = 0; k < VW; ++k) {
+                        const float xh = (xv[k] - mean[k]) * rstd[k];
+                        const float g = gv[k] * act_grad(xh, act);
+                        if (MODE == 1) { a0[k] += g; a1[k] += g * xh; }
+                        else { o[k] = rstd[k] * (g - mg[k] - xh * mgx[k]); a0[k] += o[k]; }
+                    }
+                    if (MODE == 2) stv_<VW>(dx, dxdt, p * lddx + dxoff + c, o);
+                }
             }
-            atomicAdd(work + ((long)n * C + c) * 2 + 0, (double)t0);
-            atomicAdd(work + ((long)n * C + c) * 2 + 1, (double)t1);
+        }
+        if ((MODE == 2 || MODE == 3) && !db) continue;  // uniform across the block
+#pragma unroll
+        for (int k = 0; k < VW; ++k) {
+            s0[threadIdx.x * VW + k] = a0[k];
+            s1[threadIdx.x * VW + k] = a1[k];
+        }
+        __syncthreads();
+        // first RP-row of lanes reduces over the RP rows
+        if (on && L.rl == 0) {
+#pragma unroll
+            for (int k = 0; k < VW; ++k) {
+                float t0 = 0.f, t1 = 0.f;
+                for (int j = 0; j < L.RP; ++j) {
+                    t0 += s0[(j * L.CL + L.cl) * VW + k];
+                    t1 += s1[(j * L.CL + L.cl) * VW + k];
+                }
+                if (MODE == 2 || MODE == 3) {
+                    atomicAdd(db + c + k, t0);
+                } else {
+                    atomicAdd(work + ((long)n * C + c + k) * 2 + 0, (double)t0);
+                    atomicAdd(work + ((long)n * C + c + k) * 2 + 1, (double)t1);
+                }
+            }
         }
         __syncthreads();
     }
 }
 
-__global__ void finalize_stats_kernel(const double* __restrict__ work, float* __restrict__ mr, int NC, int HW,
-                                      int mode) {
+__global__ void finalize_kernel(const double* __restrict__ work, float* __restrict__ mr, int NC, int HW, int mode) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= NC) return;
     double s = work[2 * i], q = work[2 * i + 1];
@@ -97,99 +181,74 @@ __global__ void finalize_stats_kernel(const double* __restrict__ work, float* __
     }
 }
 
-__global__ __launch_bounds__(TPB) void in_apply_kernel(const void* __restrict__ x, int dt, int HW, int C, int ldx,
-                                                       int xoff, const float* __restrict__ mr, int act,
-                                                       const void* __restrict__ res, int ldr, int roff,
-                                                       void* __restrict__ y, int ldy, int yoff,
-                                                       void* __restrict__ xhat, long total) {
+template <int VW>
+__global__ __launch_bounds__(TPB) void apply_kernel(Slice X, int HW, int C, const float* __restrict__ mr, int act,
+                                                    Slice R, void* __restrict__ y, int ldy, int yoff,
+                                                    void* __restrict__ xhat, long total) {
+    const int CV = C / VW;
     for (long idx = blockIdx.x * (long)TPB + threadIdx.x; idx < total; idx += (long)gridDim.x * TPB) {
-        const long p = idx / C;
-        const int c = (int)(idx - p * C);
+        const long p = idx / CV;
+        const int c = (int)(idx - p * CV) * VW;
         const int n = (int)(p / HW);
-        const float2 st = ((const float2*)mr)[(long)n * C + c];
-        float v = (ldv(x, dt, p * ldx + xoff + c) - st.x) * st.y;
-        if (xhat) stv(xhat, dt, p * C + c, v);
-        if (act == IRGAN_ACT_RELU) v = v > 0.f ? v : 0.f;
-        else if (act == IRGAN_ACT_LRELU) v = v > 0.f ? v : 0.2f * v;
-        if (res) v += ldv(res, dt, p * ldr + roff + c);
-        stv(y, dt, p * ldy + yoff + c, v);
+        float v[VW];
+        ldv_<VW>(X.p, X.dt, p * X.ld + X.off + c, v);
+        const float4* m4 = (const float4*)(mr + 2 * ((long)n * C + c));
+#pragma unroll
+        for (int k = 0; k < VW; k += 2) {
+            float4 st;
+            if constexpr (VW == 8) st = m4[k / 2];
+            else { st = make_float4(mr[2 * ((long)n * C + c)], mr[2 * ((long)n * C + c) + 1], 0.f, 0.f); }
+            v[k] = (v[k] - st.x) * st.y;
+            if (VW > 1) v[k + 1] = (v[k + 1] - st.z) * st.w;
+        }
+        if (xhat) stv_<VW>(xhat, X.dt, p * C + c, v);
+#pragma unroll
+        for (int k = 0; k < VW; ++k) {
+            if (act == IRGAN_ACT_RELU) v[k] = v[k] > 0.f ? v[k] : 0.f;
+            else if (act == IRGAN_ACT_LRELU) v[k] = v[k] > 0.f ? v[k] : 0.2f * v[k];
+        }
+        if (R.p) {
+            float rv[VW];
+            ldv_<VW>(R.p, R.dt, p * R.ld + R.off + c, rv);
+#pragma unroll
+            for (int k = 0; k < VW; ++k) v[k] += rv[k];
+        }
+        stv_<VW>(y, X.dt, p * ldy + yoff + c, v);
     }
 }
 
-__global__ __launch_bounds__(TPB) void in_bwd_apply_kernel(
-    const void* __restrict__ dy, int dydt, int lddy, int dyoff, const void* __restrict__ dy2, int d2dt, int ld2,
-    int off2, const void* __restrict__ a, int adt, int lda, int aoff, int act, int HW, int C,
-    const float* __restrict__ mr, const float* __restrict__ red, void* __restrict__ dx, int dxdt, int lddx,
-    int dxoff, float* __restrict__ db, int rows_per_block) {
-    __shared__ float sdb[TPB];
-    const int n = blockIdx.y;
-    const int r0 = blockIdx.x * rows_per_block;
-    const int r1 = min(HW, r0 + rows_per_block);
-    RowLayout L(C);
-    const int tid = threadIdx.x;
-    const int cl = tid % L.cpt, rl = tid / L.cpt;
-    const bool active = rl < L.rpar;
-    for (int cbase = 0; cbase < C; cbase += L.cpt) {
-        const int c = cbase + cl;
-        float accd = 0.f;
-        if (active && c < C) {
-            const float2 st = ((const float2*)mr)[(long)n * C + c];
-            const float2 rd = ((const float2*)red)[(long)n * C + c];
-            for (int r = r0 + rl; r < r1; r += L.rpar) {
-                const long p = (long)n * HW + r;
-                float v = ldv(dy, dydt, p * lddy + dyoff + c);
-                if (dy2) v += ldv(dy2, d2dt, p * ld2 + off2 + c);
-                const float xh = (ldv(a, adt, p * lda + aoff + c) - st.x) * st.y;
-                const float g = v * act_grad(xh, act);
-                const float o = st.y * (g - rd.x - xh * rd.y);
-                stv(dx, dxdt, p * lddx + dxoff + c, o);
-                accd += o;
-            }
-        }
-        if (db) {
-            sdb[tid] = accd;
-            __syncthreads();
-            if (active && rl == 0 && c < C) {
-                float t = 0.f;
-                for (int k = 0; k < L.rpar; ++k) t += sdb[cl + k * L.cpt];
-                atomicAdd(db + c, t);
-            }
-            __syncthreads();
-        }
-    }
+bool vec_ok(int C, std::initializer_list<int> lds) {
+    if (C % V) return false;
+    for (int l : lds)
+        if (l % V) return false;
+    return true;
 }
 
-__global__ __launch_bounds__(TPB) void channel_sum_kernel(const void* __restrict__ g, int dt, long P, int C, int ld,
-                                                          int off, float* __restrict__ db, int rows_per_block) {
-    __shared__ float s[TPB];
-    const long r0 = (long)blockIdx.x * rows_per_block;
-    const long r1 = min(P, r0 + rows_per_block);
-    RowLayout L(C);
-    const int tid = threadIdx.x, cl = tid % L.cpt, rl = tid / L.cpt;
-    const bool active = rl < L.rpar;
-    for (int cbase = 0; cbase < C; cbase += L.cpt) {
-        const int c = cbase + cl;
-        float acc = 0.f;
-        if (active && c < C)
-            for (long r = r0 + rl; r < r1; r += L.rpar) acc += ldv(g, dt, r * ld + off + c);
-        s[tid] = acc;
-        __syncthreads();
-        if (active && rl == 0 && c < C) {
-            float t = 0.f;
-            for (int k = 0; k < L.rpar; ++k) t += s[cl + k * L.cpt];
-            atomicAdd(db + c, t);
-        }
-        __syncthreads();
-    }
-}
-
-int rows_for(long HW, int N) {
-    // ~1-4k rows per block, enough blocks to cover 256 CUs
-    long want_blocks = 1024 / (N > 0 ? N : 1);
-    if (want_blocks < 1) want_blocks = 1;
-    long r = (HW + want_blocks - 1) / want_blocks;
-    if (r < 256) r = 256;
+int rows_for(long HW, int N, int RP) {
+    long want = (2048 + N - 1) / (N > 0 ? N : 1);  // ~2048 blocks over the grid
+    long r = (HW + want - 1) / want;
+    long minr = 4L * RP;
+    if (r < minr) r = minr;
     return (int)r;
+}
+
+int rp_of(int C, int VW) {
+    int cl = (C + VW - 1) / VW;
+    if (cl > TPB) cl = TPB;
+    return TPB / cl;
+}
+
+template <int MODE>
+int launch_rows(Slice X, Slice DY, Slice DY2, int act, const float* mr, const float* red, void* dx, int dxdt, int lddx,
+                int dxoff, int N, int HW, int C, double* work, float* db, bool vec, hipStream_t st) {
+    const int VW = vec ? V : 1;
+    const int rows = rows_for(HW, N, rp_of(C, VW));
+    dim3 g(irgan_cdiv(HW, rows), N);
+    if (vec)
+        rows_kernel<MODE, V><<<g, TPB, 0, st>>>(X, DY, DY2, act, mr, red, dx, dxdt, lddx, dxoff, HW, C, rows, work, db);
+    else
+        rows_kernel<MODE, 1><<<g, TPB, 0, st>>>(X, DY, DY2, act, mr, red, dx, dxdt, lddx, dxoff, HW, C, rows, work, db);
+    return 0;
 }
 
 }  // namespace
@@ -198,11 +257,9 @@ extern "C" int irgan_in_stats(const void* x, int32_t dtype, int32_t N, int32_t H
                               int32_t off, double* work, float* mr, irgan_stream_t s) {
     hipStream_t st = (hipStream_t)s;
     hipMemsetAsync(work, 0, sizeof(double) * 2 * (size_t)N * C, st);
-    int rows = rows_for(HW, N);
-    dim3 g(irgan_cdiv(HW, rows), N);
-    reduce2_kernel<0><<<g, TPB, 0, st>>>(x, dtype, ld, off, nullptr, 0, 0, 0, nullptr, 0, 0, 0, 0, nullptr, HW, C,
-                                         rows, work);
-    finalize_stats_kernel<<<irgan_cdiv((long)N * C, 256), 256, 0, st>>>(work, mr, N * C, HW, 0);
+    Slice X{x, dtype, ld, off}, Z{nullptr, 0, 0, 0};
+    launch_rows<0>(X, Z, Z, 0, nullptr, nullptr, nullptr, 0, 0, 0, N, HW, C, work, nullptr, vec_ok(C, {ld, off}), st);
+    finalize_kernel<<<irgan_cdiv((long)N * C, 256), 256, 0, st>>>(work, mr, N * C, HW, 0);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }
@@ -210,11 +267,16 @@ extern "C" int irgan_in_stats(const void* x, int32_t dtype, int32_t N, int32_t H
 extern "C" int irgan_in_apply(const void* x, int32_t dtype, int32_t N, int32_t HW, int32_t C, int32_t ldx,
                               int32_t xoff, const float* mr, int32_t act, const void* res, int32_t ldr, int32_t roff,
                               void* y, int32_t ldy, int32_t yoff, void* xhat, irgan_stream_t s) {
-    long total = (long)N * HW * C;
+    const bool vec = vec_ok(C, {ldx, xoff, ldy, yoff}) && (!res || vec_ok(C, {ldr, roff}));
+    const int VW = vec ? V : 1;
+    long total = (long)N * HW * (C / VW);
     if (total <= 0) return 0;
-    int blocks = (int)std::min<long>((total + TPB - 1) / TPB, 8192);
-    in_apply_kernel<<<blocks, TPB, 0, (hipStream_t)s>>>(x, dtype, HW, C, ldx, xoff, mr, act, res, ldr, roff, y, ldy,
-                                                        yoff, xhat, total);
+    int blocks = (int)std::min<long>((total + TPB - 1) / TPB, 16384);
+    Slice X{x, dtype, ldx, xoff}, R{res, dtype, ldr, roff};
+    if (vec)
+        apply_kernel<V><<<blocks, TPB, 0, (hipStream_t)s>>>(X, HW, C, mr, act, R, y, ldy, yoff, xhat, total);
+    else
+        apply_kernel<1><<<blocks, TPB, 0, (hipStream_t)s>>>(X, HW, C, mr, act, R, y, ldy, yoff, xhat, total);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }
@@ -225,11 +287,10 @@ extern "C" int irgan_in_bwd_reduce(const void* dy, int32_t dy_dtype, int32_t ldd
                                    const float* mr, double* work, float* red, irgan_stream_t s) {
     hipStream_t st = (hipStream_t)s;
     hipMemsetAsync(work, 0, sizeof(double) * 2 * (size_t)N * C, st);
-    int rows = rows_for(HW, N);
-    dim3 g(irgan_cdiv(HW, rows), N);
-    reduce2_kernel<1><<<g, TPB, 0, st>>>(dy, dy_dtype, lddy, dyoff, dy2, dy2_dtype, lddy2, dy2off, x, x_dtype, ldx,
-                                         xoff, act, mr, HW, C, rows, work);
-    finalize_stats_kernel<<<irgan_cdiv((long)N * C, 256), 256, 0, st>>>(work, red, N * C, HW, 1);
+    const bool vec = vec_ok(C, {lddy, dyoff, ldx, xoff}) && (!dy2 || vec_ok(C, {lddy2, dy2off}));
+    Slice X{x, x_dtype, ldx, xoff}, DY{dy, dy_dtype, lddy, dyoff}, DY2{dy2, dy2_dtype, lddy2, dy2off};
+    launch_rows<1>(X, DY, DY2, act, mr, nullptr, nullptr, 0, 0, 0, N, HW, C, work, nullptr, vec, st);
+    finalize_kernel<<<irgan_cdiv((long)N * C, 256), 256, 0, st>>>(work, red, N * C, HW, 1);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }
@@ -239,11 +300,9 @@ extern "C" int irgan_in_bwd_apply(const void* dy, int32_t dy_dtype, int32_t lddy
                                   int32_t ldx, int32_t xoff, int32_t act, int32_t N, int32_t HW, int32_t C,
                                   const float* mr, const float* red, void* dx, int32_t dx_dtype, int32_t lddx,
                                   int32_t dxoff, float* db, irgan_stream_t s) {
-    int rows = rows_for(HW, N);
-    dim3 g(irgan_cdiv(HW, rows), N);
-    in_bwd_apply_kernel<<<g, TPB, 0, (hipStream_t)s>>>(dy, dy_dtype, lddy, dyoff, dy2, dy2_dtype, lddy2, dy2off, x,
-                                                       x_dtype, ldx, xoff, act, HW, C, mr, red, dx, dx_dtype, lddx,
-                                                       dxoff, db, rows);
+    const bool vec = vec_ok(C, {lddy, dyoff, ldx, xoff, lddx, dxoff}) && (!dy2 || vec_ok(C, {lddy2, dy2off}));
+    Slice X{x, x_dtype, ldx, xoff}, DY{dy, dy_dtype, lddy, dyoff}, DY2{dy2, dy2_dtype, lddy2, dy2off};
+    launch_rows<2>(X, DY, DY2, act, mr, red, dx, dx_dtype, lddx, dxoff, N, HW, C, nullptr, db, vec, (hipStream_t)s);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }
@@ -251,8 +310,9 @@ extern "C" int irgan_in_bwd_apply(const void* dy, int32_t dy_dtype, int32_t lddy
 extern "C" int irgan_channel_sum(const void* g, int32_t dtype, int32_t P, int32_t C, int32_t ld, int32_t off,
                                  float* db, irgan_stream_t s) {
     if (P <= 0) return 0;
-    int rows = rows_for(P, 1);
-    channel_sum_kernel<<<irgan_cdiv(P, rows), TPB, 0, (hipStream_t)s>>>(g, dtype, P, C, ld, off, db, rows);
+    Slice X{g, dtype, ld, off}, Z{nullptr, 0, 0, 0};
+    launch_rows<3>(X, Z, Z, 0, nullptr, nullptr, nullptr, 0, 0, 0, 1, P, C, nullptr, db, vec_ok(C, {ld, off}),
+                   (hipStream_t)s);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }

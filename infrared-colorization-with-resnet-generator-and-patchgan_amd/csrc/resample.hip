@@ -1,218 +1,75 @@
 // Resampling and layout kernels (NHWC, channel-fastest threads => coalesced).
-//   blur-down   : Downsample, reflect pad 1 + binomial [1,2,1]^2/16, stride 2 (ir:269-310)
-//   upsample    : UpsampleAA, bilinear x2 align_corners=True + reflect pad 1 + blur (ir:313-355)
-//   reflect fold: backward of nn.ReflectionPad2d (ir:381, 402, 459, 528)
-//   maxpool 2x2 : VGG-16 features pooling (ir:664)
-// Backward passes are written as gathers (each output element sums its
-// contributors), so they are deterministic and need no atomics.
+//   separable resample: Downsample (ir:269-310), UpsampleAA (ir:313-355), the
+//                       nn.ReflectionPad2d fold (ir:381, 402, 459, 528) and their
+//                       adjoints, all as per-axis (index, weight) tables
+//   maxpool 2x2       : VGG-16 features pooling (ir:664)
+// Backward passes are gathers (each output element sums its contributors), so
+// they are deterministic and need no atomics.
 #include "common.h"
 
 namespace {
 
 constexpr int TPB = 256;
 
-// blur taps [1,2,1]/4 per dimension (outer product = the reference's 3x3 filt)
-IRGAN_HD float tap3(int a) { return a == 1 ? 0.5f : 0.25f; }
-
-// contributors of a padded-domain position set: input coordinate q of an axis of
-// length n receives from padded coordinates u with reflect(u - 1) == q.
-IRGAN_HD int refl_sources(int q, int n, int* u) {
-    int k = 0;
-    u[k++] = q + 1;
-    if (q == 1) u[k++] = 0;
-    if (q == n - 2 && n >= 3) u[k++] = n + 1;
-    return k;
-}
-
-__global__ __launch_bounds__(TPB) void blur_down_fwd_kernel(const void* __restrict__ x, int dt, int H, int W, int C,
-                                                            int ldx, int xoff, void* __restrict__ y, int ldy,
-                                                            int yoff, int Ho, int Wo, long total) {
+// ---------------------------------------------------------------------------
+// separable resampling: out[n][oy][ox][c] = sum_i sum_j wy[oy][i] wx[ox][j] in[n][iy][ix][c]
+// One kernel serves Downsample (blur s2), UpsampleAA (bilinear x2 + blur), the
+// reflection-pad fold and all their adjoints: each is separable per axis, so a
+// per-axis (index, weight) table of at most T taps describes it exactly.
+// Threads own 8 channels (16-byte loads) when the slices allow.
+// ---------------------------------------------------------------------------
+template <int VW>
+__global__ __launch_bounds__(TPB) void sep_kernel(const void* __restrict__ in, int idt, int Hin, int Win, int C,
+                                                  int ldi, int offi, void* __restrict__ out, int odt, int Hout,
+                                                  int Wout, int ldo, int offo, const int* __restrict__ ty,
+                                                  const float* __restrict__ wy, const int* __restrict__ tx,
+                                                  const float* __restrict__ wx, int T, int accumulate, long total) {
+    const int CV = C / VW;
     for (long idx = blockIdx.x * (long)TPB + threadIdx.x; idx < total; idx += (long)gridDim.x * TPB) {
         long t = idx;
-        const int c = (int)(t % C); t /= C;
-        const int j = (int)(t % Wo); t /= Wo;
-        const int i = (int)(t % Ho);
-        const int n = (int)(t / Ho);
-        float acc = 0.f;
+        const int c = (int)(t % CV) * VW; t /= CV;
+        const int ox = (int)(t % Wout); t /= Wout;
+        const int oy = (int)(t % Hout);
+        const int n = (int)(t / Hout);
+        float acc[VW];
 #pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const int qy = reflect_idx(2 * i + a - 1, H);
-            float row = 0.f;
+        for (int k = 0; k < VW; ++k) acc[k] = 0.f;
+        for (int i = 0; i < T; ++i) {
+            const float w1 = wy[oy * T + i];
+            if (w1 == 0.f) continue;
+            const long rowb = ((long)n * Hin + ty[oy * T + i]) * Win;
+            for (int j = 0; j < T; ++j) {
+                const float w2 = wx[ox * T + j];
+                if (w2 == 0.f) continue;
+                const float w = w1 * w2;
+                const long e = (rowb + tx[ox * T + j]) * ldi + offi + c;
+                if constexpr (VW == 8) {
+                    float v[8];
+                    if (idt == IRGAN_BF16) {
+                        const uint4 u = *(const uint4*)((const bf16_t*)in + e);
+                        const uint32_t q[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
-            for (int b = 0; b < 3; ++b) {
-                const int qx = reflect_idx(2 * j + b - 1, W);
-                row += tap3(b) * ldv(x, dt, (((long)n * H + qy) * W + qx) * ldx + xoff + c);
-            }
-            acc += tap3(a) * row;
-        }
-        stv(y, dt, (((long)n * Ho + i) * Wo + j) * ldy + yoff + c, acc);
-    }
-}
-
-// dx[q] = sum over padded u with reflect(u-1)=q, taps a with u = 2i + a
-__global__ __launch_bounds__(TPB) void blur_down_bwd_kernel(const void* __restrict__ dy, int dt, int H, int W, int C,
-                                                            int lddy, int dyoff, void* __restrict__ dx, int dxdt,
-                                                            int lddx, int dxoff, int Ho, int Wo, long total) {
-    for (long idx = blockIdx.x * (long)TPB + threadIdx.x; idx < total; idx += (long)gridDim.x * TPB) {
-        long t = idx;
-        const int c = (int)(t % C); t /= C;
-        const int qx = (int)(t % W); t /= W;
-        const int qy = (int)(t % H);
-        const int n = (int)(t / H);
-        int uy[3], ux[3];
-        const int ny = refl_sources(qy, H, uy), nx = refl_sources(qx, W, ux);
-        float acc = 0.f;
-        for (int s = 0; s < ny; ++s)
-            for (int a = 0; a < 3; ++a) {
-                const int vy = uy[s] - a;
-                if (vy < 0 || (vy & 1)) continue;
-                const int i = vy >> 1;
-                if (i >= Ho) continue;
-                for (int r = 0; r < nx; ++r)
-                    for (int b = 0; b < 3; ++b) {
-                        const int vx = ux[r] - b;
-                        if (vx < 0 || (vx & 1)) continue;
-                        const int j = vx >> 1;
-                        if (j >= Wo) continue;
-                        acc += tap3(a) * tap3(b) * ldv(dy, dt, (((long)n * Ho + i) * Wo + j) * lddy + dyoff + c);
+                        for (int k = 0; k < 4; ++k) {
+                            v[2 * k] = __uint_as_float(q[k] << 16);
+                            v[2 * k + 1] = __uint_as_float(q[k] & 0xffff0000u);
+                        }
+                    } else {
+                        const float4 a = *(const float4*)((const float*)in + e), b = *(const float4*)((const float*)in + e + 4);
+                        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
                     }
-            }
-        stv(dx, dxdt, (((long)n * H + qy) * W + qx) * lddx + dxoff + c, acc);
-    }
-}
-
-// bilinear source for output coordinate v of an axis upsampled from n (ATen
-// upsample_bilinear2d, align_corners=True: src = v * (n-1)/(2n-1))
-struct Bil {
-    int i0, i1;
-    float l0, l1;
-};
-IRGAN_HD Bil bil(int v, float scale, int n) {
-    Bil b;
-    const float r = scale * (float)v;
-    b.i0 = (int)r;
-    b.i1 = b.i0 + ((b.i0 < n - 1) ? 1 : 0);
-    b.l1 = r - (float)b.i0;
-    b.l0 = 1.f - b.l1;
-    return b;
-}
-
-__global__ __launch_bounds__(TPB) void upsample_fwd_kernel(const void* __restrict__ x, int dt, int H, int W, int C,
-                                                           int ldx, int xoff, void* __restrict__ y, int ldy, int yoff,
-                                                           float sh, float sw, long total) {
-    const int H2 = 2 * H, W2 = 2 * W;
-    for (long idx = blockIdx.x * (long)TPB + threadIdx.x; idx < total; idx += (long)gridDim.x * TPB) {
-        long t = idx;
-        const int c = (int)(t % C); t /= C;
-        const int ox = (int)(t % W2); t /= W2;
-        const int oy = (int)(t % H2);
-        const int n = (int)(t / H2);
-        const long base = (long)n * H * W;
-        float acc = 0.f;
 #pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const Bil by = bil(reflect_idx(oy + a - 1, H2), sh, H);
-            float row = 0.f;
-#pragma unroll
-            for (int b = 0; b < 3; ++b) {
-                const Bil bx = bil(reflect_idx(ox + b - 1, W2), sw, W);
-                auto X = [&](int yy, int xx) { return ldv(x, dt, (base + (long)yy * W + xx) * ldx + xoff + c); };
-                const float v = by.l0 * (bx.l0 * X(by.i0, bx.i0) + bx.l1 * X(by.i0, bx.i1)) +
-                                by.l1 * (bx.l0 * X(by.i1, bx.i0) + bx.l1 * X(by.i1, bx.i1));
-                row += tap3(b) * v;
-            }
-            acc += tap3(a) * row;
-        }
-        stv(y, dt, (((long)n * H2 + oy) * W2 + ox) * ldy + yoff + c, acc);
-    }
-}
-
-// backward part 1: transpose of (reflect pad 1 + blur, stride 1) on the 2H x 2W grid -> fp32 work
-__global__ __launch_bounds__(TPB) void upsample_bwd_blur_kernel(const void* __restrict__ dy, int dt, int H2, int W2,
-                                                                int C, int lddy, int dyoff, float* __restrict__ work,
-                                                                long total) {
-    for (long idx = blockIdx.x * (long)TPB + threadIdx.x; idx < total; idx += (long)gridDim.x * TPB) {
-        long t = idx;
-        const int c = (int)(t % C); t /= C;
-        const int qx = (int)(t % W2); t /= W2;
-        const int qy = (int)(t % H2);
-        const int n = (int)(t / H2);
-        int uy[3], ux[3];
-        const int ny = refl_sources(qy, H2, uy), nx = refl_sources(qx, W2, ux);
-        float acc = 0.f;
-        for (int s = 0; s < ny; ++s)
-            for (int a = 0; a < 3; ++a) {
-                const int oy = uy[s] - a;
-                if (oy < 0 || oy >= H2) continue;
-                for (int r = 0; r < nx; ++r)
-                    for (int b = 0; b < 3; ++b) {
-                        const int ox = ux[r] - b;
-                        if (ox < 0 || ox >= W2) continue;
-                        acc += tap3(a) * tap3(b) * ldv(dy, dt, (((long)n * H2 + oy) * W2 + ox) * lddy + dyoff + c);
-                    }
-            }
-        work[idx] = acc;
-    }
-}
-
-// backward part 2: transpose of the bilinear map (gather over the ~5 output
-// rows/cols whose stencil touches each input row/col)
-__global__ __launch_bounds__(TPB) void upsample_bwd_bil_kernel(const float* __restrict__ work, int H, int W, int C,
-                                                               float sh, float sw, void* __restrict__ dx, int dxdt,
-                                                               int lddx, int dxoff, int accumulate, long total) {
-    const int H2 = 2 * H, W2 = 2 * W;
-    for (long idx = blockIdx.x * (long)TPB + threadIdx.x; idx < total; idx += (long)gridDim.x * TPB) {
-        long t = idx;
-        const int c = (int)(t % C); t /= C;
-        const int w = (int)(t % W); t /= W;
-        const int h = (int)(t % H);
-        const int n = (int)(t / H);
-        // output rows v with bil(v).i0 or .i1 == h: v*sh in [h-1, h+1)
-        const int vy0 = max(0, (int)floorf((h - 1) / fmaxf(sh, 1e-30f)) - 1);
-        const int vy1 = min(H2 - 1, sh > 0.f ? (int)ceilf((h + 1) / sh) + 1 : H2 - 1);
-        const int vx0 = max(0, (int)floorf((w - 1) / fmaxf(sw, 1e-30f)) - 1);
-        const int vx1 = min(W2 - 1, sw > 0.f ? (int)ceilf((w + 1) / sw) + 1 : W2 - 1);
-        float acc = 0.f;
-        for (int vy = vy0; vy <= vy1; ++vy) {
-            const Bil by = bil(vy, sh, H);
-            float wy = (by.i0 == h ? by.l0 : 0.f) + (by.i1 == h ? by.l1 : 0.f);
-            if (wy == 0.f) continue;
-            for (int vx = vx0; vx <= vx1; ++vx) {
-                const Bil bx = bil(vx, sw, W);
-                float wx = (bx.i0 == w ? bx.l0 : 0.f) + (bx.i1 == w ? bx.l1 : 0.f);
-                if (wx == 0.f) continue;
-                acc += wy * wx * work[(((long)n * H2 + vy) * W2 + vx) * C + c];
+                    for (int k = 0; k < 8; ++k) acc[k] += w * v[k];
+                } else {
+                    acc[0] += w * ldv(in, idt, e);
+                }
             }
         }
-        const long o = (((long)n * H + h) * W + w) * lddx + dxoff + c;
-        if (accumulate) acc += ldv(dx, dxdt, o);
-        stv(dx, dxdt, o, acc);
-    }
-}
-
-__global__ __launch_bounds__(TPB) void reflect_fold_kernel(const float* __restrict__ dxp, int H, int W, int C, int p,
-                                                           void* __restrict__ dx, int dxdt, int lddx, int dxoff,
-                                                           int accumulate, long total) {
-    const int Hp = H + 2 * p, Wp = W + 2 * p;
-    for (long idx = blockIdx.x * (long)TPB + threadIdx.x; idx < total; idx += (long)gridDim.x * TPB) {
-        long t = idx;
-        const int c = (int)(t % C); t /= C;
-        const int qx = (int)(t % W); t /= W;
-        const int qy = (int)(t % H);
-        const int n = (int)(t / H);
-        int uy[3], ux[3], ny = 0, nx = 0;
-        uy[ny++] = qy + p;
-        if (qy >= 1 && qy <= p) uy[ny++] = p - qy;
-        if (qy <= H - 2 && qy >= H - 1 - p) uy[ny++] = p + 2 * (H - 1) - qy;
-        ux[nx++] = qx + p;
-        if (qx >= 1 && qx <= p) ux[nx++] = p - qx;
-        if (qx <= W - 2 && qx >= W - 1 - p) ux[nx++] = p + 2 * (W - 1) - qx;
-        float acc = 0.f;
-        for (int a = 0; a < ny; ++a)
-            for (int b = 0; b < nx; ++b) acc += dxp[(((long)n * Hp + uy[a]) * Wp + ux[b]) * C + c];
-        const long o = (((long)n * H + qy) * W + qx) * lddx + dxoff + c;
-        if (accumulate) acc += ldv(dx, dxdt, o);
-        stv(dx, dxdt, o, acc);
+        const long o = (((long)n * Hout + oy) * Wout + ox) * ldo + offo + c;
+#pragma unroll
+        for (int k = 0; k < VW; ++k) {
+            if (accumulate) acc[k] += ldv(out, odt, o + k);
+            stv(out, odt, o + k, acc[k]);
+        }
     }
 }
 
@@ -339,59 +196,91 @@ int nblocks(long total) { return (int)std::max<long>(1, std::min<long>((total + 
 #define RS_CHECK(total) \
     if ((total) <= 0) return 0
 
-extern "C" int irgan_blur_down_fwd(const void* x, int32_t dt, int32_t N, int32_t H, int32_t W, int32_t C, int32_t ldx,
-                                   int32_t xoff, void* y, int32_t ldy, int32_t yoff, irgan_stream_t s) {
-    const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
-    long total = (long)N * Ho * Wo * C;
-    RS_CHECK(total);
-    blur_down_fwd_kernel<<<nblocks(total), TPB, 0, (hipStream_t)s>>>(x, dt, H, W, C, ldx, xoff, y, ldy, yoff, Ho, Wo,
-                                                                     total);
-    IRGAN_LAUNCH_CHECK();
-    return 0;
+// ---- per-axis tables (host only) -------------------------------------------
+namespace {
+int refl_host(int q, int n) {
+    q = q < 0 ? -q : q;
+    return q >= n ? 2 * n - 2 - q : q;
+}
+struct Tab {
+    int n_out, T;
+    int32_t* idx;
+    float* w;
+    int add(int row, int i, float wt) {  // merge duplicate indices
+        for (int k = 0; k < T; ++k) {
+            if (w[row * T + k] != 0.f && idx[row * T + k] == i) { w[row * T + k] += wt; return 0; }
+        }
+        for (int k = 0; k < T; ++k) {
+            if (w[row * T + k] == 0.f) { idx[row * T + k] = i; w[row * T + k] = wt; return 0; }
+        }
+        return -1;  // table too narrow
+    }
+};
+// forward map of `kind` on an axis of length n_in: calls add(out_row, in_index, weight)
+template <typename F>
+int axis_map(int kind, int n_in, int p, F&& add) {
+    const float f3[3] = {0.25f, 0.5f, 0.25f};
+    if (kind == 0) {  // Downsample: reflect pad 1, [1,2,1]/4, stride 2 (ir:269-310)
+        const int n_out = (n_in - 1) / 2 + 1;
+        for (int o = 0; o < n_out; ++o)
+            for (int a = 0; a < 3; ++a)
+                if (add(o, refl_host(2 * o + a - 1, n_in), f3[a])) return -1;
+        return n_out;
+    }
+    if (kind == 1) {  // UpsampleAA: bilinear x2 align_corners=True, reflect pad 1, blur (ir:313-355)
+        const int n2 = 2 * n_in;
+        const float scale = n_in > 1 ? (float)(n_in - 1) / (float)(n2 - 1) : 0.f;
+        for (int o = 0; o < n2; ++o)
+            for (int a = 0; a < 3; ++a) {
+                const int v = refl_host(o + a - 1, n2);
+                const float r = scale * (float)v;
+                const int i0 = (int)r, i1 = i0 + (i0 < n_in - 1 ? 1 : 0);
+                const float l1 = r - (float)i0, l0 = 1.f - l1;
+                if (add(o, i0, f3[a] * l0)) return -1;
+                if (l1 != 0.f && add(o, i1, f3[a] * l1)) return -1;
+            }
+        return n2;
+    }
+    if (kind == 2) {  // nn.ReflectionPad2d(p): padded coordinate u reads refl(u - p)
+        const int n_out = n_in + 2 * p;
+        for (int u = 0; u < n_out; ++u)
+            if (add(u, refl_host(u - p, n_in), 1.f)) return -1;
+        return n_out;
+    }
+    return -1;
+}
+}  // namespace
+
+extern "C" int irgan_resample_table(int32_t kind, int32_t n_in, int32_t p, int32_t transpose, int32_t* idx,
+                                    float* w, int32_t tmax, int32_t rows_cap) {
+    // forward: rows = output coordinates; transpose: rows = input coordinates (adjoint map)
+    int n_out_fwd = axis_map(kind, n_in, p, [](int, int, float) { return 0; });
+    if (n_out_fwd < 0) return -IRGAN_EINVAL;
+    const int rows = transpose ? n_in : n_out_fwd;
+    if (rows > rows_cap) return -IRGAN_EINVAL;
+    for (long i = 0; i < (long)rows * tmax; ++i) { idx[i] = 0; w[i] = 0.f; }
+    Tab t{rows, tmax, idx, w};
+    int rc = axis_map(kind, n_in, p, [&](int o, int i, float wt) {
+        return transpose ? t.add(i, o, wt) : t.add(o, i, wt);
+    });
+    return rc < 0 ? -IRGAN_EUNSUPPORTED : rows;
 }
 
-extern "C" int irgan_blur_down_bwd(const void* dy, int32_t dt, int32_t N, int32_t H, int32_t W, int32_t C,
-                                   int32_t lddy, int32_t dyoff, void* dx, int32_t dxdt, int32_t lddx, int32_t dxoff,
-                                   irgan_stream_t s) {
-    const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
-    long total = (long)N * H * W * C;
-    RS_CHECK(total);
-    blur_down_bwd_kernel<<<nblocks(total), TPB, 0, (hipStream_t)s>>>(dy, dt, H, W, C, lddy, dyoff, dx, dxdt, lddx,
-                                                                     dxoff, Ho, Wo, total);
-    IRGAN_LAUNCH_CHECK();
-    return 0;
-}
-
-static float up_scale(int n) { return n > 1 ? (float)(n - 1) / (float)(2 * n - 1) : 0.f; }
-
-extern "C" int irgan_upsample_fwd(const void* x, int32_t dt, int32_t N, int32_t H, int32_t W, int32_t C, int32_t ldx,
-                                  int32_t xoff, void* y, int32_t ldy, int32_t yoff, irgan_stream_t s) {
-    long total = (long)N * 4 * H * W * C;
-    RS_CHECK(total);
-    upsample_fwd_kernel<<<nblocks(total), TPB, 0, (hipStream_t)s>>>(x, dt, H, W, C, ldx, xoff, y, ldy, yoff,
-                                                                    up_scale(H), up_scale(W), total);
-    IRGAN_LAUNCH_CHECK();
-    return 0;
-}
-
-extern "C" int irgan_upsample_bwd(const void* dy, int32_t dt, int32_t N, int32_t H, int32_t W, int32_t C,
-                                  int32_t lddy, int32_t dyoff, float* work, void* dx, int32_t dxdt, int32_t lddx,
-                                  int32_t dxoff, int32_t accumulate, irgan_stream_t s) {
-    long t1 = (long)N * 4 * H * W * C, t2 = (long)N * H * W * C;
-    RS_CHECK(t2);
-    upsample_bwd_blur_kernel<<<nblocks(t1), TPB, 0, (hipStream_t)s>>>(dy, dt, 2 * H, 2 * W, C, lddy, dyoff, work, t1);
-    upsample_bwd_bil_kernel<<<nblocks(t2), TPB, 0, (hipStream_t)s>>>(work, H, W, C, up_scale(H), up_scale(W), dx, dxdt,
-                                                                     lddx, dxoff, accumulate, t2);
-    IRGAN_LAUNCH_CHECK();
-    return 0;
-}
-
-extern "C" int irgan_reflect_fold(const float* dxpad, int32_t N, int32_t H, int32_t W, int32_t C, int32_t p, void* dx,
-                                  int32_t dxdt, int32_t lddx, int32_t dxoff, int32_t accumulate, irgan_stream_t s) {
-    long total = (long)N * H * W * C;
-    RS_CHECK(total);
-    reflect_fold_kernel<<<nblocks(total), TPB, 0, (hipStream_t)s>>>(dxpad, H, W, C, p, dx, dxdt, lddx, dxoff,
-                                                                    accumulate, total);
+extern "C" int irgan_sep_resample(const void* in, int32_t in_dtype, int32_t N, int32_t Hin, int32_t Win, int32_t C,
+                                  int32_t ldi, int32_t offi, void* out, int32_t out_dtype, int32_t Hout, int32_t Wout,
+                                  int32_t ldo, int32_t offo, const int32_t* ty, const float* wy, const int32_t* tx,
+                                  const float* wx, int32_t T, int32_t accumulate, irgan_stream_t s) {
+    const bool vec = (C % 8 == 0) && (ldi % 8 == 0) && (offi % 8 == 0) && (ldo % 8 == 0) && (offo % 8 == 0);
+    const int VW = vec ? 8 : 1;
+    long total = (long)N * Hout * Wout * (C / VW);
+    if (total <= 0) return 0;
+    int nb = (int)std::max<long>(1, std::min<long>((total + TPB - 1) / TPB, 16384));
+    if (vec)
+        sep_kernel<8><<<nb, TPB, 0, (hipStream_t)s>>>(in, in_dtype, Hin, Win, C, ldi, offi, out, out_dtype, Hout, Wout,
+                                                      ldo, offo, ty, wy, tx, wx, T, accumulate, total);
+    else
+        sep_kernel<1><<<nb, TPB, 0, (hipStream_t)s>>>(in, in_dtype, Hin, Win, C, ldi, offi, out, out_dtype, Hout, Wout,
+                                                      ldo, offo, ty, wy, tx, wx, T, accumulate, total);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }

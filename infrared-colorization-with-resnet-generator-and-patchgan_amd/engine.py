@@ -347,7 +347,7 @@ class GeneratorEngine:
             wg(self.up2_up, "up2_up", dy2, a3)
             ops.conv_fwd(self.up2_up, dy2, da3, bias=False)
         else:
-            ops.upsample_bwd(dy2, da3, g.flat("up_work", B * H * W * c1))
+            ops.upsample_bwd(dy2, da3)
         # up1_conv
         self.norms["up1"].bwd(g, da3, Feat(g.d["z3"]), ACT_RELU, da3, db=S.krsc("up1_conv.0.bias", G))
         wg(self.up1, "up1_conv.0", cat1, da3)
@@ -362,7 +362,7 @@ class GeneratorEngine:
             wg(self.up1_up, "up1_up", dy1, h9)
             ops.conv_fwd(self.up1_up, dy1, dh, bias=False)
         else:
-            ops.upsample_bwd(dy1, dh, g.flat("up_work", B * H * W * c1))
+            ops.upsample_bwd(dy1, dh)
         # resblocks, reversed: dh holds d h_{b+1}; becomes d h_b in place
         dt_ = Feat(g.get("dtmp", (B, H2, W2, c2), T))
         for b in reversed(range(self.n_blocks)):

@@ -33,6 +33,41 @@ def P(t):
     return ctypes.c_void_p(0 if t is None else t.data_ptr())
 
 
+class LaunchTimer:
+    """Optional HIP-event timing of tagged conv launches (bench.py's live
+    roofline).  Events are recorded on the launching stream around each launch."""
+
+    def __init__(self, tags):
+        self.tags = set(tags)
+        self.pending = []
+        self.enabled = False
+
+    def wrap(self, tag, fn):
+        if not self.enabled or tag not in self.tags:
+            return fn()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        out = fn()
+        b.record()
+        self.pending.append((tag, a, b))
+        return out
+
+    def summary(self):
+        torch.cuda.synchronize()
+        agg = {}
+        for tag, a, b in self.pending:
+            n, t = agg.get(tag, (0, 0.0))
+            agg[tag] = (n + 1, t + a.elapsed_time(b))
+        return {k: (n, t / n) for k, (n, t) in agg.items()}  # (launches, mean ms)
+
+
+TIMER = LaunchTimer(())
+
+
+def conv_tag(kind, spec, x_hw):
+    return f"{kind}:{spec.cin}x{spec.cout}k{spec.k}s{spec.stride}@{x_hw[0]}x{x_hw[1]}"
+
+
 class Feat:
     """NHWC channel slice: element (p, c) at t.view(-1)[p*ld + off + c]."""
     __slots__ = ("t", "off", "C")
@@ -138,8 +173,9 @@ def conv_fwd(pc: PackedConv, x: Feat, y: Feat, act=ACT_NONE, bias=True, accumula
               c0y=-s.pad, c0x=-s.pad, pad_mode=s.mode, act=act, accumulate=int(accumulate), dtype=pc.dtype,
               out_dtype=y.dt, mask_act=mask_act, ldm=mask.ld if mask else 0, moff=mask.off if mask else 0)
     assert x.dt == pc.dtype
-    _lib.call("irgan_conv_fwd", ctypes.byref(d), x.ptr, P(pc.fwd), P(pc.bias if bias else None), y.ptr,
-              mask.ptr if mask else None, stream())
+    TIMER.wrap(conv_tag("fwd", s, (x.H, x.W)), lambda: _lib.call(
+        "irgan_conv_fwd", ctypes.byref(d), x.ptr, P(pc.fwd), P(pc.bias if bias else None), y.ptr,
+        mask.ptr if mask else None, stream()))
 
 
 def conv_dgrad(pc: PackedConv, dy: Feat, dx: Feat, accumulate=False, mask: Feat = None, mask_act=0,
@@ -158,10 +194,10 @@ def conv_dgrad(pc: PackedConv, dy: Feat, dx: Feat, accumulate=False, mask: Feat 
                   ldy=tgt.ld, yoff=0, OH=Hp, OW=Wp, omy=1, ooy=0, omx=1, oox=0, KH=ay, KW=ax, sy=1, sx=1,
                   c0y=c0y, c0x=c0x, pad_mode=PAD_ZERO, act=0, accumulate=0, dtype=pc.dtype, out_dtype=F32,
                   mask_act=0, ldm=0, moff=0)
-        _lib.call("irgan_conv_fwd", ctypes.byref(d), dy.ptr, P(buf), None, tgt.ptr, None, stream())
+        TIMER.wrap(conv_tag("dgrad", s, (dx.H, dx.W)), lambda: _lib.call(
+            "irgan_conv_fwd", ctypes.byref(d), dy.ptr, P(buf), None, tgt.ptr, None, stream()))
         assert mask is None
-        _lib.call("irgan_reflect_fold", tgt.ptr, dx.N, dx.H, dx.W, s.cin, p, dx.ptr, dx.dt, dx.ld, dx.off,
-                  int(accumulate), stream())
+        reflect_fold(tgt, dx, p, accumulate)
         return
     st = s.stride
     for (py, _, ay, c0y), (px, _, ax, c0x), buf in pc.dg:
@@ -186,7 +222,8 @@ def conv_wgrad(spec: ConvSpec, x: Feat, dy: Feat, dw: torch.Tensor, dtype: int, 
               yoff=dy.off, OH=Ho, OW=Wo, omy=1, ooy=0, omx=1, oox=0, KH=spec.k, KW=spec.k, sy=spec.stride,
               sx=spec.stride, c0y=-spec.pad, c0x=-spec.pad, pad_mode=spec.mode, act=0, accumulate=1, dtype=dtype,
               out_dtype=F32, mask_act=0, ldm=0, moff=0)
-    _lib.call("irgan_conv_wgrad", ctypes.byref(d), x.ptr, dy.ptr, P(dw), splitk, stream())
+    TIMER.wrap(conv_tag("wgrad", spec, (x.H, x.W)), lambda: _lib.call(
+        "irgan_conv_wgrad", ctypes.byref(d), x.ptr, dy.ptr, P(dw), splitk, stream()))
 
 
 # ----------------------------------------------------------------------------
@@ -222,22 +259,63 @@ def channel_sum(g: Feat, db: torch.Tensor):
 # resampling / elementwise
 # ----------------------------------------------------------------------------
 
+RS_DOWN, RS_UP, RS_PAD = 0, 1, 2
+TMAX = 8
+_TABLES = {}
+
+
+def resample_table(kind, n_in, p=0, transpose=False, device=None):
+    """Device (idx, w, rows) per-axis table of a separable resampling map, built by
+    the C ABI on the host (irgan_resample_table) and cached."""
+    import numpy as np
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    key = (kind, n_in, p, bool(transpose), dev)
+    t = _TABLES.get(key)
+    if t is None:
+        cap = 2 * n_in + 2 * p + 8
+        idx = np.zeros(cap * TMAX, np.int32)
+        w = np.zeros(cap * TMAX, np.float32)
+        rows = _lib.load().irgan_resample_table(kind, n_in, p, int(transpose), idx.ctypes.data_as(ctypes.c_void_p),
+                                                  w.ctypes.data_as(ctypes.c_void_p), TMAX, cap)
+        if rows < 0:
+            raise _lib.IrganError(f"irgan_resample_table({kind}, {n_in}, {p}) failed: {rows}")
+        t = (torch.from_numpy(idx[:rows * TMAX].copy()).to(dev), torch.from_numpy(w[:rows * TMAX].copy()).to(dev),
+             rows)
+        _TABLES[key] = t
+    return t
+
+
+def sep_resample(x: Feat, y: Feat, ytab, xtab, accumulate=False):
+    (ty, wy, ry), (tx, wx, rx) = ytab, xtab
+    assert (ry, rx) == (y.H, y.W) and x.C == y.C and x.N == y.N, "sep_resample shape mismatch"
+    _lib.call("irgan_sep_resample", x.ptr, x.dt, x.N, x.H, x.W, x.C, x.ld, x.off, y.ptr, y.dt, y.H, y.W, y.ld, y.off,
+              P(ty), P(wy), P(tx), P(wx), TMAX, int(accumulate), stream())
+
+
 def blur_down(x: Feat, y: Feat):
-    _lib.call("irgan_blur_down_fwd", x.ptr, x.dt, x.N, x.H, x.W, x.C, x.ld, x.off, y.ptr, y.ld, y.off, stream())
+    """Downsample (ir:269-310)."""
+    sep_resample(x, y, resample_table(RS_DOWN, x.H), resample_table(RS_DOWN, x.W))
 
 
-def blur_down_bwd(dy: Feat, dx: Feat):
-    _lib.call("irgan_blur_down_bwd", dy.ptr, dy.dt, dx.N, dx.H, dx.W, dx.C, dy.ld, dy.off, dx.ptr, dx.dt, dx.ld,
-              dx.off, stream())
+def blur_down_bwd(dy: Feat, dx: Feat, accumulate=False):
+    sep_resample(dy, dx, resample_table(RS_DOWN, dx.H, transpose=True), resample_table(RS_DOWN, dx.W, transpose=True),
+                 accumulate)
 
 
 def upsample(x: Feat, y: Feat):
-    _lib.call("irgan_upsample_fwd", x.ptr, x.dt, x.N, x.H, x.W, x.C, x.ld, x.off, y.ptr, y.ld, y.off, stream())
+    """UpsampleAA (ir:313-355)."""
+    sep_resample(x, y, resample_table(RS_UP, x.H), resample_table(RS_UP, x.W))
 
 
-def upsample_bwd(dy: Feat, dx: Feat, work: torch.Tensor, accumulate=False):
-    _lib.call("irgan_upsample_bwd", dy.ptr, dy.dt, dx.N, dx.H, dx.W, dx.C, dy.ld, dy.off, P(work), dx.ptr, dx.dt,
-              dx.ld, dx.off, int(accumulate), stream())
+def upsample_bwd(dy: Feat, dx: Feat, work=None, accumulate=False):
+    sep_resample(dy, dx, resample_table(RS_UP, dx.H, transpose=True), resample_table(RS_UP, dx.W, transpose=True),
+                 accumulate)
+
+
+def reflect_fold(dxpad: Feat, dx: Feat, p: int, accumulate=False):
+    """Backward of nn.ReflectionPad2d(p): dx[q] = sum over padded u with reflect(u-p) = q."""
+    sep_resample(dxpad, dx, resample_table(RS_PAD, dx.H, p, transpose=True),
+                 resample_table(RS_PAD, dx.W, p, transpose=True), accumulate)
 
 
 def maxpool(x: Feat, y: Feat):

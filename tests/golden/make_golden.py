@@ -44,6 +44,7 @@ VARIANTS = {
     # smooth objective: drops the sign()-based terms (perceptual L1, pixel L1, TV)
     # whose discontinuities make G weight grads ill-conditioned (see make_variant)
     "s32_smooth": (32, 32, 2, False, False, {"lambda_perc": 0.0, "lambda_L1": 0.0, "lambda_tv": 0.0}),
+    "s64_smooth": (64, 64, 2, False, False, {"lambda_perc": 0.0, "lambda_L1": 0.0, "lambda_tv": 0.0}),
 }
 LAMBDA_ORDER = ("lambda_L1", "lambda_perc", "lambda_tv", "lambda_ssim", "lambda_gan")
 
