@@ -12,6 +12,12 @@
 // words feed four v_mfma_f32_16x16x4_f32 with k = 4*(lane>>4) + s, the same
 // permutation on both operands, so the K sum is complete (exact fp32 FMA chain).
 #include "common.h"
+#include <stdlib.h>
+
+extern "C" int irgan_conv_fwd_glds(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
+                                   const void* mask, hipStream_t st);
+extern "C" int irgan_conv_wgrad_glds(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, int splitk,
+                                     hipStream_t st);
 
 namespace {
 
@@ -461,6 +467,10 @@ int launch_fwd(const irgan_conv_desc* d, const void* x, const void* w, const flo
     const long M = (long)d->N * d->Ho * d->Wo;
     if (M <= 0 || d->Cout <= 0) return 0;
     const bool fast = (d->Cin % BKE == 0) && (d->ldx % EPC == 0) && (d->xoff % EPC == 0);
+    if constexpr (sizeof(T) == 2) {
+        static const bool use_glds = !getenv("IRGAN_NO_GLDS");
+        if (fast && use_glds) return irgan_conv_fwd_glds(d, x, w, bias, y, mask, st);
+    }
     const bool wide = d->Cout > 64;
     dim3 grid(irgan_cdiv(M, 128), irgan_cdiv(d->Cout, wide ? 128 : 64));
     const T* xp = (const T*)x;
@@ -489,6 +499,11 @@ int launch_wgrad(const irgan_conv_desc* d, const void* x, const void* dy, float*
     if (P <= 0) return 0;
     const bool fa = (d->Cout % EPC == 0) && (d->ldy % EPC == 0) && (d->yoff % EPC == 0);
     const bool fb = (d->Cin % 64 == 0) && (d->ldx % EPC == 0) && (d->xoff % EPC == 0);
+    if constexpr (sizeof(T) == 2) {
+        static const bool use_glds = !getenv("IRGAN_NO_GLDS");
+        if (use_glds && fb && d->Cout % 64 == 0 && d->ldy % 8 == 0 && d->yoff % 8 == 0)
+            return irgan_conv_wgrad_glds(d, x, dy, dw, splitk, st);
+    }
     const int BM = d->Cout > 64 ? 128 : 64;
     const int tiles = irgan_cdiv(d->Cout, BM) * irgan_cdiv(K, 64);
     if (splitk <= 0) {  // aim at ~4 workgroups per CU over 256 CUs

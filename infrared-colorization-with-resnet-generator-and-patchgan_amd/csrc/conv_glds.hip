@@ -1,0 +1,393 @@
+// bf16 implicit-GEMM convolution, LDS-DMA pipeline (forward and backward-data).
+//
+// 512 threads = 8 waves (4 x 2), block tile 256 pixels x BN output channels,
+// K-tile = 64 bf16 (one 128-byte channel run of one tap).  Operands move
+// HBM/L2 -> LDS with global_load_lds (16 B per lane, no VGPR staging) into a
+// 3-stage ring: tile k+2 is in flight while tile k is multiplied, with one
+// counted s_waitcnt vmcnt + one raw s_barrier per K-tile.  Zero padding and
+// tails read a zero page, reflect padding is folded into the source address.
+// The LDS image keeps the 16-byte-chunk XOR swizzle (chunk ^ (row & 7)) of the
+// register-staged kernel; with LDS-DMA the permutation is applied to the
+// per-lane SOURCE chunk so the destination stays lane-linear.
+#include "common.h"
+
+namespace {
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) const void gbl_cvoid;
+
+IRGAN_HD int lds_off(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+
+IRGAN_HD void glds16(const void* src, char* lds_base) {
+    __builtin_amdgcn_global_load_lds((gbl_cvoid*)src, (lds_void*)lds_base, 16, 0, 0);
+}
+
+template <int N>
+IRGAN_HD void wait_vmcnt() {
+    static_assert(N >= 0 && N <= 8, "vmcnt");
+    if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+}
+
+IRGAN_HD float act_fn(float v, int act) {
+    if (act == IRGAN_ACT_RELU) return v > 0.f ? v : 0.f;
+    if (act == IRGAN_ACT_LRELU) return v > 0.f ? v : 0.2f * v;
+    if (act == IRGAN_ACT_TANH) return tanhf(v);
+    return v;
+}
+
+template <int BN>
+__global__ __launch_bounds__(512, 2) void conv_fwd_glds_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
+                                                               const bf16_t* __restrict__ w,
+                                                               const float* __restrict__ bias, void* __restrict__ y,
+                                                               const void* __restrict__ mask,
+                                                               const bf16_t* __restrict__ zero) {
+    constexpr int BM = 256, STAGES = 3;
+    constexpr int ABYTES = BM * 128, STAGE = ABYTES + BN * 128;
+    constexpr int MI = 4, NJ = BN / 32;  // wave tile 64 x BN/2
+    constexpr int AU = BM / 64, BU = BN / 64;  // 1 KiB glds pieces per wave per tile
+    __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid >> 1, wn = wid & 1;
+    const int HoWo = d.Ho * d.Wo;
+    const long M = (long)d.N * HoWo;
+    const int K = d.KH * d.KW * d.Cin;
+    const long m0 = (long)blockIdx.x * BM;
+    const int n0 = blockIdx.y * BN;
+    const int sub = lane >> 3;
+    const int chunk = (lane & 7) ^ sub;  // source chunk for this lane's LDS slot (row & 7 == sub)
+
+    int a_nb[AU], a_iy[AU], a_ix[AU];
+#pragma unroll
+    for (int u = 0; u < AU; ++u) {
+        const long m = m0 + (wid * AU + u) * 8 + sub;
+        if (m < M) {
+            const int mm = (int)m;
+            const int n = mm / HoWo, r = mm - n * HoWo, i = r / d.Wo, j = r - i * d.Wo;
+            a_nb[u] = n * d.H;
+            a_iy[u] = i * d.sy + d.c0y;
+            a_ix[u] = j * d.sx + d.c0x;
+        } else {
+            a_nb[u] = -1;
+            a_iy[u] = 0;
+            a_ix[u] = 0;
+        }
+    }
+    const bf16_t* b_src[BU];
+#pragma unroll
+    for (int u = 0; u < BU; ++u) {
+        const int co = n0 + (wid * BU + u) * 8 + sub;
+        b_src[u] = co < d.Cout ? w + (long)co * K + chunk * 8 : nullptr;
+    }
+    const bool reflect = d.pad_mode == IRGAN_PAD_REFLECT;
+
+    auto issue = [&](int kt, int stage) {
+        const int k0 = kt * 64;
+        const int tap = k0 / d.Cin, cin0 = k0 - tap * d.Cin;
+        const int ty = tap / d.KW, tx = tap - ty * d.KW;
+        const int coff = d.xoff + cin0 + chunk * 8;
+        char* sA = smem + stage * STAGE;
+#pragma unroll
+        for (int u = 0; u < AU; ++u) {
+            int qy = a_iy[u] + ty, qx = a_ix[u] + tx;
+            if (reflect) {  // wave-uniform
+                qy = reflect_idx(qy, d.H);
+                qx = reflect_idx(qx, d.W);
+            }
+            // branch-free validity (bitwise, no short circuit) -> one v_cndmask on the address
+            const bool ok = (a_nb[u] >= 0) & ((unsigned)qy < (unsigned)d.H) & ((unsigned)qx < (unsigned)d.W);
+            const long off = ((long)(a_nb[u] + qy) * d.W + qx) * d.ldx;
+            const bf16_t* src = ok ? x + off + coff : zero;
+            glds16(src, sA + (wid * AU + u) * 1024);
+        }
+#pragma unroll
+        for (int u = 0; u < BU; ++u) {
+            const bf16_t* src = b_src[u] ? b_src[u] + k0 : zero;
+            glds16(src, sA + ABYTES + (wid * BU + u) * 1024);
+        }
+    };
+
+    f32x4 acc[MI][NJ];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nk = K / 64;
+    issue(0, 0);
+    if (nk > 1) issue(1, 1);
+    for (int kt = 0; kt < nk; ++kt) {
+        if (kt + 1 < nk) wait_vmcnt<AU + BU>();
+        else wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        if (kt + 2 < nk) issue(kt + 2, (kt + 2) % STAGES);
+        const char* A = smem + (kt % STAGES) * STAGE;
+        const char* B = A + ABYTES;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            uint4 af[MI], bfr[NJ];
+            const int ch = h * 4 + (lane >> 4);
+#pragma unroll
+            for (int i = 0; i < MI; ++i) af[i] = *(const uint4*)(A + lds_off(wm * 64 + i * 16 + (lane & 15), ch));
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) bfr[j] = *(const uint4*)(B + lds_off(wn * (BN / 2) + j * 16 + (lane & 15), ch));
+#pragma unroll
+            for (int i = 0; i < MI; ++i)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[i]),
+                                                                        __builtin_bit_cast(bf16x8_t, bfr[j]),
+                                                                        acc[i][j], 0, 0, 0);
+        }
+    }
+
+    // epilogue: C[row = (lane>>4)*4 + r][col = lane & 15] of each 16x16 fragment
+    const bool out_f32 = d.out_dtype == IRGAN_F32;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const long m = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+            if (m >= M) continue;
+            const int mm = (int)m;
+            const int n = mm / HoWo, rr = mm - n * HoWo, ii = rr / d.Wo, jj = rr - ii * d.Wo;
+            const long pix = ((long)n * d.OH + ii * d.omy + d.ooy) * d.OW + jj * d.omx + d.oox;
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int co = n0 + wn * (BN / 2) + j * 16 + (lane & 15);
+                if (co >= d.Cout) continue;
+                float v = acc[i][j][r] + (bias ? bias[co] : 0.f);
+                v = act_fn(v, d.act);
+                if (mask) {
+                    const float mv = bf2f(((const bf16_t*)mask)[pix * d.ldm + d.moff + co]);
+                    v *= mv > 0.f ? 1.f : (d.mask_act == 2 ? 0.2f : 0.f);
+                }
+                const long off = pix * d.ldy + d.yoff + co;
+                if (out_f32) {
+                    float* yp = (float*)y;
+                    yp[off] = d.accumulate ? yp[off] + v : v;
+                } else {
+                    bf16_t* yp = (bf16_t*)y;
+                    yp[off] = f2bf(d.accumulate ? bf2f(yp[off]) + v : v);
+                }
+            }
+        }
+    }
+}
+
+}  // namespace
+
+// zero page for padded / out-of-range glds sources (4 KiB, device global)
+__device__ __attribute__((aligned(4096))) bf16_t g_irgan_zero_page[2048];
+
+extern "C" int irgan_conv_fwd_glds(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
+                                   const void* mask, hipStream_t st) {
+    const long M = (long)d->N * d->Ho * d->Wo;
+    if (M <= 0 || d->Cout <= 0) return 0;
+    static bf16_t* zero = nullptr;  // immutable after first lookup
+    if (!zero && hipGetSymbolAddress((void**)&zero, HIP_SYMBOL(g_irgan_zero_page)) != hipSuccess)
+        return IRGAN_EUNSUPPORTED;
+    if (d->Cout > 64) {
+        dim3 grid(irgan_cdiv(M, 256), irgan_cdiv(d->Cout, 128));
+        conv_fwd_glds_kernel<128><<<grid, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, y, mask, zero);
+    } else {
+        dim3 grid(irgan_cdiv(M, 256), irgan_cdiv(d->Cout, 64));
+        conv_fwd_glds_kernel<64><<<grid, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, y, mask, zero);
+    }
+    IRGAN_LAUNCH_CHECK();
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// bf16 backward-weight, LDS-DMA + transposed LDS reads.
+//   dW[co][tap][ci] += sum_p dY[p][co] * X[q(p, tap)][ci]
+// Both operands arrive pixel-major (NHWC rows of channels).  They are DMA'd
+// into LDS in that natural layout (one row = the tile's channels of one
+// pixel) and the MFMA fragments, which need 8 consecutive PIXELS per lane, are
+// read with ds_read_b64_tr_b16 (4 pixel-rows x 16 channels per 16-lane group,
+// delivered column-major).  Rows are XOR-swizzled in 16-byte chunks so the
+// transposed reads of 8 rows per 32-lane half hit 8 distinct bank groups.
+// 512 threads = 8 waves (4 co x 2 ci), tile 128 co x 128 ci (or 64), K-tile 64
+// pixels, 3-stage ring, split-K over pixels with one fp32 atomic per element.
+// ---------------------------------------------------------------------------
+namespace {
+
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+
+// chunk XOR for a pixel row r of an RB-byte LDS row
+template <int RB>
+IRGAN_HD int wg_swz(int r) {
+    if constexpr (RB == 256) return 2 * ((r & 3) | (((r >> 3) & 1) << 2));
+    else return 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1));
+}
+template <int RB>
+IRGAN_HD int wg_off(int r, int col) {  // byte offset of channel col (16-bit) in pixel row r
+    const int c16 = col >> 3, within = (col & 7) * 2;
+    return r * RB + ((c16 ^ wg_swz<RB>(r)) << 4) + within;
+}
+
+// 8 consecutive pixel rows (k0 + 8*(lane>>4) + [0,8)) of channel (m0 + (lane&15)) -> MFMA operand
+template <int RB>
+IRGAN_HD uint4 tr_frag(const char* img, int k0, int m0, int lane) {
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int r0 = k0 + 8 * g + q;
+    typedef __attribute__((address_space(3))) s16x4 lds_s4;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + wg_off<RB>(r0, m0 + 4 * p)));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + wg_off<RB>(r0 + 4, m0 + 4 * p)));
+    uint4 out;
+    __builtin_memcpy(&out, &lo, 8);
+    __builtin_memcpy((char*)&out + 8, &hi, 8);
+    return out;
+}
+
+template <int BMC, int BNC>  // co tile, ci tile (128 or 64)
+__global__ __launch_bounds__(512, 2) void conv_wgrad_glds_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
+                                                                 const bf16_t* __restrict__ dy, float* __restrict__ dw,
+                                                                 int kchunk, const bf16_t* __restrict__ zero) {
+    constexpr int KP = 64, STAGES = 3;
+    constexpr int RA = BMC * 2, RBB = BNC * 2;          // bytes per pixel row in each image
+    constexpr int ABYTES = KP * RA, STAGE = ABYTES + KP * RBB;
+    constexpr int WM = 4, WN = 2;                       // wave grid (co x ci)
+    constexpr int MI = BMC / WM / 16, NJ = BNC / WN / 16;
+    constexpr int AU = ABYTES / 1024 / 8, BU = KP * RBB / 1024 / 8;  // glds pieces per wave per tile
+    static_assert(AU >= 1 && BU >= 1, "tile");
+    __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid / WN, wn = wid % WN;
+    const int HoWo = d.Ho * d.Wo;
+    const long P = (long)d.N * HoWo;
+    const int K = d.KH * d.KW * d.Cin;
+    const int co0 = blockIdx.x * BMC, n0 = blockIdx.y * BNC;
+    const long pb = (long)blockIdx.z * kchunk;
+    const long pe = min(P, pb + kchunk);
+    if (pb >= pe) return;
+    const int tap = n0 / d.Cin, cin0 = n0 - tap * d.Cin;
+    const int ty = tap / d.KW, tx = tap - ty * d.KW;
+    const bool reflect = d.pad_mode == IRGAN_PAD_REFLECT;
+
+    // lane -> (row within a 1 KiB piece, 16-byte slot) for each image
+    constexpr int ARPP = 1024 / RA, BRPP = 1024 / RBB;  // pixel rows per piece
+    const int a_sub = lane / (RA / 16), a_slot = lane % (RA / 16);
+    const int b_sub = lane / (RBB / 16), b_slot = lane % (RBB / 16);
+
+    auto issue = [&](long p0, int stage) {
+        char* sA = smem + stage * STAGE;
+        char* sB = sA + ABYTES;
+#pragma unroll
+        for (int u = 0; u < AU; ++u) {
+            const int piece = wid * AU + u;
+            const int r = piece * ARPP + a_sub;
+            const long p = p0 + r;
+            const int c16 = a_slot ^ wg_swz<RA>(r);
+            const bool ok = p < pe;
+            const bf16_t* src = ok ? dy + p * d.ldy + d.yoff + co0 + c16 * 8 : zero;
+            glds16(src, sA + piece * 1024);
+        }
+#pragma unroll
+        for (int u = 0; u < BU; ++u) {
+            const int piece = wid * BU + u;
+            const int r = piece * BRPP + b_sub;
+            const long p = p0 + r;
+            const int c16 = b_slot ^ wg_swz<RBB>(r);
+            const int pp = (int)min(p, P - 1);
+            const int n = pp / HoWo, rr = pp - n * HoWo, i = rr / d.Wo, j = rr - i * d.Wo;
+            int qy = i * d.sy + ty + d.c0y, qx = j * d.sx + tx + d.c0x;
+            if (reflect) {
+                qy = reflect_idx(qy, d.H);
+                qx = reflect_idx(qx, d.W);
+            }
+            const bool ok = (p < pe) & ((unsigned)qy < (unsigned)d.H) & ((unsigned)qx < (unsigned)d.W);
+            const long off = (((long)n * d.H + qy) * d.W + qx) * d.ldx + d.xoff + cin0 + c16 * 8;
+            glds16(ok ? x + off : zero, sB + piece * 1024);
+        }
+    };
+
+    f32x4 acc[MI][NJ];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nk = (int)((pe - pb + KP - 1) / KP);
+    issue(pb, 0);
+    if (nk > 1) issue(pb + KP, 1);
+    for (int kt = 0; kt < nk; ++kt) {
+        if (kt + 1 < nk) wait_vmcnt<AU + BU>();
+        else wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        if (kt + 2 < nk) issue(pb + (long)(kt + 2) * KP, (kt + 2) % STAGES);
+        const char* A = smem + (kt % STAGES) * STAGE;
+        const char* B = A + ABYTES;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {  // two 32-pixel MFMA k-steps per tile
+            uint4 af[MI], bfr[NJ];
+#pragma unroll
+            for (int i = 0; i < MI; ++i) af[i] = tr_frag<RA>(A, 32 * h, wm * (BMC / WM) + i * 16, lane);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) bfr[j] = tr_frag<RBB>(B, 32 * h, wn * (BNC / WN) + j * 16, lane);
+#pragma unroll
+            for (int i = 0; i < MI; ++i)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[i]),
+                                                                        __builtin_bit_cast(bf16x8_t, bfr[j]),
+                                                                        acc[i][j], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int co = co0 + wm * (BMC / WM) + i * 16 + (lane >> 4) * 4 + r;
+            if (co >= d.Cout) continue;
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int kc = n0 + wn * (BNC / WN) + j * 16 + (lane & 15);
+                atomicAdd(dw + (long)co * K + kc, acc[i][j][r]);
+            }
+        }
+}
+
+}  // namespace
+
+extern "C" int irgan_conv_wgrad_glds(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, int splitk,
+                                     hipStream_t st) {
+    const long P = (long)d->N * d->Ho * d->Wo;
+    const int K = d->KH * d->KW * d->Cin;
+    if (P <= 0) return 0;
+    static bf16_t* zero = nullptr;
+    if (!zero && hipGetSymbolAddress((void**)&zero, HIP_SYMBOL(g_irgan_zero_page)) != hipSuccess)
+        return IRGAN_EUNSUPPORTED;
+    const int BMC = d->Cout % 128 == 0 ? 128 : 64;
+    const int BNC = d->Cin % 128 == 0 ? 128 : 64;
+    const int tiles = (d->Cout / BMC) * (K / BNC);
+    if (splitk <= 0) {
+        splitk = irgan_cdiv(512, tiles);  // ~2 blocks per CU
+        long maxs = (P + 16 * 64 - 1) / (16 * 64);  // >= 16 K-tiles per split
+        if (splitk > maxs) splitk = (int)maxs;
+        if (splitk < 1) splitk = 1;
+    }
+    long kc = (P + splitk - 1) / splitk;
+    kc = (kc + 63) / 64 * 64;
+    splitk = (int)((P + kc - 1) / kc);
+    dim3 g(d->Cout / BMC, K / BNC, splitk);
+    const bf16_t* xp = (const bf16_t*)x;
+    const bf16_t* dp = (const bf16_t*)dy;
+    if (BMC == 128 && BNC == 128) conv_wgrad_glds_kernel<128, 128><<<g, 512, 0, st>>>(*d, xp, dp, dw, (int)kc, zero);
+    else if (BMC == 128) conv_wgrad_glds_kernel<128, 64><<<g, 512, 0, st>>>(*d, xp, dp, dw, (int)kc, zero);
+    else if (BNC == 128) conv_wgrad_glds_kernel<64, 128><<<g, 512, 0, st>>>(*d, xp, dp, dw, (int)kc, zero);
+    else conv_wgrad_glds_kernel<64, 64><<<g, 512, 0, st>>>(*d, xp, dp, dw, (int)kc, zero);
+    IRGAN_LAUNCH_CHECK();
+    return 0;
+}

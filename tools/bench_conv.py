@@ -1,0 +1,43 @@
+"""Microbenchmark of the conv kernels on the training shapes (bf16), HIP events."""
+import sys, os, json
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
+import torch
+from conftest import pkg
+ops = pkg().ops
+DEV = "cuda"
+B = 16
+CASES = [  # name, cin, cout, k, s, p, mode, H
+    ("res3x3_256@64", 256, 256, 3, 1, 1, 1, 64),
+    ("down1_64-128@256", 64, 128, 3, 1, 1, 0, 256),
+    ("up2_192-64@256", 192, 64, 3, 1, 1, 0, 256),
+    ("up1_384-128@128", 384, 128, 3, 1, 1, 0, 128),
+    ("D2_128-256s2@64", 128, 256, 4, 2, 1, 0, 64),
+    ("D3_256-512s1@32", 256, 512, 4, 1, 1, 0, 32),
+]
+def t(fn, it=20):
+    fn(); torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(it): fn()
+    b.record(); torch.cuda.synchronize()
+    return a.elapsed_time(b) / it
+res = {}
+for name, cin, cout, k, s, p, mode, H in CASES:
+    spec = ops.ConvSpec(cin, cout, k, s, p, mode)
+    w = torch.randn(cout * k * k * cin, device=DEV) * 0.05
+    pc = ops.PackedConv(spec, w, torch.zeros(cout, device=DEV), ops.BF16); pc.pack()
+    x = torch.randn(B, H, H, cin, device=DEV).bfloat16()
+    Ho, Wo = spec.out_hw(H, H)
+    y = torch.empty(B, Ho, Wo, cout, device=DEV, dtype=torch.bfloat16)
+    dy = torch.randn(B, Ho, Wo, cout, device=DEV).bfloat16()
+    dx = torch.empty(B, H, H, cin, device=DEV, dtype=torch.bfloat16)
+    pad = torch.empty(B * (H + 2 * p) ** 2 * cin, device=DEV)
+    dw = torch.zeros(cout * k * k * cin, device=DEV)
+    flop = 2.0 * B * Ho * Wo * cout * cin * k * k
+    tf = t(lambda: ops.conv_fwd(pc, ops.Feat(x), ops.Feat(y)))
+    td = t(lambda: ops.conv_dgrad(pc, ops.Feat(dy), ops.Feat(dx), pad_buf=pad))
+    tw = t(lambda: ops.conv_wgrad(spec, ops.Feat(x), ops.Feat(dy), dw, ops.BF16))
+    res[name] = {k2: (round(v, 4), round(flop / v / 1e9, 1)) for k2, v in (("fwd", tf), ("dgrad", td), ("wgrad", tw))}
+    print(name, "ms/TFLOPs", res[name], flush=True)
+print(json.dumps(res))
