@@ -70,14 +70,19 @@ int irgan_conv_fwd(const irgan_conv_desc* d, const void* x, const void* w,
 int irgan_conv_wgrad(const irgan_conv_desc* d, const void* x, const void* dy,
                      float* dw, int32_t splitk, irgan_stream_t s);
 
-/* Weight re-pack: dst[co'][a][b][ci'] (dtype) from the fp32 KRSC master
- * src[Cout][KH][KW][Cin].  transpose=0: plain cast (a=ky, b=kx, co'=co, ci'=ci).
- * transpose=1: dst[ci][a][b][co] = src[co][tyr + s*(Ay-1-a)][txr + s*(Ax-1-b)][ci]
- * (flip / phase selection for backward-data and transposed conv).  A
- * ConvTranspose2d weight [Cin][Cout][K][K] is handed over as KRSC of its own. */
+/* Weight re-pack: dst rows [R][Kp] (dtype) from the fp32 KRSC master
+ * src[Cout][KH][KW][Cin], Kp = roundup(taps*Cp, kalign), taps and channels
+ * zero-padded (Cp = max(cpad, channels)).  transpose=0: R = Cout, row =
+ * [ky][kx][ci] (plain cast).  transpose=1: R = Cin, row = [a][b][co] with
+ * (ky, kx) = (tyr + s*(Ay-1-a), txr + s*(Ax-1-b)) -- the flipped / per-phase
+ * weights of backward-data and ConvTranspose2d.  A ConvTranspose2d weight
+ * [Cin][Cout][K][K] is handed over as the KRSC master of the conv it transposes.
+ * Narrow inputs (1/3/4 channels) are zero-padded to cpad = 8 so the bf16
+ * LDS-DMA conv takes 64/8 = 8 taps per K-tile (kalign = 64). */
 int irgan_weight_pack(const float* src, void* dst, int32_t dtype, int32_t Cout, int32_t KH,
                       int32_t KW, int32_t Cin, int32_t transpose, int32_t s, int32_t tyr,
-                      int32_t Ay, int32_t txr, int32_t Ax, irgan_stream_t st);
+                      int32_t Ay, int32_t txr, int32_t Ax, int32_t cpad, int32_t kalign,
+                      irgan_stream_t st);
 
 /* ---- InstanceNorm (ir:154-165), per-(n,c) over H*W, eps 1e-5, no affine ---- */
 /* mr[n][c] = {mean, rstd}; work = 2*N*C doubles of scratch (zeroed inside). */
@@ -103,9 +108,10 @@ int irgan_in_bwd_apply(const void* dy, int32_t dy_dtype, int32_t lddy, int32_t d
                        int32_t N, int32_t HW, int32_t C, const float* mr, const float* red,
                        void* dx, int32_t dx_dtype, int32_t lddx, int32_t dxoff, float* db,
                        irgan_stream_t s);
-/* db[c] += sum over pixels of g[p][c] (bias gradient), g slice (dtype, ld, off). */
+/* db[c] += sum over pixels of g[p][c] (bias gradient), g slice (dtype, ld, off).
+ * work: 128*C doubles of scratch. */
 int irgan_channel_sum(const void* g, int32_t dtype, int32_t P, int32_t C, int32_t ld,
-                      int32_t off, float* db, irgan_stream_t s);
+                      int32_t off, float* db, double* work, irgan_stream_t s);
 
 /* ---- resampling (ir:269-355 and reflection-pad backward) ---- */
 /* Per-axis tables of a separable resampling map (host only, no GPU work).

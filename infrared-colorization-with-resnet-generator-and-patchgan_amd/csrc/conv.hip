@@ -439,22 +439,28 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const irgan_conv_desc d
         }
 }
 
+// dst rows: [R][Kp] with Kp = roundup(taps*Cp, kalign) (taps and channels zero-padded)
+//   transpose=0: R = Cout, taps = KH*KW, channel = ci (Cp >= Cin)
+//   transpose=1: R = Cin,  taps = Ay*Ax, channel = co (Cp >= Cout), flipped / phase-selected
 template <typename T>
 __global__ void weight_pack_kernel(const float* __restrict__ src, T* __restrict__ dst, int Cout, int KH, int KW,
-                                   int Cin, int transpose, int s, int tyr, int Ay, int txr, int Ax) {
-    long total = transpose ? (long)Cin * Ay * Ax * Cout : (long)Cout * KH * KW * Cin;
+                                   int Cin, int transpose, int s, int tyr, int Ay, int txr, int Ax, int Cp, int Kp) {
+    const int R = transpose ? Cin : Cout;
+    const int taps = transpose ? Ay * Ax : KH * KW;
+    const int Cr = transpose ? Cout : Cin;
+    long total = (long)R * Kp;
     for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
-        float v;
-        if (!transpose) {
-            v = src[idx];
-        } else {
-            long t = idx;
-            int co = (int)(t % Cout); t /= Cout;
-            int b = (int)(t % Ax); t /= Ax;
-            int a = (int)(t % Ay); t /= Ay;
-            int ci = (int)t;
-            int ky = tyr + s * (Ay - 1 - a), kx = txr + s * (Ax - 1 - b);
-            v = src[(((long)co * KH + ky) * KW + kx) * Cin + ci];
+        const int row = (int)(idx / Kp), k = (int)(idx - (long)row * Kp);
+        const int tap = k / Cp, c = k - tap * Cp;
+        float v = 0.f;
+        if (tap < taps && c < Cr) {
+            if (!transpose) {
+                v = src[((long)row * KH * KW + tap) * Cin + c];
+            } else {
+                const int a = tap / Ax, b = tap - a * Ax;
+                const int ky = tyr + s * (Ay - 1 - a), kx = txr + s * (Ax - 1 - b);
+                v = src[(((long)c * KH + ky) * KW + kx) * Cin + row];
+            }
         }
         dst[idx] = from_f<T>(v);
     }
@@ -469,7 +475,8 @@ int launch_fwd(const irgan_conv_desc* d, const void* x, const void* w, const flo
     const bool fast = (d->Cin % BKE == 0) && (d->ldx % EPC == 0) && (d->xoff % EPC == 0);
     if constexpr (sizeof(T) == 2) {
         static const bool use_glds = !getenv("IRGAN_NO_GLDS");
-        if (fast && use_glds) return irgan_conv_fwd_glds(d, x, w, bias, y, mask, st);
+        const bool narrow = (d->Cin == 8 || d->Cin == 16 || d->Cin == 32) && d->ldx % 8 == 0 && d->xoff % 8 == 0;
+        if ((fast || narrow) && use_glds) return irgan_conv_fwd_glds(d, x, w, bias, y, mask, st);
     }
     const bool wide = d->Cout > 64;
     dim3 grid(irgan_cdiv(M, 128), irgan_cdiv(d->Cout, wide ? 128 : 64));
@@ -501,7 +508,7 @@ int launch_wgrad(const irgan_conv_desc* d, const void* x, const void* dy, float*
     const bool fb = (d->Cin % 64 == 0) && (d->ldx % EPC == 0) && (d->xoff % EPC == 0);
     if constexpr (sizeof(T) == 2) {
         static const bool use_glds = !getenv("IRGAN_NO_GLDS");
-        if (use_glds && fb && d->Cout % 64 == 0 && d->ldy % 8 == 0 && d->yoff % 8 == 0)
+        if (use_glds && fb && (d->Cout % 64 == 0 || d->Cout < 64) && d->ldy % 8 == 0 && d->yoff % 8 == 0)
             return irgan_conv_wgrad_glds(d, x, dy, dw, splitk, st);
     }
     const int BM = d->Cout > 64 ? 128 : 64;
@@ -552,16 +559,21 @@ extern "C" int irgan_conv_wgrad(const irgan_conv_desc* d, const void* x, const v
 
 extern "C" int irgan_weight_pack(const float* src, void* dst, int32_t dtype, int32_t Cout, int32_t KH, int32_t KW,
                                  int32_t Cin, int32_t transpose, int32_t s, int32_t tyr, int32_t Ay, int32_t txr,
-                                 int32_t Ax, irgan_stream_t st) {
-    long total = transpose ? (long)Cin * Ay * Ax * Cout : (long)Cout * KH * KW * Cin;
+                                 int32_t Ax, int32_t cpad, int32_t kalign, irgan_stream_t st) {
+    const int R = transpose ? Cin : Cout, taps = transpose ? Ay * Ax : KH * KW;
+    const int Cr = transpose ? Cout : Cin;
+    const int Cp = cpad > Cr ? cpad : Cr;
+    const int ka = kalign > 0 ? kalign : 1;
+    const int Kp = (taps * Cp + ka - 1) / ka * ka;
+    long total = (long)R * Kp;
     int blocks = (int)std::min<long>((total + 255) / 256, 4096);
     if (blocks <= 0) return 0;
     if (dtype == IRGAN_BF16)
         weight_pack_kernel<bf16_t><<<blocks, 256, 0, (hipStream_t)st>>>(src, (bf16_t*)dst, Cout, KH, KW, Cin,
-                                                                          transpose, s, tyr, Ay, txr, Ax);
+                                                                          transpose, s, tyr, Ay, txr, Ax, Cp, Kp);
     else
         weight_pack_kernel<float><<<blocks, 256, 0, (hipStream_t)st>>>(src, (float*)dst, Cout, KH, KW, Cin,
-                                                                         transpose, s, tyr, Ay, txr, Ax);
+                                                                         transpose, s, tyr, Ay, txr, Ax, Cp, Kp);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }

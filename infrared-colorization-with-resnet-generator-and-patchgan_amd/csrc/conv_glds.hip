@@ -60,11 +60,16 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_glds_kernel(const irgan_conv_
     const int wm = wid >> 1, wn = wid & 1;
     const int HoWo = d.Ho * d.Wo;
     const long M = (long)d.N * HoWo;
-    const int K = d.KH * d.KW * d.Cin;
+    const int taps = d.KH * d.KW;
+    const int K = (taps * d.Cin + 63) / 64 * 64;  // weight row stride (taps zero-padded)
     const long m0 = (long)blockIdx.x * BM;
     const int n0 = blockIdx.y * BN;
     const int sub = lane >> 3;
     const int chunk = (lane & 7) ^ sub;  // source chunk for this lane's LDS slot (row & 7 == sub)
+    // K-tile = 64 channels of one tap (Cin % 64 == 0) or 64/Cin taps of a narrow
+    // (8/16/32-channel, zero-padded) input: this lane's chunk -> (tap in tile, channel offset)
+    const int cpt = d.Cin >= 64 ? 8 : d.Cin / 8;  // chunks per tap inside a tile
+    const int tap_in = chunk / cpt, ch_in = (chunk % cpt) * 8;
 
     int a_nb[AU], a_iy[AU], a_ix[AU];
 #pragma unroll
@@ -92,9 +97,16 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_glds_kernel(const irgan_conv_
 
     auto issue = [&](int kt, int stage) {
         const int k0 = kt * 64;
-        const int tap = k0 / d.Cin, cin0 = k0 - tap * d.Cin;
+        int tap, coff;
+        if (d.Cin >= 64) {
+            tap = k0 / d.Cin;
+            coff = d.xoff + (k0 - tap * d.Cin) + chunk * 8;
+        } else {
+            tap = kt * (8 / cpt) + tap_in;
+            coff = d.xoff + ch_in;
+        }
+        const bool tap_ok = tap < taps;
         const int ty = tap / d.KW, tx = tap - ty * d.KW;
-        const int coff = d.xoff + cin0 + chunk * 8;
         char* sA = smem + stage * STAGE;
 #pragma unroll
         for (int u = 0; u < AU; ++u) {
@@ -104,7 +116,7 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_glds_kernel(const irgan_conv_
                 qx = reflect_idx(qx, d.W);
             }
             // branch-free validity (bitwise, no short circuit) -> one v_cndmask on the address
-            const bool ok = (a_nb[u] >= 0) & ((unsigned)qy < (unsigned)d.H) & ((unsigned)qx < (unsigned)d.W);
+            const bool ok = tap_ok & (a_nb[u] >= 0) & ((unsigned)qy < (unsigned)d.H) & ((unsigned)qx < (unsigned)d.W);
             const long off = ((long)(a_nb[u] + qy) * d.W + qx) * d.ldx;
             const bf16_t* src = ok ? x + off + coff : zero;
             glds16(src, sA + (wid * AU + u) * 1024);
@@ -275,6 +287,7 @@ __global__ __launch_bounds__(512, 2) void conv_wgrad_glds_kernel(const irgan_con
     const int tap = n0 / d.Cin, cin0 = n0 - tap * d.Cin;
     const int ty = tap / d.KW, tx = tap - ty * d.KW;
     const bool reflect = d.pad_mode == IRGAN_PAD_REFLECT;
+    const int cout8 = (d.Cout + 7) / 8 * 8;  // dY channels beyond Cout are zero padding
 
     // lane -> (row within a 1 KiB piece, 16-byte slot) for each image
     constexpr int ARPP = 1024 / RA, BRPP = 1024 / RBB;  // pixel rows per piece
@@ -290,7 +303,7 @@ __global__ __launch_bounds__(512, 2) void conv_wgrad_glds_kernel(const irgan_con
             const int r = piece * ARPP + a_sub;
             const long p = p0 + r;
             const int c16 = a_slot ^ wg_swz<RA>(r);
-            const bool ok = p < pe;
+            const bool ok = (p < pe) & (co0 + c16 * 8 < cout8);
             const bf16_t* src = ok ? dy + p * d.ldy + d.yoff + co0 + c16 * 8 : zero;
             glds16(src, sA + piece * 1024);
         }
@@ -371,7 +384,7 @@ extern "C" int irgan_conv_wgrad_glds(const irgan_conv_desc* d, const void* x, co
         return IRGAN_EUNSUPPORTED;
     const int BMC = d->Cout % 128 == 0 ? 128 : 64;
     const int BNC = d->Cin % 128 == 0 ? 128 : 64;
-    const int tiles = (d->Cout / BMC) * (K / BNC);
+    const int tiles = irgan_cdiv(d->Cout, BMC) * (K / BNC);
     if (splitk <= 0) {
         splitk = irgan_cdiv(512, tiles);  // ~2 blocks per CU
         long maxs = (P + 16 * 64 - 1) / (16 * 64);  // >= 16 K-tiles per split
@@ -381,7 +394,7 @@ extern "C" int irgan_conv_wgrad_glds(const irgan_conv_desc* d, const void* x, co
     long kc = (P + splitk - 1) / splitk;
     kc = (kc + 63) / 64 * 64;
     splitk = (int)((P + kc - 1) / kc);
-    dim3 g(d->Cout / BMC, K / BNC, splitk);
+    dim3 g(irgan_cdiv(d->Cout, BMC), K / BNC, splitk);
     const bf16_t* xp = (const bf16_t*)x;
     const bf16_t* dp = (const bf16_t*)dy;
     if (BMC == 128 && BNC == 128) conv_wgrad_glds_kernel<128, 128><<<g, 512, 0, st>>>(*d, xp, dp, dw, (int)kc, zero);

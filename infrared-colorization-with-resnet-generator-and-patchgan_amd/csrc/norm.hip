@@ -307,12 +307,26 @@ extern "C" int irgan_in_bwd_apply(const void* dy, int32_t dy_dtype, int32_t lddy
     return 0;
 }
 
+__global__ void colsum_finalize_kernel(const double* __restrict__ work, float* __restrict__ db, int G, int C) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double t = 0.0;
+    for (int g = 0; g < G; ++g) t += work[((long)g * C + c) * 2];
+    db[c] += (float)t;
+}
+
 extern "C" int irgan_channel_sum(const void* g, int32_t dtype, int32_t P, int32_t C, int32_t ld, int32_t off,
-                                 float* db, irgan_stream_t s) {
+                                 float* db, double* work, irgan_stream_t s) {
     if (P <= 0) return 0;
+    // P rows viewed as G row-groups ("images") so the fp64 atomics spread over G*C
+    // addresses instead of all blocks hammering the same C words; G divides P.
+    hipStream_t st = (hipStream_t)s;
+    int G = 64;
+    while (G > 1 && P % G) G >>= 1;
+    hipMemsetAsync(work, 0, sizeof(double) * 2 * (size_t)G * C, st);
     Slice X{g, dtype, ld, off}, Z{nullptr, 0, 0, 0};
-    launch_rows<3>(X, Z, Z, 0, nullptr, nullptr, nullptr, 0, 0, 0, 1, P, C, nullptr, db, vec_ok(C, {ld, off}),
-                   (hipStream_t)s);
+    launch_rows<0>(X, Z, Z, 0, nullptr, nullptr, nullptr, 0, 0, 0, G, P / G, C, work, nullptr, vec_ok(C, {ld, off}), st);
+    colsum_finalize_kernel<<<irgan_cdiv(C, 256), 256, 0, st>>>(work, db, G, C);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }

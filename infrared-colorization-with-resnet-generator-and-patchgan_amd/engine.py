@@ -156,6 +156,14 @@ class Buffers:
             self.d[name] = t
         return t
 
+    def zeros(self, name, shape, dtype):
+        """Like get(), zero-filled when (re)allocated: padding channels stay 0."""
+        t = self.d.get(name)
+        if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype:
+            t = torch.zeros(shape, dtype=dtype, device=self.device)
+            self.d[name] = t
+        return t
+
     def flat(self, name, numel, dtype=torch.float32):
         t = self.d.get(name)
         if t is None or t.numel() < numel or t.dtype != dtype:
@@ -165,7 +173,15 @@ class Buffers:
 
 
 class INLayer:
-    """Per-layer InstanceNorm statistics kept from forward to backward."""
+    """Per-layer InstanceNorm statistics kept from forward to backward.
+
+    The conv bias in front of an InstanceNorm has an exactly-zero gradient
+    (IN subtracts the per-channel mean, so the bias never reaches any output);
+    the reference's fp32 autograd produces rounding noise there.
+    By default the exact zero is kept (no reduction, no atomics); set
+    ``INLayer.sum_bias_grad = True`` to accumulate the fp32 sum of dx instead.
+    """
+    sum_bias_grad = False
 
     def __init__(self):
         self.mr = None
@@ -182,7 +198,7 @@ class INLayer:
         N, C = z.N, z.C
         work = bufs.flat("in_work", 2 * N * C, torch.float64)
         red = bufs.flat("in_red", 2 * N * C)
-        ops.in_backward(dy, z, act, self.mr, work, red, dx, db=db, dy2=dy2)
+        ops.in_backward(dy, z, act, self.mr, work, red, dx, db=db if INLayer.sum_bias_grad else None, dy2=dy2)
 
 
 # ----------------------------------------------------------------------------
@@ -241,8 +257,9 @@ class GeneratorEngine:
         c0, c1, c2 = self.ngf, 2 * self.ngf, 4 * self.ngf
         H1, W1, H2, W2 = self._dims(H, W)
         self.shape = (B, H, W)
-        ir_t = Feat(g.get("ir", (B, H, W, self.input_nc), T))
-        ops.nchw_to_nhwc(ir_nchw.contiguous(), ir_t)
+        ir_buf = g.zeros("ir", (B, H, W, max(8, self.input_nc)), T)   # narrow input zero-padded to 8 ch
+        ops.nchw_to_nhwc(ir_nchw.contiguous(), Feat(ir_buf, 0, self.input_nc))
+        ir_t = Feat(ir_buf, 0, self.inc.cin_eff)
         cat2 = g.get("cat2", (B, H, W, c1 + c0), T)       # [up2 out | x0]
         cat1 = g.get("cat1", (B, H1, W1, c2 + c1), T)     # [up1 out | x1]
         x0 = Feat(cat2, c1, c0)
@@ -326,13 +343,14 @@ class GeneratorEngine:
 
         # outc: tanh' then conv backward
         fake = Feat(g.d["fake"])
-        dzo = Feat(g.get("dz_out", (B, H, W, self.output_nc), T))
+        dzo_buf = g.zeros("dz_out", (B, H, W, max(8, self.output_nc)), T)   # zero-padded to 8 ch
+        dzo = Feat(dzo_buf, 0, self.output_nc)
         ops.act_bwd(Feat(dfake), fake, ACT_TANH, dzo)
         a4 = Feat(g.d["a4"])
         wg(self.outc, "outc.1", a4, dzo)
         ops.channel_sum(dzo, S.krsc("outc.1.bias", G))
         da4 = Feat(g.get("da4", (B, H, W, c0), T))
-        ops.conv_dgrad(self.outc, dzo, da4, pad_buf=padbuf)
+        ops.conv_dgrad(self.outc, Feat(dzo_buf, 0, self.outc.cout_eff), da4, pad_buf=padbuf)
         # up2_conv
         self.norms["up2"].bwd(g, da4, Feat(g.d["z4"]), ACT_RELU, da4, db=S.krsc("up2_conv.0.bias", G))
         wg(self.up2, "up2_conv.0", cat2, da4)
@@ -456,8 +474,9 @@ class DiscriminatorEngine:
         g, T, S = self.bufs, self.tdt, self.store
         G = S.grad
         n = len(self.packs)
-        dy = Feat(g.get(f"{tag}dout_t", tuple(dout.shape), T))
-        ops.axpby(Feat(dout), 1.0, dy)
+        dbuf = g.zeros(f"{tag}dout_t", tuple(dout.shape[:3]) + (8,), T)   # 1-ch logits grad, padded to 8
+        ops.axpby(Feat(dout), 1.0, Feat(dbuf, 0, dout.shape[3]))
+        dy = Feat(dbuf, 0, self.packs[-1].cout_eff)
         for i in reversed(range(n)):
             pc, key = self.packs[i], self.LAYERS[i][0]
             x = self.acts[i]
@@ -470,11 +489,11 @@ class DiscriminatorEngine:
             elif want_wgrad:  # layer 0: LReLU mask already folded into dy by the layer-1 dgrad
                 ops.channel_sum(dy, S.krsc(key + ".bias", G))
             if want_wgrad:
-                ops.conv_wgrad(pc.spec, x, dy, S.krsc(key + ".weight", G), self.dtype)
+                ops.conv_wgrad(pc.spec, x, Feat(dy.t, dy.off, pc.spec.cout), S.krsc(key + ".weight", G), self.dtype)
             if i == 0:
                 if not want_dinput:
                     return None
-                dx = Feat(g.get(f"{tag}dinput", (x.N, x.H, x.W, x.C), torch.float32))
+                dx = Feat(g.get(f"{tag}dinput", (x.N, x.H, x.W, pc.spec.cin), torch.float32))
                 ops.conv_dgrad(pc, dy, dx)
                 return dx
             dx = Feat(g.get(f"{tag}d{i}", (x.N, x.H, x.W, x.C), T))
@@ -536,7 +555,7 @@ class VGGEngine:
             pc = self.packs[j]
             xin = acts[in_of[j]]
             if j == 0:
-                dvin = Feat(g.get("dvin", (nb, xin.H, xin.W, xin.C), torch.float32))
+                dvin = Feat(g.get("dvin", (nb, xin.H, xin.W, pc.spec.cin), torch.float32))
                 ops.conv_dgrad(pc, dz, dvin)
                 return dvin
             prev = in_of[j]
@@ -586,8 +605,9 @@ class GANStep:
 
     def _din(self, ir_t: Feat, img: torch.Tensor, out: Feat):
         """cat([ir, img], 1) (ir:1639-1640) written straight into the NHWC D input."""
-        ops.axpby(ir_t, 1.0, out.sl(0, ir_t.C))
-        ops.axpby(Feat(img), 1.0, out.sl(ir_t.C, img.shape[3]))
+        cin = self.cfg.input_nc
+        ops.axpby(Feat(ir_t.t, 0, cin), 1.0, Feat(out.t, 0, cin))
+        ops.axpby(Feat(img), 1.0, Feat(out.t, cin, img.shape[3]))
 
     def step(self, ir: torch.Tensor, rgb: torch.Tensor):
         """One train step on NCHW fp32 device tensors; returns the loss vector (device)."""
@@ -603,7 +623,8 @@ class GANStep:
         ops.nchw_to_nhwc(rgb.contiguous(), Feat(rgb_h))
         # ---- D step on [real; fake] as one 2B batch (ir:1636-1651)
         self.D.zero_grad()
-        din = Feat(b.get("din2", (2 * B, H, W, cin + cout), T))
+        dpad = max(8, cin + cout)   # D input zero-padded to 8 channels (narrow-input conv path)
+        din = Feat(b.zeros("din2", (2 * B, H, W, dpad), T), 0, self.dis.packs[0].cin_eff)
         self._din(ir_t, rgb_h, din.batch(0, B))
         self._din(ir_t, fake, din.batch(B, B))
         pred = self.dis.forward(din, tag="d")
@@ -617,7 +638,7 @@ class GANStep:
         self.G.zero_grad()
         dfake = b.get("dfake", (B, H, W, cout), torch.float32)
         dfake.zero_()
-        dinf = Feat(b.get("din1", (B, H, W, cin + cout), T))
+        dinf = Feat(b.zeros("din1", (B, H, W, dpad), T), 0, self.dis.packs[0].cin_eff)
         self._din(ir_t, fake, dinf)
         predg = self.dis.forward(dinf, tag="g")
         dpg = b.get("dpredg", tuple(predg.shape), torch.float32)
@@ -626,7 +647,7 @@ class GANStep:
         ops.axpby(dd.sl(cin, cout), 1.0, Feat(dfake), 1.0)
         ops.l1(fake, rgb_h, cfg.lambda_L1, dfake, L[2:3], accumulate=True)
         # perceptual: VGG on [fake; rgb] as one 2B batch (ir:1667-1669)
-        vin = Feat(b.get("vin", (2 * B, H, W, cout), T))
+        vin = Feat(b.zeros("vin", (2 * B, H, W, max(8, cout)), T), 0, self.vgg.packs[0].cin_eff)
         ops.affine(Feat(fake), self.vgg.scale, self.vgg.shift, vin.batch(0, B))
         ops.affine(Feat(rgb_h), self.vgg.scale, self.vgg.shift, vin.batch(B, B))
         feat = self.vgg.forward(vin)

@@ -332,13 +332,18 @@ class ResnetUNetGenerator(_StoreModule):
 # 5) Discriminator (ir:576-635)
 # =============================================================================
 
+def _nhwc_input(x, pc, tdt, scale=None, shift=None):
+    """NCHW fp32 -> NHWC compute-dtype conv input, narrow channels zero-padded to 8."""
+    B, C, H, W = x.shape
+    buf = torch.zeros(B, H, W, max(8, C), device=x.device, dtype=tdt)
+    ops.nchw_to_nhwc(x.contiguous().float(), Feat(buf, 0, C), scale, shift)
+    return Feat(buf, 0, pc.cin_eff)
+
+
 class _DFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, mod, *params):
-        B, C, H, W = x.shape
-        din = torch.empty(B, H, W, C, device=x.device, dtype=mod.engine.tdt)
-        ops.nchw_to_nhwc(x.contiguous().float(), Feat(din))
-        out = mod.engine.forward(Feat(din), tag="api")
+        out = mod.engine.forward(_nhwc_input(x, mod.engine.packs[0], mod.engine.tdt), tag="api")
         ctx.mod = mod
         return out.permute(0, 3, 1, 2).contiguous()
 
@@ -377,10 +382,8 @@ class NLayerDiscriminator(_StoreModule):
         params = [p for _, p in self.named_parameters()]
         if torch.is_grad_enabled():
             return _DFn.apply(x, self, *params)
-        B, C, H, W = x.shape
-        din = torch.empty(B, H, W, C, device=x.device, dtype=self.engine.tdt)
-        ops.nchw_to_nhwc(x.contiguous().float(), Feat(din))
-        return self.engine.forward(Feat(din), tag="api").permute(0, 3, 1, 2).contiguous()
+        din = _nhwc_input(x, self.engine.packs[0], self.engine.tdt)
+        return self.engine.forward(din, tag="api").permute(0, 3, 1, 2).contiguous()
 
 
 # =============================================================================
@@ -439,10 +442,8 @@ class VGGPerceptual(_StoreModule):
     def _features(self, x):
         _require_cuda(x, "VGGPerceptual")
         self._maybe_repack()
-        B, C, H, W = x.shape
-        vin = torch.empty(B, H, W, C, device=x.device, dtype=self.engine.tdt)
-        ops.nchw_to_nhwc(x.contiguous().float(), Feat(vin), self.engine.scale, self.engine.shift)
-        return self.engine.forward(Feat(vin))
+        vin = _nhwc_input(x, self.engine.packs[0], self.engine.tdt, self.engine.scale, self.engine.shift)
+        return self.engine.forward(vin)
 
     def forward(self, x):
         if torch.is_grad_enabled() and x.requires_grad:

@@ -130,15 +130,26 @@ def _desc(**kw):
     return d
 
 
+def _rup(a, b):
+    return (a + b - 1) // b * b
+
+
 def weight_pack(master: torch.Tensor, dst: torch.Tensor, cout, kh, kw, cin, transpose=0, s=1, tyr=0, ay=0,
-                txr=0, ax=0):
+                txr=0, ax=0, cpad=0, kalign=1):
     _lib.call("irgan_weight_pack", P(master), P(dst), dt_code(dst), cout, kh, kw, cin, transpose, s, tyr, ay, txr,
-              ax, stream())
+              ax, cpad, kalign, stream())
+
+
+def eff_channels(c, dtype):
+    """Channel count a conv input is stored with: bf16 narrow inputs (1/3/4 ch)
+    are zero-padded to 8 so the LDS-DMA kernel reads 16-byte chunks."""
+    return 8 if (dtype == BF16 and c < 8) else c
 
 
 class PackedConv:
     """Per-layer packed weights: forward (cast) and backward-data (flipped /
-    per-phase) images in the compute dtype, refreshed after each optimizer step."""
+    per-phase) images in the compute dtype, refreshed after each optimizer step.
+    bf16 rows are [taps][channels] zero-padded to a multiple of 64 (the K-tile)."""
 
     def __init__(self, spec: ConvSpec, master: torch.Tensor, bias: torch.Tensor | None, dtype: int,
                  need_dgrad=True, reflect_dgrad=None):
@@ -146,29 +157,35 @@ class PackedConv:
         dev = master.device
         tdt = TORCH_DT[dtype]
         k = spec.k
-        self.fwd = master if dtype == F32 else torch.empty(master.numel(), dtype=tdt, device=dev)
+        self.cin_eff = eff_channels(spec.cin, dtype)     # forward input channels as stored
+        self.cout_eff = eff_channels(spec.cout, dtype)   # backward-data input (dY) channels as stored
+        self.kalign = 64 if dtype == BF16 else 1
+        kf = _rup(k * k * self.cin_eff, self.kalign)
+        self.fwd = master if dtype == F32 else torch.empty(spec.cout * kf, dtype=tdt, device=dev)
         self.reflect = spec.mode == PAD_REFLECT if reflect_dgrad is None else reflect_dgrad
         self.dg = []
         if need_dgrad:
             for (py, tyr, ay, c0y) in spec.phases(self.reflect):
                 for (px, txr, ax, c0x) in spec.phases(self.reflect):
-                    buf = torch.empty(spec.cin * ay * ax * spec.cout, dtype=tdt, device=dev)
+                    kd = _rup(ay * ax * self.cout_eff, self.kalign)
+                    buf = torch.empty(spec.cin * kd, dtype=tdt, device=dev)
                     self.dg.append(((py, tyr, ay, c0y), (px, txr, ax, c0x), buf))
 
     def pack(self):
         s = self.spec
         if self.dtype != F32:
-            weight_pack(self.master, self.fwd, s.cout, s.k, s.k, s.cin)
+            weight_pack(self.master, self.fwd, s.cout, s.k, s.k, s.cin, cpad=self.cin_eff, kalign=self.kalign)
         for (py, tyr, ay, _), (px, txr, ax, _), buf in self.dg:
-            weight_pack(self.master, buf, s.cout, s.k, s.k, s.cin, 1, s.stride, tyr, ay, txr, ax)
+            weight_pack(self.master, buf, s.cout, s.k, s.k, s.cin, 1, s.stride, tyr, ay, txr, ax,
+                        cpad=self.cout_eff, kalign=self.kalign)
 
 
 def conv_fwd(pc: PackedConv, x: Feat, y: Feat, act=ACT_NONE, bias=True, accumulate=False, mask: Feat = None,
              mask_act=0):
     s = pc.spec
     Ho, Wo = s.out_hw(x.H, x.W)
-    assert (y.H, y.W, y.C) == (Ho, Wo, s.cout) and x.C == s.cin and y.N == x.N, "conv_fwd shape mismatch"
-    d = _desc(N=x.N, H=x.H, W=x.W, Cin=s.cin, ldx=x.ld, xoff=x.off, Ho=Ho, Wo=Wo, Cout=s.cout, ldy=y.ld,
+    assert (y.H, y.W, y.C) == (Ho, Wo, s.cout) and x.C == pc.cin_eff and y.N == x.N, "conv_fwd shape mismatch"
+    d = _desc(N=x.N, H=x.H, W=x.W, Cin=pc.cin_eff, ldx=x.ld, xoff=x.off, Ho=Ho, Wo=Wo, Cout=s.cout, ldy=y.ld,
               yoff=y.off, OH=Ho, OW=Wo, omy=1, ooy=0, omx=1, oox=0, KH=s.k, KW=s.k, sy=s.stride, sx=s.stride,
               c0y=-s.pad, c0x=-s.pad, pad_mode=s.mode, act=act, accumulate=int(accumulate), dtype=pc.dtype,
               out_dtype=y.dt, mask_act=mask_act, ldm=mask.ld if mask else 0, moff=mask.off if mask else 0)
@@ -183,14 +200,14 @@ def conv_dgrad(pc: PackedConv, dy: Feat, dx: Feat, accumulate=False, mask: Feat 
     """dx = d(conv)/dx^T dy.  Reflect-padded layers go through an fp32
     (H+2p)x(W+2p) buffer and the reflect fold; stride-2 layers launch per phase."""
     s = pc.spec
-    assert dy.C == s.cout and dx.C == s.cin and dy.dt == pc.dtype
+    assert dy.C == pc.cout_eff and dx.C == s.cin and dy.dt == pc.dtype
     if pc.reflect:
         p = s.pad
         Hp, Wp = dx.H + 2 * p, dx.W + 2 * p
         assert pad_buf is not None and pad_buf.numel() >= dx.N * Hp * Wp * s.cin
         tgt = Feat(pad_buf[:dx.N * Hp * Wp * s.cin].view(dx.N, Hp, Wp, s.cin))
         (_, _, ay, c0y), (_, _, ax, c0x), buf = pc.dg[0]
-        d = _desc(N=dy.N, H=dy.H, W=dy.W, Cin=s.cout, ldx=dy.ld, xoff=dy.off, Ho=Hp, Wo=Wp, Cout=s.cin,
+        d = _desc(N=dy.N, H=dy.H, W=dy.W, Cin=pc.cout_eff, ldx=dy.ld, xoff=dy.off, Ho=Hp, Wo=Wp, Cout=s.cin,
                   ldy=tgt.ld, yoff=0, OH=Hp, OW=Wp, omy=1, ooy=0, omx=1, oox=0, KH=ay, KW=ax, sy=1, sx=1,
                   c0y=c0y, c0x=c0x, pad_mode=PAD_ZERO, act=0, accumulate=0, dtype=pc.dtype, out_dtype=F32,
                   mask_act=0, ldm=0, moff=0)
@@ -205,7 +222,7 @@ def conv_dgrad(pc: PackedConv, dy: Feat, dx: Feat, accumulate=False, mask: Feat 
         if Ho <= 0 or Wo <= 0:
             continue
         assert ay > 0 and ax > 0
-        d = _desc(N=dy.N, H=dy.H, W=dy.W, Cin=s.cout, ldx=dy.ld, xoff=dy.off, Ho=Ho, Wo=Wo, Cout=s.cin,
+        d = _desc(N=dy.N, H=dy.H, W=dy.W, Cin=pc.cout_eff, ldx=dy.ld, xoff=dy.off, Ho=Ho, Wo=Wo, Cout=s.cin,
                   ldy=dx.ld, yoff=dx.off, OH=dx.H, OW=dx.W, omy=st, ooy=py, omx=st, oox=px, KH=ay, KW=ax, sy=1,
                   sx=1, c0y=c0y, c0x=c0x, pad_mode=PAD_ZERO, act=0, accumulate=int(accumulate), dtype=pc.dtype,
                   out_dtype=dx.dt, mask_act=mask_act, ldm=mask.ld if mask else 0, moff=mask.off if mask else 0)
@@ -216,7 +233,7 @@ def conv_dgrad(pc: PackedConv, dy: Feat, dx: Feat, accumulate=False, mask: Feat 
 def conv_wgrad(spec: ConvSpec, x: Feat, dy: Feat, dw: torch.Tensor, dtype: int, splitk=0):
     """dw (fp32 KRSC view, accumulated) += weight gradient of conv(x) given dy."""
     Ho, Wo = spec.out_hw(x.H, x.W)
-    assert (dy.H, dy.W, dy.C) == (Ho, Wo, spec.cout) and x.C == spec.cin
+    assert (dy.H, dy.W, dy.C) == (Ho, Wo, spec.cout) and x.C >= spec.cin
     assert x.dt == dtype and dy.dt == dtype and dw.dtype == torch.float32
     d = _desc(N=x.N, H=x.H, W=x.W, Cin=spec.cin, ldx=x.ld, xoff=x.off, Ho=Ho, Wo=Wo, Cout=spec.cout, ldy=dy.ld,
               yoff=dy.off, OH=Ho, OW=Wo, omy=1, ooy=0, omx=1, oox=0, KH=spec.k, KW=spec.k, sy=spec.stride,
@@ -251,8 +268,15 @@ def in_backward(dy: Feat, x: Feat, act: int, mr, work, red, dx: Feat, db=None, d
               P(mr), P(red), dx.ptr, dx.dt, dx.ld, dx.off, P(db), stream())
 
 
+_CS_WORK = {}
+
+
 def channel_sum(g: Feat, db: torch.Tensor):
-    _lib.call("irgan_channel_sum", g.ptr, g.dt, g.P, g.C, g.ld, g.off, P(db), stream())
+    key = (db.device, g.C)
+    w = _CS_WORK.get(key)
+    if w is None:
+        w = _CS_WORK[key] = torch.empty(128 * g.C, dtype=torch.float64, device=db.device)
+    _lib.call("irgan_channel_sum", g.ptr, g.dt, g.P, g.C, g.ld, g.off, P(db), P(w), stream())
 
 
 # ----------------------------------------------------------------------------

@@ -76,21 +76,24 @@ def test_conv_fwd_dgrad_wgrad(ops, case, dtype):
     master = w.permute(0, 2, 3, 1).contiguous().reshape(-1).to(DEV)
     pc = ops.PackedConv(spec, master, b.to(DEV), code)
     pc.pack()
-    # forward into a channel slice of a wider tensor (exercises ld/off)
-    xd = nhwc(x).to(tdt)
+    # forward into a channel slice of a wider tensor (exercises ld/off); narrow bf16
+    # inputs are stored zero-padded to pc.cin_eff channels
+    xd = torch.zeros(N, H, H, pc.cin_eff, device=DEV, dtype=tdt)
+    xd[..., :cin] = nhwc(x).to(tdt)
     Ho, Wo = y_ref.shape[2:]
     ybuf = torch.zeros(N, Ho, Wo, cout + 8, device=DEV, dtype=torch.float32)
     ops.conv_fwd(pc, ops.Feat(xd), ops.Feat(ybuf, 8, cout))
     assert relerr(nchw(ybuf[..., 8:]), y_ref.detach()) < tol
-    # backward-data
-    gyd = nhwc(gy).to(tdt)
+    # backward-data (dY zero-padded to pc.cout_eff channels)
+    gyd = torch.zeros(N, Ho, Wo, pc.cout_eff, device=DEV, dtype=tdt)
+    gyd[..., :cout] = nhwc(gy).to(tdt)
     dx = torch.zeros(N, H, H, cin, device=DEV, dtype=torch.float32)
     pad = torch.empty(N * (H + 2 * p) ** 2 * cin, device=DEV) if mode == 1 else None
     ops.conv_dgrad(pc, ops.Feat(gyd), ops.Feat(dx), pad_buf=pad)
     assert relerr(nchw(dx), xr.grad) < tol
     # backward-weight
     dw = torch.zeros(cout * k * k * cin, device=DEV)
-    ops.conv_wgrad(spec, ops.Feat(xd), ops.Feat(gyd), dw, code)
+    ops.conv_wgrad(spec, ops.Feat(xd), ops.Feat(gyd, 0, cout), dw, code)
     dw = dw.view(cout, k, k, cin).permute(0, 3, 1, 2).cpu()
     assert relerr(dw, wr.grad) < (2e-5 if dtype == "f32" else 3e-2)
 
