@@ -104,7 +104,7 @@ def main():
     rgb = (torch.rand(B, 3, H, W, generator=g) * 2 - 1).cuda()
 
     # dominant kernel for the live roofline: the resblock 3x3 conv (256->256 @ H/4)
-    res_tags = [ops.conv_tag(k, ops.ConvSpec(256, 256, 3, 1, 1, 1), (H // 4, W // 4))
+    res_tags = [ops.conv_tag(k, ops.ConvSpec(256, 256, 3, 1, 1, ops.PAD_REFLECT), (H // 4, W // 4), B)
                 for k in ("fwd", "dgrad", "wgrad")]
     for _ in range(args.warmup):
         tr.step(ir, rgb)

@@ -64,8 +64,10 @@ class LaunchTimer:
 TIMER = LaunchTimer(())
 
 
-def conv_tag(kind, spec, x_hw):
-    return f"{kind}:{spec.cin}x{spec.cout}k{spec.k}s{spec.stride}@{x_hw[0]}x{x_hw[1]}"
+def conv_tag(kind, spec, x_hw, n=None):
+    pad = "r" if spec.mode == PAD_REFLECT else "z"
+    nb = f"b{n}" if n is not None else ""
+    return f"{kind}:{spec.cin}x{spec.cout}k{spec.k}s{spec.stride}{pad}@{nb}{x_hw[0]}x{x_hw[1]}"
 
 
 class Feat:
@@ -190,7 +192,7 @@ def conv_fwd(pc: PackedConv, x: Feat, y: Feat, act=ACT_NONE, bias=True, accumula
               c0y=-s.pad, c0x=-s.pad, pad_mode=s.mode, act=act, accumulate=int(accumulate), dtype=pc.dtype,
               out_dtype=y.dt, mask_act=mask_act, ldm=mask.ld if mask else 0, moff=mask.off if mask else 0)
     assert x.dt == pc.dtype
-    TIMER.wrap(conv_tag("fwd", s, (x.H, x.W)), lambda: _lib.call(
+    TIMER.wrap(conv_tag("fwd", s, (x.H, x.W), x.N), lambda: _lib.call(
         "irgan_conv_fwd", ctypes.byref(d), x.ptr, P(pc.fwd), P(pc.bias if bias else None), y.ptr,
         mask.ptr if mask else None, stream()))
 
@@ -211,7 +213,7 @@ def conv_dgrad(pc: PackedConv, dy: Feat, dx: Feat, accumulate=False, mask: Feat 
                   ldy=tgt.ld, yoff=0, OH=Hp, OW=Wp, omy=1, ooy=0, omx=1, oox=0, KH=ay, KW=ax, sy=1, sx=1,
                   c0y=c0y, c0x=c0x, pad_mode=PAD_ZERO, act=0, accumulate=0, dtype=pc.dtype, out_dtype=F32,
                   mask_act=0, ldm=0, moff=0)
-        TIMER.wrap(conv_tag("dgrad", s, (dx.H, dx.W)), lambda: _lib.call(
+        TIMER.wrap(conv_tag("dgrad", s, (dx.H, dx.W), dx.N), lambda: _lib.call(
             "irgan_conv_fwd", ctypes.byref(d), dy.ptr, P(buf), None, tgt.ptr, None, stream()))
         assert mask is None
         reflect_fold(tgt, dx, p, accumulate)
@@ -239,7 +241,7 @@ def conv_wgrad(spec: ConvSpec, x: Feat, dy: Feat, dw: torch.Tensor, dtype: int, 
               yoff=dy.off, OH=Ho, OW=Wo, omy=1, ooy=0, omx=1, oox=0, KH=spec.k, KW=spec.k, sy=spec.stride,
               sx=spec.stride, c0y=-spec.pad, c0x=-spec.pad, pad_mode=spec.mode, act=0, accumulate=1, dtype=dtype,
               out_dtype=F32, mask_act=0, ldm=0, moff=0)
-    TIMER.wrap(conv_tag("wgrad", spec, (x.H, x.W)), lambda: _lib.call(
+    TIMER.wrap(conv_tag("wgrad", spec, (x.H, x.W), x.N), lambda: _lib.call(
         "irgan_conv_wgrad", ctypes.byref(d), x.ptr, dy.ptr, P(dw), splitk, stream()))
 
 
