@@ -36,7 +36,7 @@ from .ops import BF16, F32, Feat
 __all__ = ["Config", "Identity", "get_norm_layer", "init_weights", "init_net", "get_lr_lambda", "get_filter",
            "ResnetUNetGenerator", "NLayerDiscriminator", "VGGPerceptual", "tv_loss", "ssim_loss_torch",
            "IRColorizationModel", "GANTrainer", "validate_kaist", "train_kaist", "SyntheticPairDataset",
-           "g_param_shapes", "d_param_shapes", "vgg_param_shapes", "seeded_state"]
+           "g_param_shapes", "d_param_shapes", "vgg_param_shapes", "seeded_state", "dp_loaders"]
 
 
 # =============================================================================
@@ -586,8 +586,17 @@ class GANTrainer:
 
 
 @torch.no_grad()
+def _dp():
+    """(rank, world) of the data-parallel job, (0, 1) when not distributed."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
 def validate_kaist(model: IRColorizationModel, val_loader, device):
-    """ir:1521-1542: batch-size-weighted mean L1 of G(ir) vs rgb."""
+    """ir:1521-1542: batch-size-weighted mean L1 of G(ir) vs rgb.  Under data
+    parallelism each rank scores its val shard and (sum, count) is all-reduced."""
     total, count = 0.0, 0
     for batch in val_loader:
         ir = batch["ir"].to(device)
@@ -595,7 +604,36 @@ def validate_kaist(model: IRColorizationModel, val_loader, device):
         fake = model(ir)
         total += float((fake - rgb).abs().mean()) * ir.size(0)
         count += ir.size(0)
+    rank, world = _dp()
+    if world > 1:
+        import torch.distributed as dist
+        dev = device if dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([total, float(count)], dtype=torch.float64, device=dev)
+        dist.all_reduce(t)
+        total, count = float(t[0]), int(t[1])
     return total / max(count, 1)
+
+
+def dp_loaders(train_ds, val_ds, batch_size, seed=0):
+    """Train/val loaders (ir:1575-1581).  With world > 1 every rank gets an equal
+    shard of whole per-rank batches (DistributedSampler, drop_last) so that the
+    gradient all-reduce (engine.grad_allreduce) averages equal-sized batch means:
+    ``batch_size`` is per rank, the global batch is batch_size * world."""
+    rank, world = _dp()
+    if world == 1:
+        tl = torch.utils.data.DataLoader(train_ds, batch_size=batch_size, shuffle=True, num_workers=0,
+                                         pin_memory=True, drop_last=True)
+        vl = torch.utils.data.DataLoader(val_ds, batch_size=batch_size, shuffle=False, num_workers=0,
+                                         pin_memory=True, drop_last=False)
+        return tl, vl, None
+    from torch.utils.data.distributed import DistributedSampler
+    ts = DistributedSampler(train_ds, num_replicas=world, rank=rank, shuffle=True, seed=seed, drop_last=True)
+    vs = DistributedSampler(val_ds, num_replicas=world, rank=rank, shuffle=False, drop_last=False)
+    tl = torch.utils.data.DataLoader(train_ds, batch_size=batch_size, sampler=ts, num_workers=0,
+                                     pin_memory=True, drop_last=True)
+    vl = torch.utils.data.DataLoader(val_ds, batch_size=batch_size, sampler=vs, num_workers=0,
+                                     pin_memory=True, drop_last=False)
+    return tl, vl, ts
 
 
 class SyntheticPairDataset(torch.utils.data.Dataset):
@@ -632,20 +670,21 @@ def train_kaist(cfg: Config, dataset=None, log=print):
     random.shuffle(idxs)
     train_ds = torch.utils.data.Subset(dataset, idxs[:train_size])
     val_ds = torch.utils.data.Subset(dataset, idxs[train_size:])
-    train_loader = torch.utils.data.DataLoader(train_ds, batch_size=cfg.batch_size, shuffle=True,
-                                               num_workers=0, pin_memory=True, drop_last=True)
-    val_loader = torch.utils.data.DataLoader(val_ds, batch_size=cfg.batch_size, shuffle=False, num_workers=0,
-                                             pin_memory=True, drop_last=False)
+    train_loader, val_loader, sampler = dp_loaders(train_ds, val_ds, cfg.batch_size)
+    rank, _ = _dp()
     model = IRColorizationModel(cfg)
     if cfg.init_G_weights is not None and os.path.isfile(cfg.init_G_weights):
         log(f"Initializing generator from: {cfg.init_G_weights}")
         model.load_weights(cfg.init_G_weights)
     trainer = GANTrainer(cfg, model=model)
-    os.makedirs(cfg.save_dir, exist_ok=True)
+    if rank == 0:
+        os.makedirs(cfg.save_dir, exist_ok=True)
     best_val = float("inf")
     best_path = os.path.join(cfg.save_dir, "netG_best.pth")
     history = []
     for epoch in range(1, cfg.epochs + 1):
+        if sampler is not None:
+            sampler.set_epoch(epoch)
         acc = torch.zeros(8, dtype=torch.float64, device=device)
         steps = 0
         for i, batch in enumerate(train_loader, start=1):
@@ -666,13 +705,14 @@ def train_kaist(cfg: Config, dataset=None, log=print):
         log(f"Epoch [{epoch}/{cfg.epochs}] DONE | avg D: {avg['loss_D']:.4f} | avg G: {avg['loss_G']:.4f} | "
             f"val L1: {val_l1:.4f}")
         history.append(dict(epoch=epoch, val_l1=val_l1, **avg))
-        if (epoch % cfg.save_every == 0) or (epoch == cfg.epochs):
+        if rank == 0 and ((epoch % cfg.save_every == 0) or (epoch == cfg.epochs)):
             path = os.path.join(cfg.save_dir, f"netG_epoch_{epoch:03d}.pth")
             torch.save(_cpu_state(model.netG), path)
             log(f"Saved generator checkpoint to {path}")
         if val_l1 < best_val:
             best_val = val_l1
-            torch.save(_cpu_state(model.netG), best_path)
+            if rank == 0:
+                torch.save(_cpu_state(model.netG), best_path)
             log(f"New best model saved to {best_path} (val L1={best_val:.4f})")
         trainer.scheduler_step()
         log(f"Current LR (G): {trainer.current_lr_G:.6e}")

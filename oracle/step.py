@@ -304,7 +304,7 @@ def _trainable(P):
 
 
 def train_step(G, D, V, ir, rgb, optG, optD, lam=None, no_antialias=False,
-               no_antialias_up=False, n_blocks=9):
+               no_antialias_up=False, n_blocks=9, grad_hook=None):
     """One train step, minimal form of ir:1636-1681.
 
     D step: hinge on D(cat[ir,rgb]) and D(cat[ir,G(ir)]) (G detached), D Adam.
@@ -313,6 +313,9 @@ def train_step(G, D, V, ir, rgb, optG, optD, lam=None, no_antialias=False,
     The reference runs G forward twice with identical weights (ir:1638, 1657);
     one forward is mathematically the same.  Mutates G, D, opt states.
     Returns a dict of losses, outputs and grads (for parity checks).
+    ``grad_hook(name, grads)`` (name "D" or "G") may rewrite the grad dict in
+    place before the Adam update -- the data-parallel tests use it to insert
+    the product's gradient all-reduce.
     """
     lam = dict(LAMBDAS, **(lam or {}))
     out = {}
@@ -328,6 +331,8 @@ def train_step(G, D, V, ir, rgb, optG, optD, lam=None, no_antialias=False,
     gD = torch.autograd.grad(loss_D, [dk[k] for k in D])
     out.update(pred_real=pred_real.detach(), pred_fake=pred_fake.detach(), loss_D=loss_D.detach())
     out["gradD"] = {k: g for k, g in zip(D, gD)}
+    if grad_hook is not None:
+        grad_hook("D", out["gradD"])
     adam_update(D, out["gradD"], optD)
 
     # ---- G step (ir:1656-1681), D frozen at its updated weights
@@ -344,5 +349,7 @@ def train_step(G, D, V, ir, rgb, optG, optD, lam=None, no_antialias=False,
                loss_G_L1=l_l1.detach(), loss_G_perc=l_perc.detach(), loss_G_TV=l_tv.detach(),
                loss_G_ssim=l_ssim.detach())
     out["gradG"] = {k: g for k, g in zip(keys, gG)}
+    if grad_hook is not None:
+        grad_hook("G", out["gradG"])
     adam_update(G, out["gradG"], optG)
     return out

@@ -1,0 +1,140 @@
+"""Data-parallel plumbing on CPU (gloo, world size 2).
+
+The GPU step cannot run here, so the per-rank arithmetic is the fp64 oracle
+step (oracle/step.py, ir:1636-1681); what is under test is the product's DP
+code around it: the batch sharding (``dp_loaders``), the gradient all-reduce
+(``engine.grad_allreduce``, called on a flat buffer exactly as GANStep does
+between backward and Adam) and the val-L1 (sum, count) reduction
+(``validate_kaist``).  Claim checked: two ranks training on
+equal shards reproduce the single-process step on the union batch.  In fp64
+the only difference is summation order, so the tolerance is 1e-9 relative.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import pkg
+
+WORLD = 2
+PER_RANK = 2
+HW = 32
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class _Indexed(torch.utils.data.Dataset):
+    def __init__(self, base):
+        self.base = base
+
+    def __len__(self):
+        return len(self.base)
+
+    def __getitem__(self, i):
+        d = dict(self.base[i])
+        d["idx"] = i
+        return d
+
+
+def _params():
+    from oracle import step as O
+    dd = lambda P: {k: v.double() for k, v in P.items()}  # noqa: E731
+    return (dd(O.seeded_params(O.g_param_shapes(), 1)), dd(O.seeded_params(O.d_param_shapes(), 2)),
+            dd(O.seeded_params(O.vgg_param_shapes(), 3, kaiming=True)))
+
+
+def _dataset():
+    irc = pkg()
+    return _Indexed(irc.SyntheticPairDataset(12, img_size=HW, seed=5))
+
+
+def _flat_hook(engine):
+    """Flatten a grad dict into one buffer, all-reduce it, scatter back (GANStep's layout)."""
+    def hook(name, grads):
+        keys = list(grads)
+        flat = torch.cat([grads[k].reshape(-1) for k in keys])
+        engine.grad_allreduce(flat)
+        o = 0
+        for k in keys:
+            n = grads[k].numel()
+            grads[k] = flat[o:o + n].view_as(grads[k])
+            o += n
+    return hook
+
+
+def _worker(rank, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        irc = pkg()
+        from oracle import step as O
+        import importlib
+        engine = importlib.import_module(irc.__name__ + ".engine")
+        ds = _dataset()
+        train_ds = torch.utils.data.Subset(ds, list(range(8)))
+        val_ds = torch.utils.data.Subset(ds, list(range(8, 11)))   # 3 items: ragged over 2 ranks
+        tl, vl, sampler = irc.dp_loaders(train_ds, val_ds, PER_RANK, seed=0)
+        sampler.set_epoch(1)
+        batch = next(iter(tl))
+        G, D, V = _params()
+        out = O.train_step(G, D, V, batch["ir"].double(), batch["rgb"].double(), O.AdamState(G), O.AdamState(D),
+                           grad_hook=_flat_hook(engine))
+        val = irc.validate_kaist(lambda x: x.repeat(1, 3, 1, 1) * 0.5, vl, "cpu")
+        nval = sum(b["ir"].shape[0] for b in vl)
+        torch.save({"idx": batch["idx"].tolist(), "G": G, "D": D, "loss_D": out["loss_D"],
+                    "loss_G": out["loss_G"], "val": val, "nval": nval, "ntrain": len(tl)},
+                   os.path.join(outdir, f"rank{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_two_ranks_match_single_process(tmp_path):
+    port = _free_port()
+    mp.spawn(_worker, args=(port, str(tmp_path)), nprocs=WORLD, join=True)
+    res = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(WORLD)]
+    # sharding: disjoint equal per-rank batches, every rank the same number of steps
+    idx = [i for r in res for i in r["idx"]]
+    assert all(len(r["idx"]) == PER_RANK for r in res)
+    assert len(set(idx)) == WORLD * PER_RANK
+    assert res[0]["ntrain"] == res[1]["ntrain"] == 8 // (WORLD * PER_RANK)
+    # DistributedSampler pads the ragged val set to 2 per rank
+    assert res[0]["nval"] + res[1]["nval"] == 4
+    # single-process reference step on the union batch
+    from oracle import step as O
+    ds = _dataset()
+    ir = torch.stack([ds[i]["ir"] for i in idx]).double()
+    rgb = torch.stack([ds[i]["rgb"] for i in idx]).double()
+    G, D, V = _params()
+    ref = O.train_step(G, D, V, ir, rgb, O.AdamState(G), O.AdamState(D))
+    for r in res:   # replicas stay identical and equal the global-batch step
+        for name, P in (("G", G), ("D", D)):
+            for k in P:
+                d = (r[name][k] - P[k]).abs().max().item()
+                assert d <= 1e-9 * max(1.0, P[k].abs().max().item()), (name, k, d)
+    # the mean of per-rank losses is the global-batch loss (equal shards)
+    for key in ("loss_D", "loss_G"):
+        m = sum(float(r[key]) for r in res) / WORLD
+        assert abs(m - float(ref[key])) <= 1e-9 * abs(float(ref[key])), key
+    # val L1: (sum, count) reduced over ranks == the mean over every item the shards saw
+    want = []
+    for r_ in range(WORLD):
+        ids = list(range(8, 11))
+        ids = (ids + ids[:1])[r_::WORLD]     # DistributedSampler(shuffle=False) padding
+        want += [(ds[i]["ir"].repeat(3, 1, 1) * 0.5 - ds[i]["rgb"]).abs().mean().item() for i in ids]
+    assert res[0]["val"] == pytest.approx(sum(want) / len(want), rel=1e-6)
+    assert res[0]["val"] == res[1]["val"]
+
+
+def test_grad_allreduce_single_process_is_identity():
+    import importlib
+    engine = importlib.import_module(pkg().__name__ + ".engine")
+    t = torch.arange(5.0)
+    assert engine.grad_allreduce(t) is t and torch.equal(t, torch.arange(5.0))
