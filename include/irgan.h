@@ -85,7 +85,10 @@ int irgan_weight_pack(const float* src, void* dst, int32_t dtype, int32_t Cout, 
                       irgan_stream_t st);
 
 /* ---- InstanceNorm (ir:154-165), per-(n,c) over H*W, eps 1e-5, no affine ---- */
-/* mr[n][c] = {mean, rstd}; work = 2*N*C doubles of scratch (zeroed inside). */
+/* Reductions are two-level and atomic-free: <= IRGAN_IN_PARTS block partials per
+ * (n, c) summed in fp64 in a fixed order. */
+enum { IRGAN_IN_PARTS = 64 };
+/* mr[n][c] = {mean, rstd}; work: IRGAN_IN_PARTS*N*C doubles of scratch. */
 int irgan_in_stats(const void* x, int32_t dtype, int32_t N, int32_t HW, int32_t C,
                    int32_t ld, int32_t off, double* work, float* mr, irgan_stream_t s);
 /* y = act((x - mean) * rstd) [+ res];  optional xhat output ([P][C], dtype). */
@@ -94,7 +97,7 @@ int irgan_in_apply(const void* x, int32_t dtype, int32_t N, int32_t HW, int32_t 
                    int32_t roff, void* y, int32_t ldy, int32_t yoff, void* xhat, irgan_stream_t s);
 /* Backward of y = act(IN(x)) [+ res] given the PRE-norm input x and its
  * (mean, rstd): xhat = (x - mean)*rstd, g = (dy [+ dy2]) * act'(xhat),
- * red[n][c] = {mean g, mean g*xhat}.  work: 2*N*C doubles (zeroed inside). */
+ * red[n][c] = {mean g, mean g*xhat}.  work: IRGAN_IN_PARTS*N*C doubles of scratch. */
 int irgan_in_bwd_reduce(const void* dy, int32_t dy_dtype, int32_t lddy, int32_t dyoff,
                         const void* dy2, int32_t dy2_dtype, int32_t lddy2, int32_t dy2off,
                         const void* x, int32_t x_dtype, int32_t ldx, int32_t xoff, int32_t act,
@@ -109,7 +112,7 @@ int irgan_in_bwd_apply(const void* dy, int32_t dy_dtype, int32_t lddy, int32_t d
                        void* dx, int32_t dx_dtype, int32_t lddx, int32_t dxoff, float* db,
                        irgan_stream_t s);
 /* db[c] += sum over pixels of g[p][c] (bias gradient), g slice (dtype, ld, off).
- * work: 128*C doubles of scratch. */
+ * work: IRGAN_IN_PARTS*C doubles of scratch. */
 int irgan_channel_sum(const void* g, int32_t dtype, int32_t P, int32_t C, int32_t ld,
                       int32_t off, float* db, double* work, irgan_stream_t s);
 

@@ -20,6 +20,9 @@ PAD_ZERO, PAD_REFLECT = 0, 1
 ACT_NONE, ACT_RELU, ACT_LRELU, ACT_TANH = 0, 1, 2, 3
 
 
+IN_PARTS = int(re.search(r"IRGAN_IN_PARTS\s*=\s*(\d+)", open(HEADER).read()).group(1))
+
+
 def _desc_fields():
     src = open(HEADER).read()
     body = re.search(r"typedef struct irgan_conv_desc \{(.*?)\} irgan_conv_desc;", src, re.S).group(1)

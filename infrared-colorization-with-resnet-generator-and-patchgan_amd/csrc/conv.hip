@@ -16,6 +16,10 @@
 
 extern "C" int irgan_conv_fwd_glds(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
                                    const void* mask, hipStream_t st);
+extern "C" int irgan_conv_fwd_halo(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
+                                   const void* mask, hipStream_t st);
+extern "C" int irgan_conv_wgrad_halo(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, int splitk,
+                                     hipStream_t st);
 extern "C" int irgan_conv_wgrad_glds(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, int splitk,
                                      hipStream_t st);
 
@@ -476,6 +480,10 @@ int launch_fwd(const irgan_conv_desc* d, const void* x, const void* w, const flo
     if constexpr (sizeof(T) == 2) {
         static const bool use_glds = !getenv("IRGAN_NO_GLDS");
         const bool narrow = (d->Cin == 8 || d->Cin == 16 || d->Cin == 32) && d->ldx % 8 == 0 && d->xoff % 8 == 0;
+        static const bool use_halo = !getenv("IRGAN_NO_HALO");
+        const int taps = d->KH * d->KW;
+        if (fast && use_halo && d->sy == 1 && d->sx == 1 && taps >= 2 && d->KH <= 4 && d->KW <= 4)
+            return irgan_conv_fwd_halo(d, x, w, bias, y, mask, st);
         if ((fast || narrow) && use_glds) return irgan_conv_fwd_glds(d, x, w, bias, y, mask, st);
     }
     const bool wide = d->Cout > 64;
@@ -507,6 +515,11 @@ int launch_wgrad(const irgan_conv_desc* d, const void* x, const void* dy, float*
     const bool fa = (d->Cout % EPC == 0) && (d->ldy % EPC == 0) && (d->yoff % EPC == 0);
     const bool fb = (d->Cin % 64 == 0) && (d->ldx % EPC == 0) && (d->xoff % EPC == 0);
     if constexpr (sizeof(T) == 2) {
+        static const bool use_wgh = !getenv("IRGAN_NO_WGRAD_HALO");
+        if (use_wgh) {
+            const int rc = irgan_conv_wgrad_halo(d, x, dy, dw, splitk, st);
+            if (rc != IRGAN_EUNSUPPORTED) return rc;
+        }
         static const bool use_glds = !getenv("IRGAN_NO_GLDS");
         if (use_glds && fb && (d->Cout % 64 == 0 || d->Cout < 64) && d->ldy % 8 == 0 && d->yoff % 8 == 0)
             return irgan_conv_wgrad_glds(d, x, dy, dw, splitk, st);

@@ -36,6 +36,16 @@ IRGAN_HD void wait_vmcnt() {
     else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
 }
 
+// XCD-aware tile order.  Workgroups are dealt round-robin to the 8 XCDs
+// (b % 8), each with its own L2.  With nb % 8 == 0 the remap hands XCD k the
+// contiguous logical range [k*nb/8, (k+1)*nb/8), so tiles that share input rows
+// (neighbouring pixel tiles and their halos, the N-tiles of one pixel tile)
+// run at the same time on the same L2.  Speed only: any order is correct.
+__device__ __forceinline__ int xcd_tile(int b, int nb, int swz) {
+    if (!swz || (nb & 7)) return b;
+    return (b & 7) * (nb >> 3) + (b >> 3);
+}
+
 IRGAN_HD float act_fn(float v, int act) {
     if (act == IRGAN_ACT_RELU) return v > 0.f ? v : 0.f;
     if (act == IRGAN_ACT_LRELU) return v > 0.f ? v : 0.2f * v;
@@ -48,7 +58,7 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_glds_kernel(const irgan_conv_
                                                                const bf16_t* __restrict__ w,
                                                                const float* __restrict__ bias, void* __restrict__ y,
                                                                const void* __restrict__ mask,
-                                                               const bf16_t* __restrict__ zero) {
+                                                               const bf16_t* __restrict__ zero, int ntn, int swz) {
     constexpr int BM = 256, STAGES = 3;
     constexpr int ABYTES = BM * 128, STAGE = ABYTES + BN * 128;
     constexpr int MI = 4, NJ = BN / 32;  // wave tile 64 x BN/2
@@ -62,8 +72,10 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_glds_kernel(const irgan_conv_
     const long M = (long)d.N * HoWo;
     const int taps = d.KH * d.KW;
     const int K = (taps * d.Cin + 63) / 64 * 64;  // weight row stride (taps zero-padded)
-    const long m0 = (long)blockIdx.x * BM;
-    const int n0 = blockIdx.y * BN;
+    // 1-D grid, N-tiles fastest: the tiles of one pixel block are adjacent
+    const int t = xcd_tile(blockIdx.x, gridDim.x, swz);
+    const long m0 = (long)(t / ntn) * BM;
+    const int n0 = (t % ntn) * BN;
     const int sub = lane >> 3;
     const int chunk = (lane & 7) ^ sub;  // source chunk for this lane's LDS slot (row & 7 == sub)
     // K-tile = 64 channels of one tap (Cin % 64 == 0) or 64/Cin taps of a narrow
@@ -208,12 +220,15 @@ extern "C" int irgan_conv_fwd_glds(const irgan_conv_desc* d, const void* x, cons
     static bf16_t* zero = nullptr;  // immutable after first lookup
     if (!zero && hipGetSymbolAddress((void**)&zero, HIP_SYMBOL(g_irgan_zero_page)) != hipSuccess)
         return IRGAN_EUNSUPPORTED;
+    static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
     if (d->Cout > 64) {
-        dim3 grid(irgan_cdiv(M, 256), irgan_cdiv(d->Cout, 128));
-        conv_fwd_glds_kernel<128><<<grid, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, y, mask, zero);
+        const int ntn = irgan_cdiv(d->Cout, 128);
+        conv_fwd_glds_kernel<128><<<irgan_cdiv(M, 256) * ntn, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w,
+                                                                            bias, y, mask, zero, ntn, swz);
     } else {
-        dim3 grid(irgan_cdiv(M, 256), irgan_cdiv(d->Cout, 64));
-        conv_fwd_glds_kernel<64><<<grid, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, y, mask, zero);
+        const int ntn = irgan_cdiv(d->Cout, 64);
+        conv_fwd_glds_kernel<64><<<irgan_cdiv(M, 256) * ntn, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w,
+                                                                           bias, y, mask, zero, ntn, swz);
     }
     IRGAN_LAUNCH_CHECK();
     return 0;
@@ -264,7 +279,8 @@ IRGAN_HD uint4 tr_frag(const char* img, int k0, int m0, int lane) {
 template <int BMC, int BNC>  // co tile, ci tile (128 or 64)
 __global__ __launch_bounds__(512, 2) void conv_wgrad_glds_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
                                                                  const bf16_t* __restrict__ dy, float* __restrict__ dw,
-                                                                 int kchunk, const bf16_t* __restrict__ zero) {
+                                                                 int kchunk, const bf16_t* __restrict__ zero,
+                                                                 int ntx, int nty, int swz) {
     constexpr int KP = 64, STAGES = 3;
     constexpr int RA = BMC * 2, RBB = BNC * 2;          // bytes per pixel row in each image
     constexpr int ABYTES = KP * RA, STAGE = ABYTES + KP * RBB;
@@ -280,8 +296,12 @@ __global__ __launch_bounds__(512, 2) void conv_wgrad_glds_kernel(const irgan_con
     const int HoWo = d.Ho * d.Wo;
     const long P = (long)d.N * HoWo;
     const int K = d.KH * d.KW * d.Cin;
-    const int co0 = blockIdx.x * BMC, n0 = blockIdx.y * BNC;
-    const long pb = (long)blockIdx.z * kchunk;
+    // 1-D grid ordered (split, k-tile, co-tile): the blocks of one pixel range
+    // read the same dY / X rows and share an XCD after the remap
+    const int t = xcd_tile(blockIdx.x, gridDim.x, swz);
+    const int bx = t % ntx, by = (t / ntx) % nty, bz = t / (ntx * nty);
+    const int co0 = bx * BMC, n0 = by * BNC;
+    const long pb = (long)bz * kchunk;
     const long pe = min(P, pb + kchunk);
     if (pb >= pe) return;
     const int tap = n0 / d.Cin, cin0 = n0 - tap * d.Cin;
@@ -391,16 +411,26 @@ extern "C" int irgan_conv_wgrad_glds(const irgan_conv_desc* d, const void* x, co
         if (splitk > maxs) splitk = (int)maxs;
         if (splitk < 1) splitk = 1;
     }
+    static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
+    // prefer a split count that makes the grid a multiple of 8 (XCD remap)
+    if (swz && splitk > 1 && (tiles * splitk) % 8) {
+        for (int s2 = splitk; s2 >= 1 && s2 >= splitk - 7; --s2)
+            if ((tiles * s2) % 8 == 0) { splitk = s2; break; }
+    }
     long kc = (P + splitk - 1) / splitk;
     kc = (kc + 63) / 64 * 64;
     splitk = (int)((P + kc - 1) / kc);
-    dim3 g(irgan_cdiv(d->Cout, BMC), K / BNC, splitk);
+    const int ntx = irgan_cdiv(d->Cout, BMC), nty = K / BNC;
+    const int nb = ntx * nty * splitk;
     const bf16_t* xp = (const bf16_t*)x;
     const bf16_t* dp = (const bf16_t*)dy;
-    if (BMC == 128 && BNC == 128) conv_wgrad_glds_kernel<128, 128><<<g, 512, 0, st>>>(*d, xp, dp, dw, (int)kc, zero);
-    else if (BMC == 128) conv_wgrad_glds_kernel<128, 64><<<g, 512, 0, st>>>(*d, xp, dp, dw, (int)kc, zero);
-    else if (BNC == 128) conv_wgrad_glds_kernel<64, 128><<<g, 512, 0, st>>>(*d, xp, dp, dw, (int)kc, zero);
-    else conv_wgrad_glds_kernel<64, 64><<<g, 512, 0, st>>>(*d, xp, dp, dw, (int)kc, zero);
+    if (BMC == 128 && BNC == 128)
+        conv_wgrad_glds_kernel<128, 128><<<nb, 512, 0, st>>>(*d, xp, dp, dw, (int)kc, zero, ntx, nty, swz);
+    else if (BMC == 128)
+        conv_wgrad_glds_kernel<128, 64><<<nb, 512, 0, st>>>(*d, xp, dp, dw, (int)kc, zero, ntx, nty, swz);
+    else if (BNC == 128)
+        conv_wgrad_glds_kernel<64, 128><<<nb, 512, 0, st>>>(*d, xp, dp, dw, (int)kc, zero, ntx, nty, swz);
+    else conv_wgrad_glds_kernel<64, 64><<<nb, 512, 0, st>>>(*d, xp, dp, dw, (int)kc, zero, ntx, nty, swz);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }

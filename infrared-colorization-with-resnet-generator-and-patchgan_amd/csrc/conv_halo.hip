@@ -1,0 +1,238 @@
+// bf16 stride-1 convolution with a resident input halo (forward and the
+// stride-1 / per-phase backward-data launches).
+//
+// The per-tap implicit GEMM of conv_glds.hip streams one 256-pixel x 64-channel
+// A tile per tap, so a 3x3 conv moves its input through L2 -> LDS nine times;
+// profiled on MI355X that kernel sits at ~20 GB/s/CU of LDS-DMA with the waves
+// parked on vmcnt 48% of the time, i.e. it is bound by L2->LDS bytes, not MFMA.
+// Here a block owns a 16x16 output patch of one image: per 64-channel chunk it
+// DMAs the (16+KH-1)x(16+KW-1) input halo into LDS ONCE (reflect / zero padding
+// folded into the source address) and runs all KH*KW taps against it as LDS
+// address shifts; only the weight tile (BN x 64 per tap) streams per K-step.
+// L2->LDS bytes per chunk drop from taps*48 KiB to ~41 KiB + taps*16 KiB.
+//
+// 512 threads = 8 waves (4 pixel-row groups x 2 channel halves), block tile
+// 256 pixels x BN, K-step = 64 channels of one tap, mfma_f32_16x16x32_bf16.
+// Pipeline: K-steps (chunk, tap) flattened; weights of step k+2 are issued
+// while k runs, the halo of chunk c+1 as soon as chunk c starts (a whole
+// chunk of lead time).  Halo: two buffers (chunk parity), weights: 3-stage
+// ring.  Requires taps >= 2.
+#include "common.h"
+
+namespace {
+
+// zero page for padded / out-of-range halo rows (this translation unit's own copy)
+__device__ __attribute__((aligned(4096))) bf16_t g_halo_zero_page[2048];
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) const void gbl_cvoid;
+
+IRGAN_HD int lds_off(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+
+IRGAN_HD void glds16(const void* src, char* lds_base) {
+    __builtin_amdgcn_global_load_lds((gbl_cvoid*)src, (lds_void*)lds_base, 16, 0, 0);
+}
+
+template <int N>
+IRGAN_HD void wait_vmcnt() {
+    static_assert(N >= 0 && N <= 15, "vmcnt");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ int xcd_tile(int b, int nb, int swz) {
+    if (!swz || (nb & 7)) return b;
+    return (b & 7) * (nb >> 3) + (b >> 3);
+}
+
+IRGAN_HD float act_fn(float v, int act) {
+    if (act == IRGAN_ACT_RELU) return v > 0.f ? v : 0.f;
+    if (act == IRGAN_ACT_LRELU) return v > 0.f ? v : 0.2f * v;
+    if (act == IRGAN_ACT_TANH) return tanhf(v);
+    return v;
+}
+
+constexpr int PH = 16, PW = 16;   // output patch
+constexpr int HROWS = 384;        // halo rows capacity: (16+3)*(16+3) = 361 <= 384 = 48 pieces
+constexpr int HU = HROWS / 8 / 8; // halo pieces per wave (6)
+
+template <int BN>
+__global__ __launch_bounds__(512, 1) void conv_halo_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
+                                                           const bf16_t* __restrict__ w,
+                                                           const float* __restrict__ bias, void* __restrict__ y,
+                                                           const void* __restrict__ mask,
+                                                           const bf16_t* __restrict__ zero, int ntn, int tpx, int tpy,
+                                                           int swz) {
+    constexpr int STAGES = 3;
+    constexpr int HBYTES = HROWS * 128, BBYTES = BN * 128;
+    constexpr int MI = 4, NJ = BN / 32, BU = BN / 64;
+    __shared__ __attribute__((aligned(1024))) char smem[2 * HBYTES + STAGES * BBYTES];
+    char* const sH = smem;
+    char* const sB = smem + 2 * HBYTES;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid >> 1, wn = wid & 1;
+    int t = xcd_tile(blockIdx.x, gridDim.x, swz);
+    const int nt = t % ntn;
+    t /= ntn;
+    const int pxi = t % tpx;
+    t /= tpx;
+    const int pyi = t % tpy;
+    const int img = t / tpy;
+    const int py0 = pyi * PH, px0 = pxi * PW, n0 = nt * BN;
+    const int taps = d.KH * d.KW;
+    const int HWd = PW + d.KW - 1;
+    const int hrows = (PH + d.KH - 1) * HWd;
+    const int Kw = taps * d.Cin;  // weight row stride (Cin % 64 == 0 -> no tap padding)
+    const int nk = (d.Cin / 64) * taps;
+    const int sub = lane >> 3;
+    const int chunk = (lane & 7) ^ sub;  // source chunk for this lane's LDS slot (row & 7 == sub)
+    const bool reflect = d.pad_mode == IRGAN_PAD_REFLECT;
+
+    // halo rows this lane loads: piece (wid*HU + u), row sub of the piece
+    long h_off[HU];
+#pragma unroll
+    for (int u = 0; u < HU; ++u) {
+        const int h = (wid * HU + u) * 8 + sub;
+        const int hy = h / HWd, hx = h - hy * HWd;
+        int iy = py0 + hy + d.c0y, ix = px0 + hx + d.c0x;
+        if (reflect) {
+            iy = reflect_idx(iy, d.H);
+            ix = reflect_idx(ix, d.W);
+        }
+        const bool ok = (h < hrows) & ((unsigned)iy < (unsigned)d.H) & ((unsigned)ix < (unsigned)d.W);
+        h_off[u] = ok ? (((long)img * d.H + iy) * d.W + ix) * d.ldx + d.xoff + chunk * 8 : -1;
+    }
+    const bf16_t* b_src[BU];
+#pragma unroll
+    for (int u = 0; u < BU; ++u) {
+        const int co = n0 + (wid * BU + u) * 8 + sub;
+        b_src[u] = co < d.Cout ? w + (long)co * Kw + chunk * 8 : nullptr;
+    }
+
+    auto issue_halo = [&](int c) {
+        char* dst = sH + (c & 1) * HBYTES + wid * HU * 1024;
+#pragma unroll
+        for (int u = 0; u < HU; ++u) glds16(h_off[u] >= 0 ? x + h_off[u] + c * 64 : zero, dst + u * 1024);
+    };
+    auto issue_w = [&](int kt, int stage) {
+        const int c = kt / taps, tp = kt - c * taps;
+        const int kcol = tp * d.Cin + c * 64;
+#pragma unroll
+        for (int u = 0; u < BU; ++u)
+            glds16(b_src[u] ? b_src[u] + kcol : zero, sB + stage * BBYTES + (wid * BU + u) * 1024);
+    };
+
+    f32x4 acc[MI][NJ];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // Issue order: halo(0), W(0), W(1); then at the top of step kt (after its
+    // barrier): halo(c+1) when kt is the first tap of chunk c (its buffer held
+    // chunk c-1, retired by that barrier), then W(kt+2).  So the halo of chunk
+    // c+1 has a whole chunk of lead time, and the only loads younger than W(kt)
+    // are W(kt+1) and a halo issued at step kt-1.
+    const int nchunk = d.Cin / 64;
+    issue_halo(0);
+    issue_w(0, 0);
+    if (nk > 1) issue_w(1, 1);
+    int c = 0, tp = 0;  // chunk / tap of step kt
+    for (int kt = 0; kt < nk; ++kt) {
+        if (kt + 1 < nk) {
+            const int pk = kt - 1;  // did step kt-1 issue a halo (after W(kt))?
+            if (pk >= 0 && pk % taps == 0 && pk / taps + 1 < nchunk) wait_vmcnt<BU + HU>();
+            else wait_vmcnt<BU>();
+        } else {
+            wait_vmcnt<0>();
+        }
+        __builtin_amdgcn_s_barrier();
+        if (tp == 0 && c + 1 < nchunk) issue_halo(c + 1);
+        if (kt + 2 < nk) issue_w(kt + 2, (kt + 2) % STAGES);
+        const char* Hb = sH + (c & 1) * HBYTES;
+        const char* B = sB + (kt % STAGES) * BBYTES;
+        const int ty = tp / d.KW, tx = tp - ty * d.KW;
+        const int hbase = (wm * 4 + ty) * HWd + (lane & 15) + tx;  // halo row of fragment i = hbase + i*HWd
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            uint4 af[MI], bfr[NJ];
+            const int ch = h * 4 + (lane >> 4);
+#pragma unroll
+            for (int i = 0; i < MI; ++i) af[i] = *(const uint4*)(Hb + lds_off(hbase + i * HWd, ch));
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) bfr[j] = *(const uint4*)(B + lds_off(wn * (BN / 2) + j * 16 + (lane & 15), ch));
+#pragma unroll
+            for (int i = 0; i < MI; ++i)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[i]),
+                                                                        __builtin_bit_cast(bf16x8_t, bfr[j]),
+                                                                        acc[i][j], 0, 0, 0);
+        }
+        if (++tp == taps) {
+            tp = 0;
+            ++c;
+        }
+    }
+
+    // epilogue: fragment i = patch row wm*4+i, C[row=(lane>>4)*4+r] = patch column, col = channel
+    const bool out_f32 = d.out_dtype == IRGAN_F32;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+        const int oy = py0 + wm * 4 + i;
+        if (oy >= d.Ho) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int ox = px0 + (lane >> 4) * 4 + r;
+            if (ox >= d.Wo) continue;
+            const long pix = ((long)img * d.OH + oy * d.omy + d.ooy) * d.OW + ox * d.omx + d.oox;
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int co = n0 + wn * (BN / 2) + j * 16 + (lane & 15);
+                if (co >= d.Cout) continue;
+                float v = acc[i][j][r] + (bias ? bias[co] : 0.f);
+                v = act_fn(v, d.act);
+                if (mask) {
+                    const float mv = bf2f(((const bf16_t*)mask)[pix * d.ldm + d.moff + co]);
+                    v *= mv > 0.f ? 1.f : (d.mask_act == 2 ? 0.2f : 0.f);
+                }
+                const long off = pix * d.ldy + d.yoff + co;
+                if (out_f32) {
+                    float* yp = (float*)y;
+                    yp[off] = d.accumulate ? yp[off] + v : v;
+                } else {
+                    bf16_t* yp = (bf16_t*)y;
+                    yp[off] = f2bf(d.accumulate ? bf2f(yp[off]) + v : v);
+                }
+            }
+        }
+    }
+}
+
+}  // namespace
+
+// Preconditions (checked by the dispatcher in conv.hip): bf16, sy = sx = 1,
+// Cin % 64 == 0, ldx % 8 == 0, xoff % 8 == 0, 2 <= KH*KW, KH, KW <= 4.
+extern "C" int irgan_conv_fwd_halo(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
+                                   const void* mask, hipStream_t st) {
+    if ((long)d->N * d->Ho * d->Wo <= 0 || d->Cout <= 0) return 0;
+    if (d->sy != 1 || d->sx != 1 || d->Cin % 64 || d->KH > 4 || d->KW > 4 || d->KH * d->KW < 2)
+        return IRGAN_EUNSUPPORTED;
+    static bf16_t* zero = nullptr;
+    if (!zero && hipGetSymbolAddress((void**)&zero, HIP_SYMBOL(g_halo_zero_page)) != hipSuccess)
+        return IRGAN_EUNSUPPORTED;
+    static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
+    const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH);
+    if (d->Cout > 64) {
+        const int ntn = irgan_cdiv(d->Cout, 128);
+        conv_halo_kernel<128><<<d->N * tpy * tpx * ntn, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, y,
+                                                                     mask, zero, ntn, tpx, tpy, swz);
+    } else {
+        const int ntn = irgan_cdiv(d->Cout, 64);
+        conv_halo_kernel<64><<<d->N * tpy * tpx * ntn, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, y,
+                                                                    mask, zero, ntn, tpx, tpy, swz);
+    }
+    IRGAN_LAUNCH_CHECK();
+    return 0;
+}

@@ -4,16 +4,19 @@
 // 417-418, 601-624 and their autograd backward.
 //
 // HBM-bound: every thread owns 8 consecutive channels (one 16-byte bf16 load /
-// two 16-byte fp32 loads per pixel) and walks rows with 4 loads in flight; a
-// block covers a run of rows of one image, reduces its partial sums through
-// LDS and issues one fp64 atomic per (n, c).  A finalize launch turns the fp64
-// sums into fp32 (mean, rstd) or (mean g, mean g*xhat).
+// two 16-byte fp32 loads per pixel) and walks >= 8 rows; a block covers a run of
+// rows of one image and reduces its partial sums through LDS.  Reductions are
+// two-level and atomic-free: each block stores one float2 partial per channel
+// (<= IN_PARTS blocks per image), and the finalize launch sums the partials of
+// each (n, c) in fp64, in a fixed order (deterministic), into fp32 (mean, rstd)
+// or (mean g, mean g*xhat).
 #include "common.h"
 
 namespace {
 
 constexpr int TPB = 256;
-constexpr int V = 8;  // channels per thread
+constexpr int V = 8;          // channels per thread
+constexpr int IN_PARTS = 64;  // max blocks (partials) per image; work = IN_PARTS*N*C doubles
 
 IRGAN_HD void ld8(const void* p, int dt, long i, float* o) {
     if (dt == IRGAN_BF16) {
@@ -84,7 +87,7 @@ template <int MODE, int VW>
 __global__ __launch_bounds__(TPB) void rows_kernel(Slice X, Slice DY, Slice DY2, int act, const float* __restrict__ mr,
                                                    const float* __restrict__ red, void* __restrict__ dx, int dxdt,
                                                    int lddx, int dxoff, int HW, int C, int rows_per_block,
-                                                   double* __restrict__ work, float* __restrict__ db) {
+                                                   float2* __restrict__ part, float* __restrict__ db) {
     __shared__ float s0[TPB * VW], s1[TPB * VW];
     const int n = blockIdx.y;
     const int r0 = blockIdx.x * rows_per_block;
@@ -155,9 +158,8 @@ __global__ __launch_bounds__(TPB) void rows_kernel(Slice X, Slice DY, Slice DY2,
                 }
                 if (MODE == 2 || MODE == 3) {
                     atomicAdd(db + c + k, t0);
-                } else {
-                    atomicAdd(work + ((long)n * C + c + k) * 2 + 0, (double)t0);
-                    atomicAdd(work + ((long)n * C + c + k) * 2 + 1, (double)t1);
+                } else {  // partial of block b of image n: part[(n*nb + b)*C + c]
+                    part[((long)n * gridDim.x + blockIdx.x) * C + c + k] = make_float2(t0, t1);
                 }
             }
         }
@@ -165,10 +167,18 @@ __global__ __launch_bounds__(TPB) void rows_kernel(Slice X, Slice DY, Slice DY2,
     }
 }
 
-__global__ void finalize_kernel(const double* __restrict__ work, float* __restrict__ mr, int NC, int HW, int mode) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= NC) return;
-    double s = work[2 * i], q = work[2 * i + 1];
+// one thread per (n, c): fp64 sum of the nb block partials of image n
+__global__ void finalize_kernel(const float2* __restrict__ part, float* __restrict__ mr, int N, int C, int nb, int HW,
+                                int mode) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N * C) return;
+    const int n = i / C, c = i - n * C;
+    double s = 0.0, q = 0.0;
+    for (int b = 0; b < nb; ++b) {
+        const float2 v = part[((long)n * nb + b) * C + c];
+        s += v.x;
+        q += v.y;
+    }
     double mean = s / HW;
     if (mode == 0) {
         double var = q / HW - mean * mean;
@@ -224,30 +234,35 @@ bool vec_ok(int C, std::initializer_list<int> lds) {
     return true;
 }
 
-int rows_for(long HW, int N, int RP) {
-    long want = (2048 + N - 1) / (N > 0 ? N : 1);  // ~2048 blocks over the grid
-    long r = (HW + want - 1) / want;
-    long minr = 4L * RP;
-    if (r < minr) r = minr;
-    return (int)r;
-}
-
 int rp_of(int C, int VW) {
     int cl = (C + VW - 1) / VW;
     if (cl > TPB) cl = TPB;
     return TPB / cl;
 }
 
+// blocks per image: ~2048 blocks over the grid, >= 8 rows per thread, <= IN_PARTS
+int blocks_per_image(long HW, int N, int RP) {
+    long nb = (2048 + N - 1) / (N > 0 ? N : 1);
+    const long maxnb = (HW + 8L * RP - 1) / (8L * RP);
+    if (nb > maxnb) nb = maxnb;
+    if (nb > IN_PARTS) nb = IN_PARTS;
+    if (nb < 1) nb = 1;
+    return (int)nb;
+}
+
 template <int MODE>
 int launch_rows(Slice X, Slice DY, Slice DY2, int act, const float* mr, const float* red, void* dx, int dxdt, int lddx,
-                int dxoff, int N, int HW, int C, double* work, float* db, bool vec, hipStream_t st) {
+                int dxoff, int N, int HW, int C, float2* part, float* db, bool vec, hipStream_t st, int* nb_out) {
     const int VW = vec ? V : 1;
-    const int rows = rows_for(HW, N, rp_of(C, VW));
-    dim3 g(irgan_cdiv(HW, rows), N);
+    int nb = blocks_per_image(HW, N, rp_of(C, VW));
+    const int rows = irgan_cdiv(HW, nb);
+    nb = irgan_cdiv(HW, rows);
+    dim3 g(nb, N);
     if (vec)
-        rows_kernel<MODE, V><<<g, TPB, 0, st>>>(X, DY, DY2, act, mr, red, dx, dxdt, lddx, dxoff, HW, C, rows, work, db);
+        rows_kernel<MODE, V><<<g, TPB, 0, st>>>(X, DY, DY2, act, mr, red, dx, dxdt, lddx, dxoff, HW, C, rows, part, db);
     else
-        rows_kernel<MODE, 1><<<g, TPB, 0, st>>>(X, DY, DY2, act, mr, red, dx, dxdt, lddx, dxoff, HW, C, rows, work, db);
+        rows_kernel<MODE, 1><<<g, TPB, 0, st>>>(X, DY, DY2, act, mr, red, dx, dxdt, lddx, dxoff, HW, C, rows, part, db);
+    if (nb_out) *nb_out = nb;
     return 0;
 }
 
@@ -256,10 +271,12 @@ int launch_rows(Slice X, Slice DY, Slice DY2, int act, const float* mr, const fl
 extern "C" int irgan_in_stats(const void* x, int32_t dtype, int32_t N, int32_t HW, int32_t C, int32_t ld,
                               int32_t off, double* work, float* mr, irgan_stream_t s) {
     hipStream_t st = (hipStream_t)s;
-    hipMemsetAsync(work, 0, sizeof(double) * 2 * (size_t)N * C, st);
+    if ((long)N * HW * C <= 0) return 0;
     Slice X{x, dtype, ld, off}, Z{nullptr, 0, 0, 0};
-    launch_rows<0>(X, Z, Z, 0, nullptr, nullptr, nullptr, 0, 0, 0, N, HW, C, work, nullptr, vec_ok(C, {ld, off}), st);
-    finalize_kernel<<<irgan_cdiv((long)N * C, 256), 256, 0, st>>>(work, mr, N * C, HW, 0);
+    int nb = 1;
+    launch_rows<0>(X, Z, Z, 0, nullptr, nullptr, nullptr, 0, 0, 0, N, HW, C, (float2*)work, nullptr,
+                   vec_ok(C, {ld, off}), st, &nb);
+    finalize_kernel<<<irgan_cdiv((long)N * C, 256), 256, 0, st>>>((const float2*)work, mr, N, C, nb, HW, 0);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }
@@ -286,11 +303,12 @@ extern "C" int irgan_in_bwd_reduce(const void* dy, int32_t dy_dtype, int32_t ldd
                                    int32_t ldx, int32_t xoff, int32_t act, int32_t N, int32_t HW, int32_t C,
                                    const float* mr, double* work, float* red, irgan_stream_t s) {
     hipStream_t st = (hipStream_t)s;
-    hipMemsetAsync(work, 0, sizeof(double) * 2 * (size_t)N * C, st);
+    if ((long)N * HW * C <= 0) return 0;
     const bool vec = vec_ok(C, {lddy, dyoff, ldx, xoff}) && (!dy2 || vec_ok(C, {lddy2, dy2off}));
     Slice X{x, x_dtype, ldx, xoff}, DY{dy, dy_dtype, lddy, dyoff}, DY2{dy2, dy2_dtype, lddy2, dy2off};
-    launch_rows<1>(X, DY, DY2, act, mr, nullptr, nullptr, 0, 0, 0, N, HW, C, work, nullptr, vec, st);
-    finalize_kernel<<<irgan_cdiv((long)N * C, 256), 256, 0, st>>>(work, red, N * C, HW, 1);
+    int nb = 1;
+    launch_rows<1>(X, DY, DY2, act, mr, nullptr, nullptr, 0, 0, 0, N, HW, C, (float2*)work, nullptr, vec, st, &nb);
+    finalize_kernel<<<irgan_cdiv((long)N * C, 256), 256, 0, st>>>((const float2*)work, red, N, C, nb, HW, 1);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }
@@ -302,31 +320,30 @@ extern "C" int irgan_in_bwd_apply(const void* dy, int32_t dy_dtype, int32_t lddy
                                   int32_t dxoff, float* db, irgan_stream_t s) {
     const bool vec = vec_ok(C, {lddy, dyoff, ldx, xoff, lddx, dxoff}) && (!dy2 || vec_ok(C, {lddy2, dy2off}));
     Slice X{x, x_dtype, ldx, xoff}, DY{dy, dy_dtype, lddy, dyoff}, DY2{dy2, dy2_dtype, lddy2, dy2off};
-    launch_rows<2>(X, DY, DY2, act, mr, red, dx, dx_dtype, lddx, dxoff, N, HW, C, nullptr, db, vec, (hipStream_t)s);
+    launch_rows<2>(X, DY, DY2, act, mr, red, dx, dx_dtype, lddx, dxoff, N, HW, C, nullptr, db, vec, (hipStream_t)s,
+                   nullptr);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }
 
-__global__ void colsum_finalize_kernel(const double* __restrict__ work, float* __restrict__ db, int G, int C) {
+__global__ void colsum_finalize_kernel(const float2* __restrict__ part, float* __restrict__ db, int nb, int C) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
     double t = 0.0;
-    for (int g = 0; g < G; ++g) t += work[((long)g * C + c) * 2];
+    for (int b = 0; b < nb; ++b) t += part[(long)b * C + c].x;
     db[c] += (float)t;
 }
 
 extern "C" int irgan_channel_sum(const void* g, int32_t dtype, int32_t P, int32_t C, int32_t ld, int32_t off,
                                  float* db, double* work, irgan_stream_t s) {
     if (P <= 0) return 0;
-    // P rows viewed as G row-groups ("images") so the fp64 atomics spread over G*C
-    // addresses instead of all blocks hammering the same C words; G divides P.
+    // P rows as one "image": <= IN_PARTS block partials, summed in order (no atomics)
     hipStream_t st = (hipStream_t)s;
-    int G = 64;
-    while (G > 1 && P % G) G >>= 1;
-    hipMemsetAsync(work, 0, sizeof(double) * 2 * (size_t)G * C, st);
     Slice X{g, dtype, ld, off}, Z{nullptr, 0, 0, 0};
-    launch_rows<0>(X, Z, Z, 0, nullptr, nullptr, nullptr, 0, 0, 0, G, P / G, C, work, nullptr, vec_ok(C, {ld, off}), st);
-    colsum_finalize_kernel<<<irgan_cdiv(C, 256), 256, 0, st>>>(work, db, G, C);
+    int nb = 1;
+    launch_rows<0>(X, Z, Z, 0, nullptr, nullptr, nullptr, 0, 0, 0, 1, P, C, (float2*)work, nullptr,
+                   vec_ok(C, {ld, off}), st, &nb);
+    colsum_finalize_kernel<<<irgan_cdiv(C, 256), 256, 0, st>>>((const float2*)work, db, nb, C);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }

@@ -19,58 +19,83 @@ constexpr int TPB = 256;
 // Threads own 8 channels (16-byte loads) when the slices allow.
 // ---------------------------------------------------------------------------
 template <int VW>
+IRGAN_HD void ldvec(const void* p, int dt, long i, float* o) {
+    if constexpr (VW == 8) {
+        if (dt == IRGAN_BF16) {
+            const uint4 u = *(const uint4*)((const bf16_t*)p + i);
+            const uint32_t q[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                o[2 * k] = __uint_as_float(q[k] << 16);
+                o[2 * k + 1] = __uint_as_float(q[k] & 0xffff0000u);
+            }
+        } else {
+            const float4 a = *(const float4*)((const float*)p + i), b = *(const float4*)((const float*)p + i + 4);
+            o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+        }
+    } else {
+        o[0] = ldv(p, dt, i);
+    }
+}
+template <int VW>
+IRGAN_HD void stvec(void* p, int dt, long i, const float* v) {
+    if constexpr (VW == 8) {
+        if (dt == IRGAN_BF16) {
+            uint4 u;
+            u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+            u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+            u.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+            u.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+            *(uint4*)((bf16_t*)p + i) = u;
+        } else {
+            *(float4*)((float*)p + i) = make_float4(v[0], v[1], v[2], v[3]);
+            *(float4*)((float*)p + i + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        }
+    } else {
+        stv(p, dt, i, v[0]);
+    }
+}
+
+// One block row per output image row (blockIdx.y = n*Hout + oy): the vertical
+// taps are block-uniform (scalar loads), threads run over (ox, channel group)
+// with 32-bit index math and 16-byte loads/stores.
+template <int VW>
 __global__ __launch_bounds__(TPB) void sep_kernel(const void* __restrict__ in, int idt, int Hin, int Win, int C,
                                                   int ldi, int offi, void* __restrict__ out, int odt, int Hout,
                                                   int Wout, int ldo, int offo, const int* __restrict__ ty,
                                                   const float* __restrict__ wy, const int* __restrict__ tx,
-                                                  const float* __restrict__ wx, int T, int accumulate, long total) {
+                                                  const float* __restrict__ wx, int T, int accumulate) {
     const int CV = C / VW;
-    for (long idx = blockIdx.x * (long)TPB + threadIdx.x; idx < total; idx += (long)gridDim.x * TPB) {
-        long t = idx;
-        const int c = (int)(t % CV) * VW; t /= CV;
-        const int ox = (int)(t % Wout); t /= Wout;
-        const int oy = (int)(t % Hout);
-        const int n = (int)(t / Hout);
-        float acc[VW];
+    const int row = blockIdx.y;
+    const int n = row / Hout, oy = row - n * Hout;
+    const int idx = blockIdx.x * TPB + threadIdx.x;
+    if (idx >= Wout * CV) return;
+    const int ox = idx / CV, c = (idx - ox * CV) * VW;
+    float acc[VW];
 #pragma unroll
-        for (int k = 0; k < VW; ++k) acc[k] = 0.f;
-        for (int i = 0; i < T; ++i) {
-            const float w1 = wy[oy * T + i];
-            if (w1 == 0.f) continue;
-            const long rowb = ((long)n * Hin + ty[oy * T + i]) * Win;
-            for (int j = 0; j < T; ++j) {
-                const float w2 = wx[ox * T + j];
-                if (w2 == 0.f) continue;
-                const float w = w1 * w2;
-                const long e = (rowb + tx[ox * T + j]) * ldi + offi + c;
-                if constexpr (VW == 8) {
-                    float v[8];
-                    if (idt == IRGAN_BF16) {
-                        const uint4 u = *(const uint4*)((const bf16_t*)in + e);
-                        const uint32_t q[4] = {u.x, u.y, u.z, u.w};
+    for (int k = 0; k < VW; ++k) acc[k] = 0.f;
+    for (int i = 0; i < T; ++i) {
+        const float w1 = wy[oy * T + i];
+        if (w1 == 0.f) continue;
+        const long rowb = ((long)n * Hin + ty[oy * T + i]) * Win;
+        for (int j = 0; j < T; ++j) {
+            const float w2 = wx[ox * T + j];
+            if (w2 == 0.f) continue;
+            const float w = w1 * w2;
+            float v[VW];
+            ldvec<VW>(in, idt, (rowb + tx[ox * T + j]) * ldi + offi + c, v);
 #pragma unroll
-                        for (int k = 0; k < 4; ++k) {
-                            v[2 * k] = __uint_as_float(q[k] << 16);
-                            v[2 * k + 1] = __uint_as_float(q[k] & 0xffff0000u);
-                        }
-                    } else {
-                        const float4 a = *(const float4*)((const float*)in + e), b = *(const float4*)((const float*)in + e + 4);
-                        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-                    }
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) acc[k] += w * v[k];
-                } else {
-                    acc[0] += w * ldv(in, idt, e);
-                }
-            }
-        }
-        const long o = (((long)n * Hout + oy) * Wout + ox) * ldo + offo + c;
-#pragma unroll
-        for (int k = 0; k < VW; ++k) {
-            if (accumulate) acc[k] += ldv(out, odt, o + k);
-            stv(out, odt, o + k, acc[k]);
+            for (int k = 0; k < VW; ++k) acc[k] += w * v[k];
         }
     }
+    const long o = (((long)n * Hout + oy) * Wout + ox) * ldo + offo + c;
+    if (accumulate) {
+        float v[VW];
+        ldvec<VW>(out, odt, o, v);
+#pragma unroll
+        for (int k = 0; k < VW; ++k) acc[k] += v[k];
+    }
+    stvec<VW>(out, odt, o, acc);
 }
 
 __global__ __launch_bounds__(TPB) void maxpool_fwd_kernel(const void* __restrict__ x, int dt, int H, int W, int C,
@@ -272,15 +297,15 @@ extern "C" int irgan_sep_resample(const void* in, int32_t in_dtype, int32_t N, i
                                   const float* wx, int32_t T, int32_t accumulate, irgan_stream_t s) {
     const bool vec = (C % 8 == 0) && (ldi % 8 == 0) && (offi % 8 == 0) && (ldo % 8 == 0) && (offo % 8 == 0);
     const int VW = vec ? 8 : 1;
-    long total = (long)N * Hout * Wout * (C / VW);
-    if (total <= 0) return 0;
-    int nb = (int)std::max<long>(1, std::min<long>((total + TPB - 1) / TPB, 16384));
+    if ((long)N * Hout * Wout * C <= 0) return 0;
+    if ((long)N * Hout > 65535) return IRGAN_EUNSUPPORTED;
+    dim3 g(irgan_cdiv((long)Wout * (C / VW), TPB), N * Hout);
     if (vec)
-        sep_kernel<8><<<nb, TPB, 0, (hipStream_t)s>>>(in, in_dtype, Hin, Win, C, ldi, offi, out, out_dtype, Hout, Wout,
-                                                      ldo, offo, ty, wy, tx, wx, T, accumulate, total);
+        sep_kernel<8><<<g, TPB, 0, (hipStream_t)s>>>(in, in_dtype, Hin, Win, C, ldi, offi, out, out_dtype, Hout, Wout,
+                                                     ldo, offo, ty, wy, tx, wx, T, accumulate);
     else
-        sep_kernel<1><<<nb, TPB, 0, (hipStream_t)s>>>(in, in_dtype, Hin, Win, C, ldi, offi, out, out_dtype, Hout, Wout,
-                                                      ldo, offo, ty, wy, tx, wx, T, accumulate, total);
+        sep_kernel<1><<<g, TPB, 0, (hipStream_t)s>>>(in, in_dtype, Hin, Win, C, ldi, offi, out, out_dtype, Hout, Wout,
+                                                     ldo, offo, ty, wy, tx, wx, T, accumulate);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }

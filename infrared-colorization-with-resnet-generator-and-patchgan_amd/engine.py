@@ -188,7 +188,7 @@ class INLayer:
 
     def fwd(self, bufs: Buffers, name: str, x: Feat, y: Feat, act, res: Feat = None, xhat=None):
         N, C = x.N, x.C
-        work = bufs.flat("in_work", 2 * N * C, torch.float64)
+        work = bufs.flat("in_work", ops.IN_PARTS * N * C, torch.float64)
         self.mr = bufs.get("mr_" + name, (N * C * 2,), torch.float32)
         ops.in_stats(x, work, self.mr)
         ops.in_apply(x, self.mr, y, act=act, res=res, xhat=xhat)
@@ -196,7 +196,7 @@ class INLayer:
     def bwd(self, bufs: Buffers, dy: Feat, z: Feat, act, dx: Feat, db=None, dy2: Feat = None):
         """z: the PRE-norm input kept from forward; act: the activation after IN."""
         N, C = z.N, z.C
-        work = bufs.flat("in_work", 2 * N * C, torch.float64)
+        work = bufs.flat("in_work", ops.IN_PARTS * N * C, torch.float64)
         red = bufs.flat("in_red", 2 * N * C)
         ops.in_backward(dy, z, act, self.mr, work, red, dx, db=db if INLayer.sum_bias_grad else None, dy2=dy2)
 

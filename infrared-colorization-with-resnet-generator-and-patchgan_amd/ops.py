@@ -12,7 +12,7 @@ import math
 import torch
 
 from . import _lib
-from ._lib import ACT_LRELU, ACT_NONE, ACT_RELU, ACT_TANH, BF16, F32, PAD_REFLECT, PAD_ZERO  # noqa: F401
+from ._lib import ACT_LRELU, ACT_NONE, ACT_RELU, ACT_TANH, BF16, F32, IN_PARTS, PAD_REFLECT, PAD_ZERO  # noqa: F401
 
 TORCH_DT = {F32: torch.float32, BF16: torch.bfloat16}
 
@@ -277,7 +277,7 @@ def channel_sum(g: Feat, db: torch.Tensor):
     key = (db.device, g.C)
     w = _CS_WORK.get(key)
     if w is None:
-        w = _CS_WORK[key] = torch.empty(128 * g.C, dtype=torch.float64, device=db.device)
+        w = _CS_WORK[key] = torch.empty(IN_PARTS * g.C, dtype=torch.float64, device=db.device)
     _lib.call("irgan_channel_sum", g.ptr, g.dt, g.P, g.C, g.ld, g.off, P(db), P(w), stream())
 
 

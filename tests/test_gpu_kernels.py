@@ -51,6 +51,18 @@ CONV_CASES = [
     (3, 64, 3, 1, 1, 0, 16),
     (64, 128, 3, 2, 1, 0, 16),
     (192, 64, 3, 1, 1, 0, 8),
+    # multi-patch / ragged-edge cases for the halo kernel (16x16 output patches)
+    (128, 256, 3, 1, 1, 1, 37),
+    (64, 64, 3, 1, 1, 0, 40),
+    (128, 128, 4, 2, 1, 0, 34),
+    (256, 512, 4, 1, 1, 0, 20),
+    # Wo % 64 == 0: the segment (row-span) wgrad kernel
+    (256, 256, 3, 1, 1, 1, 64),
+    (192, 64, 3, 1, 1, 0, 64),
+    (64, 3, 7, 1, 3, 1, 64),
+    (64, 128, 4, 2, 1, 0, 128),
+    (64, 128, 3, 2, 1, 0, 128),
+    (128, 64, 4, 1, 1, 0, 67),
 ]
 
 
@@ -117,10 +129,21 @@ def test_conv_act_and_mask(ops):
     assert relerr(nchw(y), ref) < 2e-5
 
 
+@pytest.mark.parametrize("P,C,ld", [(100003, 3, 8), (65536, 64, 64), (777, 256, 264)])
+def test_channel_sum(ops, P, C, ld):
+    torch.manual_seed(5)
+    g = torch.randn(P, ld, device=DEV)
+    db = torch.full((C,), 0.5, device=DEV)
+    ops.channel_sum(ops.Feat(g.view(1, P, 1, ld), 0, C), db)
+    ref = g[:, :C].double().sum(0) + 0.5
+    assert torch.allclose(db.double(), ref, rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("shape", [(2, 96, 12), (1, 64, 96), (3, 256, 40)])
 @pytest.mark.parametrize("act", [0, 1, 2])
-def test_instance_norm_fwd_bwd(ops, act):
+def test_instance_norm_fwd_bwd(ops, act, shape):
     torch.manual_seed(2)
-    N, C, H = 2, 96, 12
+    N, C, H = shape
     x = (torch.randn(N, C, H, H) * 3 + 1).requires_grad_(True)
     res = torch.randn(N, C, H, H)
     xh = F.instance_norm(x, eps=1e-5)
@@ -130,7 +153,7 @@ def test_instance_norm_fwd_bwd(ops, act):
     gy = torch.randn_like(y)
     y.backward(gy)
     xd = nhwc(x.detach())
-    work = torch.empty(2 * N * C, dtype=torch.float64, device=DEV)
+    work = torch.empty(ops.IN_PARTS * N * C, dtype=torch.float64, device=DEV)
     mr = torch.empty(2 * N * C, device=DEV)
     red = torch.empty(2 * N * C, device=DEV)
     ops.in_stats(ops.Feat(xd), work, mr)

@@ -22,8 +22,16 @@ def t(fn, it=20):
     for _ in range(it): fn()
     b.record(); torch.cuda.synchronize()
     return a.elapsed_time(b) / it
+import argparse
+ap = argparse.ArgumentParser()
+ap.add_argument("--case", default=None, help="substring filter on case names")
+ap.add_argument("--which", default="fwd,dgrad,wgrad")
+ap.add_argument("--iters", type=int, default=20)
+args = ap.parse_args()
 res = {}
 for name, cin, cout, k, s, p, mode, H in CASES:
+    if args.case and args.case not in name:
+        continue
     spec = ops.ConvSpec(cin, cout, k, s, p, mode)
     w = torch.randn(cout * k * k * cin, device=DEV) * 0.05
     pc = ops.PackedConv(spec, w, torch.zeros(cout, device=DEV), ops.BF16); pc.pack()
@@ -35,9 +43,12 @@ for name, cin, cout, k, s, p, mode, H in CASES:
     pad = torch.empty(B * (H + 2 * p) ** 2 * cin, device=DEV)
     dw = torch.zeros(cout * k * k * cin, device=DEV)
     flop = 2.0 * B * Ho * Wo * cout * cin * k * k
-    tf = t(lambda: ops.conv_fwd(pc, ops.Feat(x), ops.Feat(y)))
-    td = t(lambda: ops.conv_dgrad(pc, ops.Feat(dy), ops.Feat(dx), pad_buf=pad))
-    tw = t(lambda: ops.conv_wgrad(spec, ops.Feat(x), ops.Feat(dy), dw, ops.BF16))
-    res[name] = {k2: (round(v, 4), round(flop / v / 1e9, 1)) for k2, v in (("fwd", tf), ("dgrad", td), ("wgrad", tw))}
+    fns = {"fwd": lambda: ops.conv_fwd(pc, ops.Feat(x), ops.Feat(y)),
+           "dgrad": lambda: ops.conv_dgrad(pc, ops.Feat(dy), ops.Feat(dx), pad_buf=pad),
+           "wgrad": lambda: ops.conv_wgrad(spec, ops.Feat(x), ops.Feat(dy), dw, ops.BF16)}
+    res[name] = {}
+    for k2 in args.which.split(","):
+        v = t(fns[k2], args.iters)
+        res[name][k2] = (round(v, 4), round(flop / v / 1e9, 1))
     print(name, "ms/TFLOPs", res[name], flush=True)
 print(json.dumps(res))

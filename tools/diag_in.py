@@ -15,7 +15,7 @@ for (N, C, H, ld, off, inplace, act) in [(2, 64, 32, 64, 0, False, 1), (2, 512, 
     gy = torch.randn_like(y)
     y.backward(gy)
     xd = nhwc(x.detach())
-    work = torch.empty(2 * N * C, dtype=torch.float64, device=DEV); mr = torch.empty(2 * N * C, device=DEV); red = torch.empty(2 * N * C, device=DEV)
+    work = torch.empty(ops.IN_PARTS * N * C, dtype=torch.float64, device=DEV); mr = torch.empty(2 * N * C, device=DEV); red = torch.empty(2 * N * C, device=DEV)
     ops.in_stats(ops.Feat(xd), work, mr)
     buf = torch.zeros(N, H, H, ld, device=DEV)
     buf[..., off:off + C] = nhwc(gy)
