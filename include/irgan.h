@@ -125,6 +125,12 @@ int irgan_channel_sum(const void* g, int32_t dtype, int32_t P, int32_t C, int32_
  * or a negative IRGAN_E* code. */
 int irgan_resample_table(int32_t kind, int32_t n_in, int32_t p, int32_t transpose, int32_t* idx,
                          float* w, int32_t tmax, int32_t rows_cap);
+/* Border half of the nn.ReflectionPad2d(p) backward (ir:381, 402, 459, 528):
+ * g (fp32 NHWC, (H+2p) x (W+2p)) holds the backward-data result on the padded
+ * RING only (the interior went straight to dx); dx[band] += every mirrored ring
+ * value.  Together: dx = fold(g) without materialising the padded interior. */
+int irgan_reflect_ring_fold(const float* g, int32_t N, int32_t H, int32_t W, int32_t C, int32_t p,
+                            void* dx, int32_t dx_dtype, int32_t lddx, int32_t dxoff, irgan_stream_t s);
 /* out = (Wy (x) Wx) in on NHWC slices, tables from irgan_resample_table (device
  * copies); accumulate: out += result.  Downsample / UpsampleAA forward and
  * backward, and the reflect-pad fold, are all this one launch. */

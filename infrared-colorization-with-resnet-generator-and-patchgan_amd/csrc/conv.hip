@@ -482,8 +482,10 @@ int launch_fwd(const irgan_conv_desc* d, const void* x, const void* w, const flo
         const bool narrow = (d->Cin == 8 || d->Cin == 16 || d->Cin == 32) && d->ldx % 8 == 0 && d->xoff % 8 == 0;
         static const bool use_halo = !getenv("IRGAN_NO_HALO");
         const int taps = d->KH * d->KW;
-        if (fast && use_halo && d->sy == 1 && d->sx == 1 && taps >= 2 && d->KH <= 4 && d->KW <= 4)
-            return irgan_conv_fwd_halo(d, x, w, bias, y, mask, st);
+        if (fast && use_halo && d->sy == 1 && d->sx == 1 && taps >= 2) {
+            const int rc = irgan_conv_fwd_halo(d, x, w, bias, y, mask, st);
+            if (rc != IRGAN_EUNSUPPORTED) return rc;
+        }
         if ((fast || narrow) && use_glds) return irgan_conv_fwd_glds(d, x, w, bias, y, mask, st);
     }
     const bool wide = d->Cout > 64;

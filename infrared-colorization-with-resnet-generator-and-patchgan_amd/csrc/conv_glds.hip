@@ -9,7 +9,7 @@
 // The LDS image keeps the 16-byte-chunk XOR swizzle (chunk ^ (row & 7)) of the
 // register-staged kernel; with LDS-DMA the permutation is applied to the
 // per-lane SOURCE chunk so the destination stays lane-linear.
-#include "common.h"
+#include "conv_epilogue.h"
 
 namespace {
 
@@ -44,13 +44,6 @@ IRGAN_HD void wait_vmcnt() {
 __device__ __forceinline__ int xcd_tile(int b, int nb, int swz) {
     if (!swz || (nb & 7)) return b;
     return (b & 7) * (nb >> 3) + (b >> 3);
-}
-
-IRGAN_HD float act_fn(float v, int act) {
-    if (act == IRGAN_ACT_RELU) return v > 0.f ? v : 0.f;
-    if (act == IRGAN_ACT_LRELU) return v > 0.f ? v : 0.2f * v;
-    if (act == IRGAN_ACT_TANH) return tanhf(v);
-    return v;
 }
 
 template <int BN>
@@ -175,37 +168,12 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_glds_kernel(const irgan_conv_
     }
 
     // epilogue: C[row = (lane>>4)*4 + r][col = lane & 15] of each 16x16 fragment
-    const bool out_f32 = d.out_dtype == IRGAN_F32;
-#pragma unroll
-    for (int i = 0; i < MI; ++i) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const long m = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-            if (m >= M) continue;
-            const int mm = (int)m;
-            const int n = mm / HoWo, rr = mm - n * HoWo, ii = rr / d.Wo, jj = rr - ii * d.Wo;
-            const long pix = ((long)n * d.OH + ii * d.omy + d.ooy) * d.OW + jj * d.omx + d.oox;
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                const int co = n0 + wn * (BN / 2) + j * 16 + (lane & 15);
-                if (co >= d.Cout) continue;
-                float v = acc[i][j][r] + (bias ? bias[co] : 0.f);
-                v = act_fn(v, d.act);
-                if (mask) {
-                    const float mv = bf2f(((const bf16_t*)mask)[pix * d.ldm + d.moff + co]);
-                    v *= mv > 0.f ? 1.f : (d.mask_act == 2 ? 0.2f : 0.f);
-                }
-                const long off = pix * d.ldy + d.yoff + co;
-                if (out_f32) {
-                    float* yp = (float*)y;
-                    yp[off] = d.accumulate ? yp[off] + v : v;
-                } else {
-                    bf16_t* yp = (bf16_t*)y;
-                    yp[off] = f2bf(d.accumulate ? bf2f(yp[off]) + v : v);
-                }
-            }
-        }
-    }
+    conv_epilogue<BN, MI, NJ, 4, 2, 512>(d, acc, smem, wm, wn, n0, bias, y, mask, [&](int m) -> long {
+        const long mm = m0 + m;
+        if (mm >= M) return -1;
+        const int n = (int)(mm / HoWo), rr = (int)(mm - (long)n * HoWo), ii = rr / d.Wo, jj = rr - ii * d.Wo;
+        return ((long)n * d.OH + ii * d.omy + d.ooy) * d.OW + jj * d.omx + d.oox;
+    });
 }
 
 }  // namespace

@@ -17,7 +17,7 @@
 // while k runs, the halo of chunk c+1 as soon as chunk c starts (a whole
 // chunk of lead time).  Halo: two buffers (chunk parity), weights: 3-stage
 // ring.  Requires taps >= 2.
-#include "common.h"
+#include "conv_epilogue.h"
 
 namespace {
 
@@ -44,34 +44,35 @@ __device__ __forceinline__ int xcd_tile(int b, int nb, int swz) {
     return (b & 7) * (nb >> 3) + (b >> 3);
 }
 
-IRGAN_HD float act_fn(float v, int act) {
-    if (act == IRGAN_ACT_RELU) return v > 0.f ? v : 0.f;
-    if (act == IRGAN_ACT_LRELU) return v > 0.f ? v : 0.2f * v;
-    if (act == IRGAN_ACT_TANH) return tanhf(v);
-    return v;
-}
+constexpr int PH = 16, PW = 16;  // output patch
 
-constexpr int PH = 16, PW = 16;   // output patch
-constexpr int HROWS = 384;        // halo rows capacity: (16+3)*(16+3) = 361 <= 384 = 48 pieces
-constexpr int HU = HROWS / 8 / 8; // halo pieces per wave (6)
-
-template <int BN>
+// BN: output-channel tile (128 | 64 | 16); HU: halo pieces per wave (HROWS =
+// HU*64 rows: 6 -> 384 >= 19*19 for taps <= 4x4, 8 -> 512 >= 22*22 for 7x7);
+// WM x WN waves over (pixels, channels).
+template <int BN, int HU, int WM, int WN>
 __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
                                                            const bf16_t* __restrict__ w,
                                                            const float* __restrict__ bias, void* __restrict__ y,
                                                            const void* __restrict__ mask,
                                                            const bf16_t* __restrict__ zero, int ntn, int tpx, int tpy,
                                                            int swz) {
-    constexpr int STAGES = 3;
+    static_assert(WM * WN == 8, "8 waves");
+    constexpr int STAGES = 3, HROWS = HU * 64;
     constexpr int HBYTES = HROWS * 128, BBYTES = BN * 128;
-    constexpr int MI = 4, NJ = BN / 32, BU = BN / 64;
-    __shared__ __attribute__((aligned(1024))) char smem[2 * HBYTES + STAGES * BBYTES];
+    constexpr int MI = 256 / WM / 16, NJ = BN / WN / 16;
+    constexpr int BP = BN / 8;                  // weight-tile pieces (1 KiB = 8 channel rows)
+    constexpr int BU = BP >= 8 ? BP / 8 : 1;    // pieces per issuing wave
+    constexpr int LDS = 2 * HBYTES + STAGES * BBYTES;
+    static_assert(MI * 16 * WM == 256 && NJ * 16 * WN == BN, "tile");
+    static_assert(256 * (BN + 4) * 4 <= LDS, "epilogue staging fits");
+    __shared__ __attribute__((aligned(1024))) char smem[LDS];
     char* const sH = smem;
     char* const sB = smem + 2 * HBYTES;
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wid >> 1, wn = wid & 1;
+    const int wm = wid / WN, wn = wid % WN;
+    const bool bload = BP >= 8 || wid < BP;     // does this wave load weight pieces
     int t = xcd_tile(blockIdx.x, gridDim.x, swz);
     const int nt = t % ntn;
     t /= ntn;
@@ -116,6 +117,7 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const irgan_conv_desc
         for (int u = 0; u < HU; ++u) glds16(h_off[u] >= 0 ? x + h_off[u] + c * 64 : zero, dst + u * 1024);
     };
     auto issue_w = [&](int kt, int stage) {
+        if (!bload) return;
         const int c = kt / taps, tp = kt - c * taps;
         const int kcol = tp * d.Cin + c * 64;
 #pragma unroll
@@ -142,8 +144,12 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const irgan_conv_desc
     for (int kt = 0; kt < nk; ++kt) {
         if (kt + 1 < nk) {
             const int pk = kt - 1;  // did step kt-1 issue a halo (after W(kt))?
-            if (pk >= 0 && pk % taps == 0 && pk / taps + 1 < nchunk) wait_vmcnt<BU + HU>();
-            else wait_vmcnt<BU>();
+            const bool h = pk >= 0 && pk % taps == 0 && pk / taps + 1 < nchunk;
+            if (bload) {
+                if (h) wait_vmcnt<BU + HU>(); else wait_vmcnt<BU>();
+            } else {
+                if (h) wait_vmcnt<HU>(); else wait_vmcnt<0>();
+            }
         } else {
             wait_vmcnt<0>();
         }
@@ -153,7 +159,8 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const irgan_conv_desc
         const char* Hb = sH + (c & 1) * HBYTES;
         const char* B = sB + (kt % STAGES) * BBYTES;
         const int ty = tp / d.KW, tx = tp - ty * d.KW;
-        const int hbase = (wm * 4 + ty) * HWd + (lane & 15) + tx;  // halo row of fragment i = hbase + i*HWd
+        // fragment i covers patch row wm*MI + i, columns lane&15
+        const int hbase = (wm * MI + ty) * HWd + (lane & 15) + tx;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             uint4 af[MI], bfr[NJ];
@@ -161,7 +168,8 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const irgan_conv_desc
 #pragma unroll
             for (int i = 0; i < MI; ++i) af[i] = *(const uint4*)(Hb + lds_off(hbase + i * HWd, ch));
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) bfr[j] = *(const uint4*)(B + lds_off(wn * (BN / 2) + j * 16 + (lane & 15), ch));
+            for (int j = 0; j < NJ; ++j)
+                bfr[j] = *(const uint4*)(B + lds_off(wn * (BN / WN) + j * 16 + (lane & 15), ch));
 #pragma unroll
             for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -176,62 +184,46 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const irgan_conv_desc
         }
     }
 
-    // epilogue: fragment i = patch row wm*4+i, C[row=(lane>>4)*4+r] = patch column, col = channel
-    const bool out_f32 = d.out_dtype == IRGAN_F32;
-#pragma unroll
-    for (int i = 0; i < MI; ++i) {
-        const int oy = py0 + wm * 4 + i;
-        if (oy >= d.Ho) continue;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int ox = px0 + (lane >> 4) * 4 + r;
-            if (ox >= d.Wo) continue;
-            const long pix = ((long)img * d.OH + oy * d.omy + d.ooy) * d.OW + ox * d.omx + d.oox;
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                const int co = n0 + wn * (BN / 2) + j * 16 + (lane & 15);
-                if (co >= d.Cout) continue;
-                float v = acc[i][j][r] + (bias ? bias[co] : 0.f);
-                v = act_fn(v, d.act);
-                if (mask) {
-                    const float mv = bf2f(((const bf16_t*)mask)[pix * d.ldm + d.moff + co]);
-                    v *= mv > 0.f ? 1.f : (d.mask_act == 2 ? 0.2f : 0.f);
-                }
-                const long off = pix * d.ldy + d.yoff + co;
-                if (out_f32) {
-                    float* yp = (float*)y;
-                    yp[off] = d.accumulate ? yp[off] + v : v;
-                } else {
-                    bf16_t* yp = (bf16_t*)y;
-                    yp[off] = f2bf(d.accumulate ? bf2f(yp[off]) + v : v);
-                }
-            }
-        }
-    }
+    // epilogue: fragment i = patch row wm*MI+i, C row (lane>>4)*4+r = patch column
+    conv_epilogue<BN, MI, NJ, WM, WN, 512>(d, acc, smem, wm, wn, n0, bias, y, mask, [&](int m) -> long {
+        const int oy = py0 + (m >> 4), ox = px0 + (m & 15);
+        if (oy >= d.Ho || ox >= d.Wo) return -1;
+        return ((long)img * d.OH + oy * d.omy + d.ooy) * d.OW + ox * d.omx + d.oox;
+    });
+}
+
+template <int BN, int HU, int WM, int WN>
+void launch_halo(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y, const void* mask,
+                 hipStream_t st, const bf16_t* zero, int swz) {
+    const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH);
+    const int ntn = irgan_cdiv(d->Cout, BN);
+    conv_halo_kernel<BN, HU, WM, WN><<<d->N * tpy * tpx * ntn, 512, 0, st>>>(
+        *d, (const bf16_t*)x, (const bf16_t*)w, bias, y, mask, zero, ntn, tpx, tpy, swz);
 }
 
 }  // namespace
 
 // Preconditions (checked by the dispatcher in conv.hip): bf16, sy = sx = 1,
-// Cin % 64 == 0, ldx % 8 == 0, xoff % 8 == 0, 2 <= KH*KW, KH, KW <= 4.
+// Cin % 64 == 0, ldx % 8 == 0, xoff % 8 == 0, 2 <= KH*KW, KH, KW <= 7 (taps
+// beyond 4x4 only for Cout <= 64).
 extern "C" int irgan_conv_fwd_halo(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
                                    const void* mask, hipStream_t st) {
     if ((long)d->N * d->Ho * d->Wo <= 0 || d->Cout <= 0) return 0;
-    if (d->sy != 1 || d->sx != 1 || d->Cin % 64 || d->KH > 4 || d->KW > 4 || d->KH * d->KW < 2)
+    if (d->sy != 1 || d->sx != 1 || d->Cin % 64 || d->KH > 7 || d->KW > 7 || d->KH * d->KW < 2)
         return IRGAN_EUNSUPPORTED;
+    const bool big = d->KH > 4 || d->KW > 4;
+    if (big && d->Cout > 64) return IRGAN_EUNSUPPORTED;
     static bf16_t* zero = nullptr;
     if (!zero && hipGetSymbolAddress((void**)&zero, HIP_SYMBOL(g_halo_zero_page)) != hipSuccess)
         return IRGAN_EUNSUPPORTED;
     static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
-    const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH);
-    if (d->Cout > 64) {
-        const int ntn = irgan_cdiv(d->Cout, 128);
-        conv_halo_kernel<128><<<d->N * tpy * tpx * ntn, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, y,
-                                                                     mask, zero, ntn, tpx, tpy, swz);
+    if (d->Cout > 64) launch_halo<128, 6, 4, 2>(d, x, w, bias, y, mask, st, zero, swz);
+    else if (d->Cout > 16) {
+        if (big) launch_halo<64, 8, 4, 2>(d, x, w, bias, y, mask, st, zero, swz);
+        else launch_halo<64, 6, 4, 2>(d, x, w, bias, y, mask, st, zero, swz);
     } else {
-        const int ntn = irgan_cdiv(d->Cout, 64);
-        conv_halo_kernel<64><<<d->N * tpy * tpx * ntn, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, y,
-                                                                    mask, zero, ntn, tpx, tpy, swz);
+        if (big) launch_halo<16, 8, 8, 1>(d, x, w, bias, y, mask, st, zero, swz);
+        else launch_halo<16, 6, 8, 1>(d, x, w, bias, y, mask, st, zero, swz);
     }
     IRGAN_LAUNCH_CHECK();
     return 0;

@@ -24,6 +24,10 @@ IRGAN_HD void block_add(double* dst, float v) {
 IRGAN_HD float sgn(float x) { return x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f); }
 
 int nblocks(long total) { return (int)std::max<long>(1, std::min<long>((total + TPB - 1) / TPB, 8192)); }
+// kernels that finish with block_add: every block adds into the SAME fp64 word,
+// and same-address atomics serialise at the memory side (~10 ns each), so keep
+// the grid small and let threads loop
+int nblocks_red(long total) { return (int)std::max<long>(1, std::min<long>((total + TPB - 1) / TPB, 512)); }
 
 // mode 0: pred = [real (n) ; fake (n)] -> 0.5*(mean relu(1-r) + mean relu(1+f))   (ir:1647-1649)
 // mode 1: pred = fake (n) -> -mean(p) * scale                                    (ir:1662, x lambda_gan)
@@ -52,47 +56,101 @@ __global__ __launch_bounds__(TPB) void hinge_kernel(const float* __restrict__ pr
     block_add(loss, mode == 0 ? 0.5f * acc * inv * scale : -acc * inv * scale);
 }
 
-template <typename T, typename G>
+template <typename T>
+IRGAN_HD void ld8t(const T* p, long i, float* o) {
+    if constexpr (sizeof(T) == 2) {
+        const uint4 u = *(const uint4*)(p + i);
+        const uint32_t q[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            o[2 * k] = __uint_as_float(q[k] << 16);
+            o[2 * k + 1] = __uint_as_float(q[k] & 0xffff0000u);
+        }
+    } else {
+        const float4 x0 = *(const float4*)(p + i), x1 = *(const float4*)(p + i + 4);
+        o[0] = x0.x; o[1] = x0.y; o[2] = x0.z; o[3] = x0.w; o[4] = x1.x; o[5] = x1.y; o[6] = x1.z; o[7] = x1.w;
+    }
+}
+template <typename T>
+IRGAN_HD void st8t(T* p, long i, const float* v) {
+    if constexpr (sizeof(T) == 2) {
+        uint4 u;
+        u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        u.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+        u.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+        *(uint4*)(p + i) = u;
+    } else {
+        *(float4*)(p + i) = make_float4(v[0], v[1], v[2], v[3]);
+        *(float4*)(p + i + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    }
+}
+
+// VEC: 8 elements per thread-iteration (16/32-byte accesses; count % 8 == 0)
+template <typename T, typename G, bool VEC>
 __global__ __launch_bounds__(TPB) void l1_kernel(const T* __restrict__ a, const T* __restrict__ b, long count, float w,
                                                  G* __restrict__ ga, int accumulate, double* __restrict__ loss) {
     float acc = 0.f;
     const float inv = w / (float)count;
-    for (long i = blockIdx.x * (long)TPB + threadIdx.x; i < count; i += (long)gridDim.x * TPB) {
-        const float d = to_f<T>(a[i]) - to_f<T>(b[i]);
-        acc += fabsf(d);
-        if (ga) {
-            float gv = sgn(d) * inv;
-            if (accumulate) gv += to_f<G>(ga[i]);
-            ga[i] = from_f<G>(gv);
+    if constexpr (VEC) {
+        for (long i = (blockIdx.x * (long)TPB + threadIdx.x) * 8; i < count; i += (long)gridDim.x * TPB * 8) {
+            float av[8], bv[8], gv[8];
+            ld8t<T>(a, i, av);
+            ld8t<T>(b, i, bv);
+            if (ga && accumulate) ld8t<G>(ga, i, gv);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const float d = av[k] - bv[k];
+                acc += fabsf(d);
+                gv[k] = (ga && accumulate ? gv[k] : 0.f) + sgn(d) * inv;
+            }
+            if (ga) st8t<G>(ga, i, gv);
+        }
+    } else {
+        for (long i = blockIdx.x * (long)TPB + threadIdx.x; i < count; i += (long)gridDim.x * TPB) {
+            const float d = to_f<T>(a[i]) - to_f<T>(b[i]);
+            acc += fabsf(d);
+            if (ga) {
+                float gv = sgn(d) * inv;
+                if (accumulate) gv += to_f<G>(ga[i]);
+                ga[i] = from_f<G>(gv);
+            }
         }
     }
     block_add(loss, acc * inv);
 }
 
-// TV (ir:686-694): mean|x[h+1]-x[h]| + mean|x[w+1]-x[w]| over N*C*(H-1)*W and N*C*H*(W-1)
-__global__ __launch_bounds__(TPB) void tv_kernel(const float* __restrict__ x, int H, int W, int C, float w,
-                                                 float* __restrict__ g, double* __restrict__ loss, long total,
-                                                 float inv_v, float inv_h) {
+// TV (ir:686-694): mean|x[h+1]-x[h]| + mean|x[w+1]-x[w]| over N*C*(H-1)*W and N*C*H*(W-1).
+// Grid-stride over image rows (n*H + y), threads over pixels x, channel loop.
+__global__ __launch_bounds__(TPB) void tv_kernel(const float* __restrict__ x, int N, int H, int W, int C, float w,
+                                                 float* __restrict__ g, double* __restrict__ loss, float inv_v,
+                                                 float inv_h) {
     float acc = 0.f;
-    for (long idx = blockIdx.x * (long)TPB + threadIdx.x; idx < total; idx += (long)gridDim.x * TPB) {
-        long t = idx / C;
-        const int xw = (int)(t % W); t /= W;
-        const int yh = (int)(t % H);
-        const float v = x[idx];
-        float gv = 0.f;
-        if (yh + 1 < H) {
-            const float d = x[idx + (long)W * C] - v;
-            acc += fabsf(d) * inv_v;
-            gv -= sgn(d) * inv_v;
+    const int WC = W * C;
+    for (int row = blockIdx.x; row < N * H; row += gridDim.x) {
+        const int yh = row % H;
+        const float* xr = x + (long)row * WC;
+        float* gr = g + (long)row * WC;
+        for (int xw = threadIdx.x; xw < W; xw += TPB) {
+            for (int c = 0; c < C; ++c) {
+                const int e = xw * C + c;
+                const float v = xr[e];
+                float gv = 0.f;
+                if (yh + 1 < H) {
+                    const float d = xr[e + WC] - v;
+                    acc += fabsf(d) * inv_v;
+                    gv -= sgn(d) * inv_v;
+                }
+                if (yh > 0) gv += sgn(v - xr[e - WC]) * inv_v;
+                if (xw + 1 < W) {
+                    const float d = xr[e + C] - v;
+                    acc += fabsf(d) * inv_h;
+                    gv -= sgn(d) * inv_h;
+                }
+                if (xw > 0) gv += sgn(v - xr[e - C]) * inv_h;
+                gr[e] += w * gv;
+            }
         }
-        if (yh > 0) gv += sgn(v - x[idx - (long)W * C]) * inv_v;
-        if (xw + 1 < W) {
-            const float d = x[idx + C] - v;
-            acc += fabsf(d) * inv_h;
-            gv -= sgn(d) * inv_h;
-        }
-        if (xw > 0) gv += sgn(v - x[idx - C]) * inv_h;
-        g[idx] += w * gv;
     }
     block_add(loss, w * acc);
 }
@@ -105,8 +163,11 @@ struct Win11 {
 // Gaussian (sigma 1.5) and zero padding 5.  Planar fp32 work maps of size S.
 __global__ __launch_bounds__(TPB) void ssim_h5_kernel(const float* __restrict__ a, const float* __restrict__ b, int W,
                                                       int C, Win11 win, float* __restrict__ out, long S) {
-    for (long idx = blockIdx.x * (long)TPB + threadIdx.x; idx < S; idx += (long)gridDim.x * TPB) {
-        const int xw = (int)((idx / C) % W);
+    const int xw = blockIdx.x * TPB + threadIdx.x;
+    if (xw >= W) return;
+    const long rowb = (long)blockIdx.y * W * C;
+    for (int c = 0; c < C; ++c) {
+        const long idx = rowb + (long)xw * C + c;
         float m1 = 0.f, m2 = 0.f, e11 = 0.f, e22 = 0.f, e12 = 0.f;
 #pragma unroll
         for (int k = 0; k < 11; ++k) {
@@ -128,32 +189,38 @@ __global__ __launch_bounds__(TPB) void ssim_h5_kernel(const float* __restrict__ 
     }
 }
 
+// vertical 11-tap pass over NM planar maps; blockIdx.y = n*H + y
 template <int NM>
 __global__ __launch_bounds__(TPB) void ssim_v_kernel(const float* __restrict__ in, int H, int W, int C, Win11 win,
                                                      float* __restrict__ out, long S) {
-    for (long idx = blockIdx.x * (long)TPB + threadIdx.x; idx < S; idx += (long)gridDim.x * TPB) {
-        const int yh = (int)((idx / ((long)C * W)) % H);
-        float acc[NM];
+    const int e = blockIdx.x * TPB + threadIdx.x;  // element within the row (x*C + c)
+    if (e >= W * C) return;
+    const int yh = blockIdx.y % H;
+    const long idx = (long)blockIdx.y * W * C + e;
+    float acc[NM];
 #pragma unroll
-        for (int m = 0; m < NM; ++m) acc[m] = 0.f;
+    for (int m = 0; m < NM; ++m) acc[m] = 0.f;
 #pragma unroll
-        for (int k = 0; k < 11; ++k) {
-            const int yy = yh + k - 5;
-            if (yy < 0 || yy >= H) continue;
-            const long j = idx + (long)(k - 5) * W * C;
+    for (int k = 0; k < 11; ++k) {
+        const int yy = yh + k - 5;
+        if (yy < 0 || yy >= H) continue;
+        const long j = idx + (long)(k - 5) * W * C;
 #pragma unroll
-            for (int m = 0; m < NM; ++m) acc[m] += win.g[k] * in[m * S + j];
-        }
-#pragma unroll
-        for (int m = 0; m < NM; ++m) out[m * S + idx] = acc[m];
+        for (int m = 0; m < NM; ++m) acc[m] += win.g[k] * in[m * S + j];
     }
+#pragma unroll
+    for (int m = 0; m < NM; ++m) out[m * S + idx] = acc[m];
 }
 
+// horizontal 11-tap pass over NM planar maps
 template <int NM>
 __global__ __launch_bounds__(TPB) void ssim_h_kernel(const float* __restrict__ in, int W, int C, Win11 win,
                                                      float* __restrict__ out, long S) {
-    for (long idx = blockIdx.x * (long)TPB + threadIdx.x; idx < S; idx += (long)gridDim.x * TPB) {
-        const int xw = (int)((idx / C) % W);
+    const int xw = blockIdx.x * TPB + threadIdx.x;
+    if (xw >= W) return;
+    const long rowb = (long)blockIdx.y * W * C;
+    for (int c = 0; c < C; ++c) {
+        const long idx = rowb + (long)xw * C + c;
         float acc[NM];
 #pragma unroll
         for (int m = 0; m < NM; ++m) acc[m] = 0.f;
@@ -241,7 +308,7 @@ Win11 gauss11() {
 extern "C" int irgan_hinge(const float* pred, int32_t n_half, int32_t mode, float scale, float* grad, double* loss,
                            irgan_stream_t s) {
     long total = mode == 0 ? 2L * n_half : n_half;
-    hinge_kernel<<<nblocks(total), TPB, 0, (hipStream_t)s>>>(pred, n_half, mode, scale, grad, loss);
+    hinge_kernel<<<nblocks_red(total), TPB, 0, (hipStream_t)s>>>(pred, n_half, mode, scale, grad, loss);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }
@@ -249,32 +316,37 @@ extern "C" int irgan_hinge(const float* pred, int32_t n_half, int32_t mode, floa
 extern "C" int irgan_l1(const void* a, const void* b, int32_t dtype, int64_t count, float w, void* ga,
                         int32_t ga_dtype, int32_t accumulate, double* loss, irgan_stream_t s) {
     hipStream_t st = (hipStream_t)s;
-    int nb = nblocks(count);
+    if (count <= 0) return 0;
+    const bool vec = count % 8 == 0 && ((uintptr_t)a % 16 == 0) && ((uintptr_t)b % 16 == 0) &&
+                     (!ga || (uintptr_t)ga % 16 == 0);
+    const int nb = nblocks_red(vec ? count / 8 : count);
+#define L1_LAUNCH(T, G)                                                                                       \
+    do {                                                                                                      \
+        if (vec)                                                                                              \
+            l1_kernel<T, G, true><<<nb, TPB, 0, st>>>((const T*)a, (const T*)b, count, w, (G*)ga, accumulate, \
+                                                      loss);                                                  \
+        else                                                                                                  \
+            l1_kernel<T, G, false><<<nb, TPB, 0, st>>>((const T*)a, (const T*)b, count, w, (G*)ga, accumulate, \
+                                                       loss);                                                 \
+    } while (0)
     if (dtype == IRGAN_F32) {
-        if (ga_dtype == IRGAN_BF16)
-            l1_kernel<float, bf16_t><<<nb, TPB, 0, st>>>((const float*)a, (const float*)b, count, w, (bf16_t*)ga,
-                                                         accumulate, loss);
-        else
-            l1_kernel<float, float><<<nb, TPB, 0, st>>>((const float*)a, (const float*)b, count, w, (float*)ga,
-                                                        accumulate, loss);
+        if (ga_dtype == IRGAN_BF16) L1_LAUNCH(float, bf16_t);
+        else L1_LAUNCH(float, float);
     } else {
-        if (ga_dtype == IRGAN_BF16)
-            l1_kernel<bf16_t, bf16_t><<<nb, TPB, 0, st>>>((const bf16_t*)a, (const bf16_t*)b, count, w, (bf16_t*)ga,
-                                                          accumulate, loss);
-        else
-            l1_kernel<bf16_t, float><<<nb, TPB, 0, st>>>((const bf16_t*)a, (const bf16_t*)b, count, w, (float*)ga,
-                                                         accumulate, loss);
+        if (ga_dtype == IRGAN_BF16) L1_LAUNCH(bf16_t, bf16_t);
+        else L1_LAUNCH(bf16_t, float);
     }
+#undef L1_LAUNCH
     IRGAN_LAUNCH_CHECK();
     return 0;
 }
 
 extern "C" int irgan_tv(const float* x, int32_t N, int32_t H, int32_t W, int32_t C, float w, float* g, double* loss,
                         irgan_stream_t s) {
-    long total = (long)N * H * W * C;
+    if ((long)N * H * W * C <= 0) return 0;
     float inv_v = H > 1 ? 1.f / (float)((long)N * C * (H - 1) * W) : 0.f;
     float inv_h = W > 1 ? 1.f / (float)((long)N * C * H * (W - 1)) : 0.f;
-    tv_kernel<<<nblocks(total), TPB, 0, (hipStream_t)s>>>(x, H, W, C, w, g, loss, total, inv_v, inv_h);
+    tv_kernel<<<std::min(N * H, 512), TPB, 0, (hipStream_t)s>>>(x, N, H, W, C, w, g, loss, inv_v, inv_h);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }
@@ -286,12 +358,15 @@ extern "C" int irgan_ssim(const float* a, const float* b, int32_t N, int32_t H, 
     const Win11 win = gauss11();
     float* w0 = work;          // 5 maps
     float* w1 = work + 5 * S;  // 5 maps
+    if (S <= 0) return 0;
+    if ((long)N * H > 65535) return IRGAN_EUNSUPPORTED;
     const int nb = nblocks(S);
-    ssim_h5_kernel<<<nb, TPB, 0, st>>>(a, b, W, C, win, w0, S);
-    ssim_v_kernel<5><<<nb, TPB, 0, st>>>(w0, H, W, C, win, w1, S);
-    ssim_map_kernel<<<nb, TPB, 0, st>>>(w1, w, w0, loss, S);
-    ssim_h_kernel<3><<<nb, TPB, 0, st>>>(w0, W, C, win, w1, S);
-    ssim_v_kernel<3><<<nb, TPB, 0, st>>>(w1, H, W, C, win, w0, S);
+    const dim3 gx(irgan_cdiv(W, TPB), N * H), ge(irgan_cdiv((long)W * C, TPB), N * H);
+    ssim_h5_kernel<<<gx, TPB, 0, st>>>(a, b, W, C, win, w0, S);
+    ssim_v_kernel<5><<<ge, TPB, 0, st>>>(w0, H, W, C, win, w1, S);
+    ssim_map_kernel<<<nblocks_red(S), TPB, 0, st>>>(w1, w, w0, loss, S);
+    ssim_h_kernel<3><<<gx, TPB, 0, st>>>(w0, W, C, win, w1, S);
+    ssim_v_kernel<3><<<ge, TPB, 0, st>>>(w1, H, W, C, win, w0, S);
     ssim_grad_kernel<<<nb, TPB, 0, st>>>(w0, a, b, g, S);
     IRGAN_LAUNCH_CHECK();
     return 0;

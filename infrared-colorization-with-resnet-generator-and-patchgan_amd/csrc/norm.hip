@@ -167,19 +167,35 @@ __global__ __launch_bounds__(TPB) void rows_kernel(Slice X, Slice DY, Slice DY2,
     }
 }
 
-// one thread per (n, c): fp64 sum of the nb block partials of image n
-__global__ void finalize_kernel(const float2* __restrict__ part, float* __restrict__ mr, int N, int C, int nb, int HW,
-                                int mode) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= N * C) return;
-    const int n = i / C, c = i - n * C;
+// fp64 sum of the nb block partials of each (n, c).  Block (32 channels x 8
+// partial lanes) per (image, channel group): loads are 256-byte rows of
+// consecutive channels, the 8 lanes of a channel combine through LDS in a fixed
+// order (deterministic).
+__global__ __launch_bounds__(256) void finalize_kernel(const float2* __restrict__ part, float* __restrict__ mr, int N,
+                                                       int C, int nb, int HW, int mode) {
+    __shared__ double s0[8][32], s1[8][32];
+    const int n = blockIdx.y, cl = threadIdx.x & 31, sub = threadIdx.x >> 5;
+    const int c = blockIdx.x * 32 + cl;
     double s = 0.0, q = 0.0;
-    for (int b = 0; b < nb; ++b) {
-        const float2 v = part[((long)n * nb + b) * C + c];
-        s += v.x;
-        q += v.y;
+    if (c < C) {
+        for (int b = sub; b < nb; b += 8) {
+            const float2 v = part[((long)n * nb + b) * C + c];
+            s += v.x;
+            q += v.y;
+        }
     }
-    double mean = s / HW;
+    s0[sub][cl] = s;
+    s1[sub][cl] = q;
+    __syncthreads();
+    if (sub != 0 || c >= C) return;
+    s = 0.0;
+    q = 0.0;
+    for (int k = 0; k < 8; ++k) {
+        s += s0[k][cl];
+        q += s1[k][cl];
+    }
+    const long i = (long)n * C + c;
+    const double mean = s / HW;
     if (mode == 0) {
         double var = q / HW - mean * mean;
         if (var < 0) var = 0;
@@ -276,7 +292,7 @@ extern "C" int irgan_in_stats(const void* x, int32_t dtype, int32_t N, int32_t H
     int nb = 1;
     launch_rows<0>(X, Z, Z, 0, nullptr, nullptr, nullptr, 0, 0, 0, N, HW, C, (float2*)work, nullptr,
                    vec_ok(C, {ld, off}), st, &nb);
-    finalize_kernel<<<irgan_cdiv((long)N * C, 256), 256, 0, st>>>((const float2*)work, mr, N, C, nb, HW, 0);
+    finalize_kernel<<<dim3(irgan_cdiv(C, 32), N), 256, 0, st>>>((const float2*)work, mr, N, C, nb, HW, 0);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }
@@ -308,7 +324,7 @@ extern "C" int irgan_in_bwd_reduce(const void* dy, int32_t dy_dtype, int32_t ldd
     Slice X{x, x_dtype, ldx, xoff}, DY{dy, dy_dtype, lddy, dyoff}, DY2{dy2, dy2_dtype, lddy2, dy2off};
     int nb = 1;
     launch_rows<1>(X, DY, DY2, act, mr, nullptr, nullptr, 0, 0, 0, N, HW, C, (float2*)work, nullptr, vec, st, &nb);
-    finalize_kernel<<<irgan_cdiv((long)N * C, 256), 256, 0, st>>>((const float2*)work, red, N, C, nb, HW, 1);
+    finalize_kernel<<<dim3(irgan_cdiv(C, 32), N), 256, 0, st>>>((const float2*)work, red, N, C, nb, HW, 1);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }

@@ -98,45 +98,110 @@ __global__ __launch_bounds__(TPB) void sep_kernel(const void* __restrict__ in, i
     stvec<VW>(out, odt, o, acc);
 }
 
-__global__ __launch_bounds__(TPB) void maxpool_fwd_kernel(const void* __restrict__ x, int dt, int H, int W, int C,
-                                                          void* __restrict__ y, long total) {
-    const int Ho = H / 2, Wo = W / 2;
-    for (long idx = blockIdx.x * (long)TPB + threadIdx.x; idx < total; idx += (long)gridDim.x * TPB) {
-        long t = idx;
-        const int c = (int)(t % C); t /= C;
-        const int j = (int)(t % Wo); t /= Wo;
-        const int i = (int)(t % Ho);
-        const int n = (int)(t / Ho);
-        float m = -INFINITY;
-        for (int a = 0; a < 2; ++a)
-            for (int b = 0; b < 2; ++b) {
-                float v = ldv(x, dt, (((long)n * H + 2 * i + a) * W + 2 * j + b) * C + c);
-                if (v > m || isnan(v)) m = v;
-            }
-        stv(y, dt, idx, m);
-    }
+// Reflect-pad backward, border part.  g is the backward-data result over the
+// padded domain (Hp = H+2p) of which only the RING (padded rows/cols outside
+// [p, H+p) x [p, W+p)) has been computed; the interior was written straight to
+// dx.  Along one axis, dx index i receives padded u = i+p (interior) and at most
+// one mirror: u = p-i (1 <= i <= p) or u = 2H-2-i+p (H-1-p <= i <= H-2).  Each
+// band element of dx gathers every (uy, ux) pair except the interior-interior
+// one (deterministic, no atomics).  blockIdx.y = n*H + iy, threads over (ix, c8).
+IRGAN_HD int mirrors(int i, int n, int p, int* u) {  // padded coords != i+p mapping to i
+    int k = 0;
+    if (i >= 1 && i <= p) u[k++] = p - i;
+    if (i >= n - 1 - p && i <= n - 2) u[k++] = 2 * n - 2 - i + p;
+    return k;
 }
 
+template <int VW>
+__global__ __launch_bounds__(TPB) void ring_fold_kernel(const float* __restrict__ g, int H, int W, int C, int p,
+                                                        void* __restrict__ dx, int dt, int lddx, int dxoff) {
+    const int CV = C / VW;
+    const int e = blockIdx.x * TPB + threadIdx.x;
+    if (e >= W * CV) return;
+    const int ix = e / CV, c = (e - ix * CV) * VW;
+    const int n = blockIdx.y / H, iy = blockIdx.y - n * H;
+    int uy[3], ux[3];
+    uy[0] = iy + p;
+    ux[0] = ix + p;
+    const int ky = 1 + mirrors(iy, H, p, uy + 1), kx = 1 + mirrors(ix, W, p, ux + 1);
+    if (ky == 1 && kx == 1) return;  // not in the band
+    const int Hp = H + 2 * p, Wp = W + 2 * p;
+    float acc[VW];
+#pragma unroll
+    for (int k = 0; k < VW; ++k) acc[k] = 0.f;
+    for (int a = 0; a < ky; ++a)
+        for (int b = 0; b < kx; ++b) {
+            if (a == 0 && b == 0) continue;
+            float v[VW];
+            ldvec<VW>(g, IRGAN_F32, (((long)n * Hp + uy[a]) * Wp + ux[b]) * C + c, v);
+#pragma unroll
+            for (int k = 0; k < VW; ++k) acc[k] += v[k];
+        }
+    const long o = (((long)n * H + iy) * W + ix) * lddx + dxoff + c;
+    float d[VW];
+    ldvec<VW>(dx, dt, o, d);
+#pragma unroll
+    for (int k = 0; k < VW; ++k) d[k] += acc[k];
+    stvec<VW>(dx, dt, o, d);
+}
+
+// 2x2/2 max pooling; blockIdx.y = n*Ho + i, threads over (j, channel group of VW)
+template <int VW>
+__global__ __launch_bounds__(TPB) void maxpool_fwd_kernel(const void* __restrict__ x, int dt, int H, int W, int C,
+                                                          void* __restrict__ y) {
+    const int Ho = H / 2, Wo = W / 2, CV = C / VW;
+    const int e = blockIdx.x * TPB + threadIdx.x;
+    if (e >= Wo * CV) return;
+    const int j = e / CV, c = (e - j * CV) * VW;
+    const int n = blockIdx.y / Ho, i = blockIdx.y - n * Ho;
+    float m[VW];
+#pragma unroll
+    for (int k = 0; k < VW; ++k) m[k] = -INFINITY;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            float v[VW];
+            ldvec<VW>(x, dt, (((long)n * H + 2 * i + a) * W + 2 * j + b) * C + c, v);
+#pragma unroll
+            for (int k = 0; k < VW; ++k)
+                if (v[k] > m[k] || isnan(v[k])) m[k] = v[k];
+        }
+    stvec<VW>(y, dt, (((long)n * Ho + i) * Wo + j) * C + c, m);
+}
+
+// gradient routed to the (first) argmax; relu_mask folds the ReLU' of the pool input
+template <int VW>
 __global__ __launch_bounds__(TPB) void maxpool_bwd_kernel(const void* __restrict__ x, const void* __restrict__ dy,
                                                           int dt, int H, int W, int C, void* __restrict__ dx,
-                                                          int relu_mask, long total) {
-    const int Ho = H / 2, Wo = W / 2;
-    for (long idx = blockIdx.x * (long)TPB + threadIdx.x; idx < total; idx += (long)gridDim.x * TPB) {
-        long t = idx;
-        const int c = (int)(t % C); t /= C;
-        const int j = (int)(t % Wo); t /= Wo;
-        const int i = (int)(t % Ho);
-        const int n = (int)(t / Ho);
-        float m = -INFINITY;
-        int am = 0;
-        for (int k = 0; k < 4; ++k) {
-            float v = ldv(x, dt, (((long)n * H + 2 * i + (k >> 1)) * W + 2 * j + (k & 1)) * C + c);
-            if (v > m || isnan(v)) { m = v; am = k; }
-        }
-        float g = ldv(dy, dt, idx);
-        if (relu_mask && !(m > 0.f)) g = 0.f;  // pool input is a ReLU output: fold relu' in
-        for (int k = 0; k < 4; ++k)
-            stv(dx, dt, (((long)n * H + 2 * i + (k >> 1)) * W + 2 * j + (k & 1)) * C + c, k == am ? g : 0.f);
+                                                          int relu_mask) {
+    const int Ho = H / 2, Wo = W / 2, CV = C / VW;
+    const int e = blockIdx.x * TPB + threadIdx.x;
+    if (e >= Wo * CV) return;
+    const int j = e / CV, c = (e - j * CV) * VW;
+    const int n = blockIdx.y / Ho, i = blockIdx.y - n * Ho;
+    float xv[4][VW], m[VW];
+    int am[VW];
+#pragma unroll
+    for (int k = 0; k < VW; ++k) { m[k] = -INFINITY; am[k] = 0; }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        ldvec<VW>(x, dt, (((long)n * H + 2 * i + (q >> 1)) * W + 2 * j + (q & 1)) * C + c, xv[q]);
+#pragma unroll
+        for (int k = 0; k < VW; ++k)
+            if (xv[q][k] > m[k] || isnan(xv[q][k])) { m[k] = xv[q][k]; am[k] = q; }
+    }
+    float g[VW];
+    ldvec<VW>(dy, dt, (((long)n * Ho + i) * Wo + j) * C + c, g);
+#pragma unroll
+    for (int k = 0; k < VW; ++k)
+        if (relu_mask && !(m[k] > 0.f)) g[k] = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        float o[VW];
+#pragma unroll
+        for (int k = 0; k < VW; ++k) o[k] = am[k] == q ? g[k] : 0.f;
+        stvec<VW>(dx, dt, (((long)n * H + 2 * i + (q >> 1)) * W + 2 * j + (q & 1)) * C + c, o);
     }
 }
 
@@ -310,11 +375,34 @@ extern "C" int irgan_sep_resample(const void* in, int32_t in_dtype, int32_t N, i
     return 0;
 }
 
+extern "C" int irgan_reflect_ring_fold(const float* g, int32_t N, int32_t H, int32_t W, int32_t C, int32_t p,
+                                      void* dx, int32_t dx_dtype, int32_t lddx, int32_t dxoff, irgan_stream_t s) {
+    if ((long)N * H * W * C <= 0 || p <= 0) return 0;
+    if ((long)N * H > 65535 || p >= H || p >= W) return IRGAN_EUNSUPPORTED;
+    const bool vec = C % 8 == 0 && lddx % 8 == 0 && dxoff % 8 == 0;
+    if (vec) {
+        dim3 gr(irgan_cdiv((long)W * (C / 8), TPB), N * H);
+        ring_fold_kernel<8><<<gr, TPB, 0, (hipStream_t)s>>>(g, H, W, C, p, dx, dx_dtype, lddx, dxoff);
+    } else {
+        dim3 gr(irgan_cdiv((long)W * C, TPB), N * H);
+        ring_fold_kernel<1><<<gr, TPB, 0, (hipStream_t)s>>>(g, H, W, C, p, dx, dx_dtype, lddx, dxoff);
+    }
+    IRGAN_LAUNCH_CHECK();
+    return 0;
+}
+
 extern "C" int irgan_maxpool_fwd(const void* x, int32_t dt, int32_t N, int32_t H, int32_t W, int32_t C, void* y,
                                  irgan_stream_t s) {
     long total = (long)N * (H / 2) * (W / 2) * C;
     RS_CHECK(total);
-    maxpool_fwd_kernel<<<nblocks(total), TPB, 0, (hipStream_t)s>>>(x, dt, H, W, C, y, total);
+    if ((long)N * (H / 2) > 65535) return IRGAN_EUNSUPPORTED;
+    if (C % 8 == 0) {
+        dim3 g(irgan_cdiv((long)(W / 2) * (C / 8), TPB), N * (H / 2));
+        maxpool_fwd_kernel<8><<<g, TPB, 0, (hipStream_t)s>>>(x, dt, H, W, C, y);
+    } else {
+        dim3 g(irgan_cdiv((long)(W / 2) * C, TPB), N * (H / 2));
+        maxpool_fwd_kernel<1><<<g, TPB, 0, (hipStream_t)s>>>(x, dt, H, W, C, y);
+    }
     IRGAN_LAUNCH_CHECK();
     return 0;
 }
@@ -323,7 +411,14 @@ extern "C" int irgan_maxpool_bwd(const void* x, const void* dy, int32_t dt, int3
                                  void* dx, int32_t relu_mask, irgan_stream_t s) {
     long total = (long)N * (H / 2) * (W / 2) * C;
     RS_CHECK(total);
-    maxpool_bwd_kernel<<<nblocks(total), TPB, 0, (hipStream_t)s>>>(x, dy, dt, H, W, C, dx, relu_mask, total);
+    if ((long)N * (H / 2) > 65535) return IRGAN_EUNSUPPORTED;
+    if (C % 8 == 0) {
+        dim3 g(irgan_cdiv((long)(W / 2) * (C / 8), TPB), N * (H / 2));
+        maxpool_bwd_kernel<8><<<g, TPB, 0, (hipStream_t)s>>>(x, dy, dt, H, W, C, dx, relu_mask);
+    } else {
+        dim3 g(irgan_cdiv((long)(W / 2) * C, TPB), N * (H / 2));
+        maxpool_bwd_kernel<1><<<g, TPB, 0, (hipStream_t)s>>>(x, dy, dt, H, W, C, dx, relu_mask);
+    }
     IRGAN_LAUNCH_CHECK();
     return 0;
 }

@@ -204,19 +204,35 @@ def conv_dgrad(pc: PackedConv, dy: Feat, dx: Feat, accumulate=False, mask: Feat 
     s = pc.spec
     assert dy.C == pc.cout_eff and dx.C == s.cin and dy.dt == pc.dtype
     if pc.reflect:
+        # Backward-data over the reflect-padded domain g (Hp x Wp) folded back:
+        # the interior u in [p, H+p) maps 1:1 onto dx and is written there
+        # directly; only the ring of width p goes to the fp32 pad buffer (2p
+        # strided launches), and irgan_reflect_ring_fold adds it onto dx's band.
         p = s.pad
-        Hp, Wp = dx.H + 2 * p, dx.W + 2 * p
-        assert pad_buf is not None and pad_buf.numel() >= dx.N * Hp * Wp * s.cin
-        tgt = Feat(pad_buf[:dx.N * Hp * Wp * s.cin].view(dx.N, Hp, Wp, s.cin))
-        (_, _, ay, c0y), (_, _, ax, c0x), buf = pc.dg[0]
-        d = _desc(N=dy.N, H=dy.H, W=dy.W, Cin=pc.cout_eff, ldx=dy.ld, xoff=dy.off, Ho=Hp, Wo=Wp, Cout=s.cin,
-                  ldy=tgt.ld, yoff=0, OH=Hp, OW=Wp, omy=1, ooy=0, omx=1, oox=0, KH=ay, KW=ax, sy=1, sx=1,
-                  c0y=c0y, c0x=c0x, pad_mode=PAD_ZERO, act=0, accumulate=0, dtype=pc.dtype, out_dtype=F32,
-                  mask_act=0, ldm=0, moff=0)
-        TIMER.wrap(conv_tag("dgrad", s, (dx.H, dx.W), dx.N), lambda: _lib.call(
-            "irgan_conv_fwd", ctypes.byref(d), dy.ptr, P(buf), None, tgt.ptr, None, stream()))
+        H, W = dx.H, dx.W
+        Hp, Wp = H + 2 * p, W + 2 * p
         assert mask is None
-        reflect_fold(tgt, dx, p, accumulate)
+        (_, _, ay, c0y), (_, _, ax, c0x), buf = pc.dg[0]
+        base = dict(N=dy.N, H=dy.H, W=dy.W, Cin=pc.cout_eff, ldx=dy.ld, xoff=dy.off, Cout=s.cin, KH=ay, KW=ax,
+                    pad_mode=PAD_ZERO, act=0, dtype=pc.dtype, mask_act=0, ldm=0, moff=0)
+        d = _desc(**base, Ho=H, Wo=W, ldy=dx.ld, yoff=dx.off, OH=H, OW=W, omy=1, ooy=0, omx=1, oox=0, sy=1, sx=1,
+                  c0y=c0y + p, c0x=c0x + p, accumulate=int(accumulate), out_dtype=dx.dt)
+        TIMER.wrap(conv_tag("dgrad", s, (H, W), dx.N), lambda: _lib.call(
+            "irgan_conv_fwd", ctypes.byref(d), dy.ptr, P(buf), None, dx.ptr, None, stream()))
+        if p == 0:
+            return
+        assert pad_buf is not None and pad_buf.numel() >= dx.N * Hp * Wp * s.cin
+        tgt = pad_buf[:dx.N * Hp * Wp * s.cin]
+        ring = dict(base, ldy=s.cin, yoff=0, OH=Hp, OW=Wp, accumulate=0, out_dtype=F32)
+        for k in range(p):
+            # padded rows k and H+p+k (full width)
+            dr = _desc(**ring, Ho=2, Wo=Wp, omy=H + p, ooy=k, omx=1, oox=0, sy=H + p, sx=1, c0y=c0y + k, c0x=c0x)
+            _lib.call("irgan_conv_fwd", ctypes.byref(dr), dy.ptr, P(buf), None, P(tgt), None, stream())
+            # padded columns k and W+p+k (interior rows)
+            dcl = _desc(**ring, Ho=H, Wo=2, omy=1, ooy=p, omx=W + p, oox=k, sy=1, sx=W + p, c0y=c0y + p,
+                        c0x=c0x + k)
+            _lib.call("irgan_conv_fwd", ctypes.byref(dcl), dy.ptr, P(buf), None, P(tgt), None, stream())
+        _lib.call("irgan_reflect_ring_fold", P(tgt), dx.N, H, W, s.cin, p, dx.ptr, dx.dt, dx.ld, dx.off, stream())
         return
     st = s.stride
     for (py, _, ay, c0y), (px, _, ax, c0x), buf in pc.dg:

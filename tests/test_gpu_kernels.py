@@ -243,6 +243,21 @@ def test_losses(ops):
     assert relerr(gp.cpu(), pr.grad) < 1e-6
 
 
+@pytest.mark.parametrize("count", [1 << 20, 1001])
+def test_l1_bf16_feature_maps(ops, count):
+    torch.manual_seed(6)
+    a = torch.randn(count).to(torch.bfloat16)
+    b = torch.randn(count).to(torch.bfloat16)
+    ga = torch.zeros(count, dtype=torch.bfloat16, device=DEV)
+    loss = torch.zeros(1, dtype=torch.float64, device=DEV)
+    ops.l1(a.to(DEV), b.to(DEV), 30.0, ga, loss)
+    d = a.double() - b.double()
+    ref = d.abs().mean().item() * 30
+    assert abs(loss.item() - ref) < 1e-5 * ref
+    want = (torch.sign(d) * 30 / count).float()
+    assert torch.allclose(ga.cpu().float(), want, rtol=8e-3, atol=0)
+
+
 def test_adam_matches_torch(ops):
     torch.manual_seed(5)
     p = torch.randn(1000)
