@@ -63,6 +63,13 @@ typedef struct irgan_conv_desc {
 int irgan_conv_fwd(const irgan_conv_desc* d, const void* x, const void* w,
                    const float* bias, void* y, const void* mask, irgan_stream_t s);
 
+/* Split-K partial sums of irgan_conv_fwd (fp32 out; no bias, activation, mask or
+ * accumulate): the K range is cut into ksplit parts and part ks lands at
+ * y + ks*split_stride.  The consumer sums the parts (e.g. irgan_reflect_ring_fold).
+ * bf16 LDS-DMA path; other dtypes support ksplit == 1 only. */
+int irgan_conv_fwd_splitk(const irgan_conv_desc* d, const void* x, const void* w, float* y,
+                          int32_t ksplit, int64_t split_stride, irgan_stream_t s);
+
 /* dw[cout][ky][kx][cin] += sum_pixels dy * im2col(x)  (fp32 atomics, split-K
  * over pixels) -- replaces the weight half of convolution_backward.  d is the
  * FORWARD descriptor (x = forward input, dy = grad at the forward output with
@@ -125,12 +132,16 @@ int irgan_channel_sum(const void* g, int32_t dtype, int32_t P, int32_t C, int32_
  * or a negative IRGAN_E* code. */
 int irgan_resample_table(int32_t kind, int32_t n_in, int32_t p, int32_t transpose, int32_t* idx,
                          float* w, int32_t tmax, int32_t rows_cap);
-/* Border half of the nn.ReflectionPad2d(p) backward (ir:381, 402, 459, 528):
- * g (fp32 NHWC, (H+2p) x (W+2p)) holds the backward-data result on the padded
- * RING only (the interior went straight to dx); dx[band] += every mirrored ring
- * value.  Together: dx = fold(g) without materialising the padded interior. */
-int irgan_reflect_ring_fold(const float* g, int32_t N, int32_t H, int32_t W, int32_t C, int32_t p,
-                            void* dx, int32_t dx_dtype, int32_t lddx, int32_t dxoff, irgan_stream_t s);
+/* Border half of the nn.ReflectionPad2d(p) backward (ir:381, 402, 459, 528).
+ * The backward-data result g over the padded (H+2p) x (W+2p) domain has its
+ * interior written straight to dx; its RING arrives as nsplit fp32 split-K
+ * partials in two compact NHWC buffers: rows[ks][N][2p][W+2p][C] (padded rows
+ * k and H+p+k at compact rows k and p+k) and cols[ks][N][H][2p][C] (padded
+ * columns k and W+p+k of the interior rows).  dx[band] += every mirrored ring
+ * value (a gather: deterministic).  Together: dx = fold(g). */
+int irgan_reflect_ring_fold(const float* rows, const float* cols, int32_t nsplit, int32_t N, int32_t H,
+                            int32_t W, int32_t C, int32_t p, void* dx, int32_t dx_dtype, int32_t lddx,
+                            int32_t dxoff, irgan_stream_t s);
 /* out = (Wy (x) Wx) in on NHWC slices, tables from irgan_resample_table (device
  * copies); accumulate: out += result.  Downsample / UpsampleAA forward and
  * backward, and the reflect-pad fold, are all this one launch. */

@@ -16,6 +16,8 @@
 
 extern "C" int irgan_conv_fwd_glds(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
                                    const void* mask, hipStream_t st);
+extern "C" int irgan_conv_fwd_glds_split(const irgan_conv_desc* d, const void* x, const void* w, const float* bias,
+                                         void* y, const void* mask, int ksplit, long sstride, hipStream_t st);
 extern "C" int irgan_conv_fwd_halo(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
                                    const void* mask, hipStream_t st);
 extern "C" int irgan_conv_wgrad_halo(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, int splitk,
@@ -594,3 +596,17 @@ extern "C" int irgan_weight_pack(const float* src, void* dst, int32_t dtype, int
 }
 
 extern "C" int irgan_version(void) { return 1; }
+
+// Split-K partial sums (no bias / activation / mask): partial ks of the
+// fp32 output lands at y + ks*split_stride.  Used for thin output domains
+// (the reflect-pad ring) whose full-K blocks would run a long serial K loop.
+extern "C" int irgan_conv_fwd_splitk(const irgan_conv_desc* d, const void* x, const void* w, float* y,
+                                     int32_t ksplit, int64_t split_stride, irgan_stream_t s) {
+    if (d->out_dtype != IRGAN_F32 || d->act != IRGAN_ACT_NONE || d->accumulate || ksplit < 1) return IRGAN_EINVAL;
+    const bool fast = (d->Cin % 64 == 0) && (d->ldx % 8 == 0) && (d->xoff % 8 == 0);
+    const bool narrow = (d->Cin == 8 || d->Cin == 16 || d->Cin == 32) && d->ldx % 8 == 0 && d->xoff % 8 == 0;
+    if (d->dtype == IRGAN_BF16 && (fast || narrow))
+        return irgan_conv_fwd_glds_split(d, x, w, nullptr, y, nullptr, ksplit, (long)split_stride, (hipStream_t)s);
+    if (ksplit != 1) return IRGAN_EUNSUPPORTED;
+    return irgan_conv_fwd(d, x, w, nullptr, y, nullptr, s);
+}

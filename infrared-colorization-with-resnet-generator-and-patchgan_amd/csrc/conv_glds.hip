@@ -51,7 +51,8 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_glds_kernel(const irgan_conv_
                                                                const bf16_t* __restrict__ w,
                                                                const float* __restrict__ bias, void* __restrict__ y,
                                                                const void* __restrict__ mask,
-                                                               const bf16_t* __restrict__ zero, int ntn, int swz) {
+                                                               const bf16_t* __restrict__ zero, int ntn, int swz,
+                                                               int ksplit, long sstride) {
     constexpr int BM = 256, STAGES = 3;
     constexpr int ABYTES = BM * 128, STAGE = ABYTES + BN * 128;
     constexpr int MI = 4, NJ = BN / 32;  // wave tile 64 x BN/2
@@ -65,8 +66,12 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_glds_kernel(const irgan_conv_
     const long M = (long)d.N * HoWo;
     const int taps = d.KH * d.KW;
     const int K = (taps * d.Cin + 63) / 64 * 64;  // weight row stride (taps zero-padded)
-    // 1-D grid, N-tiles fastest: the tiles of one pixel block are adjacent
-    const int t = xcd_tile(blockIdx.x, gridDim.x, swz);
+    // 1-D grid, N-tiles fastest: the tiles of one pixel block are adjacent;
+    // K-splits outermost (split ks writes its partial sums at y + ks*sstride)
+    int t = xcd_tile(blockIdx.x, gridDim.x, swz);
+    const int tiles_mn = gridDim.x / ksplit;
+    const int ks = t / tiles_mn;
+    t -= ks * tiles_mn;
     const long m0 = (long)(t / ntn) * BM;
     const int n0 = (t % ntn) * BN;
     const int sub = lane >> 3;
@@ -139,14 +144,15 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_glds_kernel(const irgan_conv_
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    const int nk = K / 64;
-    issue(0, 0);
-    if (nk > 1) issue(1, 1);
+    const int nk_all = K / 64, kper = (nk_all + ksplit - 1) / ksplit;
+    const int kb = ks * kper, nk = min(nk_all - kb, kper);  // this split's K-tiles [kb, kb+nk)
+    if (nk > 0) issue(kb, 0);
+    if (nk > 1) issue(kb + 1, 1);
     for (int kt = 0; kt < nk; ++kt) {
         if (kt + 1 < nk) wait_vmcnt<AU + BU>();
         else wait_vmcnt<0>();
         __builtin_amdgcn_s_barrier();
-        if (kt + 2 < nk) issue(kt + 2, (kt + 2) % STAGES);
+        if (kt + 2 < nk) issue(kb + kt + 2, (kt + 2) % STAGES);
         const char* A = smem + (kt % STAGES) * STAGE;
         const char* B = A + ABYTES;
 #pragma unroll
@@ -168,7 +174,8 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_glds_kernel(const irgan_conv_
     }
 
     // epilogue: C[row = (lane>>4)*4 + r][col = lane & 15] of each 16x16 fragment
-    conv_epilogue<BN, MI, NJ, 4, 2, 512>(d, acc, smem, wm, wn, n0, bias, y, mask, [&](int m) -> long {
+    void* yk = ks ? (void*)((float*)y + ks * sstride) : y;  // split partials are fp32
+    conv_epilogue<BN, MI, NJ, 4, 2, 512>(d, acc, smem, wm, wn, n0, bias, yk, mask, [&](int m) -> long {
         const long mm = m0 + m;
         if (mm >= M) return -1;
         const int n = (int)(mm / HoWo), rr = (int)(mm - (long)n * HoWo), ii = rr / d.Wo, jj = rr - ii * d.Wo;
@@ -181,25 +188,31 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_glds_kernel(const irgan_conv_
 // zero page for padded / out-of-range glds sources (4 KiB, device global)
 __device__ __attribute__((aligned(4096))) bf16_t g_irgan_zero_page[2048];
 
-extern "C" int irgan_conv_fwd_glds(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
-                                   const void* mask, hipStream_t st) {
+extern "C" int irgan_conv_fwd_glds_split(const irgan_conv_desc* d, const void* x, const void* w, const float* bias,
+                                         void* y, const void* mask, int ksplit, long sstride, hipStream_t st) {
     const long M = (long)d->N * d->Ho * d->Wo;
     if (M <= 0 || d->Cout <= 0) return 0;
     static bf16_t* zero = nullptr;  // immutable after first lookup
     if (!zero && hipGetSymbolAddress((void**)&zero, HIP_SYMBOL(g_irgan_zero_page)) != hipSuccess)
         return IRGAN_EUNSUPPORTED;
     static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
+    if (ksplit < 1) ksplit = 1;
     if (d->Cout > 64) {
         const int ntn = irgan_cdiv(d->Cout, 128);
-        conv_fwd_glds_kernel<128><<<irgan_cdiv(M, 256) * ntn, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w,
-                                                                            bias, y, mask, zero, ntn, swz);
+        conv_fwd_glds_kernel<128><<<irgan_cdiv(M, 256) * ntn * ksplit, 512, 0, st>>>(
+            *d, (const bf16_t*)x, (const bf16_t*)w, bias, y, mask, zero, ntn, swz, ksplit, sstride);
     } else {
         const int ntn = irgan_cdiv(d->Cout, 64);
-        conv_fwd_glds_kernel<64><<<irgan_cdiv(M, 256) * ntn, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w,
-                                                                           bias, y, mask, zero, ntn, swz);
+        conv_fwd_glds_kernel<64><<<irgan_cdiv(M, 256) * ntn * ksplit, 512, 0, st>>>(
+            *d, (const bf16_t*)x, (const bf16_t*)w, bias, y, mask, zero, ntn, swz, ksplit, sstride);
     }
     IRGAN_LAUNCH_CHECK();
     return 0;
+}
+
+extern "C" int irgan_conv_fwd_glds(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
+                                   const void* mask, hipStream_t st) {
+    return irgan_conv_fwd_glds_split(d, x, w, bias, y, mask, 1, 0, st);
 }
 
 // ---------------------------------------------------------------------------

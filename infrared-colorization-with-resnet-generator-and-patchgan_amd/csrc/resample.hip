@@ -98,13 +98,14 @@ __global__ __launch_bounds__(TPB) void sep_kernel(const void* __restrict__ in, i
     stvec<VW>(out, odt, o, acc);
 }
 
-// Reflect-pad backward, border part.  g is the backward-data result over the
-// padded domain (Hp = H+2p) of which only the RING (padded rows/cols outside
-// [p, H+p) x [p, W+p)) has been computed; the interior was written straight to
-// dx.  Along one axis, dx index i receives padded u = i+p (interior) and at most
-// one mirror: u = p-i (1 <= i <= p) or u = 2H-2-i+p (H-1-p <= i <= H-2).  Each
-// band element of dx gathers every (uy, ux) pair except the interior-interior
-// one (deterministic, no atomics).  blockIdx.y = n*H + iy, threads over (ix, c8).
+// Reflect-pad backward, border part.  The backward-data result g over the
+// padded domain (H+2p) x (W+2p) has its interior in dx already; its RING comes
+// as nsplit split-K partials in compact buffers rows[ks][N][2p][Wp][C] and
+// cols[ks][N][H][2p][C].  Along one axis dx index i receives padded u = i+p
+// (interior) and at most one mirror: u = p-i (1 <= i <= p) or u = 2H-2-i+p
+// (H-1-p <= i <= H-2).  Each band element of dx gathers every (uy, ux) pair
+// except the interior-interior one (deterministic, no atomics).
+// blockIdx.y = n*H + iy, threads over (ix, channel group).
 IRGAN_HD int mirrors(int i, int n, int p, int* u) {  // padded coords != i+p mapping to i
     int k = 0;
     if (i >= 1 && i <= p) u[k++] = p - i;
@@ -113,7 +114,8 @@ IRGAN_HD int mirrors(int i, int n, int p, int* u) {  // padded coords != i+p map
 }
 
 template <int VW>
-__global__ __launch_bounds__(TPB) void ring_fold_kernel(const float* __restrict__ g, int H, int W, int C, int p,
+__global__ __launch_bounds__(TPB) void ring_fold_kernel(const float* __restrict__ rows, const float* __restrict__ cols,
+                                                        int nsplit, int N, int H, int W, int C, int p,
                                                         void* __restrict__ dx, int dt, int lddx, int dxoff) {
     const int CV = C / VW;
     const int e = blockIdx.x * TPB + threadIdx.x;
@@ -125,17 +127,32 @@ __global__ __launch_bounds__(TPB) void ring_fold_kernel(const float* __restrict_
     ux[0] = ix + p;
     const int ky = 1 + mirrors(iy, H, p, uy + 1), kx = 1 + mirrors(ix, W, p, ux + 1);
     if (ky == 1 && kx == 1) return;  // not in the band
-    const int Hp = H + 2 * p, Wp = W + 2 * p;
+    const int Wp = W + 2 * p;
+    const long rstride = (long)N * 2 * p * Wp * C, cstride = (long)N * H * 2 * p * C;
     float acc[VW];
 #pragma unroll
     for (int k = 0; k < VW; ++k) acc[k] = 0.f;
     for (int a = 0; a < ky; ++a)
         for (int b = 0; b < kx; ++b) {
             if (a == 0 && b == 0) continue;
-            float v[VW];
-            ldvec<VW>(g, IRGAN_F32, (((long)n * Hp + uy[a]) * Wp + ux[b]) * C + c, v);
+            const int y = uy[a], x = ux[b];
+            const float* src;
+            long stride;
+            if (y < p || y >= H + p) {
+                const int r = y < p ? y : p + (y - H - p);
+                src = rows + (((long)n * 2 * p + r) * Wp + x) * C + c;
+                stride = rstride;
+            } else {
+                const int cc = x < p ? x : p + (x - W - p);
+                src = cols + (((long)n * H + (y - p)) * 2 * p + cc) * C + c;
+                stride = cstride;
+            }
+            for (int ks = 0; ks < nsplit; ++ks) {
+                float v[VW];
+                ldvec<VW>(src, IRGAN_F32, ks * stride, v);
 #pragma unroll
-            for (int k = 0; k < VW; ++k) acc[k] += v[k];
+                for (int k = 0; k < VW; ++k) acc[k] += v[k];
+            }
         }
     const long o = (((long)n * H + iy) * W + ix) * lddx + dxoff + c;
     float d[VW];
@@ -375,17 +392,20 @@ extern "C" int irgan_sep_resample(const void* in, int32_t in_dtype, int32_t N, i
     return 0;
 }
 
-extern "C" int irgan_reflect_ring_fold(const float* g, int32_t N, int32_t H, int32_t W, int32_t C, int32_t p,
-                                      void* dx, int32_t dx_dtype, int32_t lddx, int32_t dxoff, irgan_stream_t s) {
+extern "C" int irgan_reflect_ring_fold(const float* rows, const float* cols, int32_t nsplit, int32_t N, int32_t H,
+                                      int32_t W, int32_t C, int32_t p, void* dx, int32_t dx_dtype, int32_t lddx,
+                                      int32_t dxoff, irgan_stream_t s) {
     if ((long)N * H * W * C <= 0 || p <= 0) return 0;
-    if ((long)N * H > 65535 || p >= H || p >= W) return IRGAN_EUNSUPPORTED;
+    if ((long)N * H > 65535 || p >= H || p >= W || nsplit < 1) return IRGAN_EUNSUPPORTED;
     const bool vec = C % 8 == 0 && lddx % 8 == 0 && dxoff % 8 == 0;
     if (vec) {
         dim3 gr(irgan_cdiv((long)W * (C / 8), TPB), N * H);
-        ring_fold_kernel<8><<<gr, TPB, 0, (hipStream_t)s>>>(g, H, W, C, p, dx, dx_dtype, lddx, dxoff);
+        ring_fold_kernel<8><<<gr, TPB, 0, (hipStream_t)s>>>(rows, cols, nsplit, N, H, W, C, p, dx, dx_dtype, lddx,
+                                                            dxoff);
     } else {
         dim3 gr(irgan_cdiv((long)W * C, TPB), N * H);
-        ring_fold_kernel<1><<<gr, TPB, 0, (hipStream_t)s>>>(g, H, W, C, p, dx, dx_dtype, lddx, dxoff);
+        ring_fold_kernel<1><<<gr, TPB, 0, (hipStream_t)s>>>(rows, cols, nsplit, N, H, W, C, p, dx, dx_dtype, lddx,
+                                                            dxoff);
     }
     IRGAN_LAUNCH_CHECK();
     return 0;

@@ -199,15 +199,17 @@ def conv_fwd(pc: PackedConv, x: Feat, y: Feat, act=ACT_NONE, bias=True, accumula
 
 def conv_dgrad(pc: PackedConv, dy: Feat, dx: Feat, accumulate=False, mask: Feat = None, mask_act=0,
                pad_buf: torch.Tensor = None, bias=False):
-    """dx = d(conv)/dx^T dy.  Reflect-padded layers go through an fp32
-    (H+2p)x(W+2p) buffer and the reflect fold; stride-2 layers launch per phase."""
+    """dx = d(conv)/dx^T dy.  Reflect-padded layers: interior straight into dx,
+    the padded ring as split-K partials in pad_buf (fp32 scratch) folded back by
+    irgan_reflect_ring_fold; stride-2 layers launch per phase."""
     s = pc.spec
     assert dy.C == pc.cout_eff and dx.C == s.cin and dy.dt == pc.dtype
     if pc.reflect:
         # Backward-data over the reflect-padded domain g (Hp x Wp) folded back:
         # the interior u in [p, H+p) maps 1:1 onto dx and is written there
-        # directly; only the ring of width p goes to the fp32 pad buffer (2p
-        # strided launches), and irgan_reflect_ring_fold adds it onto dx's band.
+        # directly; only the ring of width p is computed separately (2p strided
+        # split-K launches into pad_buf), and irgan_reflect_ring_fold adds it
+        # onto dx's border band.
         p = s.pad
         H, W = dx.H, dx.W
         Hp, Wp = H + 2 * p, W + 2 * p
@@ -221,18 +223,26 @@ def conv_dgrad(pc: PackedConv, dy: Feat, dx: Feat, accumulate=False, mask: Feat 
             "irgan_conv_fwd", ctypes.byref(d), dy.ptr, P(buf), None, dx.ptr, None, stream()))
         if p == 0:
             return
-        assert pad_buf is not None and pad_buf.numel() >= dx.N * Hp * Wp * s.cin
-        tgt = pad_buf[:dx.N * Hp * Wp * s.cin]
-        ring = dict(base, ldy=s.cin, yoff=0, OH=Hp, OW=Wp, accumulate=0, out_dtype=F32)
+        # ring in split-K partials: rows[ks][N][2p][Wp][C], cols[ks][N][H][2p][C]
+        rsz, csz = dx.N * 2 * p * Wp * s.cin, dx.N * H * 2 * p * s.cin
+        nk = -(-(ay * ax * pc.cout_eff) // 64)
+        ksplit = 1 if pc.dtype == F32 else max(1, min(nk // 2, 16))
+        assert pad_buf is not None
+        ksplit = max(1, min(ksplit, pad_buf.numel() // (rsz + csz)))
+        rows_b = pad_buf[:ksplit * rsz]
+        cols_b = pad_buf[ksplit * rsz:ksplit * (rsz + csz)]
+        ring = dict(base, ldy=s.cin, yoff=0, accumulate=0, out_dtype=F32)
         for k in range(p):
-            # padded rows k and H+p+k (full width)
-            dr = _desc(**ring, Ho=2, Wo=Wp, omy=H + p, ooy=k, omx=1, oox=0, sy=H + p, sx=1, c0y=c0y + k, c0x=c0x)
-            _lib.call("irgan_conv_fwd", ctypes.byref(dr), dy.ptr, P(buf), None, P(tgt), None, stream())
-            # padded columns k and W+p+k (interior rows)
-            dcl = _desc(**ring, Ho=H, Wo=2, omy=1, ooy=p, omx=W + p, oox=k, sy=1, sx=W + p, c0y=c0y + p,
-                        c0x=c0x + k)
-            _lib.call("irgan_conv_fwd", ctypes.byref(dcl), dy.ptr, P(buf), None, P(tgt), None, stream())
-        _lib.call("irgan_reflect_ring_fold", P(tgt), dx.N, H, W, s.cin, p, dx.ptr, dx.dt, dx.ld, dx.off, stream())
+            # padded rows k and H+p+k (full width) -> compact rows k, p+k
+            dr = _desc(**ring, Ho=2, Wo=Wp, OH=2 * p, OW=Wp, omy=p, ooy=k, omx=1, oox=0, sy=H + p, sx=1,
+                       c0y=c0y + k, c0x=c0x)
+            _lib.call("irgan_conv_fwd_splitk", ctypes.byref(dr), dy.ptr, P(buf), P(rows_b), ksplit, rsz, stream())
+            # padded columns k and W+p+k of the interior rows -> compact columns k, p+k
+            dcl = _desc(**ring, Ho=H, Wo=2, OH=H, OW=2 * p, omy=1, ooy=0, omx=p, oox=k, sy=1, sx=W + p,
+                        c0y=c0y + p, c0x=c0x + k)
+            _lib.call("irgan_conv_fwd_splitk", ctypes.byref(dcl), dy.ptr, P(buf), P(cols_b), ksplit, csz, stream())
+        _lib.call("irgan_reflect_ring_fold", P(rows_b), P(cols_b), ksplit, dx.N, H, W, s.cin, p, dx.ptr, dx.dt,
+                  dx.ld, dx.off, stream())
         return
     st = s.stride
     for (py, _, ay, c0y), (px, _, ax, c0x), buf in pc.dg:
