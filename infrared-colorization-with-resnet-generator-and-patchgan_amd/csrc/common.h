@@ -44,7 +44,35 @@ IRGAN_HD float wave_sum(float v) {
     return v;
 }
 
-#define IRGAN_LAUNCH_CHECK()                      \
+// ---- LDS-DMA pipelines ---------------------------------------------------
+// global_load_lds_dwordx4: 16 bytes per lane from `src` into lds + 16*lane
+// (M0 = the LDS byte offset, wave-uniform).  Issued through inline asm on
+// purpose: when the compiler sees the builtin's LDS write it cannot tell the
+// ring stage being prefetched from the one being read, and puts
+// `s_waitcnt vmcnt(0)` in front of the next ds_read -- which waits for the
+// prefetch just issued and serialises the whole pipeline.  The kernels order
+// the stages themselves with counted wait_vmcnt<N>() + lds_barrier().
+IRGAN_HD void glds16(const void* src, const void* lds) {
+    const uint32_t m = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)lds;
+    asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "{m0}"(m) : "memory");
+}
+template <int N>
+IRGAN_HD void wait_vmcnt() {
+    static_assert(N >= 0 && N <= 63, "vmcnt");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+IRGAN_HD void lds_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+// XCD-aware tile order.  Workgroups are dealt round-robin to the 8 XCDs
+// (b % 8), each with its own L2.  With nb % 8 == 0 the remap hands XCD k the
+// contiguous logical range [k*nb/8, (k+1)*nb/8), so tiles that share input rows
+// run at the same time on the same L2.  Speed only: any order is correct.
+IRGAN_HD int xcd_tile(int b, int nb, int swz) {
+    if (!swz || (nb & 7)) return b;
+    return (b & 7) * (nb >> 3) + (b >> 3);
+}
+
+#define IRGAN_LAUNCH_CHECK()                    \
     do {                                          \
         hipError_t e__ = hipGetLastError();       \
         if (e__ != hipSuccess) return (int)e__;   \

@@ -13,38 +13,7 @@
 
 namespace {
 
-typedef __attribute__((address_space(3))) void lds_void;
-typedef __attribute__((address_space(1))) const void gbl_cvoid;
-
 IRGAN_HD int lds_off(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
-
-IRGAN_HD void glds16(const void* src, char* lds_base) {
-    __builtin_amdgcn_global_load_lds((gbl_cvoid*)src, (lds_void*)lds_base, 16, 0, 0);
-}
-
-template <int N>
-IRGAN_HD void wait_vmcnt() {
-    static_assert(N >= 0 && N <= 8, "vmcnt");
-    if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-    else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-    else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-    else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-}
-
-// XCD-aware tile order.  Workgroups are dealt round-robin to the 8 XCDs
-// (b % 8), each with its own L2.  With nb % 8 == 0 the remap hands XCD k the
-// contiguous logical range [k*nb/8, (k+1)*nb/8), so tiles that share input rows
-// (neighbouring pixel tiles and their halos, the N-tiles of one pixel tile)
-// run at the same time on the same L2.  Speed only: any order is correct.
-__device__ __forceinline__ int xcd_tile(int b, int nb, int swz) {
-    if (!swz || (nb & 7)) return b;
-    return (b & 7) * (nb >> 3) + (b >> 3);
-}
 
 template <int BN>
 __global__ __launch_bounds__(512, 2) void conv_fwd_glds_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
@@ -151,7 +120,7 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_glds_kernel(const irgan_conv_
     for (int kt = 0; kt < nk; ++kt) {
         if (kt + 1 < nk) wait_vmcnt<AU + BU>();
         else wait_vmcnt<0>();
-        __builtin_amdgcn_s_barrier();
+        lds_barrier();
         if (kt + 2 < nk) issue(kb + kt + 2, (kt + 2) % STAGES);
         const char* A = smem + (kt % STAGES) * STAGE;
         const char* B = A + ABYTES;
@@ -339,7 +308,7 @@ __global__ __launch_bounds__(512, 2) void conv_wgrad_glds_kernel(const irgan_con
     for (int kt = 0; kt < nk; ++kt) {
         if (kt + 1 < nk) wait_vmcnt<AU + BU>();
         else wait_vmcnt<0>();
-        __builtin_amdgcn_s_barrier();
+        lds_barrier();
         if (kt + 2 < nk) issue(pb + (long)(kt + 2) * KP, (kt + 2) % STAGES);
         const char* A = smem + (kt % STAGES) * STAGE;
         const char* B = A + ABYTES;

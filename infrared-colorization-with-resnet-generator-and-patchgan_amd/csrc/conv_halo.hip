@@ -24,25 +24,8 @@ namespace {
 // zero page for padded / out-of-range halo rows (this translation unit's own copy)
 __device__ __attribute__((aligned(4096))) bf16_t g_halo_zero_page[2048];
 
-typedef __attribute__((address_space(3))) void lds_void;
-typedef __attribute__((address_space(1))) const void gbl_cvoid;
 
 IRGAN_HD int lds_off(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
-
-IRGAN_HD void glds16(const void* src, char* lds_base) {
-    __builtin_amdgcn_global_load_lds((gbl_cvoid*)src, (lds_void*)lds_base, 16, 0, 0);
-}
-
-template <int N>
-IRGAN_HD void wait_vmcnt() {
-    static_assert(N >= 0 && N <= 15, "vmcnt");
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-__device__ __forceinline__ int xcd_tile(int b, int nb, int swz) {
-    if (!swz || (nb & 7)) return b;
-    return (b & 7) * (nb >> 3) + (b >> 3);
-}
 
 constexpr int PH = 16, PW = 16;  // output patch
 
@@ -153,7 +136,7 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const irgan_conv_desc
         } else {
             wait_vmcnt<0>();
         }
-        __builtin_amdgcn_s_barrier();
+        lds_barrier();
         if (tp == 0 && c + 1 < nchunk) issue_halo(c + 1);
         if (kt + 2 < nk) issue_w(kt + 2, (kt + 2) % STAGES);
         const char* Hb = sH + (c & 1) * HBYTES;

@@ -25,25 +25,8 @@ namespace {
 
 __device__ __attribute__((aligned(4096))) bf16_t g_wgh_zero_page[2048];
 
-typedef __attribute__((address_space(3))) void lds_void;
-typedef __attribute__((address_space(1))) const void gbl_cvoid;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((address_space(3))) s16x4 lds_s4;
-
-IRGAN_HD void glds16(const void* src, char* lds_base) {
-    __builtin_amdgcn_global_load_lds((gbl_cvoid*)src, (lds_void*)lds_base, 16, 0, 0);
-}
-
-template <int N>
-IRGAN_HD void wait_vmcnt() {
-    static_assert(N >= 0 && N <= 63, "vmcnt");
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-__device__ __forceinline__ int xcd_tile(int b, int nb, int swz) {
-    if (!swz || (nb & 7)) return b;
-    return (b & 7) * (nb >> 3) + (b >> 3);
-}
 
 IRGAN_HD int t128(int r) { return ((r >> 1) & 1) | (((r >> 3) & 1) << 1); }
 IRGAN_HD int t256(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
@@ -163,7 +146,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void wgrad_halo_kernel(const irgan
         } else {
             wait_vmcnt<0>();
         }
-        __builtin_amdgcn_s_barrier();
+        lds_barrier();
         if (kt + 2 < nk) issue(s_beg + kt + 2, (kt + 2) % STAGES);
         const char* A = smem + (kt % STAGES) * STAGE;
         const char* X = A + APIECES * 1024;
