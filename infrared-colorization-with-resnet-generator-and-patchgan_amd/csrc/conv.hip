@@ -18,6 +18,8 @@ extern "C" int irgan_conv_fwd_glds(const irgan_conv_desc* d, const void* x, cons
                                    const void* mask, hipStream_t st);
 extern "C" int irgan_conv_fwd_glds_split(const irgan_conv_desc* d, const void* x, const void* w, const float* bias,
                                          void* y, const void* mask, int ksplit, long sstride, hipStream_t st);
+extern "C" int irgan_conv_fwd_pp(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
+                                 const void* mask, hipStream_t st);
 extern "C" int irgan_conv_fwd_halo(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
                                    const void* mask, hipStream_t st);
 extern "C" int irgan_conv_wgrad_halo(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, int splitk,
@@ -484,6 +486,11 @@ int launch_fwd(const irgan_conv_desc* d, const void* x, const void* w, const flo
         const bool narrow = (d->Cin == 8 || d->Cin == 16 || d->Cin == 32) && d->ldx % 8 == 0 && d->xoff % 8 == 0;
         static const bool use_halo = !getenv("IRGAN_NO_HALO");
         const int taps = d->KH * d->KW;
+        static const bool use_pp = !getenv("IRGAN_NO_PP");
+        if (fast && use_pp && d->sy == 1 && d->sx == 1 && taps >= 2 && d->Cout > 128) {
+            const int rc = irgan_conv_fwd_pp(d, x, w, bias, y, mask, st);
+            if (rc != IRGAN_EUNSUPPORTED) return rc;
+        }
         if (fast && use_halo && d->sy == 1 && d->sx == 1 && taps >= 2) {
             const int rc = irgan_conv_fwd_halo(d, x, w, bias, y, mask, st);
             if (rc != IRGAN_EUNSUPPORTED) return rc;

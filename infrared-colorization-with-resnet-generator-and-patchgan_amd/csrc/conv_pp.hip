@@ -1,0 +1,341 @@
+// bf16 stride-1 convolution, resident input halo, ping-pong wave groups.
+//
+// Same operand staging as conv_halo.hip (a block owns a 16x16 output patch of
+// one image; per 64-channel chunk the (16+KH-1)x(16+KW-1) input halo is DMA'd
+// into LDS once and every tap is an LDS row shift of it; the weight tile of a
+// K-step = one tap x 64 channels streams through a 2-stage ring), but the
+// schedule is built for MFMA occupancy at one block per CU:
+//
+//  * block tile 256 pixels x 256 output channels, 8 waves = 2 groups x 4 waves;
+//    group g owns patch rows [8g, 8g+8), wave wn owns channels [64wn, 64wn+64):
+//    a 128 x 64 wave tile (8 x 4 fragments of mfma_f32_16x16x32_bf16), so a
+//    32-deep sub-step is 12 ds_read_b128 per 32 MFMAs;
+//  * each sub-step (one tap, 32 channels) is two phases per wave: READ (issue
+//    the 12 fragment reads and this wave's share of the next K-step's DMA) and
+//    MFMA (32 MFMAs), each closed by a block barrier.  Group 1 starts one
+//    barrier late, so in every barrier window one group multiplies while the
+//    other reads: each SIMD holds one wave of each group;
+//  * taps are compile-time (KH, KW template); the K-step loop keeps its
+//    chunk / tap counters in scalars, so a phase costs a few SALU ops plus
+//    4 VALU per swizzled fragment address;
+//  * the MFMA computes C^T (weights are the A operand): a lane's 4 accumulator
+//    rows are 4 consecutive output channels of one pixel, so the epilogue
+//    stages bf16 [pixel][channel] rows with 8-byte LDS writes in one pass and
+//    stores 16-byte runs.
+//
+// DMA ordering: K-step k's weights sit in stage k&1 and are read in windows
+// 4k..4k+3 (group 0: 4k, 4k+2; group 1: 4k+1, 4k+3).  W(k+1) is issued in each
+// wave's first READ of step k (that stage was last read in window 4k-1) and is
+// retired by every wave with a counted vmcnt before the barrier closing window
+// 4k+3.  The halo of chunk c+1 is issued after W(k+1) at the first tap of chunk
+// c (its buffer last served chunk c-1).  Reads need no lgkmcnt wait before
+// their barrier except group 1's last READ of a K-step (window 4k+3): the next
+// window may overwrite that stage; every other READ is consumed by the same
+// wave's MFMA phase before any DMA can target its buffer.
+//
+// Preconditions (checked by irgan_conv_fwd_pp): bf16, sy = sx = 1, Cin % 64 == 0,
+// (KH, KW) in {(3,3), (4,4)}, ldx, xoff % 8 == 0, Cout > 128 (channel tiles of
+// 256), no tanh epilogue, input slice and weights < 2^31 elements.
+#include <type_traits>
+
+#include "conv_epilogue.h"
+
+namespace {
+
+__device__ __attribute__((aligned(4096))) bf16_t g_pp_zero_page[2048];
+
+IRGAN_HD int lds_off(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+
+IRGAN_HD void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
+// block barrier that the scheduler cannot move instructions across
+IRGAN_HD void phase_barrier() {
+    sched_fence();
+    lds_barrier();
+    sched_fence();
+}
+IRGAN_HD void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+constexpr int PH = 16, PW = 16;   // output patch
+constexpr int BN = 256;           // output channels per block
+constexpr int HPMAX = 46;         // halo pieces (8 rows of 128 B) for taps up to 4x4: 19*19 = 361 rows
+constexpr int HBYTES = HPMAX * 1024, BBYTES = BN * 128;
+constexpr int LDS = 2 * HBYTES + 2 * BBYTES;
+constexpr int MI = 8, NJ = 4;     // wave tile 128 pixels x 64 channels
+constexpr int WU = BBYTES / 1024 / 8;  // weight pieces per wave per K-step (4)
+constexpr int RSB = BN * 2 + 16;  // bf16 staging row (pixel) stride, bytes
+constexpr int RSF = BN + 4;       // fp32 staging row stride, floats
+static_assert(256 * RSB <= LDS && 128 * RSF * 4 <= LDS, "epilogue staging fits");
+
+template <int KH, int KW>
+__global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
+                                                         const bf16_t* __restrict__ w, const float* __restrict__ bias,
+                                                         void* __restrict__ y, const void* __restrict__ mask,
+                                                         const bf16_t* __restrict__ zero, int ntn, int tpx, int tpy,
+                                                         int swz) {
+    constexpr int TAPS = KH * KW, HWd = PW + KW - 1, HROWS = (PH + KH - 1) * HWd, HP = (HROWS + 7) / 8;
+    static_assert(HP <= HPMAX && HP > 40 && TAPS >= 2, "halo pieces per wave are 5 or 6");
+    __shared__ __attribute__((aligned(1024))) char smem[LDS];
+    char* const sH = smem;
+    char* const sB = smem + 2 * HBYTES;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wid >> 2, wn = wid & 3;
+    int t = xcd_tile(blockIdx.x, gridDim.x, swz);
+    const int nt = t % ntn;
+    t /= ntn;
+    const int pxi = t % tpx;
+    t /= tpx;
+    const int pyi = t % tpy;
+    const int img = t / tpy;
+    const int py0 = pyi * PH, px0 = pxi * PW, n0 = nt * BN;
+    const int nh = (HP - wid + 7) >> 3;  // halo pieces this wave loads: wid, wid+8, ... (5 or 6)
+    const int Kw = TAPS * d.Cin;
+    const int nchunk = d.Cin / 64;
+    const int sub = lane >> 3;
+    const int chunk = (lane & 7) ^ sub;  // source chunk for this lane's LDS slot (row & 7 == sub)
+    const bool reflect = d.pad_mode == IRGAN_PAD_REFLECT;
+
+    int h_off[6];  // element offsets of this lane's halo rows, -1: zero padding
+#pragma unroll
+    for (int u = 0; u < 6; ++u) {
+        const int h = (u * 8 + wid) * 8 + sub;
+        const int hy = h / HWd, hx = h - hy * HWd;
+        int iy = py0 + hy + d.c0y, ix = px0 + hx + d.c0x;
+        if (reflect) {
+            iy = reflect_idx(iy, d.H);
+            ix = reflect_idx(ix, d.W);
+        }
+        const bool ok = (h < HROWS) & ((unsigned)iy < (unsigned)d.H) & ((unsigned)ix < (unsigned)d.W);
+        h_off[u] = ok ? ((img * d.H + iy) * d.W + ix) * d.ldx + d.xoff + chunk * 8 : -1;
+    }
+    int b_off[WU];  // weight row offsets, -1 beyond Cout
+#pragma unroll
+    for (int u = 0; u < WU; ++u) {
+        const int co = n0 + (wid * WU + u) * 8 + sub;
+        b_off[u] = co < d.Cout ? co * Kw + chunk * 8 : -1;
+    }
+
+    // (the asm("" : "+s") fences keep the compiler from hoisting per-tap
+    // address tables out of the chunk loop: they would not fit in registers)
+    auto issue_halo = [&](int c) {
+        char* dst = sH + (c & 1) * HBYTES;
+        int coff = c * 64;
+        asm volatile("" : "+s"(coff));
+#pragma unroll
+        for (int u = 0; u < 6; ++u)
+            if (u < nh) glds16(h_off[u] >= 0 ? x + (h_off[u] + coff) : zero, dst + (u * 8 + wid) * 1024);
+    };
+    auto issue_w = [&](int c, int tp, int stage) {
+        int kcol = tp * d.Cin + c * 64;
+        asm volatile("" : "+s"(kcol));
+        char* dst = sB + stage * BBYTES + wid * WU * 1024;
+#pragma unroll
+        for (int u = 0; u < WU; ++u) glds16(b_off[u] >= 0 ? w + (b_off[u] + kcol) : zero, dst + u * 1024);
+    };
+    // W(k+1) landed; the halo issued at step k (after W(k+1)) may stay in flight
+    auto retire = [&](bool halo_now) {
+        if (!halo_now) wait_vmcnt<0>();
+        else if (nh == 6) wait_vmcnt<6>();
+        else wait_vmcnt<5>();
+    };
+
+    f32x4 acc[MI][NJ];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    uint4 af[MI], bfr[NJ];
+
+    // prologue: W(0), halo(0), W(1); retire the first two
+    issue_w(0, 0, 0);
+    issue_halo(0);
+    issue_w(0, 1, 1);
+    wait_vmcnt<WU>();
+    phase_barrier();
+    if (grp == 1) phase_barrier();  // group 1 runs one window behind
+
+    const int arow0 = grp * MI * HWd + (lane & 15);  // halo row of fragment 0 at tap (0,0)
+    const int brow0 = wn * 64 + (lane & 15);         // weight row of fragment 0 (rows +16j share the XOR)
+    const int bb0 = lds_off(brow0, lane >> 4), bb1 = lds_off(brow0, 4 + (lane >> 4));
+    const int nk = nchunk * TAPS;
+    int c = 0, ty = 0, tx = 0;  // chunk / tap of K-step k (scalar)
+#pragma unroll 1
+    for (int k = 0; k < nk; ++k) {
+        const int tp = ty * KW + tx;
+        const char* Hb = sH + (c & 1) * HBYTES;
+        const char* B = sB + (k & 1) * BBYTES;
+        const bool last_k = k + 1 == nk;
+        const bool halo_now = tp == 0 && c + 1 < nchunk;
+        const int arow = arow0 + ty * HWd + tx;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            // ---- READ phase (group 0: even windows, group 1: odd)
+            const int bb = h ? bb1 : bb0;
+            const int ch = h * 4 + (lane >> 4);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) bfr[j] = *(const uint4*)(B + bb + j * 2048);
+#pragma unroll
+            for (int i = 0; i < MI; ++i) af[i] = *(const uint4*)(Hb + lds_off(arow + i * HWd, ch));
+            if (h == 0) {
+                // W(k+1) (W(1) came with the prologue), then the next chunk's halo
+                if (k >= 1 && !last_k) {
+                    if (tp + 1 < TAPS) issue_w(c, tp + 1, (k + 1) & 1);
+                    else issue_w(c + 1, 0, (k + 1) & 1);
+                }
+                if (halo_now) issue_halo(c + 1);
+            }
+            if (h == 1 && grp == 1) {  // window 4k+3: last reads of step k, then retire
+                wait_lgkm0();
+                if (!last_k) retire(halo_now);
+            }
+            phase_barrier();
+            // ---- MFMA phase: C^T fragment (weights as A, pixels as B)
+#pragma unroll
+            for (int i = 0; i < MI; ++i)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, bfr[j]),
+                                                                        __builtin_bit_cast(bf16x8_t, af[i]),
+                                                                        acc[i][j], 0, 0, 0);
+            if (h == 1 && grp == 0 && !last_k) retire(halo_now);  // window 4k+3
+            phase_barrier();
+        }
+        if (++tx == KW) {
+            tx = 0;
+            if (++ty == KH) {
+                ty = 0;
+                ++c;
+            }
+        }
+    }
+    if (grp == 0) phase_barrier();  // match group 1's extra barrier
+    __syncthreads();                // all operand reads done: LDS becomes the staging buffer
+
+    // ---- epilogue.  Fragment (i, j): pixel m = (grp*8 + i)*16 + (lane & 15),
+    // channels co = n0 + wn*64 + j*16 + 4*(lane >> 4) + r, r = 0..3.
+    const int cl0 = wn * 64 + 4 * (lane >> 4);  // block-local channel of r = 0, j = 0
+    float4 b4[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int co = n0 + cl0 + j * 16;
+        b4[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (bias) {
+            if (co + 3 < d.Cout) {
+                b4[j] = *(const float4*)(bias + co);
+            } else {
+                if (co < d.Cout) b4[j].x = bias[co];
+                if (co + 1 < d.Cout) b4[j].y = bias[co + 1];
+                if (co + 2 < d.Cout) b4[j].z = bias[co + 2];
+            }
+        }
+    }
+    auto pix_of = [&](int m) -> long {
+        const int oy = py0 + (m >> 4), ox = px0 + (m & 15);
+        if (oy >= d.Ho || ox >= d.Wo) return -1;
+        return ((long)img * d.OH + oy * d.omy + d.ooy) * d.OW + ox * d.omx + d.oox;
+    };
+    // Each lane owns (pixel, 4 consecutive channels) per fragment: mask and
+    // accumulate are applied right here on those 4 channels (8-byte loads).
+    // bf16 output: stage bf16 [256 px][256 ch] in LDS, then 16-byte row stores;
+    // fp32 output: 16-byte stores straight from the registers.
+    const bool out_f32 = d.out_dtype == IRGAN_F32;
+    auto emit = [&](auto actc) {
+        constexpr int A = decltype(actc)::value;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+            const int m = (grp * MI + i) * 16 + (lane & 15);
+            const long pix = pix_of(m);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int cl = cl0 + j * 16, co = n0 + cl;
+                const float4 b = b4[j];
+                float v[4] = {acc[i][j][0] + b.x, acc[i][j][1] + b.y, acc[i][j][2] + b.z, acc[i][j][3] + b.w};
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = conv_act(v[r], A);
+                const bool full = co + 4 <= d.Cout;
+                if (pix >= 0 && mask) {
+                    const bf16_t* mp = (const bf16_t*)mask + pix * d.ldm + d.moff + co;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (full || co + r < d.Cout) v[r] *= mask_mul(bf2f(mp[r]), d.mask_act);
+                }
+                if (out_f32) {
+                    if (pix < 0) continue;
+                    float* yp = (float*)y + pix * d.ldy + d.yoff + co;
+                    if (full && ((pix * d.ldy + d.yoff + co) & 3) == 0) {
+                        float4 o = make_float4(v[0], v[1], v[2], v[3]);
+                        if (d.accumulate) {
+                            const float4 p = *(const float4*)yp;
+                            o.x += p.x; o.y += p.y; o.z += p.z; o.w += p.w;
+                        }
+                        *(float4*)yp = o;
+                    } else {
+                        for (int r = 0; r < 4 && co + r < d.Cout; ++r) yp[r] = d.accumulate ? yp[r] + v[r] : v[r];
+                    }
+                } else {
+                    if (d.accumulate && pix >= 0) {
+                        const bf16_t* yp = (const bf16_t*)y + pix * d.ldy + d.yoff + co;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            if (full || co + r < d.Cout) v[r] += bf2f(yp[r]);
+                    }
+                    uint2 pk;
+                    pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+                    pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+                    *(uint2*)(smem + m * RSB + cl * 2) = pk;
+                }
+            }
+        }
+    };
+    switch (d.act) {
+        case IRGAN_ACT_RELU: emit(std::integral_constant<int, IRGAN_ACT_RELU>()); break;
+        case IRGAN_ACT_LRELU: emit(std::integral_constant<int, IRGAN_ACT_LRELU>()); break;
+        default: emit(std::integral_constant<int, IRGAN_ACT_NONE>()); break;
+    }
+    if (out_f32) return;
+    __syncthreads();
+    const int c8 = (tid & 31) * 8, co8 = n0 + c8;
+    if (co8 >= d.Cout) return;
+    const bool vec = co8 + 8 <= d.Cout && d.ldy % 8 == 0 && d.yoff % 8 == 0;
+    for (int m = tid >> 5; m < 256; m += 16) {
+        const long pix = pix_of(m);
+        if (pix < 0) continue;
+        bf16_t* yp = (bf16_t*)y + pix * d.ldy + d.yoff + co8;
+        const char* sp = smem + m * RSB + c8 * 2;
+        if (vec) {
+            *(uint4*)yp = *(const uint4*)sp;
+        } else {
+            for (int q = 0; q < 8 && co8 + q < d.Cout; ++q) yp[q] = ((const bf16_t*)sp)[q];
+        }
+    }
+}
+
+template <int KH, int KW>
+void launch_pp(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y, const void* mask,
+               hipStream_t st, const bf16_t* zero, int swz) {
+    const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH);
+    const int ntn = irgan_cdiv(d->Cout, BN);
+    conv_pp_kernel<KH, KW><<<d->N * tpy * tpx * ntn, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, y,
+                                                                  mask, zero, ntn, tpx, tpy, swz);
+}
+
+}  // namespace
+
+extern "C" int irgan_conv_fwd_pp(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
+                                 const void* mask, hipStream_t st) {
+    if ((long)d->N * d->Ho * d->Wo <= 0 || d->Cout <= 0) return 0;
+    const bool k33 = d->KH == 3 && d->KW == 3, k44 = d->KH == 4 && d->KW == 4;
+    if (d->dtype != IRGAN_BF16 || d->act == IRGAN_ACT_TANH || d->sy != 1 || d->sx != 1 || d->Cin % 64 || !(k33 || k44) || d->Cout <= 128 ||
+        d->ldx % 8 || d->xoff % 8 || (long)d->N * d->H * d->W * d->ldx >= (1L << 31) ||
+        (long)d->Cout * d->KH * d->KW * d->Cin >= (1L << 31))
+        return IRGAN_EUNSUPPORTED;
+    static bf16_t* zero = nullptr;
+    if (!zero && hipGetSymbolAddress((void**)&zero, HIP_SYMBOL(g_pp_zero_page)) != hipSuccess)
+        return IRGAN_EUNSUPPORTED;
+    static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
+    if (k33) launch_pp<3, 3>(d, x, w, bias, y, mask, st, zero, swz);
+    else launch_pp<4, 4>(d, x, w, bias, y, mask, st, zero, swz);
+    IRGAN_LAUNCH_CHECK();
+    return 0;
+}
