@@ -56,6 +56,26 @@ IRGAN_HD void glds16(const void* src, const void* lds) {
     const uint32_t m = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)lds;
     asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "{m0}"(m) : "memory");
 }
+// Raw buffer resource (gfx9 V#: 64-bit base, num_records bytes, stride 0).
+// Wave-uniform: the compiler keeps it in SGPRs.  A lane whose byte offset is
+// >= num_records is dropped by the range check and its 16 bytes arrive as zeros.
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+IRGAN_HD i32x4 make_rsrc(const void* base, uint32_t bytes) {
+    const uint64_t a = (uint64_t)(uintptr_t)base;
+    i32x4 r;
+    r.x = (int32_t)(uint32_t)a;
+    r.y = (int32_t)(uint32_t)(a >> 32);
+    r.z = (int32_t)bytes;
+    r.w = 0x00020000;
+    return r;
+}
+constexpr uint32_t IRGAN_OOB = 0x80000000u;  // byte offset that is out of range (num_records < 2^31)
+// buffer_load_dwordx4 ... lds: 16 bytes per lane from rsrc.base + voff into
+// lds + 16*lane (same M0 contract as glds16); no 64-bit address math per lane.
+IRGAN_HD void blds16(i32x4 rsrc, uint32_t voff, const void* lds) {
+    const uint32_t m = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)lds;
+    asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rsrc), "{m0}"(m) : "memory");
+}
 template <int N>
 IRGAN_HD void wait_vmcnt() {
     static_assert(N >= 0 && N <= 63, "vmcnt");

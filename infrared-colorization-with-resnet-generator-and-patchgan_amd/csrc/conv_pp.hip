@@ -35,14 +35,13 @@
 //
 // Preconditions (checked by irgan_conv_fwd_pp): bf16, sy = sx = 1, Cin % 64 == 0,
 // (KH, KW) in {(3,3), (4,4)}, ldx, xoff % 8 == 0, Cout > 128 (channel tiles of
-// 256), no tanh epilogue, input slice and weights < 2^31 elements.
+// 256), no tanh epilogue, input slice and weights < 2^30 elements (byte offsets
+// below the buffer-resource out-of-range marker 2^31).
 #include <type_traits>
 
 #include "conv_epilogue.h"
 
 namespace {
-
-__device__ __attribute__((aligned(4096))) bf16_t g_pp_zero_page[2048];
 
 IRGAN_HD int lds_off(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
 
@@ -70,8 +69,7 @@ template <int KH, int KW>
 __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
                                                          const bf16_t* __restrict__ w, const float* __restrict__ bias,
                                                          void* __restrict__ y, const void* __restrict__ mask,
-                                                         const bf16_t* __restrict__ zero, int ntn, int tpx, int tpy,
-                                                         int swz) {
+                                                         int ntn, int tpx, int tpy, int swz) {
     constexpr int TAPS = KH * KW, HWd = PW + KW - 1, HROWS = (PH + KH - 1) * HWd, HP = (HROWS + 7) / 8;
     static_assert(HP <= HPMAX && HP > 40 && TAPS >= 2, "halo pieces per wave are 5 or 6");
     __shared__ __attribute__((aligned(1024))) char smem[LDS];
@@ -96,7 +94,10 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
     const int chunk = (lane & 7) ^ sub;  // source chunk for this lane's LDS slot (row & 7 == sub)
     const bool reflect = d.pad_mode == IRGAN_PAD_REFLECT;
 
-    int h_off[6];  // element offsets of this lane's halo rows, -1: zero padding
+    // DMA sources as byte offsets into buffer resources (out-of-range offsets
+    // arrive as zeros: padding and Cout tails cost no address math in the loop)
+    const uint32_t xbytes = (uint32_t)((long)d.N * d.H * d.W * d.ldx * 2);
+    uint32_t h_off[6];
 #pragma unroll
     for (int u = 0; u < 6; ++u) {
         const int h = (u * 8 + wid) * 8 + sub;
@@ -107,31 +108,29 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
             ix = reflect_idx(ix, d.W);
         }
         const bool ok = (h < HROWS) & ((unsigned)iy < (unsigned)d.H) & ((unsigned)ix < (unsigned)d.W);
-        h_off[u] = ok ? ((img * d.H + iy) * d.W + ix) * d.ldx + d.xoff + chunk * 8 : -1;
+        h_off[u] = ok ? (uint32_t)((((img * d.H + iy) * d.W + ix) * d.ldx + d.xoff + chunk * 8) * 2) : IRGAN_OOB;
     }
-    int b_off[WU];  // weight row offsets, -1 beyond Cout
+    const uint32_t wbytes = (uint32_t)((long)d.Cout * Kw * 2);
+    uint32_t b_off[WU];
 #pragma unroll
     for (int u = 0; u < WU; ++u) {
         const int co = n0 + (wid * WU + u) * 8 + sub;
-        b_off[u] = co < d.Cout ? co * Kw + chunk * 8 : -1;
+        b_off[u] = co < d.Cout ? (uint32_t)((co * Kw + chunk * 8) * 2) : IRGAN_OOB;
     }
 
-    // (the asm("" : "+s") fences keep the compiler from hoisting per-tap
-    // address tables out of the chunk loop: they would not fit in registers)
     auto issue_halo = [&](int c) {
         char* dst = sH + (c & 1) * HBYTES;
-        int coff = c * 64;
-        asm volatile("" : "+s"(coff));
+        const i32x4 rs = make_rsrc(x + c * 64, xbytes - c * 128);
 #pragma unroll
         for (int u = 0; u < 6; ++u)
-            if (u < nh) glds16(h_off[u] >= 0 ? x + (h_off[u] + coff) : zero, dst + (u * 8 + wid) * 1024);
+            if (u < nh) blds16(rs, h_off[u], dst + (u * 8 + wid) * 1024);
     };
     auto issue_w = [&](int c, int tp, int stage) {
-        int kcol = tp * d.Cin + c * 64;
-        asm volatile("" : "+s"(kcol));
+        const int kcol = tp * d.Cin + c * 64;
+        const i32x4 rs = make_rsrc(w + kcol, wbytes - kcol * 2);
         char* dst = sB + stage * BBYTES + wid * WU * 1024;
 #pragma unroll
-        for (int u = 0; u < WU; ++u) glds16(b_off[u] >= 0 ? w + (b_off[u] + kcol) : zero, dst + u * 1024);
+        for (int u = 0; u < WU; ++u) blds16(rs, b_off[u], dst + u * 1024);
     };
     // W(k+1) landed; the halo issued at step k (after W(k+1)) may stay in flight
     auto retire = [&](bool halo_now) {
@@ -313,11 +312,11 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
 
 template <int KH, int KW>
 void launch_pp(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y, const void* mask,
-               hipStream_t st, const bf16_t* zero, int swz) {
+               hipStream_t st, int swz) {
     const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH);
     const int ntn = irgan_cdiv(d->Cout, BN);
     conv_pp_kernel<KH, KW><<<d->N * tpy * tpx * ntn, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, y,
-                                                                  mask, zero, ntn, tpx, tpy, swz);
+                                                                  mask, ntn, tpx, tpy, swz);
 }
 
 }  // namespace
@@ -327,15 +326,12 @@ extern "C" int irgan_conv_fwd_pp(const irgan_conv_desc* d, const void* x, const 
     if ((long)d->N * d->Ho * d->Wo <= 0 || d->Cout <= 0) return 0;
     const bool k33 = d->KH == 3 && d->KW == 3, k44 = d->KH == 4 && d->KW == 4;
     if (d->dtype != IRGAN_BF16 || d->act == IRGAN_ACT_TANH || d->sy != 1 || d->sx != 1 || d->Cin % 64 || !(k33 || k44) || d->Cout <= 128 ||
-        d->ldx % 8 || d->xoff % 8 || (long)d->N * d->H * d->W * d->ldx >= (1L << 31) ||
-        (long)d->Cout * d->KH * d->KW * d->Cin >= (1L << 31))
-        return IRGAN_EUNSUPPORTED;
-    static bf16_t* zero = nullptr;
-    if (!zero && hipGetSymbolAddress((void**)&zero, HIP_SYMBOL(g_pp_zero_page)) != hipSuccess)
+        d->ldx % 8 || d->xoff % 8 || (long)d->N * d->H * d->W * d->ldx >= (1L << 30) ||
+        (long)d->Cout * d->KH * d->KW * d->Cin >= (1L << 30))
         return IRGAN_EUNSUPPORTED;
     static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
-    if (k33) launch_pp<3, 3>(d, x, w, bias, y, mask, st, zero, swz);
-    else launch_pp<4, 4>(d, x, w, bias, y, mask, st, zero, swz);
+    if (k33) launch_pp<3, 3>(d, x, w, bias, y, mask, st, swz);
+    else launch_pp<4, 4>(d, x, w, bias, y, mask, st, swz);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }
