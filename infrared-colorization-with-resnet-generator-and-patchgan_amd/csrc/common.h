@@ -76,6 +76,12 @@ IRGAN_HD void blds16(i32x4 rsrc, uint32_t voff, const void* lds) {
     const uint32_t m = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)lds;
     asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rsrc), "{m0}"(m) : "memory");
 }
+// same with a wave-uniform byte offset in the instruction's soffset (SGPR)
+IRGAN_HD void blds16(i32x4 rsrc, uint32_t voff, uint32_t soff, const void* lds) {
+    const uint32_t m = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)lds;
+    asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(voff), "s"(rsrc), "s"(soff), "{m0}"(m)
+                 : "memory");
+}
 template <int N>
 IRGAN_HD void wait_vmcnt() {
     static_assert(N >= 0 && N <= 63, "vmcnt");

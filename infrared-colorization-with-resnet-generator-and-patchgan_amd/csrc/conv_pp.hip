@@ -97,10 +97,11 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
     // DMA sources as byte offsets into buffer resources (out-of-range offsets
     // arrive as zeros: padding and Cout tails cost no address math in the loop)
     const uint32_t xbytes = (uint32_t)((long)d.N * d.H * d.W * d.ldx * 2);
-    uint32_t h_off[6];
-#pragma unroll
-    for (int u = 0; u < 6; ++u) {
-        const int h = (u * 8 + wid) * 8 + sub;
+    // byte offset of this lane's row of halo piece (u*8 + wid) (computed at issue
+    // time, once per chunk: keeping six offsets live costs registers the MFMA
+    // tile needs)
+    auto halo_off = [&](int u, int lsub) -> uint32_t {
+        const int h = (u * 8 + wid) * 8 + lsub;
         const int hy = h / HWd, hx = h - hy * HWd;
         int iy = py0 + hy + d.c0y, ix = px0 + hx + d.c0x;
         if (reflect) {
@@ -108,29 +109,27 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
             ix = reflect_idx(ix, d.W);
         }
         const bool ok = (h < HROWS) & ((unsigned)iy < (unsigned)d.H) & ((unsigned)ix < (unsigned)d.W);
-        h_off[u] = ok ? (uint32_t)((((img * d.H + iy) * d.W + ix) * d.ldx + d.xoff + chunk * 8) * 2) : IRGAN_OOB;
-    }
+        return ok ? (uint32_t)((((img * d.H + iy) * d.W + ix) * d.ldx + d.xoff + ((lane & 7) ^ lsub) * 8) * 2)
+                  : IRGAN_OOB;
+    };
+    // weight rows co >= Cout lie beyond num_records: they arrive as zeros
     const uint32_t wbytes = (uint32_t)((long)d.Cout * Kw * 2);
-    uint32_t b_off[WU];
-#pragma unroll
-    for (int u = 0; u < WU; ++u) {
-        const int co = n0 + (wid * WU + u) * 8 + sub;
-        b_off[u] = co < d.Cout ? (uint32_t)((co * Kw + chunk * 8) * 2) : IRGAN_OOB;
-    }
-
+    const uint32_t b_off = (uint32_t)(((n0 + wid * WU * 8 + sub) * Kw + chunk * 8) * 2);  // piece u: + u*16*Kw
     auto issue_halo = [&](int c) {
         char* dst = sH + (c & 1) * HBYTES;
         const i32x4 rs = make_rsrc(x + c * 64, xbytes - c * 128);
+        int lsub = sub;
+        asm volatile("" : "+v"(lsub));  // recompute the offsets here instead of hoisting them out of the loop
 #pragma unroll
         for (int u = 0; u < 6; ++u)
-            if (u < nh) blds16(rs, h_off[u], dst + (u * 8 + wid) * 1024);
+            if (u < nh) blds16(rs, halo_off(u, lsub), dst + (u * 8 + wid) * 1024);
     };
     auto issue_w = [&](int c, int tp, int stage) {
         const int kcol = tp * d.Cin + c * 64;
         const i32x4 rs = make_rsrc(w + kcol, wbytes - kcol * 2);
         char* dst = sB + stage * BBYTES + wid * WU * 1024;
 #pragma unroll
-        for (int u = 0; u < WU; ++u) blds16(rs, b_off[u], dst + u * 1024);
+        for (int u = 0; u < WU; ++u) blds16(rs, b_off, (uint32_t)(u * 16 * Kw), dst + u * 1024);
     };
     // W(k+1) landed; the halo issued at step k (after W(k+1)) may stay in flight
     auto retire = [&](bool halo_now) {
@@ -154,57 +153,63 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
     phase_barrier();
     if (grp == 1) phase_barrier();  // group 1 runs one window behind
 
+    // LDS addressing.  Fragment rows of a tap are constant shifts K of the
+    // lane's row arow0 and lds_off's XOR term depends only on (arow0 + K) & 7,
+    // so with the tap loop unrolled an A address is tsw[K & 7] + hb plus the
+    // ds_read immediate K * 128: one VALU add per fragment read.
     const int arow0 = grp * MI * HWd + (lane & 15);  // halo row of fragment 0 at tap (0,0)
     const int brow0 = wn * 64 + (lane & 15);         // weight row of fragment 0 (rows +16j share the XOR)
     const int bb0 = lds_off(brow0, lane >> 4), bb1 = lds_off(brow0, 4 + (lane >> 4));
-    const int nk = nchunk * TAPS;
-    int c = 0, ty = 0, tx = 0;  // chunk / tap of K-step k (scalar)
+    int tsw[8];  // h = 1 flips chunk bit 2: tsw ^ 64 (v_xad_u32)
+#pragma unroll
+    for (int k8 = 0; k8 < 8; ++k8) tsw[k8] = ((lane >> 4) ^ ((arow0 + k8) & 7)) << 4;
 #pragma unroll 1
-    for (int k = 0; k < nk; ++k) {
-        const int tp = ty * KW + tx;
-        const char* Hb = sH + (c & 1) * HBYTES;
-        const char* B = sB + (k & 1) * BBYTES;
-        const bool last_k = k + 1 == nk;
-        const bool halo_now = tp == 0 && c + 1 < nchunk;
-        const int arow = arow0 + ty * HWd + tx;
+    for (int c = 0; c < nchunk; ++c) {
+        const int hb = arow0 * 128 + (c & 1) * HBYTES;
+        const bool more = c + 1 < nchunk;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            // ---- READ phase (group 0: even windows, group 1: odd)
-            const int bb = h ? bb1 : bb0;
-            const int ch = h * 4 + (lane >> 4);
+        for (int tp = 0; tp < TAPS; ++tp) {
+            const int ty = tp / KW, tx = tp % KW;
+            const int k = c * TAPS + tp;  // K-step
+            const char* B = sB + (k & 1) * BBYTES;
+            const bool last_k = !more && tp == TAPS - 1;
+            const bool halo_now = tp == 0 && more;
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) bfr[j] = *(const uint4*)(B + bb + j * 2048);
+            for (int h = 0; h < 2; ++h) {
+                // ---- READ phase (group 0: even windows, group 1: odd)
+                const int bb = h ? bb1 : bb0;
+                int hbp = hb;
+                asm volatile("" : "+v"(hbp));  // per-phase base: the address adds stay here, not hoisted
 #pragma unroll
-            for (int i = 0; i < MI; ++i) af[i] = *(const uint4*)(Hb + lds_off(arow + i * HWd, ch));
-            if (h == 0) {
-                // W(k+1) (W(1) came with the prologue), then the next chunk's halo
-                if (k >= 1 && !last_k) {
-                    if (tp + 1 < TAPS) issue_w(c, tp + 1, (k + 1) & 1);
-                    else issue_w(c + 1, 0, (k + 1) & 1);
+                for (int j = 0; j < NJ; ++j) bfr[j] = *(const uint4*)(B + bb + j * 2048);
+#pragma unroll
+                for (int i = 0; i < MI; ++i) {
+                    const int K = (i + ty) * HWd + tx;
+                    af[i] = *(const uint4*)(sH + (hbp + (tsw[K & 7] ^ (h * 64))) + K * 128);
                 }
-                if (halo_now) issue_halo(c + 1);
-            }
-            if (h == 1 && grp == 1) {  // window 4k+3: last reads of step k, then retire
-                wait_lgkm0();
-                if (!last_k) retire(halo_now);
-            }
-            phase_barrier();
-            // ---- MFMA phase: C^T fragment (weights as A, pixels as B)
+                if (h == 0) {
+                    // W(k+1) (W(1) came with the prologue), then the next chunk's halo
+                    if (k >= 1 && !last_k) {
+                        if (tp + 1 < TAPS) issue_w(c, tp + 1, (k + 1) & 1);
+                        else issue_w(c + 1, 0, (k + 1) & 1);
+                    }
+                    if (halo_now) issue_halo(c + 1);
+                }
+                if (h == 1 && grp == 1) {  // window 4k+3: last reads of step k, then retire
+                    wait_lgkm0();
+                    if (!last_k) retire(halo_now);
+                }
+                phase_barrier();
+                // ---- MFMA phase: C^T fragment (weights as A, pixels as B)
 #pragma unroll
-            for (int i = 0; i < MI; ++i)
+                for (int i = 0; i < MI; ++i)
 #pragma unroll
-                for (int j = 0; j < NJ; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, bfr[j]),
-                                                                        __builtin_bit_cast(bf16x8_t, af[i]),
-                                                                        acc[i][j], 0, 0, 0);
-            if (h == 1 && grp == 0 && !last_k) retire(halo_now);  // window 4k+3
-            phase_barrier();
-        }
-        if (++tx == KW) {
-            tx = 0;
-            if (++ty == KH) {
-                ty = 0;
-                ++c;
+                    for (int j = 0; j < NJ; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, bfr[j]),
+                                                                            __builtin_bit_cast(bf16x8_t, af[i]),
+                                                                            acc[i][j], 0, 0, 0);
+                if (h == 1 && grp == 0 && !last_k) retire(halo_now);  // window 4k+3
+                phase_barrier();
             }
         }
     }
