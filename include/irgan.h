@@ -94,7 +94,7 @@ int irgan_weight_pack(const float* src, void* dst, int32_t dtype, int32_t Cout, 
 /* ---- InstanceNorm (ir:154-165), per-(n,c) over H*W, eps 1e-5, no affine ---- */
 /* Reductions are two-level and atomic-free: <= IRGAN_IN_PARTS block partials per
  * (n, c) summed in fp64 in a fixed order. */
-enum { IRGAN_IN_PARTS = 64 };
+enum { IRGAN_IN_PARTS = 128 };
 /* mr[n][c] = {mean, rstd}; work: IRGAN_IN_PARTS*N*C doubles of scratch. */
 int irgan_in_stats(const void* x, int32_t dtype, int32_t N, int32_t HW, int32_t C,
                    int32_t ld, int32_t off, double* work, float* mr, irgan_stream_t s);
@@ -142,14 +142,23 @@ int irgan_resample_table(int32_t kind, int32_t n_in, int32_t p, int32_t transpos
 int irgan_reflect_ring_fold(const float* rows, const float* cols, int32_t nsplit, int32_t N, int32_t H,
                             int32_t W, int32_t C, int32_t p, void* dx, int32_t dx_dtype, int32_t lddx,
                             int32_t dxoff, irgan_stream_t s);
+/* Same fold in one launch, without the fp32 partials (bf16, stride-1 reflect
+ * convs, dY channels % 32 == 0, H, W >= 2p+2): d is the descriptor of the
+ * interior backward-data launch (irgan_conv_fwd on the flipped weights w,
+ * Ho = H, Wo = W, c0 shifted by p), which must already have written dx; this
+ * evaluates every ring value of g with MFMA and adds it onto its mirrored
+ * border pixel of dx (one owner per pixel, no atomics). */
+int irgan_reflect_dgrad_ring(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p, void* dx,
+                             irgan_stream_t s);
 /* out = (Wy (x) Wx) in on NHWC slices, tables from irgan_resample_table (device
- * copies); accumulate: out += result.  Downsample / UpsampleAA forward and
- * backward, and the reflect-pad fold, are all this one launch. */
+ * copies, rows [Hout][Ty] and [Wout][Tx]: the host may drop trailing all-zero
+ * tap columns); accumulate: out += result.  Downsample / UpsampleAA forward
+ * and backward, and the reflect-pad fold, are all this one launch. */
 int irgan_sep_resample(const void* in, int32_t in_dtype, int32_t N, int32_t Hin, int32_t Win,
                        int32_t C, int32_t ldi, int32_t offi, void* out, int32_t out_dtype,
                        int32_t Hout, int32_t Wout, int32_t ldo, int32_t offo, const int32_t* ty,
-                       const float* wy, const int32_t* tx, const float* wx, int32_t T,
-                       int32_t accumulate, irgan_stream_t s);
+                       const float* wy, int32_t Ty, const int32_t* tx, const float* wx,
+                       int32_t Tx, int32_t accumulate, irgan_stream_t s);
 /* 2x2 max pool (VGG features) forward / backward (first max wins, as ATen). */
 int irgan_maxpool_fwd(const void* x, int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t C,
                       void* y, irgan_stream_t s);

@@ -34,8 +34,8 @@
 // wave's MFMA phase before any DMA can target its buffer.
 //
 // Preconditions (checked by irgan_conv_fwd_pp): bf16, sy = sx = 1, Cin % 64 == 0,
-// (KH, KW) in {(3,3), (4,4)}, ldx, xoff % 8 == 0, Cout > 128 (channel tiles of
-// 256), no tanh epilogue, input slice and weights < 2^30 elements (byte offsets
+// (KH, KW) in {(3,3), (4,4)}, ldx, xoff % 8 == 0, Cout % 256 == 0 (channel
+// tiles of 256), no tanh epilogue, input slice and weights < 2^30 elements (byte offsets
 // below the buffer-resource out-of-range marker 2^31).
 #include <type_traits>
 
@@ -330,7 +330,7 @@ extern "C" int irgan_conv_fwd_pp(const irgan_conv_desc* d, const void* x, const 
                                  const void* mask, hipStream_t st) {
     if ((long)d->N * d->Ho * d->Wo <= 0 || d->Cout <= 0) return 0;
     const bool k33 = d->KH == 3 && d->KW == 3, k44 = d->KH == 4 && d->KW == 4;
-    if (d->dtype != IRGAN_BF16 || d->act == IRGAN_ACT_TANH || d->sy != 1 || d->sx != 1 || d->Cin % 64 || !(k33 || k44) || d->Cout <= 128 ||
+    if (d->dtype != IRGAN_BF16 || d->act == IRGAN_ACT_TANH || d->sy != 1 || d->sx != 1 || d->Cin % 64 || !(k33 || k44) || d->Cout % 256 ||
         d->ldx % 8 || d->xoff % 8 || (long)d->N * d->H * d->W * d->ldx >= (1L << 30) ||
         (long)d->Cout * d->KH * d->KW * d->Cin >= (1L << 30))
         return IRGAN_EUNSUPPORTED;

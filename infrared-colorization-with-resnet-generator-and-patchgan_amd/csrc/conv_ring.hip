@@ -1,0 +1,234 @@
+// Border band of the nn.ReflectionPad2d(p) backward-data (ir:381, 402: the
+// reflect-padded 3x3 convs of every ResnetBlock), computed and folded in one
+// launch.
+//
+// Backward-data of conv(reflect_pad(x)) is fold(g), g = the zero-padded
+// correlation of dy with the flipped weights over the padded (H+2p) x (W+2p)
+// domain.  The interior of g maps 1:1 onto dx and is written by the regular
+// conv launch (descriptor d: dx[i] = sum_t Wd[t] dy[i + t + c0]).  What is
+// left are the ring values of g: g at padded coordinate u is that same
+// formula at the "virtual" dx position V = u - p (outside [0, H)), and it folds
+// onto the mirrored pixel.  Along one axis dx index i (n = H or W) receives the
+// virtual position V = -i when 1 <= i <= p, or V = 2n-2-i when n-1-p <= i <= n-2.
+// A band pixel (y, x) therefore gets up to three ring terms: (Vy, x), (y, Vx),
+// (Vy, Vx).  One owner per band pixel (no atomics, deterministic):
+//   row segments: band rows y (2p of them), all x;
+//   column segments: band columns x (2p of them), rows y outside the band rows.
+//
+// The band is thin (~4 pixel rows per image for 3x3), so the launch is built
+// for parallelism rather than operand reuse: block = 32 band pixels x 64
+// output channels, 4 waves that split the K loop (term, tap, 32-channel step)
+// round-robin, each holding the full 32 x 64 tile (2 x 4 fragments of
+// mfma_f32_16x16x32_bf16, weights as A: a lane's 4 accumulator rows are 4
+// consecutive channels of one pixel).  Operands come straight from L2 (no
+// LDS staging); the 4 partial tiles are summed through LDS in a fixed order
+// and added into dx with 16-byte read-modify-writes.
+#include "common.h"
+
+namespace {
+
+constexpr int NPIX = 32;  // band pixels per block (2 fragments)
+constexpr int NCO = 64;   // output channels per block (4 fragments)
+constexpr int NWV = 4;    // waves per block (K split)
+
+IRGAN_HD int mirror_pos(int i, int n, int p) {  // virtual position folding onto i, or INT_MIN
+    if (i >= 1 && i <= p) return -i;
+    if (i >= n - 1 - p && i <= n - 2) return 2 * n - 2 - i;
+    return -0x40000000;
+}
+
+__global__ __launch_bounds__(256) void reflect_ring_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ dy,
+                                                           const bf16_t* __restrict__ w, int p, void* __restrict__ dx,
+                                                           int segs_row, int segs_col) {
+    __shared__ __attribute__((aligned(16))) float red[NWV][NPIX][NCO + 4];  // +4: conflict-free row writes
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int H = d.Ho, W = d.Wo;               // dx spatial size (stride 1)
+    const int Kw = (d.KH * d.KW * d.Cin + 63) / 64 * 64;  // packed weight row stride
+    const int per_img = 2 * p * (segs_row + segs_col);
+    const int n = blockIdx.x / per_img;
+    int s = blockIdx.x - n * per_img;
+    const bool rowseg = s < 2 * p * segs_row;
+    int band, seg;
+    if (rowseg) {
+        band = s / segs_row;
+        seg = s - band * segs_row;
+    } else {
+        s -= 2 * p * segs_row;
+        band = s / segs_col;
+        seg = s - band * segs_col;
+    }
+    // band index -> dx row (row segments) or column (column segments): 1..p, n-1-p..n-2
+    const int nb = rowseg ? H : W;
+    const int bpos = band < p ? band + 1 : nb - 1 - p + (band - p);
+    const int co0 = blockIdx.y * NCO;
+
+    // this lane's pixel in fragment f: index q = seg*NPIX + f*16 + (lane & 15) along the band line
+    int py[2], px[2];
+    bool pv[2];
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+        const int q = seg * NPIX + f * 16 + (lane & 15);
+        if (rowseg) {
+            py[f] = bpos;
+            px[f] = q;
+            pv[f] = q < W;
+        } else {
+            py[f] = q;
+            px[f] = bpos;
+            pv[f] = q < H && mirror_pos(q, H, p) == -0x40000000;  // band rows belong to the row segments
+        }
+    }
+    // block-uniform: which terms can occur.  Row segment: term 0 (Vy, x) for all
+    // pixels; terms 1 (y, Vx) and 2 (Vy, Vx) only for pixels in band columns.
+    // Column segment: term 1 only.
+    const int qlo = seg * NPIX, qhi = min(qlo + NPIX, rowseg ? W : H) - 1;
+    const bool has_bandcol = rowseg && (qlo <= p || qhi >= W - 1 - p);
+    const int vby = rowseg ? mirror_pos(bpos, H, p) : 0;   // row segments: Vy (uniform)
+    const int vbx = rowseg ? 0 : mirror_pos(bpos, W, p);   // column segments: Vx (uniform)
+
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[f][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int kc = (lane >> 4) * 8;  // channel offset of this lane within a 32-deep k step
+    const bf16_t* wrow[4];
+    bool wok[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int co = co0 + j * 16 + (lane & 15);
+        wok[j] = co < d.Cout;
+        wrow[j] = w + (long)(wok[j] ? co : 0) * Kw + kc;
+    }
+    const int nc = d.Cin / 32;
+    int it = 0;  // block-uniform K-step counter: wave wv takes steps it % NWV == wv
+    for (int term = 0; term < 3; ++term) {
+        if (rowseg ? (term > 0 && !has_bandcol) : term != 1) continue;
+        int vy[2], vx[2];
+        bool tv[2];
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+            if (term == 0) { vy[f] = vby; vx[f] = px[f]; tv[f] = pv[f]; }
+            else {
+                const int mx = rowseg ? mirror_pos(px[f], W, p) : vbx;
+                vy[f] = term == 1 ? py[f] : vby;
+                vx[f] = mx;
+                tv[f] = pv[f] && mx != -0x40000000;
+            }
+        }
+        for (int ty = 0; ty < d.KH; ++ty) {
+            if (rowseg && term != 1) {  // uniform row: skip taps that miss dy entirely
+                const int r = vby + ty + d.c0y;
+                if ((unsigned)r >= (unsigned)d.H) continue;
+            }
+            for (int tx = 0; tx < d.KW; ++tx) {
+                if (!rowseg) {  // uniform column
+                    const int c = vbx + tx + d.c0x;
+                    if ((unsigned)c >= (unsigned)d.W) continue;
+                }
+                // this wave's steps of the tap: c in [first, nc) step NWV
+                const int first = (wv - it % NWV + NWV) % NWV;
+                it += nc;
+                if (first >= nc) continue;
+                const bf16_t* ap[2];
+                bool aok[2];
+#pragma unroll
+                for (int f = 0; f < 2; ++f) {
+                    const int r = vy[f] + ty + d.c0y, c = vx[f] + tx + d.c0x;
+                    aok[f] = tv[f] && (unsigned)r < (unsigned)d.H && (unsigned)c < (unsigned)d.W;
+                    ap[f] = dy + (aok[f] ? (((long)n * d.H + r) * d.W + c) * d.ldx + d.xoff + kc : 0);
+                }
+                const int wb = (ty * d.KW + tx) * d.Cin;
+#pragma unroll 2
+                for (int c = first; c < nc; c += NWV) {
+                    uint4 a[2], b[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        b[j] = wok[j] ? *(const uint4*)(wrow[j] + wb + c * 32) : uint4{0, 0, 0, 0};
+#pragma unroll
+                    for (int f = 0; f < 2; ++f) a[f] = aok[f] ? *(const uint4*)(ap[f] + c * 32) : uint4{0, 0, 0, 0};
+#pragma unroll
+                    for (int f = 0; f < 2; ++f)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, b[j]),
+                                                                                __builtin_bit_cast(bf16x8_t, a[f]),
+                                                                                acc[f][j], 0, 0, 0);
+                }
+            }
+        }
+    }
+    // partial tiles -> LDS: lane holds pixel f*16 + (lane & 15), channels j*16 + 4*(lane>>4) + r
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            *(float4*)&red[wv][f * 16 + (lane & 15)][j * 16 + 4 * (lane >> 4)] =
+                make_float4(acc[f][j][0], acc[f][j][1], acc[f][j][2], acc[f][j][3]);
+    __syncthreads();
+    // thread -> (pixel, 8 channels): sum the 4 partials in order, add into dx
+    const int pix_l = threadIdx.x >> 3, cg = (threadIdx.x & 7) * 8;
+    const int q = seg * NPIX + pix_l;
+    const int yy = rowseg ? bpos : q, xx = rowseg ? q : bpos;
+    const bool own = rowseg ? q < W : (q < H && mirror_pos(q, H, p) == -0x40000000);
+    const int co = co0 + cg;
+    if (!own || co >= d.Cout) return;
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = 0.f;
+#pragma unroll
+    for (int u = 0; u < NWV; ++u) {
+        const float4 lo = *(const float4*)&red[u][pix_l][cg], hi = *(const float4*)&red[u][pix_l][cg + 4];
+        v[0] += lo.x; v[1] += lo.y; v[2] += lo.z; v[3] += lo.w;
+        v[4] += hi.x; v[5] += hi.y; v[6] += hi.z; v[7] += hi.w;
+    }
+    const long pix = ((long)n * d.OH + yy * d.omy + d.ooy) * d.OW + xx * d.omx + d.oox;
+    const long o = pix * d.ldy + d.yoff + co;
+    const bool full = co + 8 <= d.Cout;
+    if (d.out_dtype == IRGAN_F32) {
+        float* yp = (float*)dx + o;
+        if (full && (o & 3) == 0) {
+            float4 a = *(float4*)yp, b = *(float4*)(yp + 4);
+            a.x += v[0]; a.y += v[1]; a.z += v[2]; a.w += v[3];
+            b.x += v[4]; b.y += v[5]; b.z += v[6]; b.w += v[7];
+            *(float4*)yp = a;
+            *(float4*)(yp + 4) = b;
+        } else {
+            for (int k = 0; k < 8 && co + k < d.Cout; ++k) yp[k] += v[k];
+        }
+    } else {
+        bf16_t* yp = (bf16_t*)dx + o;
+        if (full && (o & 7) == 0) {
+            uint4 u = *(uint4*)yp;
+            uint32_t wds[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float a = __uint_as_float(wds[k] << 16) + v[2 * k];
+                const float b = __uint_as_float(wds[k] & 0xffff0000u) + v[2 * k + 1];
+                wds[k] = (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+            }
+            *(uint4*)yp = uint4{wds[0], wds[1], wds[2], wds[3]};
+        } else {
+            for (int k = 0; k < 8 && co + k < d.Cout; ++k) yp[k] = f2bf(bf2f(yp[k]) + v[k]);
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" int irgan_reflect_dgrad_ring(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p, void* dx,
+                                        irgan_stream_t s) {
+    if (!d || !dy || !w || !dx) return IRGAN_EINVAL;
+    if ((long)d->N * d->Ho * d->Wo <= 0 || d->Cout <= 0 || p <= 0) return 0;
+    if (d->dtype != IRGAN_BF16 || d->Cin % 32 || d->ldx % 8 || d->xoff % 8 || d->sy != 1 || d->sx != 1 ||
+        d->Ho != d->H || d->Wo != d->W || d->H < 2 * p + 2 || d->W < 2 * p + 2 || d->accumulate < 0)
+        return IRGAN_EUNSUPPORTED;
+    const int segs_row = irgan_cdiv(d->Wo, NPIX), segs_col = irgan_cdiv(d->Ho, NPIX);
+    dim3 grid(d->N * 2 * p * (segs_row + segs_col), irgan_cdiv(d->Cout, NCO));
+    reflect_ring_kernel<<<grid, 256, 0, (hipStream_t)s>>>(*d, (const bf16_t*)dy, (const bf16_t*)w, p, dx, segs_row,
+                                                         segs_col);
+    IRGAN_LAUNCH_CHECK();
+    return 0;
+}

@@ -35,7 +35,9 @@ IRGAN_HD int t256(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
 template <int RB>
 IRGAN_HD int img_off(int pos, int col) {
     const int c16 = col >> 3, within = (col & 7) * 2;
-    if constexpr (RB == 256) return pos * 256 + ((c16 ^ (2 * t256(pos))) << 4) + within;
+    // 512-B rows start on bank 0 like 256-B rows: the same XOR spreads the
+    // eight rows of a transposed read over all 64 banks
+    if constexpr (RB >= 256) return pos * RB + ((c16 ^ (2 * t256(pos))) << 4) + within;
     else if constexpr (RB == 128) return pos * 128 + ((c16 ^ (2 * t128(pos))) << 4) + within;
     else return pos * RB + c16 * 16 + within;
 }
@@ -109,7 +111,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void wgrad_halo_kernel(const irgan
                 constexpr int RPP = 1024 / RA, SLOTS = RA / 16;
                 const int pos = j * RPP + lane / SLOTS, slot = lane % SLOTS;
                 int row, c16;
-                if constexpr (RA == 256) { row = pos; c16 = slot ^ (2 * t256(pos)); }
+                if constexpr (RA >= 256) { row = pos; c16 = slot ^ (2 * t256(pos)); }
                 else if constexpr (RA == 128) { row = pos; c16 = slot ^ (2 * t128(pos)); }
                 else { row = pos ^ (((pos >> 3) & 1) << 2); c16 = slot; }
                 if (co0 + c16 * 8 < cout8) src = dy + (pix0 + row) * d.ldy + d.yoff + co0 + c16 * 8;
@@ -205,16 +207,32 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void wgrad_halo_kernel(const irgan
 template <int BMC, int KW, int SX, int WM, int WN>
 void launch_t(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, int splitk, hipStream_t st,
               const bf16_t* zero, int swz) {
+    constexpr int NW = WM * WN;
+    // resident blocks per CU (LDS and VGPR limits, from the runtime) x 256 CUs: the
+    // grid is sized to at most one full round -- a grid just above the resident
+    // capacity runs a second, nearly empty round
+    static int slots = 0;
+    if (!slots) {
+        int b = 0, dev = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, wgrad_halo_kernel<BMC, KW, SX, WM, WN>, NW * 64, 0) !=
+                hipSuccess || b < 1)
+            b = 1;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+            cus = 256;
+        slots = b * cus;
+    }
     const int ntco = irgan_cdiv(d->Cout, BMC), nci = d->Cin / 64;
     const int tiles = ntco * nci * d->KH;
     const int nseg = d->N * d->Ho * (d->Wo / 64);
     if (splitk <= 0) {
-        splitk = irgan_cdiv(512, tiles);
         const int maxs = irgan_cdiv(nseg, 4);  // >= 4 segments per split
+        splitk = slots / tiles;
+        if (splitk < 1) splitk = irgan_cdiv(slots, tiles);  // more tiles than slots: whole rounds anyway
         if (splitk > maxs) splitk = maxs;
         if (splitk < 1) splitk = 1;
-        if (swz && (tiles * splitk) % 8) {  // grid multiple of 8 for the XCD remap
-            for (int s2 = splitk + 1; s2 <= splitk + 8 && s2 <= maxs; ++s2)
+        if (swz && (tiles * splitk) % 8) {  // grid multiple of 8 for the XCD remap, within the slots
+            for (int s2 = splitk - 1; s2 >= 1 && s2 >= splitk - 8; --s2)
                 if ((tiles * s2) % 8 == 0) { splitk = s2; break; }
         }
     }
@@ -239,7 +257,10 @@ extern "C" int irgan_conv_wgrad_halo(const irgan_conv_desc* d, const void* x, co
         return IRGAN_EUNSUPPORTED;
     static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
     const int s2 = d->sx == 2;
-    if (d->Cout % 128 == 0 && d->KW == 3) {
+    static const bool wide = getenv("IRGAN_WGH_256") != nullptr;
+    if (wide && d->Cout % 256 == 0 && d->KW == 3 && !s2) {
+        launch_t<256, 3, 1, 4, 2>(d, x, dy, dw, splitk, st, zero, swz);
+    } else if (d->Cout % 128 == 0 && d->KW == 3) {
         if (s2) launch_t<128, 3, 2, 2, 4>(d, x, dy, dw, splitk, st, zero, swz);
         else launch_t<128, 3, 1, 2, 4>(d, x, dy, dw, splitk, st, zero, swz);
     } else if (d->Cout % 128 == 0 && d->KW == 4) {

@@ -16,7 +16,7 @@ namespace {
 
 constexpr int TPB = 256;
 constexpr int V = 8;          // channels per thread
-constexpr int IN_PARTS = 64;  // max blocks (partials) per image; work = IN_PARTS*N*C doubles
+constexpr int IN_PARTS = 128; // max blocks (partials) per image; work = IN_PARTS*N*C doubles
 
 IRGAN_HD void ld8(const void* p, int dt, long i, float* o) {
     if (dt == IRGAN_BF16) {
@@ -112,7 +112,7 @@ __global__ __launch_bounds__(TPB) void rows_kernel(Slice X, Slice DY, Slice DY2,
             }
         }
         if (on) {
-#pragma unroll 4
+#pragma unroll 8
             for (int r = r0 + L.rl; r < r1; r += L.RP) {
                 const long p = (long)n * HW + r;
                 float xv[VW];
@@ -141,6 +141,41 @@ __global__ __launch_bounds__(TPB) void rows_kernel(Slice X, Slice DY, Slice DY2,
             }
         }
         if ((MODE == 2 || MODE == 3) && !db) continue;  // uniform across the block
+        if (L.CL <= 64 && (64 % L.CL) == 0) {
+            // rows of one wave share a lane's channels every CL lanes: butterfly
+            // over them, then one LDS slot per (wave, channel lane)
+            for (int o = L.CL; o < 64; o <<= 1) {
+#pragma unroll
+                for (int k = 0; k < VW; ++k) {
+                    a0[k] += __shfl_xor(a0[k], o, 64);
+                    a1[k] += __shfl_xor(a1[k], o, 64);
+                }
+            }
+            const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+            if (lane < L.CL) {
+#pragma unroll
+                for (int k = 0; k < VW; ++k) {
+                    s0[(wv * L.CL + lane) * VW + k] = a0[k];
+                    s1[(wv * L.CL + lane) * VW + k] = a1[k];
+                }
+            }
+            __syncthreads();
+            if (threadIdx.x < L.CL && cb + threadIdx.x * VW < C) {
+                const int cc = cb + threadIdx.x * VW;
+#pragma unroll
+                for (int k = 0; k < VW; ++k) {
+                    float t0 = 0.f, t1 = 0.f;
+                    for (int j = 0; j < TPB / 64; ++j) {
+                        t0 += s0[(j * L.CL + threadIdx.x) * VW + k];
+                        t1 += s1[(j * L.CL + threadIdx.x) * VW + k];
+                    }
+                    if (MODE == 2 || MODE == 3) atomicAdd(db + cc + k, t0);
+                    else part[((long)n * gridDim.x + blockIdx.x) * C + cc + k] = make_float2(t0, t1);
+                }
+            }
+            __syncthreads();
+            continue;
+        }
 #pragma unroll
         for (int k = 0; k < VW; ++k) {
             s0[threadIdx.x * VW + k] = a0[k];
@@ -256,9 +291,9 @@ int rp_of(int C, int VW) {
     return TPB / cl;
 }
 
-// blocks per image: ~2048 blocks over the grid, >= 8 rows per thread, <= IN_PARTS
+// blocks per image: ~4096 blocks over the grid, >= 8 rows per thread, <= IN_PARTS
 int blocks_per_image(long HW, int N, int RP) {
-    long nb = (2048 + N - 1) / (N > 0 ? N : 1);
+    long nb = (4096 + N - 1) / (N > 0 ? N : 1);
     const long maxnb = (HW + 8L * RP - 1) / (8L * RP);
     if (nb > maxnb) nb = maxnb;
     if (nb > IN_PARTS) nb = IN_PARTS;

@@ -63,8 +63,8 @@ template <int VW>
 __global__ __launch_bounds__(TPB) void sep_kernel(const void* __restrict__ in, int idt, int Hin, int Win, int C,
                                                   int ldi, int offi, void* __restrict__ out, int odt, int Hout,
                                                   int Wout, int ldo, int offo, const int* __restrict__ ty,
-                                                  const float* __restrict__ wy, const int* __restrict__ tx,
-                                                  const float* __restrict__ wx, int T, int accumulate) {
+                                                  const float* __restrict__ wy, int Ty, const int* __restrict__ tx,
+                                                  const float* __restrict__ wx, int Tx, int accumulate) {
     const int CV = C / VW;
     const int row = blockIdx.y;
     const int n = row / Hout, oy = row - n * Hout;
@@ -74,16 +74,16 @@ __global__ __launch_bounds__(TPB) void sep_kernel(const void* __restrict__ in, i
     float acc[VW];
 #pragma unroll
     for (int k = 0; k < VW; ++k) acc[k] = 0.f;
-    for (int i = 0; i < T; ++i) {
-        const float w1 = wy[oy * T + i];
+    for (int i = 0; i < Ty; ++i) {
+        const float w1 = wy[oy * Ty + i];
         if (w1 == 0.f) continue;
-        const long rowb = ((long)n * Hin + ty[oy * T + i]) * Win;
-        for (int j = 0; j < T; ++j) {
-            const float w2 = wx[ox * T + j];
+        const long rowb = ((long)n * Hin + ty[oy * Ty + i]) * Win;
+        for (int j = 0; j < Tx; ++j) {
+            const float w2 = wx[ox * Tx + j];
             if (w2 == 0.f) continue;
             const float w = w1 * w2;
             float v[VW];
-            ldvec<VW>(in, idt, (rowb + tx[ox * T + j]) * ldi + offi + c, v);
+            ldvec<VW>(in, idt, (rowb + tx[ox * Tx + j]) * ldi + offi + c, v);
 #pragma unroll
             for (int k = 0; k < VW; ++k) acc[k] += w * v[k];
         }
@@ -96,6 +96,86 @@ __global__ __launch_bounds__(TPB) void sep_kernel(const void* __restrict__ in, i
         for (int k = 0; k < VW; ++k) acc[k] += v[k];
     }
     stvec<VW>(out, odt, o, acc);
+}
+
+// Two-stage form of the same map through LDS.  Block = one output row (n, oy)
+// x a group of CB channels, 1024 threads.  Stage 1 applies the row's vertical
+// taps to every input column (16-byte coalesced loads of the <= TM input rows;
+// the taps are block-uniform, so they come from scalar loads) and keeps the
+// fp32 result [Win][CB] in LDS; stage 2 applies the horizontal taps from LDS and
+// writes the output row with 16-byte stores.  The tap loops run to the
+// compile-time bound TM (tables are compacted to their widest row on the host),
+// so a thread's loads are issued back to back.  Global loads per output drop
+// from Ty*Tx (sep_kernel) to about Ty*Win/Wout.
+constexpr int LTPB = 1024;
+template <int TM>
+__global__ __launch_bounds__(LTPB) void sep_lds_kernel(const void* __restrict__ in, int idt, int Hin, int Win,
+                                                       int ldi, int offi, void* __restrict__ out, int odt, int Hout,
+                                                       int Wout, int ldo, int offo, const int* __restrict__ ty,
+                                                       const float* __restrict__ wy, int Ty,
+                                                       const int* __restrict__ tx, const float* __restrict__ wx,
+                                                       int Tx, int accumulate, int CB) {
+    extern __shared__ float4 sm4[];
+    float* const sm = (float*)sm4;
+    const int row = blockIdx.x;
+    const int n = row / Hout, oy = row - n * Hout;
+    const int c0 = blockIdx.y * CB;
+    const int G = CB >> 3;  // 8-channel groups
+    float wyv[TM];
+    long rb[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        wyv[i] = i < Ty ? wy[oy * Ty + i] : 0.f;
+        rb[i] = i < Ty ? (long)(n * Hin + ty[oy * Ty + i]) * Win : 0;
+    }
+    for (int v = threadIdx.x; v < Win * G; v += LTPB) {
+        const int col = v / G, g = v - col * G;
+        float acc[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            if (wyv[i] == 0.f) continue;
+            float xv[8];
+            ldvec<8>(in, idt, (rb[i] + col) * ldi + offi + c0 + g * 8, xv);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[k] += wyv[i] * xv[k];
+        }
+        float4* d = (float4*)(sm + (col * CB + g * 8));
+        d[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        d[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+    }
+    __syncthreads();
+    for (int v = threadIdx.x; v < Wout * G; v += LTPB) {
+        const int ox = v / G, g = v - ox * G;
+        float wxv[TM];
+        int ix[TM];
+#pragma unroll
+        for (int j = 0; j < TM; ++j) {
+            wxv[j] = j < Tx ? wx[ox * Tx + j] : 0.f;
+            ix[j] = j < Tx ? tx[ox * Tx + j] : 0;
+        }
+        float acc[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+#pragma unroll
+        for (int j = 0; j < TM; ++j) {
+            const float w = wxv[j];
+            if (w == 0.f) continue;  // padding slot (keeps inf/nan in a skipped column out)
+            const float4* sp = (const float4*)(sm + (ix[j] * CB + g * 8));
+            const float4 a = sp[0], b = sp[1];
+            acc[0] += w * a.x; acc[1] += w * a.y; acc[2] += w * a.z; acc[3] += w * a.w;
+            acc[4] += w * b.x; acc[5] += w * b.y; acc[6] += w * b.z; acc[7] += w * b.w;
+        }
+        const long o = (((long)n * Hout + oy) * Wout + ox) * ldo + offo + c0 + g * 8;
+        if (accumulate) {
+            float pv[8];
+            ldvec<8>(out, odt, o, pv);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[k] += pv[k];
+        }
+        stvec<8>(out, odt, o, acc);
+    }
 }
 
 // Reflect-pad backward, border part.  The backward-data result g over the
@@ -375,19 +455,44 @@ extern "C" int irgan_resample_table(int32_t kind, int32_t n_in, int32_t p, int32
 
 extern "C" int irgan_sep_resample(const void* in, int32_t in_dtype, int32_t N, int32_t Hin, int32_t Win, int32_t C,
                                   int32_t ldi, int32_t offi, void* out, int32_t out_dtype, int32_t Hout, int32_t Wout,
-                                  int32_t ldo, int32_t offo, const int32_t* ty, const float* wy, const int32_t* tx,
-                                  const float* wx, int32_t T, int32_t accumulate, irgan_stream_t s) {
+                                  int32_t ldo, int32_t offo, const int32_t* ty, const float* wy, int32_t Ty,
+                                  const int32_t* tx, const float* wx, int32_t Tx, int32_t accumulate,
+                                  irgan_stream_t s) {
     const bool vec = (C % 8 == 0) && (ldi % 8 == 0) && (offi % 8 == 0) && (ldo % 8 == 0) && (offo % 8 == 0);
     const int VW = vec ? 8 : 1;
     if ((long)N * Hout * Wout * C <= 0) return 0;
+    if (Ty < 1 || Tx < 1) return IRGAN_EINVAL;
+    static const bool use_lds = !getenv("IRGAN_NO_SEP_LDS");
+    const int TM = Ty > Tx ? Ty : Tx;
+    if (vec && use_lds && TM <= 8) {
+        // channel group: the widest of 128..8 dividing C whose fp32 row [Win][CB] fits 64 KiB
+        int CB = 0;
+        for (int cb = 128; cb >= 8 && !CB; cb >>= 1)
+            if (C % cb == 0 && (long)Win * cb <= 16384) CB = cb;
+        if (CB) {
+            dim3 g(N * Hout, C / CB);
+            const size_t sh = (size_t)Win * CB * 4;
+            hipStream_t st = (hipStream_t)s;
+#define SEPL(T)                                                                                                      \
+    sep_lds_kernel<T><<<g, LTPB, sh, st>>>(in, in_dtype, Hin, Win, ldi, offi, out, out_dtype, Hout, Wout, ldo, offo, \
+                                           ty, wy, Ty, tx, wx, Tx, accumulate, CB)
+            if (TM <= 2) SEPL(2);
+            else if (TM <= 4) SEPL(4);
+            else if (TM <= 6) SEPL(6);
+            else SEPL(8);
+#undef SEPL
+            IRGAN_LAUNCH_CHECK();
+            return 0;
+        }
+    }
     if ((long)N * Hout > 65535) return IRGAN_EUNSUPPORTED;
     dim3 g(irgan_cdiv((long)Wout * (C / VW), TPB), N * Hout);
     if (vec)
         sep_kernel<8><<<g, TPB, 0, (hipStream_t)s>>>(in, in_dtype, Hin, Win, C, ldi, offi, out, out_dtype, Hout, Wout,
-                                                     ldo, offo, ty, wy, tx, wx, T, accumulate);
+                                                     ldo, offo, ty, wy, Ty, tx, wx, Tx, accumulate);
     else
         sep_kernel<1><<<g, TPB, 0, (hipStream_t)s>>>(in, in_dtype, Hin, Win, C, ldi, offi, out, out_dtype, Hout, Wout,
-                                                     ldo, offo, ty, wy, tx, wx, T, accumulate);
+                                                     ldo, offo, ty, wy, Ty, tx, wx, Tx, accumulate);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }

@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import torch
 
@@ -197,11 +198,15 @@ def conv_fwd(pc: PackedConv, x: Feat, y: Feat, act=ACT_NONE, bias=True, accumula
         mask.ptr if mask else None, stream()))
 
 
+RING_MFMA = not os.environ.get("IRGAN_NO_RING_MFMA")
+
+
 def conv_dgrad(pc: PackedConv, dy: Feat, dx: Feat, accumulate=False, mask: Feat = None, mask_act=0,
                pad_buf: torch.Tensor = None, bias=False):
     """dx = d(conv)/dx^T dy.  Reflect-padded layers: interior straight into dx,
-    the padded ring as split-K partials in pad_buf (fp32 scratch) folded back by
-    irgan_reflect_ring_fold; stride-2 layers launch per phase."""
+    then the padded ring folded onto dx's border band -- by irgan_reflect_dgrad_ring
+    (bf16, one MFMA launch) or as split-K partials in pad_buf (fp32 scratch)
+    folded by irgan_reflect_ring_fold; stride-2 layers launch per phase."""
     s = pc.spec
     assert dy.C == pc.cout_eff and dx.C == s.cin and dy.dt == pc.dtype
     if pc.reflect:
@@ -222,6 +227,11 @@ def conv_dgrad(pc: PackedConv, dy: Feat, dx: Feat, accumulate=False, mask: Feat 
         TIMER.wrap(conv_tag("dgrad", s, (H, W), dx.N), lambda: _lib.call(
             "irgan_conv_fwd", ctypes.byref(d), dy.ptr, P(buf), None, dx.ptr, None, stream()))
         if p == 0:
+            return
+        if (pc.dtype == BF16 and RING_MFMA and pc.cout_eff % 32 == 0 and H >= 2 * p + 2 and W >= 2 * p + 2
+                and dy.ld % 8 == 0 and dy.off % 8 == 0):
+            # one launch: ring values of g by MFMA, added onto their mirrored border pixels
+            _lib.call("irgan_reflect_dgrad_ring", ctypes.byref(d), dy.ptr, P(buf), p, dx.ptr, stream())
             return
         # ring in split-K partials: rows[ks][N][2p][Wp][C], cols[ks][N][H][2p][C]
         rsz, csz = dx.N * 2 * p * Wp * s.cin, dx.N * H * 2 * p * s.cin
@@ -331,17 +341,20 @@ def resample_table(kind, n_in, p=0, transpose=False, device=None):
                                                   w.ctypes.data_as(ctypes.c_void_p), TMAX, cap)
         if rows < 0:
             raise _lib.IrganError(f"irgan_resample_table({kind}, {n_in}, {p}) failed: {rows}")
-        t = (torch.from_numpy(idx[:rows * TMAX].copy()).to(dev), torch.from_numpy(w[:rows * TMAX].copy()).to(dev),
-             rows)
+        # the table fills each row's taps from slot 0: keep only the widest row's count
+        idx, w = idx[:rows * TMAX].reshape(rows, TMAX), w[:rows * TMAX].reshape(rows, TMAX)
+        T = max(1, int((w != 0).sum(axis=1).max()))
+        t = (torch.from_numpy(np.ascontiguousarray(idx[:, :T])).to(dev),
+             torch.from_numpy(np.ascontiguousarray(w[:, :T])).to(dev), rows, T)
         _TABLES[key] = t
     return t
 
 
 def sep_resample(x: Feat, y: Feat, ytab, xtab, accumulate=False):
-    (ty, wy, ry), (tx, wx, rx) = ytab, xtab
+    (ty, wy, ry, Ty), (tx, wx, rx, Tx) = ytab, xtab
     assert (ry, rx) == (y.H, y.W) and x.C == y.C and x.N == y.N, "sep_resample shape mismatch"
     _lib.call("irgan_sep_resample", x.ptr, x.dt, x.N, x.H, x.W, x.C, x.ld, x.off, y.ptr, y.dt, y.H, y.W, y.ld, y.off,
-              P(ty), P(wy), P(tx), P(wx), TMAX, int(accumulate), stream())
+              P(ty), P(wy), Ty, P(tx), P(wx), Tx, int(accumulate), stream())
 
 
 def blur_down(x: Feat, y: Feat):

@@ -27,6 +27,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--case", default=None, help="substring filter on case names")
 ap.add_argument("--which", default="fwd,dgrad,wgrad")
 ap.add_argument("--iters", type=int, default=20)
+ap.add_argument("--splitk", default="0", help="comma list of wgrad split-K values (0 = the kernel's choice)")
 args = ap.parse_args()
 res = {}
 for name, cin, cout, k, s, p, mode, H in CASES:
@@ -48,6 +49,11 @@ for name, cin, cout, k, s, p, mode, H in CASES:
            "wgrad": lambda: ops.conv_wgrad(spec, ops.Feat(x), ops.Feat(dy), dw, ops.BF16)}
     res[name] = {}
     for k2 in args.which.split(","):
+        if k2 == "wgrad":
+            for sk in (int(s) for s in args.splitk.split(",")):
+                v = t(lambda: ops.conv_wgrad(spec, ops.Feat(x), ops.Feat(dy), dw, ops.BF16, splitk=sk), args.iters)
+                res[name][k2 if sk == 0 else f"wgrad@{sk}"] = (round(v, 4), round(flop / v / 1e9, 1))
+            continue
         v = t(fns[k2], args.iters)
         res[name][k2] = (round(v, 4), round(flop / v / 1e9, 1))
     print(name, "ms/TFLOPs", res[name], flush=True)
