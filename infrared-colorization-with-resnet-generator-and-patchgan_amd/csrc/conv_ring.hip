@@ -29,7 +29,8 @@ namespace {
 
 constexpr int NPIX = 32;  // band pixels per block (2 fragments)
 constexpr int NCO = 64;   // output channels per block (4 fragments)
-constexpr int NWV = 4;    // waves per block (K split)
+constexpr int NWV = 8;    // waves per block (K split)
+constexpr int MAXT = 160; // (term, tap) pairs: 3 terms x KH*KW (7x7: 147)
 
 IRGAN_HD int mirror_pos(int i, int n, int p) {  // virtual position folding onto i, or INT_MIN
     if (i >= 1 && i <= p) return -i;
@@ -37,10 +38,12 @@ IRGAN_HD int mirror_pos(int i, int n, int p) {  // virtual position folding onto
     return -0x40000000;
 }
 
-__global__ __launch_bounds__(256) void reflect_ring_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ dy,
+__global__ __launch_bounds__(NWV * 64) void reflect_ring_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ dy,
                                                            const bf16_t* __restrict__ w, int p, void* __restrict__ dx,
                                                            int segs_row, int segs_col) {
     __shared__ __attribute__((aligned(16))) float red[NWV][NPIX][NCO + 4];  // +4: conflict-free row writes
+    __shared__ int tap_list[MAXT];
+    __shared__ int ntap_s;
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int H = d.Ho, W = d.Wo;               // dx spatial size (stride 1)
@@ -93,6 +96,29 @@ __global__ __launch_bounds__(256) void reflect_ring_kernel(const irgan_conv_desc
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[f][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    // block-uniform list of the (term, ty, tx) taps that can touch dy
+    if (threadIdx.x == 0) {
+        int nt = 0;
+        for (int term = 0; term < 3; ++term) {
+            if (rowseg ? (term > 0 && !has_bandcol) : term != 1) continue;
+            for (int ty = 0; ty < d.KH; ++ty) {
+                if (rowseg && term != 1 && (unsigned)(vby + ty + d.c0y) >= (unsigned)d.H) continue;
+                for (int tx = 0; tx < d.KW; ++tx) {
+                    if (!rowseg && (unsigned)(vbx + tx + d.c0x) >= (unsigned)d.W) continue;
+                    tap_list[nt++] = (term << 8) | (ty << 4) | tx;
+                }
+            }
+        }
+        ntap_s = nt;
+    }
+    __syncthreads();
+    const int ntap = ntap_s;
+
+    // mirrored column of fragment f's pixel (terms 1 and 2)
+    int mxf[2];
+#pragma unroll
+    for (int f = 0; f < 2; ++f) mxf[f] = rowseg ? mirror_pos(px[f], W, p) : vbx;
+
     const int kc = (lane >> 4) * 8;  // channel offset of this lane within a 32-deep k step
     const bf16_t* wrow[4];
     bool wok[4];
@@ -103,62 +129,48 @@ __global__ __launch_bounds__(256) void reflect_ring_kernel(const irgan_conv_desc
         wrow[j] = w + (long)(wok[j] ? co : 0) * Kw + kc;
     }
     const int nc = d.Cin / 32;
-    int it = 0;  // block-uniform K-step counter: wave wv takes steps it % NWV == wv
-    for (int term = 0; term < 3; ++term) {
-        if (rowseg ? (term > 0 && !has_bandcol) : term != 1) continue;
-        int vy[2], vx[2];
-        bool tv[2];
+    const int total = ntap * nc;  // flattened K steps (tap, 32-channel step); wave wv takes s = wv mod NWV
+    auto load_step = [&](int q, uint4 (&a)[2], uint4 (&b)[4]) {
+        const int tp = q / nc, c = q - tp * nc;
+        const int e = tap_list[tp];
+        const int term = e >> 8, ty = (e >> 4) & 15, tx = e & 15;
+        const int wb = (ty * d.KW + tx) * d.Cin + c * 32;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = wok[j] ? *(const uint4*)(wrow[j] + wb) : uint4{0, 0, 0, 0};
 #pragma unroll
         for (int f = 0; f < 2; ++f) {
-            if (term == 0) { vy[f] = vby; vx[f] = px[f]; tv[f] = pv[f]; }
-            else {
-                const int mx = rowseg ? mirror_pos(px[f], W, p) : vbx;
-                vy[f] = term == 1 ? py[f] : vby;
-                vx[f] = mx;
-                tv[f] = pv[f] && mx != -0x40000000;
-            }
+            // term 0: (Vy, x); term 1: (y, Vx); term 2: (Vy, Vx)  (term is wave-uniform)
+            const int vy = term == 1 ? py[f] : vby;
+            const int vx = term == 0 ? px[f] : mxf[f];
+            const bool tv = pv[f] && (term == 0 || mxf[f] != -0x40000000);
+            const int r = vy + ty + d.c0y, cc = vx + tx + d.c0x;
+            const bool ok = tv && (unsigned)r < (unsigned)d.H && (unsigned)cc < (unsigned)d.W;
+            a[f] = ok ? *(const uint4*)(dy + (((long)n * d.H + r) * d.W + cc) * d.ldx + d.xoff + kc + c * 32)
+                      : uint4{0, 0, 0, 0};
         }
-        for (int ty = 0; ty < d.KH; ++ty) {
-            if (rowseg && term != 1) {  // uniform row: skip taps that miss dy entirely
-                const int r = vby + ty + d.c0y;
-                if ((unsigned)r >= (unsigned)d.H) continue;
-            }
-            for (int tx = 0; tx < d.KW; ++tx) {
-                if (!rowseg) {  // uniform column
-                    const int c = vbx + tx + d.c0x;
-                    if ((unsigned)c >= (unsigned)d.W) continue;
-                }
-                // this wave's steps of the tap: c in [first, nc) step NWV
-                const int first = (wv - it % NWV + NWV) % NWV;
-                it += nc;
-                if (first >= nc) continue;
-                const bf16_t* ap[2];
-                bool aok[2];
+    };
+    auto mma = [&](const uint4 (&a)[2], const uint4 (&b)[4]) {
 #pragma unroll
-                for (int f = 0; f < 2; ++f) {
-                    const int r = vy[f] + ty + d.c0y, c = vx[f] + tx + d.c0x;
-                    aok[f] = tv[f] && (unsigned)r < (unsigned)d.H && (unsigned)c < (unsigned)d.W;
-                    ap[f] = dy + (aok[f] ? (((long)n * d.H + r) * d.W + c) * d.ldx + d.xoff + kc : 0);
-                }
-                const int wb = (ty * d.KW + tx) * d.Cin;
-#pragma unroll 2
-                for (int c = first; c < nc; c += NWV) {
-                    uint4 a[2], b[4];
+        for (int f = 0; f < 2; ++f)
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        b[j] = wok[j] ? *(const uint4*)(wrow[j] + wb + c * 32) : uint4{0, 0, 0, 0};
-#pragma unroll
-                    for (int f = 0; f < 2; ++f) a[f] = aok[f] ? *(const uint4*)(ap[f] + c * 32) : uint4{0, 0, 0, 0};
-#pragma unroll
-                    for (int f = 0; f < 2; ++f)
-#pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, b[j]),
-                                                                                __builtin_bit_cast(bf16x8_t, a[f]),
-                                                                                acc[f][j], 0, 0, 0);
-                }
-            }
-        }
+            for (int j = 0; j < 4; ++j)
+                acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, b[j]),
+                                                                    __builtin_bit_cast(bf16x8_t, a[f]), acc[f][j], 0,
+                                                                    0, 0);
+    };
+    // two steps of operands in flight: step s+NWV loads while step s multiplies
+    uint4 a0[2], b0[4], a1[2], b1[4];
+    int ks = wv;
+    if (ks < total) load_step(ks, a0, b0);
+    while (ks < total) {
+        const int k1 = ks + NWV;
+        if (k1 < total) load_step(k1, a1, b1);
+        mma(a0, b0);
+        if (k1 >= total) break;
+        const int k2 = k1 + NWV;
+        if (k2 < total) load_step(k2, a0, b0);
+        mma(a1, b1);
+        ks = k2;
     }
     // partial tiles -> LDS: lane holds pixel f*16 + (lane & 15), channels j*16 + 4*(lane>>4) + r
 #pragma unroll
@@ -168,7 +180,8 @@ __global__ __launch_bounds__(256) void reflect_ring_kernel(const irgan_conv_desc
             *(float4*)&red[wv][f * 16 + (lane & 15)][j * 16 + 4 * (lane >> 4)] =
                 make_float4(acc[f][j][0], acc[f][j][1], acc[f][j][2], acc[f][j][3]);
     __syncthreads();
-    // thread -> (pixel, 8 channels): sum the 4 partials in order, add into dx
+    // thread -> (pixel, 8 channels): sum the NWV partials in order, add into dx
+    if (threadIdx.x >= NPIX * NCO / 8) return;
     const int pix_l = threadIdx.x >> 3, cg = (threadIdx.x & 7) * 8;
     const int q = seg * NPIX + pix_l;
     const int yy = rowseg ? bpos : q, xx = rowseg ? q : bpos;
@@ -223,11 +236,12 @@ extern "C" int irgan_reflect_dgrad_ring(const irgan_conv_desc* d, const void* dy
     if (!d || !dy || !w || !dx) return IRGAN_EINVAL;
     if ((long)d->N * d->Ho * d->Wo <= 0 || d->Cout <= 0 || p <= 0) return 0;
     if (d->dtype != IRGAN_BF16 || d->Cin % 32 || d->ldx % 8 || d->xoff % 8 || d->sy != 1 || d->sx != 1 ||
-        d->Ho != d->H || d->Wo != d->W || d->H < 2 * p + 2 || d->W < 2 * p + 2 || d->accumulate < 0)
+        d->Ho != d->H || d->Wo != d->W || d->H < 2 * p + 2 || d->W < 2 * p + 2 || d->accumulate < 0 ||
+        d->KH > 15 || d->KW > 15 || 3 * d->KH * d->KW > MAXT)
         return IRGAN_EUNSUPPORTED;
     const int segs_row = irgan_cdiv(d->Wo, NPIX), segs_col = irgan_cdiv(d->Ho, NPIX);
     dim3 grid(d->N * 2 * p * (segs_row + segs_col), irgan_cdiv(d->Cout, NCO));
-    reflect_ring_kernel<<<grid, 256, 0, (hipStream_t)s>>>(*d, (const bf16_t*)dy, (const bf16_t*)w, p, dx, segs_row,
+    reflect_ring_kernel<<<grid, NWV * 64, 0, (hipStream_t)s>>>(*d, (const bf16_t*)dy, (const bf16_t*)w, p, dx, segs_row,
                                                          segs_col);
     IRGAN_LAUNCH_CHECK();
     return 0;

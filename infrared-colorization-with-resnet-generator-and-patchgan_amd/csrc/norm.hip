@@ -202,6 +202,173 @@ __global__ __launch_bounds__(TPB) void rows_kernel(Slice X, Slice DY, Slice DY2,
     }
 }
 
+IRGAN_HD void bf8f(const uint4 u, float* o) {
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        o[2 * k] = __uint_as_float(w[k] << 16);
+        o[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+    }
+}
+
+// Block-wide per-channel sums of (a0, a1) (8 channels per thread) ->
+// part[(n*gridDim.x + blockIdx.x)*C + c]; the same order as rows_kernel's.
+IRGAN_HD void block_partials8(float* a0, float* a1, const Lay& L, bool on, int cb, int c, int C, int n, float* s0,
+                              float* s1, float2* __restrict__ part) {
+    if (L.CL <= 64 && (64 % L.CL) == 0) {
+        for (int o = L.CL; o < 64; o <<= 1) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                a0[k] += __shfl_xor(a0[k], o, 64);
+                a1[k] += __shfl_xor(a1[k], o, 64);
+            }
+        }
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        if (lane < L.CL) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                s0[(wv * L.CL + lane) * 8 + k] = a0[k];
+                s1[(wv * L.CL + lane) * 8 + k] = a1[k];
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < L.CL && cb + threadIdx.x * 8 < C) {
+            const int cc = cb + threadIdx.x * 8;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                float t0 = 0.f, t1 = 0.f;
+                for (int j = 0; j < TPB / 64; ++j) {
+                    t0 += s0[(j * L.CL + threadIdx.x) * 8 + k];
+                    t1 += s1[(j * L.CL + threadIdx.x) * 8 + k];
+                }
+                part[((long)n * gridDim.x + blockIdx.x) * C + cc + k] = make_float2(t0, t1);
+            }
+        }
+        __syncthreads();
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        s0[threadIdx.x * 8 + k] = a0[k];
+        s1[threadIdx.x * 8 + k] = a1[k];
+    }
+    __syncthreads();
+    if (on && L.rl == 0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            float t0 = 0.f, t1 = 0.f;
+            for (int j = 0; j < L.RP; ++j) {
+                t0 += s0[(j * L.CL + L.cl) * 8 + k];
+                t1 += s1[(j * L.CL + L.cl) * 8 + k];
+            }
+            part[((long)n * gridDim.x + blockIdx.x) * C + c + k] = make_float2(t0, t1);
+        }
+    }
+    __syncthreads();
+}
+
+// All-bf16 fast path of rows_kernel<MODE, 8> for MODE 0 (stats), 1 (backward
+// reduce) and 2 (backward apply without db).  rows_kernel issues one row's
+// loads at a time at ~150 VGPRs (3 waves per SIMD), so only ~24 KB of loads are
+// in flight per CU and the backward reduce streams at ~2 TB/s.  Here each
+// thread walks its rows in batches of U and issues every 16-byte load of a
+// batch, unconverted, before using any; tail rows of the last batch re-load a
+// valid row and are masked.  dx may alias dy (no __restrict__ on either): a
+// thread stores only rows it has already loaded.
+template <int MODE, int U>
+__global__ __launch_bounds__(TPB) void rows8_kernel(const bf16_t* x, int ldx, int xoff, const bf16_t* dy, int lddy,
+                                                    int dyoff, const bf16_t* dy2, int lddy2, int dy2off, int act,
+                                                    const float* __restrict__ mr, const float* __restrict__ red,
+                                                    bf16_t* dx, int lddx, int dxoff, int HW, int C, int rows_per_block,
+                                                    float2* __restrict__ part) {
+    __shared__ float s0[TPB * 8], s1[TPB * 8];
+    const int n = blockIdx.y;
+    const int r0 = blockIdx.x * rows_per_block;
+    const int r1 = min(HW, r0 + rows_per_block);
+    Lay L(C, 8);
+    const bool active = L.rl < L.RP;
+    const long pb = (long)n * HW;
+    for (int cb = 0; cb < C; cb += L.CL * 8) {
+        const int c = cb + L.cl * 8;
+        const bool on = active && c < C;
+        float a0[8], a1[8], mean[8], rstd[8], mg[8], mgx[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { a0[k] = 0.f; a1[k] = 0.f; }
+        if (on && MODE >= 1) {
+            const float4* m4 = (const float4*)(mr + 2 * ((long)n * C + c));
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float4 t = m4[k];
+                mean[2 * k] = t.x; rstd[2 * k] = t.y; mean[2 * k + 1] = t.z; rstd[2 * k + 1] = t.w;
+            }
+            if (MODE == 2) {
+                const float4* r4 = (const float4*)(red + 2 * ((long)n * C + c));
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float4 t = r4[k];
+                    mg[2 * k] = t.x; mgx[2 * k] = t.y; mg[2 * k + 1] = t.z; mgx[2 * k + 1] = t.w;
+                }
+            }
+        }
+        if (on) {
+#pragma unroll 1
+            for (int r = r0 + L.rl; r < r1; r += U * L.RP) {
+                uint4 xr[U], gr[U], hr[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const long p = pb + min(r + u * L.RP, r1 - 1);
+                    xr[u] = *(const uint4*)(x + p * ldx + xoff + c);
+                    if (MODE != 0) gr[u] = *(const uint4*)(dy + p * lddy + dyoff + c);
+                }
+                if (MODE != 0 && dy2) {
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const long p = pb + min(r + u * L.RP, r1 - 1);
+                        hr[u] = *(const uint4*)(dy2 + p * lddy2 + dy2off + c);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    if (r + u * L.RP >= r1) break;
+                    float xv[8];
+                    bf8f(xr[u], xv);
+                    if (MODE == 0) {
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) { a0[k] += xv[k]; a1[k] += xv[k] * xv[k]; }
+                        continue;
+                    }
+                    float gv[8];
+                    bf8f(gr[u], gv);
+                    if (dy2) {
+                        float hv[8];
+                        bf8f(hr[u], hv);
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) gv[k] += hv[k];
+                    }
+                    float o[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const float xh = (xv[k] - mean[k]) * rstd[k];
+                        const float g = gv[k] * act_grad(xh, act);
+                        if (MODE == 1) { a0[k] += g; a1[k] += g * xh; }
+                        else o[k] = rstd[k] * (g - mg[k] - xh * mgx[k]);
+                    }
+                    if (MODE == 2) {
+                        uint4 w;
+                        w.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
+                        w.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
+                        w.z = (uint32_t)f2bf(o[4]) | ((uint32_t)f2bf(o[5]) << 16);
+                        w.w = (uint32_t)f2bf(o[6]) | ((uint32_t)f2bf(o[7]) << 16);
+                        *(uint4*)(dx + (pb + r + u * L.RP) * lddx + dxoff + c) = w;
+                    }
+                }
+            }
+        }
+        if (MODE == 2) continue;  // uniform across the block
+        block_partials8(a0, a1, L, on, cb, c, C, n, s0, s1, part);
+    }
+}
+
 // fp64 sum of the nb block partials of each (n, c).  Block (32 channels x 8
 // partial lanes) per (image, channel group): loads are 256-byte rows of
 // consecutive channels, the 8 lanes of a channel combine through LDS in a fixed
@@ -309,6 +476,20 @@ int launch_rows(Slice X, Slice DY, Slice DY2, int act, const float* mr, const fl
     const int rows = irgan_cdiv(HW, nb);
     nb = irgan_cdiv(HW, rows);
     dim3 g(nb, N);
+    static const bool fast = !getenv("IRGAN_NO_ROWS8");
+    const bool bf = X.dt == IRGAN_BF16 && (MODE == 0 || (DY.dt == IRGAN_BF16 && (!DY2.p || DY2.dt == IRGAN_BF16))) &&
+                    (MODE != 2 || (dxdt == IRGAN_BF16 && !db));
+    if (fast && vec && bf && MODE <= 2) {
+        const bf16_t *xp = (const bf16_t*)X.p, *gp = (const bf16_t*)DY.p, *hp = (const bf16_t*)DY2.p;
+        if (MODE == 0)
+            rows8_kernel<0, 8><<<g, TPB, 0, st>>>(xp, X.ld, X.off, nullptr, 0, 0, nullptr, 0, 0, act, mr, red, nullptr,
+                                                  0, 0, HW, C, rows, part);
+        else
+            rows8_kernel<MODE, 4><<<g, TPB, 0, st>>>(xp, X.ld, X.off, gp, DY.ld, DY.off, hp, DY2.ld, DY2.off, act, mr,
+                                                     red, (bf16_t*)dx, lddx, dxoff, HW, C, rows, part);
+        if (nb_out) *nb_out = nb;
+        return 0;
+    }
     if (vec)
         rows_kernel<MODE, V><<<g, TPB, 0, st>>>(X, DY, DY2, act, mr, red, dx, dxdt, lddx, dxoff, HW, C, rows, part, db);
     else

@@ -296,14 +296,26 @@ def in_apply(x: Feat, mr, y: Feat, act=ACT_NONE, res: Feat = None, xhat: torch.T
               stream())
 
 
-def in_backward(dy: Feat, x: Feat, act: int, mr, work, red, dx: Feat, db=None, dy2: Feat = None):
-    """dx = backward of act(IN(x)) applied to (dy [+ dy2]); x = PRE-norm input."""
+def in_bwd_parts(dy: Feat, x: Feat, act: int, mr, work, red, dx: Feat, db=None, dy2: Feat = None):
+    """(reduce, apply) launch closures of in_backward (also used for per-pass timing)."""
     N, HW, C = x.N, x.H * x.W, x.C
     d2 = (dy2.ptr, dy2.dt, dy2.ld, dy2.off) if dy2 is not None else (None, 0, 0, 0)
-    _lib.call("irgan_in_bwd_reduce", dy.ptr, dy.dt, dy.ld, dy.off, *d2, x.ptr, x.dt, x.ld, x.off, act, N, HW, C,
-              P(mr), P(work), P(red), stream())
-    _lib.call("irgan_in_bwd_apply", dy.ptr, dy.dt, dy.ld, dy.off, *d2, x.ptr, x.dt, x.ld, x.off, act, N, HW, C,
-              P(mr), P(red), dx.ptr, dx.dt, dx.ld, dx.off, P(db), stream())
+
+    def reduce():
+        _lib.call("irgan_in_bwd_reduce", dy.ptr, dy.dt, dy.ld, dy.off, *d2, x.ptr, x.dt, x.ld, x.off, act, N, HW, C,
+                  P(mr), P(work), P(red), stream())
+
+    def apply():
+        _lib.call("irgan_in_bwd_apply", dy.ptr, dy.dt, dy.ld, dy.off, *d2, x.ptr, x.dt, x.ld, x.off, act, N, HW, C,
+                  P(mr), P(red), dx.ptr, dx.dt, dx.ld, dx.off, P(db), stream())
+    return reduce, apply
+
+
+def in_backward(dy: Feat, x: Feat, act: int, mr, work, red, dx: Feat, db=None, dy2: Feat = None):
+    """dx = backward of act(IN(x)) applied to (dy [+ dy2]); x = PRE-norm input."""
+    reduce, apply = in_bwd_parts(dy, x, act, mr, work, red, dx, db, dy2)
+    reduce()
+    apply()
 
 
 _CS_WORK = {}

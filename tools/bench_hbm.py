@@ -60,6 +60,9 @@ for name, C, H in IN_CASES:
     rec(f"in_apply:{name}", t(lambda: ops.in_apply(ops.Feat(z), mr, ops.Feat(y), act=ops.ACT_RELU), args.iters), 2 * n)
     rec(f"in_bwd:{name}", t(lambda: ops.in_backward(ops.Feat(dy), ops.Feat(z), ops.ACT_RELU, mr, work, red,
                                                     ops.Feat(dx)), args.iters), 5 * n)
+    red_fn, app_fn = ops.in_bwd_parts(ops.Feat(dy), ops.Feat(z), ops.ACT_RELU, mr, work, red, ops.Feat(dx))
+    rec(f"in_bwd_reduce:{name}", t(red_fn, args.iters), 2 * n)
+    rec(f"in_bwd_apply:{name}", t(app_fn, args.iters), 3 * n)
 
 for name, kind, C, H in RS_CASES:
     if args.case and args.case not in name:
