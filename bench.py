@@ -36,6 +36,19 @@ def min_gflop_per_img(H, W):
     return MIN_GFLOP_PER_IMG_256 * (H * W) / (256 * 256)
 
 
+def pmc_traffic(family):
+    """HBM bytes per launch of the resblock conv `family` (fwd / dgrad / wgrad),
+    from the committed rocprofv3 --pmc passes of tools/gpu_traffic.sh (FETCH_SIZE
+    doubled per the gfx950 correction, plus WRITE_SIZE).  PMC counters cannot be
+    collected inside this process, so the measured figure is read, not recomputed."""
+    p = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+    try:
+        with open(p) as f:
+            return json.load(f)[family]["hbm_bytes"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def cpu_baseline(H, W, batch=1, budget_s=20.0):
     """The CPU oracle (fp32 PyTorch-CPU restatement of ir:1636-1681) on host cores."""
     import torch
@@ -145,6 +158,7 @@ def main():
                             "tflops": round(res_flop / (mean_ms * 1e-3) / 1e12, 2)}
         dom = max(kern, key=lambda k: kern[k]["launches"] * kern[k]["mean_ms"]) if kern else None
         achieved = kern[dom]["tflops"] if dom else None
+        traffic = pmc_traffic(dom.split(":")[0]) if (dom and H == 256 and B == 16 and args.dtype == "bf16") else None
         step_tflops = value * min_gflop_per_img(H, W) / 1e3 / world
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "img/s", "n_gpus": world, "steps": args.steps,
@@ -157,7 +171,9 @@ def main():
                        "step_tflops_per_gpu": round(step_tflops, 2),
                        "step_frac_of_bf16_peak": round(step_tflops / BF16_DENSE_PEAK_TFLOPS, 4)},
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                         "frac": round(achieved / peak, 4) if achieved else None, "traffic": None,
+                         "frac": round(achieved / peak, 4) if achieved else None, "traffic": traffic,
+                         "traffic_unit": "HBM bytes per launch (rocprofv3 PMC: 2*FETCH_SIZE + WRITE_SIZE, "
+                                         "profiles/r01_pmc_traffic.json)",
                          "flop_per_launch": res_flop, "per_kernel": kern},
             "losses": {k: round(v, 5) for k, v in losses.items()},
         }

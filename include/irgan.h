@@ -211,6 +211,21 @@ int irgan_ssim(const float* a, const float* b, int32_t N, int32_t H, int32_t W, 
 int irgan_adam(float* p, const float* g, float* m, float* v, int64_t n, float step_size,
                float beta1, float beta2, float bc2_sqrt, float eps, irgan_stream_t s);
 
+/* ---- inference / evaluation ---- */
+/* out[p][c] = uint8(clip((x + 1) / 2, 0, 1) * 255) for every pixel p and
+ * channel c of an NHWC fp32 slice (x, ldx, xoff), out dense [N][H][W][C]
+ * (16-byte aligned) -- the float32 pipeline of tensor_to_rgb_image
+ * (ir:865-876) for a whole batch, on the device; truncation as numpy astype. */
+int irgan_to_rgb_u8(const float* x, int32_t N, int32_t H, int32_t W, int32_t C, int32_t ldx,
+                    int32_t xoff, void* out, irgan_stream_t s);
+/* Per-image error sums of compute_metrics (ir:1184-1206) over uint8 images
+ * (as run_test feeds it, ir:1412-1415): d = pred/255 - gt/255 in fp32,
+ * sums[2n] = sum |d|, sums[2n+1] = sum d^2 over the per_image bytes of image n
+ * (MAE = sums[2n]/per_image, MSE = sums[2n+1]/per_image).  work: >= 128*N
+ * doubles of scratch (work_cap = its size in doubles). */
+int irgan_image_metrics_u8(const void* pred, const void* gt, int32_t N, int64_t per_image,
+                           double* work, int64_t work_cap, double* sums, irgan_stream_t s);
+
 /* Version / capability probe (no GPU work). */
 int irgan_version(void);
 

@@ -21,3 +21,5 @@ except ImportError as _e:  # pragma: no cover - only while the API module is abs
     _api_all = []
 
 __all__ = ["_lib", "ops"] + list(_api_all)
+
+from . import inference  # noqa: E402,F401  -- batched test-mode path

@@ -87,3 +87,26 @@ def test_lr_lambda_schedule():
     assert O.lr_lambda(0) == 1.0 and O.lr_lambda(39) == 1.0
     assert abs(O.lr_lambda(40) - 0.9) < 1e-12 and abs(O.lr_lambda(44) - 0.5) < 1e-12
     assert O.lr_lambda(49) == 0.0
+
+
+def test_infer_oracle_matches_reference_golden():
+    """oracle/infer.py against tests/golden/infer.npz (executed reference,
+    tests/golden/make_infer_golden.py): uint8 conversion bit-exact, ir_to_tensor
+    exact, compute_metrics to float64 round-off."""
+    import os
+    from conftest import GOLDEN
+    from oracle import infer as OI
+    fx = dict(np.load(os.path.join(GOLDEN, "infer.npz")))
+    assert np.array_equal(OI.tensor_to_rgb_image(fx["t2rgb_in"]), fx["t2rgb_out"])
+    nhwc = np.transpose(fx["t2rgb_in"], (0, 2, 3, 1))
+    assert np.array_equal(OI.rgb_u8_batch(nhwc)[0], fx["t2rgb_out"])
+    assert np.array_equal(OI.ir_to_array(fx["ir_img"]), fx["ir_tensor"])
+    for i in range(fx["met_out"].shape[0]):
+        mae, mse, psnr, ssim = OI.compute_metrics(fx["met_pred_u8"][i].astype(np.float32) / 255.0,
+                                                  fx["met_gt_u8"][i].astype(np.float32) / 255.0)
+        assert ssim is None
+        np.testing.assert_allclose([mae, mse], fx["met_out"][i, :2], rtol=1e-12)
+        assert psnr == fx["met_out"][i, 2] or abs(psnr - fx["met_out"][i, 2]) < 1e-9
+    # the generator's test-mode output converts to the stored uint8 images
+    for i in range(fx["g_fake"].shape[0]):
+        assert np.array_equal(OI.tensor_to_rgb_image(fx["g_fake"][i:i + 1]), fx["g_u8"][i])
