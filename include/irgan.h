@@ -77,6 +77,14 @@ int irgan_conv_fwd_splitk(const irgan_conv_desc* d, const void* x, const void* w
 int irgan_conv_wgrad(const irgan_conv_desc* d, const void* x, const void* dy,
                      float* dw, int32_t splitk, irgan_stream_t s);
 
+/* Same as irgan_conv_wgrad with a caller-owned fp32 workspace of ws_floats
+ * floats: when it holds splitk x (Cout*KH*KW*Cin) floats, the split-K partials
+ * are written there with plain stores and summed into dw by a second launch in
+ * a fixed order (deterministic, no atomics); otherwise identical to
+ * irgan_conv_wgrad.  ws may be NULL. */
+int irgan_conv_wgrad_ws(const irgan_conv_desc* d, const void* x, const void* dy, float* dw,
+                        int32_t splitk, float* ws, int64_t ws_floats, irgan_stream_t s);
+
 /* Weight re-pack: dst rows [R][Kp] (dtype) from the fp32 KRSC master
  * src[Cout][KH][KW][Cin], Kp = roundup(taps*Cp, kalign), taps and channels
  * zero-padded (Cp = max(cpad, channels)).  transpose=0: R = Cout, row =

@@ -23,7 +23,7 @@ extern "C" int irgan_conv_fwd_pp(const irgan_conv_desc* d, const void* x, const 
 extern "C" int irgan_conv_fwd_halo(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
                                    const void* mask, hipStream_t st);
 extern "C" int irgan_conv_wgrad_halo(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, int splitk,
-                                     hipStream_t st);
+                                     float* ws, long ws_cap, hipStream_t st);
 extern "C" int irgan_conv_wgrad_glds(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, int splitk,
                                      hipStream_t st);
 
@@ -518,7 +518,8 @@ void wg_launch(dim3 g, hipStream_t st, const irgan_conv_desc* d, const void* x, 
 }
 
 template <typename T>
-int launch_wgrad(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, int splitk, hipStream_t st) {
+int launch_wgrad(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, int splitk, hipStream_t st,
+                 float* ws = nullptr, long ws_cap = 0) {
     constexpr int EPC = TT<T>::EPC, BKP = ROWB / (int)sizeof(T);
     const long P = (long)d->N * d->Ho * d->Wo;
     const int K = d->KH * d->KW * d->Cin;
@@ -528,7 +529,7 @@ int launch_wgrad(const irgan_conv_desc* d, const void* x, const void* dy, float*
     if constexpr (sizeof(T) == 2) {
         static const bool use_wgh = !getenv("IRGAN_NO_WGRAD_HALO");
         if (use_wgh) {
-            const int rc = irgan_conv_wgrad_halo(d, x, dy, dw, splitk, st);
+            const int rc = irgan_conv_wgrad_halo(d, x, dy, dw, splitk, ws, ws_cap, st);
             if (rc != IRGAN_EUNSUPPORTED) return rc;
         }
         static const bool use_glds = !getenv("IRGAN_NO_GLDS");
@@ -577,6 +578,17 @@ extern "C" int irgan_conv_wgrad(const irgan_conv_desc* d, const void* x, const v
     if (!d || !x || !dy || !dw) return IRGAN_EINVAL;
     hipStream_t st = (hipStream_t)s;
     if (d->dtype == IRGAN_BF16) return launch_wgrad<bf16_t>(d, x, dy, dw, splitk, st);
+    if (d->dtype == IRGAN_F32) return launch_wgrad<float>(d, x, dy, dw, splitk, st);
+    return IRGAN_EUNSUPPORTED;
+}
+
+extern "C" int irgan_conv_wgrad_ws(const irgan_conv_desc* d, const void* x, const void* dy, float* dw,
+                                   int32_t splitk, float* ws, int64_t ws_floats, irgan_stream_t s) {
+    if (!d || !x || !dy || !dw) return IRGAN_EINVAL;
+    static const bool use_slab = !getenv("IRGAN_NO_WGRAD_SLAB");
+    hipStream_t st = (hipStream_t)s;
+    if (d->dtype == IRGAN_BF16)
+        return launch_wgrad<bf16_t>(d, x, dy, dw, splitk, st, use_slab ? ws : nullptr, ws_floats);
     if (d->dtype == IRGAN_F32) return launch_wgrad<float>(d, x, dy, dw, splitk, st);
     return IRGAN_EUNSUPPORTED;
 }

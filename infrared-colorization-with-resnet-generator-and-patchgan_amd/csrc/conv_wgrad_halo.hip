@@ -59,7 +59,8 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void wgrad_halo_kernel(const irgan
                                                                      const bf16_t* __restrict__ dy,
                                                                      float* __restrict__ dw, int segs_per_block,
                                                                      int nseg, int ntco, int nci,
-                                                                     const bf16_t* __restrict__ zero, int swz) {
+                                                                     const bf16_t* __restrict__ zero, int swz,
+                                                                     float* __restrict__ slab) {
     constexpr int NW = WM * WN, STAGES = 3;
     constexpr int RA = BMC * 2;                          // bytes per dY pixel row
     constexpr int APIECES = 64 * RA / 1024;              // dY tile pieces
@@ -187,8 +188,11 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void wgrad_halo_kernel(const irgan
                                                                         acc[i][j], 0, 0, 0);
         }
     }
-    // C[row = co][col = ci]: row = (lane>>4)*4 + r, col = lane & 15
+    // C[row = co][col = ci]: row = (lane>>4)*4 + r, col = lane & 15.  Split-K
+    // partials: plain stores into this split's slab (summed in a fixed order by
+    // wgrad_slab_reduce) or, without a slab, fp32 atomics into dw.
     const int K = d.KH * KW * d.Cin;
+    float* const dst = slab ? slab + (long)split * d.Cout * K : nullptr;
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -199,14 +203,31 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void wgrad_halo_kernel(const irgan
             for (int j = 0; j < NJ; ++j) {
                 const int jj = wn * NJ + j, tx = jj >> 2;
                 const int ci = ci0 + (jj & 3) * 16 + (lane & 15);
-                atomicAdd(dw + (long)co * K + (ty * KW + tx) * d.Cin + ci, acc[i][j][rr]);
+                const long o = (long)co * K + (ty * KW + tx) * d.Cin + ci;
+                if (dst) dst[o] = acc[i][j][rr];
+                else atomicAdd(dw + o, acc[i][j][rr]);
             }
         }
 }
 
+// dw[i] += sum over splits s (in order) of slab[s][i]: the second stage of the
+// split-K reduction (deterministic, no atomics).  n % 4 == 0.
+__global__ __launch_bounds__(256) void wgrad_slab_reduce(const float* __restrict__ slab, int splits, long n,
+                                                         float* __restrict__ dw) {
+    const long n4 = n / 4;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+        float4 a = ((const float4*)dw)[i];
+        for (int s = 0; s < splits; ++s) {
+            const float4 v = ((const float4*)(slab + (long)s * n))[i];
+            a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+        }
+        ((float4*)dw)[i] = a;
+    }
+}
+
 template <int BMC, int KW, int SX, int WM, int WN>
 void launch_t(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, int splitk, hipStream_t st,
-              const bf16_t* zero, int swz) {
+              const bf16_t* zero, int swz, float* ws, long ws_cap) {
     constexpr int NW = WM * WN;
     // resident blocks per CU (LDS and VGPR limits, from the runtime) x 256 CUs: the
     // grid is sized to at most one full round -- a grid just above the resident
@@ -238,8 +259,17 @@ void launch_t(const irgan_conv_desc* d, const void* x, const void* dy, float* dw
     }
     const int spb = irgan_cdiv(nseg, splitk);
     splitk = irgan_cdiv(nseg, spb);
+    const long n = (long)d->Cout * d->KH * d->KW * d->Cin;
+    // slabs pay splitk*n*4 bytes twice (store + reduce); measured on MI355X they beat
+    // fp32 atomics only at low split counts (resblock 3x3: 21 splits, -7 %), and
+    // lose at 56-170 splits (down1 / up2 at 256^2: +3..12 %)
+    float* slab = (ws && splitk > 1 && splitk <= 24 && n % 4 == 0 && (long)splitk * n <= ws_cap) ? ws : nullptr;
     wgrad_halo_kernel<BMC, KW, SX, WM, WN><<<tiles * splitk, WM * WN * 64, 0, st>>>(
-        *d, (const bf16_t*)x, (const bf16_t*)dy, dw, spb, nseg, ntco, nci, zero, swz);
+        *d, (const bf16_t*)x, (const bf16_t*)dy, dw, spb, nseg, ntco, nci, zero, swz, slab);
+    if (slab) {
+        const int blocks = (int)std::min<long>(irgan_cdiv(n / 4, 256), 2048);
+        wgrad_slab_reduce<<<blocks, 256, 0, st>>>(slab, splitk, n, dw);
+    }
 }
 
 }  // namespace
@@ -247,7 +277,7 @@ void launch_t(const irgan_conv_desc* d, const void* x, const void* dy, float* dw
 // Preconditions: bf16; Cin % 64 == 0; ldx, xoff, ldy, yoff % 8 == 0; Wo % 64 == 0;
 // sx == sy in {1, 2}; (Cout % 64 == 0 and KW in {3, 4}) or (Cout <= 8, KW == 7, stride 1).
 extern "C" int irgan_conv_wgrad_halo(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, int splitk,
-                                     hipStream_t st) {
+                                     float* ws, long ws_cap, hipStream_t st) {
     if ((long)d->N * d->Ho * d->Wo <= 0) return 0;
     if (d->Cin % 64 || d->ldx % 8 || d->xoff % 8 || d->ldy % 8 || d->yoff % 8 || d->Wo % 64 || d->sx != d->sy ||
         (d->sx != 1 && d->sx != 2))
@@ -259,21 +289,21 @@ extern "C" int irgan_conv_wgrad_halo(const irgan_conv_desc* d, const void* x, co
     const int s2 = d->sx == 2;
     static const bool wide = getenv("IRGAN_WGH_256") != nullptr;
     if (wide && d->Cout % 256 == 0 && d->KW == 3 && !s2) {
-        launch_t<256, 3, 1, 4, 2>(d, x, dy, dw, splitk, st, zero, swz);
+        launch_t<256, 3, 1, 4, 2>(d, x, dy, dw, splitk, st, zero, swz, ws, ws_cap);
     } else if (d->Cout % 128 == 0 && d->KW == 3) {
-        if (s2) launch_t<128, 3, 2, 2, 4>(d, x, dy, dw, splitk, st, zero, swz);
-        else launch_t<128, 3, 1, 2, 4>(d, x, dy, dw, splitk, st, zero, swz);
+        if (s2) launch_t<128, 3, 2, 2, 4>(d, x, dy, dw, splitk, st, zero, swz, ws, ws_cap);
+        else launch_t<128, 3, 1, 2, 4>(d, x, dy, dw, splitk, st, zero, swz, ws, ws_cap);
     } else if (d->Cout % 128 == 0 && d->KW == 4) {
-        if (s2) launch_t<128, 4, 2, 2, 4>(d, x, dy, dw, splitk, st, zero, swz);
-        else launch_t<128, 4, 1, 2, 4>(d, x, dy, dw, splitk, st, zero, swz);
+        if (s2) launch_t<128, 4, 2, 2, 4>(d, x, dy, dw, splitk, st, zero, swz, ws, ws_cap);
+        else launch_t<128, 4, 1, 2, 4>(d, x, dy, dw, splitk, st, zero, swz, ws, ws_cap);
     } else if (d->Cout % 64 == 0 && d->KW == 3) {
-        if (s2) launch_t<64, 3, 2, 2, 4>(d, x, dy, dw, splitk, st, zero, swz);
-        else launch_t<64, 3, 1, 2, 4>(d, x, dy, dw, splitk, st, zero, swz);
+        if (s2) launch_t<64, 3, 2, 2, 4>(d, x, dy, dw, splitk, st, zero, swz, ws, ws_cap);
+        else launch_t<64, 3, 1, 2, 4>(d, x, dy, dw, splitk, st, zero, swz, ws, ws_cap);
     } else if (d->Cout % 64 == 0 && d->KW == 4) {
-        if (s2) launch_t<64, 4, 2, 2, 4>(d, x, dy, dw, splitk, st, zero, swz);
-        else launch_t<64, 4, 1, 2, 4>(d, x, dy, dw, splitk, st, zero, swz);
+        if (s2) launch_t<64, 4, 2, 2, 4>(d, x, dy, dw, splitk, st, zero, swz, ws, ws_cap);
+        else launch_t<64, 4, 1, 2, 4>(d, x, dy, dw, splitk, st, zero, swz, ws, ws_cap);
     } else if (d->Cout <= 8 && d->KW == 7 && !s2) {
-        launch_t<16, 7, 1, 1, 4>(d, x, dy, dw, splitk, st, zero, swz);
+        launch_t<16, 7, 1, 1, 4>(d, x, dy, dw, splitk, st, zero, swz, ws, ws_cap);
     } else {
         return IRGAN_EUNSUPPORTED;
     }

@@ -277,8 +277,23 @@ def conv_wgrad(spec: ConvSpec, x: Feat, dy: Feat, dw: torch.Tensor, dtype: int, 
               yoff=dy.off, OH=Ho, OW=Wo, omy=1, ooy=0, omx=1, oox=0, KH=spec.k, KW=spec.k, sy=spec.stride,
               sx=spec.stride, c0y=-spec.pad, c0x=-spec.pad, pad_mode=spec.mode, act=0, accumulate=1, dtype=dtype,
               out_dtype=F32, mask_act=0, ldm=0, moff=0)
+    ws = _wgrad_ws(dw.device) if dtype == BF16 else None
     TIMER.wrap(conv_tag("wgrad", spec, (x.H, x.W), x.N), lambda: _lib.call(
-        "irgan_conv_wgrad", ctypes.byref(d), x.ptr, dy.ptr, P(dw), splitk, stream()))
+        "irgan_conv_wgrad_ws", ctypes.byref(d), x.ptr, dy.ptr, P(dw), splitk, P(ws), 0 if ws is None else ws.numel(),
+        stream()))
+
+
+WGRAD_WS_FLOATS = 24 << 20   # split-K slab workspace (96 MB): >= slots x tile for every layer of the step
+_WGRAD_WS = {}
+
+
+def _wgrad_ws(dev):
+    """Per-device fp32 workspace for the wgrad split-K partials (irgan_conv_wgrad_ws):
+    plain-store slabs + an ordered reduce instead of fp32 atomics into dw."""
+    w = _WGRAD_WS.get(dev)
+    if w is None:
+        w = _WGRAD_WS[dev] = torch.empty(WGRAD_WS_FLOATS, dtype=torch.float32, device=dev)
+    return w
 
 
 # ----------------------------------------------------------------------------

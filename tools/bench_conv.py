@@ -50,7 +50,7 @@ for name, cin, cout, k, s, p, mode, H in CASES:
     res[name] = {}
     for k2 in args.which.split(","):
         if k2 == "wgrad":
-            for sk in (int(s) for s in args.splitk.split(",")):
+            for sk in (int(s) for s in args.splitk.split(",")):  # noqa: B007
                 v = t(lambda: ops.conv_wgrad(spec, ops.Feat(x), ops.Feat(dy), dw, ops.BF16, splitk=sk), args.iters)
                 res[name][k2 if sk == 0 else f"wgrad@{sk}"] = (round(v, 4), round(flop / v / 1e9, 1))
             continue
