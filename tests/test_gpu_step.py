@@ -178,3 +178,26 @@ def test_generator_module_api_and_checkpoint_layout(tmp_path):
             continue
         err = float((p.grad.cpu() - Gr[k].grad).norm() / Gr[k].grad.norm().clamp_min(1e-12))
         assert err < 5e-3, (k, err)
+
+
+def test_kaist_native_resolution_512x640():
+    """BASELINE config 4 shape (512x640, KAIST native): W/4 = 160 is not a
+    multiple of 64, so the wgrad row-segment kernel and several tile paths take
+    their general branches.  G forward (fp32) vs the CPU oracle, and a bf16
+    train step at batch 4 vs the fp32 step on the same inputs and weights."""
+    fx = load_golden("s32")
+    g = torch.Generator().manual_seed(21)
+    ir = torch.rand(4, 1, 512, 640, generator=g) * 2 - 1
+    rgb = torch.rand(4, 3, 512, 640, generator=g) * 2 - 1
+    tr32, _ = make_trainer(fx, "fp32")
+    fake = tr32.netG.engine.forward(ir[:1].to(DEV))          # NHWC fp32
+    G = O.seeded_params(O.g_param_shapes(), 1, bias_std=0.02)
+    with torch.no_grad():
+        ref = O.g_forward(G, ir[:1])
+    assert float((fake.cpu().permute(0, 3, 1, 2) - ref).abs().max()) < 1e-4
+    l32 = tr32.losses(tr32.step(ir.to(DEV), rgb.to(DEV)))
+    tr16, _ = make_trainer(fx, "bf16")
+    l16 = tr16.losses(tr16.step(ir.to(DEV), rgb.to(DEV)))
+    for k in ("loss_D", "loss_G", "loss_G_L1", "loss_G_perc", "loss_G_ssim"):
+        assert np.isfinite(l16[k]) and np.isfinite(l32[k]), k
+        assert abs(l16[k] - l32[k]) <= 3e-2 * max(1.0, abs(l32[k])), (k, l16[k], l32[k])
