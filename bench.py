@@ -68,7 +68,7 @@ def cpu_baseline(H, W, batch=1, budget_s=20.0):
         O.train_step(G, D, V, ir, rgb, oG, oD)
         n += 1
         el = time.perf_counter() - t0
-        if el >= budget_s or n >= 20:
+        if el >= budget_s or n >= 60:
             break
     return {"value": round(n * batch / el, 4), "unit": "img/s", "cores": threads, "kind": "port",
             "sample": f"{n} oracle steps of batch {batch} at {H}x{W} fp32 after 1 warm-up ({el:.1f}s, "

@@ -55,22 +55,28 @@ IRGAN_HD void phase_barrier() {
 IRGAN_HD void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 constexpr int PH = 16, PW = 16;   // output patch
-constexpr int BN = 256;           // output channels per block
 constexpr int HPMAX = 46;         // halo pieces (8 rows of 128 B) for taps up to 4x4: 19*19 = 361 rows
-constexpr int HBYTES = HPMAX * 1024, BBYTES = BN * 128;
-constexpr int LDS = 2 * HBYTES + 2 * BBYTES;
-constexpr int MI = 8, NJ = 4;     // wave tile 128 pixels x 64 channels
-constexpr int WU = BBYTES / 1024 / 8;  // weight pieces per wave per K-step (4)
-constexpr int RSB = BN * 2 + 16;  // bf16 staging row (pixel) stride, bytes
-constexpr int RSF = BN + 4;       // fp32 staging row stride, floats
-static_assert(256 * RSB <= LDS && 128 * RSF * 4 <= LDS, "epilogue staging fits");
+constexpr int HBYTES = HPMAX * 1024;
+constexpr int MI = 8;             // wave tile: 128 pixels x BN/4 channels (NJ fragments)
+// per output-channel tile BN (256: resblock / D / VGG conv3; 128: down1, up1, VGG conv2)
+template <int BN>
+struct PP {
+    static constexpr int BBYTES = BN * 128;
+    static constexpr int LDS = 2 * HBYTES + 2 * BBYTES;
+    static constexpr int NJ = BN / 64;                 // 16-channel fragments per wave
+    static constexpr int WU = BBYTES / 1024 / 8;       // weight pieces per wave per K-step
+    static constexpr int RSB = BN * 2 + 16;            // bf16 staging row (pixel) stride, bytes
+    static constexpr int LPP = BN / 8;                 // epilogue lanes per pixel row (8 channels each)
+    static_assert(256 * RSB <= LDS, "epilogue staging fits");
+};
 
-template <int KH, int KW>
+template <int KH, int KW, int BN>
 __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
                                                          const bf16_t* __restrict__ w, const float* __restrict__ bias,
                                                          void* __restrict__ y, const void* __restrict__ mask,
                                                          int ntn, int tpx, int tpy, int swz) {
     constexpr int TAPS = KH * KW, HWd = PW + KW - 1, HROWS = (PH + KH - 1) * HWd, HP = (HROWS + 7) / 8;
+    constexpr int BBYTES = PP<BN>::BBYTES, LDS = PP<BN>::LDS, NJ = PP<BN>::NJ, WU = PP<BN>::WU, RSB = PP<BN>::RSB;
     static_assert(HP <= HPMAX && HP > 40 && TAPS >= 2, "halo pieces per wave are 5 or 6");
     __shared__ __attribute__((aligned(1024))) char smem[LDS];
     char* const sH = smem;
@@ -158,7 +164,7 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
     // so with the tap loop unrolled an A address is tsw[K & 7] + hb plus the
     // ds_read immediate K * 128: one VALU add per fragment read.
     const int arow0 = grp * MI * HWd + (lane & 15);  // halo row of fragment 0 at tap (0,0)
-    const int brow0 = wn * 64 + (lane & 15);         // weight row of fragment 0 (rows +16j share the XOR)
+    const int brow0 = wn * (BN / 4) + (lane & 15);   // weight row of fragment 0 (rows +16j share the XOR)
     const int bb0 = lds_off(brow0, lane >> 4), bb1 = lds_off(brow0, 4 + (lane >> 4));
     int tsw[8];  // h = 1 flips chunk bit 2: tsw ^ 64 (v_xad_u32)
 #pragma unroll
@@ -218,7 +224,7 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
 
     // ---- epilogue.  Fragment (i, j): pixel m = (grp*8 + i)*16 + (lane & 15),
     // channels co = n0 + wn*64 + j*16 + 4*(lane >> 4) + r, r = 0..3.
-    const int cl0 = wn * 64 + 4 * (lane >> 4);  // block-local channel of r = 0, j = 0
+    const int cl0 = wn * (BN / 4) + 4 * (lane >> 4);  // block-local channel of r = 0, j = 0
     float4 b4[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
@@ -299,10 +305,11 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
     }
     if (out_f32) return;
     __syncthreads();
-    const int c8 = (tid & 31) * 8, co8 = n0 + c8;
+    constexpr int LPP = PP<BN>::LPP;
+    const int c8 = (tid % LPP) * 8, co8 = n0 + c8;
     if (co8 >= d.Cout) return;
     const bool vec = co8 + 8 <= d.Cout && d.ldy % 8 == 0 && d.yoff % 8 == 0;
-    for (int m = tid >> 5; m < 256; m += 16) {
+    for (int m = tid / LPP; m < 256; m += 512 / LPP) {
         const long pix = pix_of(m);
         if (pix < 0) continue;
         bf16_t* yp = (bf16_t*)y + pix * d.ldy + d.yoff + co8;
@@ -315,12 +322,12 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
     }
 }
 
-template <int KH, int KW>
+template <int KH, int KW, int BN>
 void launch_pp(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y, const void* mask,
                hipStream_t st, int swz) {
     const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH);
     const int ntn = irgan_cdiv(d->Cout, BN);
-    conv_pp_kernel<KH, KW><<<d->N * tpy * tpx * ntn, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, y,
+    conv_pp_kernel<KH, KW, BN><<<d->N * tpy * tpx * ntn, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, y,
                                                                   mask, ntn, tpx, tpy, swz);
 }
 
@@ -330,13 +337,20 @@ extern "C" int irgan_conv_fwd_pp(const irgan_conv_desc* d, const void* x, const 
                                  const void* mask, hipStream_t st) {
     if ((long)d->N * d->Ho * d->Wo <= 0 || d->Cout <= 0) return 0;
     const bool k33 = d->KH == 3 && d->KW == 3, k44 = d->KH == 4 && d->KW == 4;
-    if (d->dtype != IRGAN_BF16 || d->act == IRGAN_ACT_TANH || d->sy != 1 || d->sx != 1 || d->Cin % 64 || !(k33 || k44) || d->Cout % 256 ||
+    if (d->dtype != IRGAN_BF16 || d->act == IRGAN_ACT_TANH || d->sy != 1 || d->sx != 1 || d->Cin % 64 || !(k33 || k44) || d->Cout % 128 ||
         d->ldx % 8 || d->xoff % 8 || (long)d->N * d->H * d->W * d->ldx >= (1L << 30) ||
         (long)d->Cout * d->KH * d->KW * d->Cin >= (1L << 30))
         return IRGAN_EUNSUPPORTED;
     static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
-    if (k33) launch_pp<3, 3>(d, x, w, bias, y, mask, st, swz);
-    else launch_pp<4, 4>(d, x, w, bias, y, mask, st, swz);
+    static const bool pp128 = !getenv("IRGAN_NO_PP128");
+    if (d->Cout % 256 == 0) {
+        if (k33) launch_pp<3, 3, 256>(d, x, w, bias, y, mask, st, swz);
+        else launch_pp<4, 4, 256>(d, x, w, bias, y, mask, st, swz);
+    } else {
+        if (!pp128) return IRGAN_EUNSUPPORTED;
+        if (k33) launch_pp<3, 3, 128>(d, x, w, bias, y, mask, st, swz);
+        else launch_pp<4, 4, 128>(d, x, w, bias, y, mask, st, swz);
+    }
     IRGAN_LAUNCH_CHECK();
     return 0;
 }
