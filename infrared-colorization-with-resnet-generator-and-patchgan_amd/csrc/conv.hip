@@ -487,7 +487,7 @@ int launch_fwd(const irgan_conv_desc* d, const void* x, const void* w, const flo
         static const bool use_halo = !getenv("IRGAN_NO_HALO");
         const int taps = d->KH * d->KW;
         static const bool use_pp = !getenv("IRGAN_NO_PP");
-        if (fast && use_pp && d->sy == 1 && d->sx == 1 && taps >= 2 && d->Cout % 128 == 0) {
+        if (fast && use_pp && d->sy == 1 && d->sx == 1 && taps >= 2 && d->Cout % 64 == 0) {
             const int rc = irgan_conv_fwd_pp(d, x, w, bias, y, mask, st);
             if (rc != IRGAN_EUNSUPPORTED) return rc;
         }

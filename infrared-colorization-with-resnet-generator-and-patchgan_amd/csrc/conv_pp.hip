@@ -67,7 +67,8 @@ struct PP {
     static constexpr int WU = BBYTES / 1024 / 8;       // weight pieces per wave per K-step
     static constexpr int RSB = BN * 2 + 16;            // bf16 staging row (pixel) stride, bytes
     static constexpr int LPP = BN / 8;                 // epilogue lanes per pixel row (8 channels each)
-    static_assert(256 * RSB <= LDS, "epilogue staging fits");
+    static constexpr int PPASS = 512 / LPP;            // pixel rows stored per pass (BN = 192: 21, lanes 504+ idle)
+    static_assert(256 * RSB <= LDS && BN % 64 == 0 && WU * 8 * 1024 == BBYTES, "tile");
 };
 
 template <int KH, int KW, int BN>
@@ -306,10 +307,12 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
     if (out_f32) return;
     __syncthreads();
     constexpr int LPP = PP<BN>::LPP;
+    constexpr int PPASS = PP<BN>::PPASS;
+    if (tid >= PPASS * LPP) return;
     const int c8 = (tid % LPP) * 8, co8 = n0 + c8;
     if (co8 >= d.Cout) return;
     const bool vec = co8 + 8 <= d.Cout && d.ldy % 8 == 0 && d.yoff % 8 == 0;
-    for (int m = tid / LPP; m < 256; m += 512 / LPP) {
+    for (int m = tid / LPP; m < 256; m += PPASS) {
         const long pix = pix_of(m);
         if (pix < 0) continue;
         bf16_t* yp = (bf16_t*)y + pix * d.ldy + d.yoff + co8;
@@ -337,19 +340,30 @@ extern "C" int irgan_conv_fwd_pp(const irgan_conv_desc* d, const void* x, const 
                                  const void* mask, hipStream_t st) {
     if ((long)d->N * d->Ho * d->Wo <= 0 || d->Cout <= 0) return 0;
     const bool k33 = d->KH == 3 && d->KW == 3, k44 = d->KH == 4 && d->KW == 4;
-    if (d->dtype != IRGAN_BF16 || d->act == IRGAN_ACT_TANH || d->sy != 1 || d->sx != 1 || d->Cin % 64 || !(k33 || k44) || d->Cout % 128 ||
+    if (d->dtype != IRGAN_BF16 || d->act == IRGAN_ACT_TANH || d->sy != 1 || d->sx != 1 || d->Cin % 64 || !(k33 || k44) || d->Cout % 64 ||
         d->ldx % 8 || d->xoff % 8 || (long)d->N * d->H * d->W * d->ldx >= (1L << 30) ||
         (long)d->Cout * d->KH * d->KW * d->Cin >= (1L << 30))
         return IRGAN_EUNSUPPORTED;
     static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
     static const bool pp128 = !getenv("IRGAN_NO_PP128");
+    // measured (profiles/r01_s7_pp_ab.txt): up2 dgrad (Cout 192) 539 -> 351 us, Cout-64 layers +6 %
+    static const bool pp192 = !getenv("IRGAN_NO_PP192");
+    static const bool pp64 = !getenv("IRGAN_NO_PP64");
     if (d->Cout % 256 == 0) {
         if (k33) launch_pp<3, 3, 256>(d, x, w, bias, y, mask, st, swz);
         else launch_pp<4, 4, 256>(d, x, w, bias, y, mask, st, swz);
-    } else {
+    } else if (d->Cout % 128 == 0) {
         if (!pp128) return IRGAN_EUNSUPPORTED;
         if (k33) launch_pp<3, 3, 128>(d, x, w, bias, y, mask, st, swz);
         else launch_pp<4, 4, 128>(d, x, w, bias, y, mask, st, swz);
+    } else if (d->Cout == 192) {  // up2_conv backward-data (dx = [up | skip] = 128 + 64 channels)
+        if (!pp192) return IRGAN_EUNSUPPORTED;
+        if (k33) launch_pp<3, 3, 192>(d, x, w, bias, y, mask, st, swz);
+        else launch_pp<4, 4, 192>(d, x, w, bias, y, mask, st, swz);
+    } else {
+        if (!pp64) return IRGAN_EUNSUPPORTED;
+        if (k33) launch_pp<3, 3, 64>(d, x, w, bias, y, mask, st, swz);
+        else launch_pp<4, 4, 64>(d, x, w, bias, y, mask, st, swz);
     }
     IRGAN_LAUNCH_CHECK();
     return 0;
