@@ -99,6 +99,16 @@ int irgan_weight_pack(const float* src, void* dst, int32_t dtype, int32_t Cout, 
                       int32_t Ay, int32_t txr, int32_t Ax, int32_t cpad, int32_t kalign,
                       irgan_stream_t st);
 
+/* One weight re-pack job (the arguments of irgan_weight_pack as a POD record). */
+typedef struct irgan_pack_desc {
+    const float* src;
+    void* dst;
+    int32_t dtype, Cout, KH, KW, Cin, transpose, s, tyr, Ay, txr, Ax, cpad, kalign, reserved;
+} irgan_pack_desc;
+/* n irgan_weight_pack jobs in ONE launch (a network's post-Adam re-pack: ~50
+ * small launches -> 1).  descs: device array of n records. */
+int irgan_weight_pack_batch(const irgan_pack_desc* descs, int32_t n, irgan_stream_t st);
+
 /* ---- InstanceNorm (ir:154-165), per-(n,c) over H*W, eps 1e-5, no affine ---- */
 /* Reductions are two-level and atomic-free: <= IRGAN_IN_PARTS block partials per
  * (n, c) summed in fp64 in a fixed order. */

@@ -474,6 +474,34 @@ __global__ void weight_pack_kernel(const float* __restrict__ src, T* __restrict_
     }
 }
 
+// irgan_weight_pack_batch: block row y serves descs[y] (grid-stride over its R x Kp)
+__global__ __launch_bounds__(256) void weight_pack_batch_kernel(const irgan_pack_desc* __restrict__ descs) {
+    const irgan_pack_desc q = descs[blockIdx.y];
+    const int R = q.transpose ? q.Cin : q.Cout;
+    const int taps = q.transpose ? q.Ay * q.Ax : q.KH * q.KW;
+    const int Cr = q.transpose ? q.Cout : q.Cin;
+    const int Cp = q.cpad > Cr ? q.cpad : Cr;
+    const int ka = q.kalign > 0 ? q.kalign : 1;
+    const int Kp = (taps * Cp + ka - 1) / ka * ka;
+    const long total = (long)R * Kp;
+    for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
+        const int row = (int)(idx / Kp), k = (int)(idx - (long)row * Kp);
+        const int tap = k / Cp, c = k - tap * Cp;
+        float v = 0.f;
+        if (tap < taps && c < Cr) {
+            if (!q.transpose) {
+                v = q.src[((long)row * q.KH * q.KW + tap) * q.Cin + c];
+            } else {
+                const int a = tap / q.Ax, b = tap - a * q.Ax;
+                const int ky = q.tyr + q.s * (q.Ay - 1 - a), kx = q.txr + q.s * (q.Ax - 1 - b);
+                v = q.src[(((long)c * q.KH + ky) * q.KW + kx) * q.Cin + row];
+            }
+        }
+        if (q.dtype == IRGAN_BF16) ((bf16_t*)q.dst)[idx] = f2bf(v);
+        else ((float*)q.dst)[idx] = v;
+    }
+}
+
 template <typename T>
 int launch_fwd(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
                const void* mask, hipStream_t st) {
@@ -610,6 +638,14 @@ extern "C" int irgan_weight_pack(const float* src, void* dst, int32_t dtype, int
     else
         weight_pack_kernel<float><<<blocks, 256, 0, (hipStream_t)st>>>(src, (float*)dst, Cout, KH, KW, Cin,
                                                                          transpose, s, tyr, Ay, txr, Ax, Cp, Kp);
+    IRGAN_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int irgan_weight_pack_batch(const irgan_pack_desc* descs, int32_t n, irgan_stream_t st) {
+    if (n <= 0) return 0;
+    if (!descs || n > 65535) return IRGAN_EINVAL;
+    weight_pack_batch_kernel<<<dim3(128, n), 256, 0, (hipStream_t)st>>>(descs);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }

@@ -206,6 +206,8 @@ class INLayer:
 # ----------------------------------------------------------------------------
 
 class GeneratorEngine:
+    _pack_batch = None  # ops.PackBatch of self.packs, built on the first pack()
+
     def __init__(self, store: ParamStore, dtype=BF16, ngf=64, input_nc=1, output_nc=3, n_blocks=9,
                  no_antialias=False, no_antialias_up=False):
         self.store, self.dtype, self.ngf = store, dtype, ngf
@@ -238,8 +240,9 @@ class GeneratorEngine:
         self.shape = None
 
     def pack(self):
-        for p in self.packs:
-            p.pack()
+        if self._pack_batch is None:
+            self._pack_batch = ops.PackBatch(self.packs)
+        self._pack_batch.run()
 
     # -- shapes
     def _dims(self, H, W):
@@ -429,6 +432,8 @@ class GeneratorEngine:
 # ----------------------------------------------------------------------------
 
 class DiscriminatorEngine:
+    _pack_batch = None  # ops.PackBatch of self.packs, built on the first pack()
+
     LAYERS = (("model.0", 2, False), ("model.2", 2, True), ("model.5", 2, True), ("model.8", 1, True),
               ("model.11", 1, False))
 
@@ -442,8 +447,9 @@ class DiscriminatorEngine:
         self.bufs = Buffers(store.device)
 
     def pack(self):
-        for p in self.packs:
-            p.pack()
+        if self._pack_batch is None:
+            self._pack_batch = ops.PackBatch(self.packs)
+        self._pack_batch.run()
 
     def forward(self, din: Feat, tag="") -> torch.Tensor:
         """din: NHWC (NB, H, W, 4) compute-dtype -> patch logits (NB, h, w, 1) fp32."""
@@ -510,6 +516,8 @@ class DiscriminatorEngine:
 # ----------------------------------------------------------------------------
 
 class VGGEngine:
+    _pack_batch = None  # ops.PackBatch of self.packs, built on the first pack()
+
     def __init__(self, store: ParamStore, dtype=BF16):
         self.store, self.dtype, self.tdt = store, dtype, ops.TORCH_DT[dtype]
         self.packs = [_pc(store, str(i), ConvSpec(ci, co, 3, 1, 1, PAD_ZERO), dtype) for i, ci, co in VGG_CONVS]
@@ -522,8 +530,9 @@ class VGGEngine:
         self.bufs = Buffers(dev)
 
     def pack(self):
-        for p in self.packs:
-            p.pack()
+        if self._pack_batch is None:
+            self._pack_batch = ops.PackBatch(self.packs)
+        self._pack_batch.run()
 
     def forward(self, vin: Feat) -> Feat:
         g, T = self.bufs, self.tdt

@@ -174,6 +174,17 @@ class PackedConv:
                     buf = torch.empty(spec.cin * kd, dtype=tdt, device=dev)
                     self.dg.append(((py, tyr, ay, c0y), (px, txr, ax, c0x), buf))
 
+    def jobs(self):
+        """The weight_pack jobs of this layer as irgan_pack_desc records."""
+        s, out = self.spec, []
+        if self.dtype != F32:
+            out.append(PackDesc(self.master.data_ptr(), self.fwd.data_ptr(), dt_code(self.fwd), s.cout, s.k, s.k,
+                                s.cin, 0, 1, 0, 0, 0, 0, self.cin_eff, self.kalign, 0))
+        for (py, tyr, ay, _), (px, txr, ax, _), buf in self.dg:
+            out.append(PackDesc(self.master.data_ptr(), buf.data_ptr(), dt_code(buf), s.cout, s.k, s.k, s.cin, 1,
+                                s.stride, tyr, ay, txr, ax, self.cout_eff, self.kalign, 0))
+        return out
+
     def pack(self):
         s = self.spec
         if self.dtype != F32:
@@ -181,6 +192,33 @@ class PackedConv:
         for (py, tyr, ay, _), (px, txr, ax, _), buf in self.dg:
             weight_pack(self.master, buf, s.cout, s.k, s.k, s.cin, 1, s.stride, tyr, ay, txr, ax,
                         cpad=self.cout_eff, kalign=self.kalign)
+
+
+class PackDesc(ctypes.Structure):
+    """irgan_pack_desc (include/irgan.h)."""
+    _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p)] + [
+        (n, ctypes.c_int32) for n in "dtype Cout KH KW Cin transpose s tyr Ay txr Ax cpad kalign reserved".split()]
+
+
+class PackBatch:
+    """All re-pack jobs of a set of layers as ONE irgan_weight_pack_batch launch.
+    The descriptor table lives on the device; it is rebuilt only if a packed
+    buffer moved (buffers are allocated once, so normally never)."""
+
+    def __init__(self, packs):
+        self.packs = list(packs)
+        self.key, self.table, self.n = None, None, 0
+
+    def run(self):
+        jobs = [j for p in self.packs for j in p.jobs()]
+        key = tuple((j.src, j.dst) for j in jobs)
+        if key != self.key:
+            arr = (PackDesc * len(jobs))(*jobs)
+            raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+            self.table = raw.to(self.packs[0].master.device)
+            self.key, self.n = key, len(jobs)
+        if self.n:
+            _lib.call("irgan_weight_pack_batch", P(self.table), self.n, stream())
 
 
 def conv_fwd(pc: PackedConv, x: Feat, y: Feat, act=ACT_NONE, bias=True, accumulate=False, mask: Feat = None,

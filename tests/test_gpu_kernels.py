@@ -270,3 +270,27 @@ def test_adam_matches_torch(ops):
         opt.step()
         ops.adam(pd, gr.to(DEV), m, v, i + 1, 2e-4, 0.5, 0.999, 1e-8)
     assert float((pd.cpu() - pt.detach()).abs().max()) < 5e-7  # a few fp32 ulps of |p|~2
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_weight_pack_batch_matches_single_packs(ops, dtype):
+    """irgan_weight_pack_batch (one launch) == one irgan_weight_pack per job:
+    plain, narrow-padded, stride-2 per-phase and reflect-flipped packs."""
+    code = ops.F32 if dtype == "f32" else ops.BF16
+    torch.manual_seed(5)
+    specs = [ops.ConvSpec(64, 128, 3, 1, 1, 0), ops.ConvSpec(1, 64, 7, 1, 3, 1), ops.ConvSpec(128, 256, 4, 2, 1, 0),
+             ops.ConvSpec(256, 256, 3, 1, 1, 1), ops.ConvSpec(64, 3, 7, 1, 3, 1)]
+    pcs = [ops.PackedConv(s, torch.randn(s.cout * s.k * s.k * s.cin, device=DEV), None, code) for s in specs]
+    for pc in pcs:
+        pc.pack()
+    single = [[t.clone() for t in ([pc.fwd] if code == ops.BF16 else []) + [b for *_, b in pc.dg]] for pc in pcs]
+    for pc in pcs:
+        if code == ops.BF16:
+            pc.fwd.zero_()
+        for *_, b in pc.dg:
+            b.zero_()
+    ops.PackBatch(pcs).run()
+    for pc, ref in zip(pcs, single):
+        got = ([pc.fwd] if code == ops.BF16 else []) + [b for *_, b in pc.dg]
+        for g, r in zip(got, ref):
+            assert torch.equal(g, r)
