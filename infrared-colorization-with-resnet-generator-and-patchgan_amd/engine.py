@@ -330,8 +330,13 @@ class GeneratorEngine:
         ops.conv_fwd(self.outc, a4, Feat(fake), act=ACT_TANH)
         return fake
 
-    def backward(self, dfake: torch.Tensor):
-        """dfake: dL/dfake, NHWC fp32 (B,H,W,3).  Accumulates into store.grad."""
+    def backward(self, dfake: torch.Tensor, ready=None):
+        """dfake: dL/dfake, NHWC fp32 (B,H,W,3).  Accumulates into store.grad.
+
+        ``ready(key)``, if given, is called each time every gradient from parameter
+        ``key`` to the end of the flat buffer is final (reverse layer order), so the
+        caller can start reducing that tail while the rest of the backward runs."""
+        ready = ready or (lambda key: None)
         B, H, W = self.shape
         g, T, S, dt = self.bufs, self.tdt, self.store, self.dtype
         c0, c1, c2 = self.ngf, 2 * self.ngf, 4 * self.ngf
@@ -384,6 +389,7 @@ class GeneratorEngine:
             ops.conv_fwd(self.up1_up, dy1, dh, bias=False)
         else:
             ops.upsample_bwd(dy1, dh)
+        ready("up1_up.weight" if self.no_aa_up else "up1_conv.0.weight")
         # resblocks, reversed: dh holds d h_{b+1}; becomes d h_b in place
         dt_ = Feat(g.get("dtmp", (B, H2, W2, c2), T))
         for b in reversed(range(self.n_blocks)):
@@ -398,6 +404,7 @@ class GeneratorEngine:
             self.norms[f"r{b}_1"].bwd(g, dr, r1, ACT_RELU, dr, db=S.krsc(key + "1.bias", G))
             wg(p1, key + "1", hb, dr)
             ops.conv_dgrad(p1, dr, dh, accumulate=True, pad_buf=padbuf)
+            ready(key + "1.weight")
         # down2 (+ blur-down)
         z2 = Feat(g.d["z2"])
         if self.no_aa:
@@ -425,6 +432,7 @@ class GeneratorEngine:
         # inc
         self.norms["inc"].bwd(g, dx0, Feat(g.d["z0"]), ACT_RELU, dx0, db=S.krsc("inc.1.bias", G))
         wg(self.inc, "inc.1", Feat(g.d["ir"]), dx0)
+        ready("inc.1.weight")
 
 
 # ----------------------------------------------------------------------------
@@ -609,6 +617,64 @@ def grad_allreduce(t: torch.Tensor, group=None) -> torch.Tensor:
     return t
 
 
+class BucketedAllreduce:
+    """Mean of a flat gradient buffer over the ranks, reduced tail-first in buckets
+    while the producing backward is still running (SURVEY.md 8e overlap schedule).
+
+    The backward calls ``ready(key)`` when every grad from ``key`` to the end of the
+    flat buffer is final.  Once the not-yet-reduced tail reaches ``bucket_bytes`` it
+    is handed to the collective with ``async_op=True``: RCCL runs it on its own
+    stream after an event on the compute stream, so the all-reduce of layer L
+    overlaps the backward of layers < L.  ``finish()`` reduces the remainder and
+    makes the compute stream wait for every bucket (Adam reads the result).
+    Buckets are contiguous slices of the flat buffer, so the reduction is the
+    same element-wise mean as one whole-buffer all-reduce.
+    """
+
+    def __init__(self, store: ParamStore, group=None, bucket_bytes=8 << 20):
+        self.store, self.group, self.bucket_bytes = store, group, bucket_bytes
+        self.end, self.works, self.world, self.avg = store.numel, [], 1, True
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            self.world = dist.get_world_size(group)
+            self.avg = dist.get_backend(group) == "nccl"
+
+    @property
+    def active(self):
+        return self.world > 1
+
+    def _launch(self, start):
+        import torch.distributed as dist
+        if start >= self.end:
+            return
+        t = self.store.grad[start:self.end]
+        op = dist.ReduceOp.AVG if self.avg else dist.ReduceOp.SUM
+        self.works.append((dist.all_reduce(t, op=op, group=self.group, async_op=True), t))
+        self.end = start
+
+    def start(self):
+        """Reduce the whole buffer as one asynchronous collective."""
+        if self.active:
+            self._launch(0)
+
+    def ready(self, key):
+        if not self.active:
+            return
+        start = self.store.offsets[key]
+        if (self.end - start) * 4 >= self.bucket_bytes:
+            self._launch(start)
+
+    def finish(self):
+        if not self.active:
+            return
+        self._launch(0)
+        for w, t in self.works:
+            w.wait()
+            if not self.avg:
+                t.div_(self.world)
+        self.works, self.end = [], self.store.numel
+
+
 class GANStep:
     """Buffers, engines and the fused step for one rank.
 
@@ -626,13 +692,12 @@ class GANStep:
         self.bufs = Buffers(G.device)
         self.losses = torch.zeros(8, dtype=torch.float64, device=G.device)
         self.pg = process_group
+        self.g_reduce = BucketedAllreduce(G, process_group)
+        self.d_reduce = BucketedAllreduce(D, process_group)
         self.lr_scale = 1.0
         self.vgg.pack()
         self.gen.pack()
         self.dis.pack()
-
-    def _allreduce(self, t):
-        grad_allreduce(t, self.pg)
 
     def _din(self, ir_t: Feat, img: torch.Tensor, out: Feat):
         """cat([ir, img], 1) (ir:1639-1640) written straight into the NHWC D input."""
@@ -662,20 +727,12 @@ class GANStep:
         dpred = b.get("dpred", tuple(pred.shape), torch.float32)
         ops.hinge(pred, pred[:B].numel(), 0, 1.0, dpred, L[0:1])
         self.dis.backward(dpred, want_wgrad=True, want_dinput=False, tag="d")
-        self._allreduce(self.D.grad)
-        self.D.adam_step(cfg.lr_D * self.lr_scale, cfg.beta1, cfg.beta2)
-        self.dis.pack()
-        # ---- G step (ir:1656-1681)
+        self.d_reduce.start()
+        # ---- G step (ir:1656-1681).  The terms that do not read D (L1, VGG, TV, SSIM)
+        # go first so they overlap the D-grad all-reduce; the GAN term follows D Adam.
         self.G.zero_grad()
         dfake = b.get("dfake", (B, H, W, cout), torch.float32)
         dfake.zero_()
-        dinf = Feat(b.zeros("din1", (B, H, W, dpad), T), 0, self.dis.packs[0].cin_eff)
-        self._din(ir_t, fake, dinf)
-        predg = self.dis.forward(dinf, tag="g")
-        dpg = b.get("dpredg", tuple(predg.shape), torch.float32)
-        ops.hinge(predg, predg.numel(), 1, cfg.lambda_gan, dpg, L[1:2])
-        dd = self.dis.backward(dpg, want_wgrad=False, want_dinput=True, tag="g")
-        ops.axpby(dd.sl(cin, cout), 1.0, Feat(dfake), 1.0)
         ops.l1(fake, rgb_h, cfg.lambda_L1, dfake, L[2:3], accumulate=True)
         # perceptual: VGG on [fake; rgb] as one 2B batch (ir:1667-1669)
         vin = Feat(b.zeros("vin", (2 * B, H, W, max(8, cout)), T), 0, self.vgg.packs[0].cin_eff)
@@ -689,8 +746,19 @@ class GANStep:
         ops.tv(Feat(fake), cfg.lambda_tv, dfake, L[4:5])
         ssim_work = b.flat("ssim_work", 10 * fake.numel())
         ops.ssim(Feat(fake), Feat(rgb_h), cfg.lambda_ssim, dfake, L[5:6], ssim_work)
-        self.gen.backward(dfake)
-        self._allreduce(self.G.grad)
+        self.d_reduce.finish()
+        self.D.adam_step(cfg.lr_D * self.lr_scale, cfg.beta1, cfg.beta2)
+        self.dis.pack()
+        # GAN term through the updated D (ir:1659-1662)
+        dinf = Feat(b.zeros("din1", (B, H, W, dpad), T), 0, self.dis.packs[0].cin_eff)
+        self._din(ir_t, fake, dinf)
+        predg = self.dis.forward(dinf, tag="g")
+        dpg = b.get("dpredg", tuple(predg.shape), torch.float32)
+        ops.hinge(predg, predg.numel(), 1, cfg.lambda_gan, dpg, L[1:2])
+        dd = self.dis.backward(dpg, want_wgrad=False, want_dinput=True, tag="g")
+        ops.axpby(dd.sl(cin, cout), 1.0, Feat(dfake), 1.0)
+        self.gen.backward(dfake, ready=self.g_reduce.ready)
+        self.g_reduce.finish()
         self.G.adam_step(cfg.lr_G * self.lr_scale, cfg.beta1, cfg.beta2)
         self.gen.pack()
         return L
