@@ -9,7 +9,8 @@
 //  * block tile 256 pixels x 256 output channels, 8 waves = 2 groups x 4 waves;
 //    group g owns patch rows [8g, 8g+8), wave wn owns channels [64wn, 64wn+64):
 //    a 128 x 64 wave tile (8 x 4 fragments of mfma_f32_16x16x32_bf16), so a
-//    32-deep sub-step is 12 ds_read_b128 per 32 MFMAs;
+//    32-deep sub-step is 12 ds_read_b128 per 32 MFMAs (narrower channel tiles
+//    split the group's rows instead, see PP<BN>);
 //  * each sub-step (one tap, 32 channels) is two phases per wave: READ (issue
 //    the 12 fragment reads and this wave's share of the next K-step's DMA) and
 //    MFMA (32 MFMAs), each closed by a block barrier.  Group 1 starts one
@@ -57,27 +58,35 @@ IRGAN_HD void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); 
 constexpr int PH = 16, PW = 16;   // output patch
 constexpr int HPMAX = 46;         // halo pieces (8 rows of 128 B) for taps up to 4x4: 19*19 = 361 rows
 constexpr int HBYTES = HPMAX * 1024;
-constexpr int MI = 8;             // wave tile: 128 pixels x BN/4 channels (NJ fragments)
-// per output-channel tile BN (256: resblock / D / VGG conv3; 128: down1, up1, VGG conv2)
+// per output-channel tile BN (256: resblock / D / VGG conv3; 192: up2 dgrad; 128: down1,
+// up1, VGG conv2; 64: up2, down1 dgrad, VGG conv1_2).  A group's 128 pixels (8 patch rows)
+// x BN channels are split over its 4 waves as RW row bands x CW channel bands; the wave
+// tile is MIW pixel fragments x NJ channel fragments.  Narrow BN splits rows rather than
+// channels, so every wave keeps 4 channel fragments: LDS fragment reads per MFMA are
+// (MIW + NJ) / (MIW * NJ) = 0.375 (BN 256), 0.5 (128), 0.75 (64) instead of
+// 0.625 / 1.125 with 128-pixel wave tiles.
 template <int BN>
 struct PP {
     static constexpr int BBYTES = BN * 128;
     static constexpr int LDS = 2 * HBYTES + 2 * BBYTES;
-    static constexpr int NJ = BN / 64;                 // 16-channel fragments per wave
+    static constexpr int MIW = BN >= 192 ? 8 : (BN == 128 ? 4 : 2);  // pixel fragments (patch rows) per wave
+    static constexpr int RW = 8 / MIW, CW = 4 / RW;
+    static constexpr int NJ = BN / 16 / CW;            // 16-channel fragments per wave
     static constexpr int WU = BBYTES / 1024 / 8;       // weight pieces per wave per K-step
     static constexpr int RSB = BN * 2 + 16;            // bf16 staging row (pixel) stride, bytes
     static constexpr int LPP = BN / 8;                 // epilogue lanes per pixel row (8 channels each)
     static constexpr int PPASS = 512 / LPP;            // pixel rows stored per pass (BN = 192: 21, lanes 504+ idle)
-    static_assert(256 * RSB <= LDS && BN % 64 == 0 && WU * 8 * 1024 == BBYTES, "tile");
+    static_assert(256 * RSB <= LDS && BN % 64 == 0 && WU * 8 * 1024 == BBYTES && NJ * 16 * CW == BN, "tile");
 };
 
-template <int KH, int KW, int BN>
+template <int KH, int KW, int BN, bool ACC>
 __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
                                                          const bf16_t* __restrict__ w, const float* __restrict__ bias,
                                                          void* __restrict__ y, const void* __restrict__ mask,
                                                          int ntn, int tpx, int tpy, int swz) {
     constexpr int TAPS = KH * KW, HWd = PW + KW - 1, HROWS = (PH + KH - 1) * HWd, HP = (HROWS + 7) / 8;
     constexpr int BBYTES = PP<BN>::BBYTES, LDS = PP<BN>::LDS, NJ = PP<BN>::NJ, WU = PP<BN>::WU, RSB = PP<BN>::RSB;
+    constexpr int MI = PP<BN>::MIW, RW = PP<BN>::RW;
     static_assert(HP <= HPMAX && HP > 40 && TAPS >= 2, "halo pieces per wave are 5 or 6");
     __shared__ __attribute__((aligned(1024))) char smem[LDS];
     char* const sH = smem;
@@ -86,6 +95,8 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int grp = wid >> 2, wn = wid & 3;
+    const int prow = grp * 8 + (wn % RW) * MI;  // first patch row of this wave's pixel fragments
+    const int cb = (wn / RW) * NJ * 16;         // first block-local channel of this wave
     int t = xcd_tile(blockIdx.x, gridDim.x, swz);
     const int nt = t % ntn;
     t /= ntn;
@@ -164,8 +175,8 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
     // lane's row arow0 and lds_off's XOR term depends only on (arow0 + K) & 7,
     // so with the tap loop unrolled an A address is tsw[K & 7] + hb plus the
     // ds_read immediate K * 128: one VALU add per fragment read.
-    const int arow0 = grp * MI * HWd + (lane & 15);  // halo row of fragment 0 at tap (0,0)
-    const int brow0 = wn * (BN / 4) + (lane & 15);   // weight row of fragment 0 (rows +16j share the XOR)
+    const int arow0 = prow * HWd + (lane & 15);  // halo row of fragment 0 at tap (0,0)
+    const int brow0 = cb + (lane & 15);          // weight row of fragment 0 (rows +16j share the XOR)
     const int bb0 = lds_off(brow0, lane >> 4), bb1 = lds_off(brow0, 4 + (lane >> 4));
     int tsw[8];  // h = 1 flips chunk bit 2: tsw ^ 64 (v_xad_u32)
 #pragma unroll
@@ -223,9 +234,9 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
     if (grp == 0) phase_barrier();  // match group 1's extra barrier
     __syncthreads();                // all operand reads done: LDS becomes the staging buffer
 
-    // ---- epilogue.  Fragment (i, j): pixel m = (grp*8 + i)*16 + (lane & 15),
-    // channels co = n0 + wn*64 + j*16 + 4*(lane >> 4) + r, r = 0..3.
-    const int cl0 = wn * (BN / 4) + 4 * (lane >> 4);  // block-local channel of r = 0, j = 0
+    // ---- epilogue.  Fragment (i, j): pixel m = (prow + i)*16 + (lane & 15),
+    // channels co = n0 + cb + j*16 + 4*(lane >> 4) + r, r = 0..3.
+    const int cl0 = cb + 4 * (lane >> 4);  // block-local channel of r = 0, j = 0
     float4 b4[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
@@ -251,12 +262,27 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
     // bf16 output: stage bf16 [256 px][256 ch] in LDS, then 16-byte row stores;
     // fp32 output: 16-byte stores straight from the registers.
     const bool out_f32 = d.out_dtype == IRGAN_F32;
+    // bf16 accumulate (dgrad into a tensor that already holds another branch's
+    // gradient): the 4 old channels of a fragment are one 8-byte load, and a
+    // fragment row's NJ loads are all issued before the row is combined, so the
+    // read latency is paid once per row instead of once per 2-byte element.
+    // (a template flag, so the plain-store kernels keep their register allocation)
+    const bool acc_vec = ACC && !out_f32 && d.ldy % 4 == 0 && d.yoff % 4 == 0;
     auto emit = [&](auto actc) {
         constexpr int A = decltype(actc)::value;
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
-            const int m = (grp * MI + i) * 16 + (lane & 15);
+            const int m = (prow + i) * 16 + (lane & 15);
             const long pix = pix_of(m);
+            uint2 old[NJ];
+            if (acc_vec && pix >= 0) {
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                    const int co = n0 + cl0 + j * 16;
+                    old[j] = co + 4 <= d.Cout ? *(const uint2*)((const bf16_t*)y + pix * d.ldy + d.yoff + co)
+                                              : make_uint2(0u, 0u);
+                }
+            }
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
                 const int cl = cl0 + j * 16, co = n0 + cl;
@@ -276,16 +302,21 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
                     float* yp = (float*)y + pix * d.ldy + d.yoff + co;
                     if (full && ((pix * d.ldy + d.yoff + co) & 3) == 0) {
                         float4 o = make_float4(v[0], v[1], v[2], v[3]);
-                        if (d.accumulate) {
+                        if (ACC) {
                             const float4 p = *(const float4*)yp;
                             o.x += p.x; o.y += p.y; o.z += p.z; o.w += p.w;
                         }
                         *(float4*)yp = o;
                     } else {
-                        for (int r = 0; r < 4 && co + r < d.Cout; ++r) yp[r] = d.accumulate ? yp[r] + v[r] : v[r];
+                        for (int r = 0; r < 4 && co + r < d.Cout; ++r) yp[r] = ACC ? yp[r] + v[r] : v[r];
                     }
                 } else {
-                    if (d.accumulate && pix >= 0) {
+                    if (acc_vec && pix >= 0 && full) {
+                        v[0] += bf2f((bf16_t)(old[j].x & 0xffffu));
+                        v[1] += bf2f((bf16_t)(old[j].x >> 16));
+                        v[2] += bf2f((bf16_t)(old[j].y & 0xffffu));
+                        v[3] += bf2f((bf16_t)(old[j].y >> 16));
+                    } else if (ACC && pix >= 0) {
                         const bf16_t* yp = (const bf16_t*)y + pix * d.ldy + d.yoff + co;
 #pragma unroll
                         for (int r = 0; r < 4; ++r)
@@ -330,8 +361,13 @@ void launch_pp(const irgan_conv_desc* d, const void* x, const void* w, const flo
                hipStream_t st, int swz) {
     const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH);
     const int ntn = irgan_cdiv(d->Cout, BN);
-    conv_pp_kernel<KH, KW, BN><<<d->N * tpy * tpx * ntn, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, y,
-                                                                  mask, ntn, tpx, tpy, swz);
+    const int nb = d->N * tpy * tpx * ntn;
+    if (d->accumulate)
+        conv_pp_kernel<KH, KW, BN, true><<<nb, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, y, mask, ntn,
+                                                             tpx, tpy, swz);
+    else
+        conv_pp_kernel<KH, KW, BN, false><<<nb, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, y, mask, ntn,
+                                                              tpx, tpy, swz);
 }
 
 }  // namespace
