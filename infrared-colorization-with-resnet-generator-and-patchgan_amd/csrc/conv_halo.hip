@@ -184,6 +184,122 @@ void launch_halo(const irgan_conv_desc* d, const void* x, const void* w, const f
         *d, (const bf16_t*)x, (const bf16_t*)w, bias, y, mask, zero, ntn, tpx, tpy, swz);
 }
 
+// ---------------------------------------------------------------------------
+// Narrow output (Cout <= 8: G outc 64->3 7x7, VGG conv1_1 backward-data, D's
+// last 4x4 layer).  The tile-per-tap pipeline above pays a barrier and a weight
+// DMA per K-step for 2 MFMAs per wave; with Cout <= 8 the weights of ALL taps
+// of a 64-channel chunk are only taps x 8 rows x 128 B (<= 49 KiB), so they
+// land in LDS with the halo and the whole chunk (taps x 2 sub-steps) runs
+// without a barrier.  Weight lanes >= 8 of the B fragment are zero registers.
+// 8 waves, wave w = patch rows 2w, 2w+1 (2 pixel fragments), NB halo/weight
+// buffers: 2 for multi-chunk layers (chunk c+1 streams in under chunk c).
+template <int KH, int KW, int HU, int NB>
+__global__ __launch_bounds__(512, 1) void conv_narrow_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
+                                                             const bf16_t* __restrict__ w,
+                                                             const float* __restrict__ bias, void* __restrict__ y,
+                                                             const void* __restrict__ mask,
+                                                             const bf16_t* __restrict__ zero, int tpx, int tpy,
+                                                             int swz) {
+    constexpr int TAPS = KH * KW, HWd = PW + KW - 1, HROWS = (PH + KH - 1) * HWd;
+    constexpr int WPC = (TAPS * 8 + 7) / 8;             // weight pieces (8 rows of 128 B) per chunk
+    constexpr int WPW = (WPC + 7) / 8;                  // weight pieces per wave
+    constexpr int HB = HU * 8 * 1024, BUF = HB + WPC * 1024;
+    static_assert(HU * 64 >= HROWS && NB * BUF <= 160 * 1024 && 256 * 20 * 4 <= NB * BUF, "lds");
+    __shared__ __attribute__((aligned(1024))) char smem[NB * BUF];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int t = xcd_tile(blockIdx.x, gridDim.x, swz);
+    const int pxi = t % tpx;
+    t /= tpx;
+    const int pyi = t % tpy;
+    const int img = t / tpy;
+    const int py0 = pyi * PH, px0 = pxi * PW;
+    const int Kw = TAPS * d.Cin;
+    const int sub = lane >> 3;
+    const int chunk = (lane & 7) ^ sub;
+    const bool reflect = d.pad_mode == IRGAN_PAD_REFLECT;
+
+    long h_off[HU];
+#pragma unroll
+    for (int u = 0; u < HU; ++u) {
+        const int h = (u * 8 + wid) * 8 + sub;
+        const int hy = h / HWd, hx = h - hy * HWd;
+        int iy = py0 + hy + d.c0y, ix = px0 + hx + d.c0x;
+        if (reflect) {
+            iy = reflect_idx(iy, d.H);
+            ix = reflect_idx(ix, d.W);
+        }
+        const bool ok = (h < HROWS) & ((unsigned)iy < (unsigned)d.H) & ((unsigned)ix < (unsigned)d.W);
+        h_off[u] = ok ? (((long)img * d.H + iy) * d.W + ix) * d.ldx + d.xoff + chunk * 8 : -1;
+    }
+    long w_off[WPW];  // weight LDS row r = tap*8 + co
+#pragma unroll
+    for (int v = 0; v < WPW; ++v) {
+        const int r = (v * 8 + wid) * 8 + sub, tp = r >> 3, co = r & 7;
+        w_off[v] = (v * 8 + wid < WPC && tp < TAPS && co < d.Cout) ? (long)co * Kw + tp * d.Cin + chunk * 8 : -1;
+    }
+    auto issue = [&](int c, int buf) {
+        char* base = smem + buf * BUF;
+#pragma unroll
+        for (int u = 0; u < HU; ++u)
+            glds16(h_off[u] >= 0 ? x + h_off[u] + c * 64 : zero, base + (u * 8 + wid) * 1024);
+#pragma unroll
+        for (int v = 0; v < WPW; ++v)
+            if (v * 8 + wid < WPC) glds16(w_off[v] >= 0 ? w + w_off[v] + c * 64 : zero, base + HB + (v * 8 + wid) * 1024);
+    };
+
+    f32x4 acc[2][1];
+    acc[0][0] = acc[1][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int nchunk = d.Cin / 64;
+    const bool wlane = (lane & 15) < 8;
+    issue(0, 0);
+#pragma unroll 1
+    for (int c = 0; c < nchunk; ++c) {
+        wait_vmcnt<0>();
+        lds_barrier();
+        if (NB == 2 && c + 1 < nchunk) issue(c + 1, (c + 1) & 1);
+        const char* Hb = smem + (NB == 2 ? (c & 1) : 0) * BUF;
+        const char* Wb = Hb + HB;
+#pragma unroll 1
+        for (int ty = 0; ty < KH; ++ty)
+#pragma unroll
+        for (int tx = 0; tx < KW; ++tx) {
+            const int tp = ty * KW + tx;
+            const int hrow = (wid * 2 + ty) * HWd + (lane & 15) + tx;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int ch = h * 4 + (lane >> 4);
+                const uint4 a0 = *(const uint4*)(Hb + lds_off(hrow, ch));
+                const uint4 a1 = *(const uint4*)(Hb + lds_off(hrow + HWd, ch));
+                uint4 b = make_uint4(0u, 0u, 0u, 0u);
+                if (wlane) b = *(const uint4*)(Wb + lds_off(tp * 8 + (lane & 15), ch));
+                acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a0),
+                                                                    __builtin_bit_cast(bf16x8_t, b), acc[0][0], 0, 0, 0);
+                acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a1),
+                                                                    __builtin_bit_cast(bf16x8_t, b), acc[1][0], 0, 0, 0);
+            }
+        }
+        if (NB == 1 && c + 1 < nchunk) {
+            lds_barrier();  // every wave is done with the single buffer
+            issue(c + 1, 0);
+        }
+    }
+    conv_epilogue<16, 2, 1, 8, 1, 512>(d, acc, smem, wid, 0, 0, bias, y, mask, [&](int m) -> long {
+        const int oy = py0 + (m >> 4), ox = px0 + (m & 15);
+        if (oy >= d.Ho || ox >= d.Wo) return -1;
+        return ((long)img * d.OH + oy * d.omy + d.ooy) * d.OW + ox * d.omx + d.oox;
+    });
+}
+
+template <int KH, int KW, int HU, int NB>
+void launch_narrow(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
+                   const void* mask, hipStream_t st, const bf16_t* zero, int swz) {
+    const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH);
+    conv_narrow_kernel<KH, KW, HU, NB><<<d->N * tpy * tpx, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias,
+                                                                        y, mask, zero, tpx, tpy, swz);
+}
+
 }  // namespace
 
 // Preconditions (checked by the dispatcher in conv.hip): bf16, sy = sx = 1,
@@ -200,6 +316,12 @@ extern "C" int irgan_conv_fwd_halo(const irgan_conv_desc* d, const void* x, cons
     if (!zero && hipGetSymbolAddress((void**)&zero, HIP_SYMBOL(g_halo_zero_page)) != hipSuccess)
         return IRGAN_EUNSUPPORTED;
     static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
+    static const bool narrow = !getenv("IRGAN_NO_NARROW");
+    if (narrow && d->Cout <= 8) {
+        if (d->KH == 7 && d->KW == 7) { launch_narrow<7, 7, 8, 1>(d, x, w, bias, y, mask, st, zero, swz); IRGAN_LAUNCH_CHECK(); return 0; }
+        if (d->KH == 4 && d->KW == 4) { launch_narrow<4, 4, 6, 2>(d, x, w, bias, y, mask, st, zero, swz); IRGAN_LAUNCH_CHECK(); return 0; }
+        if (d->KH == 3 && d->KW == 3) { launch_narrow<3, 3, 6, 2>(d, x, w, bias, y, mask, st, zero, swz); IRGAN_LAUNCH_CHECK(); return 0; }
+    }
     if (d->Cout > 64) launch_halo<128, 6, 4, 2>(d, x, w, bias, y, mask, st, zero, swz);
     else if (d->Cout > 16) {
         if (big) launch_halo<64, 8, 4, 2>(d, x, w, bias, y, mask, st, zero, swz);

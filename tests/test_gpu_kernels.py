@@ -52,6 +52,8 @@ CONV_CASES = [
     (64, 128, 3, 2, 1, 0, 16),
     (192, 64, 3, 1, 1, 0, 8),
     # multi-patch / ragged-edge cases for the halo kernel (16x16 output patches)
+    (64, 3, 7, 1, 3, 1, 37),      # narrow-Cout kernel: G outc shape, several patches, ragged edge
+    (512, 1, 4, 1, 1, 0, 31),     # narrow-Cout kernel, 8 chunks double-buffered: D's last layer
     (128, 256, 3, 1, 1, 1, 37),
     (64, 64, 3, 1, 1, 0, 40),
     (128, 128, 4, 2, 1, 0, 34),
