@@ -22,6 +22,8 @@ extern "C" int irgan_conv_fwd_pp(const irgan_conv_desc* d, const void* x, const 
                                  const void* mask, hipStream_t st);
 extern "C" int irgan_conv_fwd_halo(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
                                    const void* mask, hipStream_t st);
+extern "C" int irgan_conv_fwd_c8(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
+                                 const void* mask, hipStream_t st);
 extern "C" int irgan_conv_wgrad_halo(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, int splitk,
                                      float* ws, long ws_cap, hipStream_t st);
 extern "C" int irgan_conv_wgrad_glds(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, int splitk,
@@ -521,6 +523,12 @@ int launch_fwd(const irgan_conv_desc* d, const void* x, const void* w, const flo
         }
         if (fast && use_halo && d->sy == 1 && d->sx == 1 && taps >= 2) {
             const int rc = irgan_conv_fwd_halo(d, x, w, bias, y, mask, st);
+            if (rc != IRGAN_EUNSUPPORTED) return rc;
+        }
+        // 8-channel inputs: (tap, channel) flattened into the MFMA K axis (conv_c8.hip)
+        static const bool use_c8 = !getenv("IRGAN_NO_C8");
+        if (narrow && use_c8 && d->Cin == 8) {
+            const int rc = irgan_conv_fwd_c8(d, x, w, bias, y, mask, st);
             if (rc != IRGAN_EUNSUPPORTED) return rc;
         }
         if ((fast || narrow) && use_glds) return irgan_conv_fwd_glds(d, x, w, bias, y, mask, st);

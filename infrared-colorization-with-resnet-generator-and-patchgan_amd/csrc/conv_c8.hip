@@ -1,0 +1,231 @@
+// bf16 stride-1 convolution for 8-channel inputs (the zero-padded narrow layers:
+// G inc 1->64 7x7, G outc backward-data 3->64 7x7, VGG conv1_1 3->64 3x3).
+//
+// With Cin = 8 a tap contributes only 8 of the 32 k-values an
+// mfma_f32_16x16x32_bf16 consumes, so a per-tap K-step wastes 3/4 of the MFMA.
+// Here the K axis is (tap, channel) flattened, exactly the packed weight row
+// [co][tap][8]: one 32-deep K-step covers 4 taps, and lane group g (lane >> 4)
+// of a pixel fragment reads its 8 channels (16 bytes) at the pixel shifted by
+// tap 4s + g.  The input halo of a 16x16 output patch is (16+KH-1)(16+KW-1)
+// pixels x 16 B (7.6 KiB for 7x7) and the whole weight matrix (64 x 416 bf16 for
+// 7x7) stays resident in LDS, so the block is persistent: it loads the weights
+// once and walks patches blockIdx.x, +gridDim.x, ..., double-buffering the
+// halo (global loads of patch p+1 are in flight while patch p multiplies).
+//
+// C^T orientation (weights are the MFMA A operand): a lane's 4 accumulator
+// rows are 4 consecutive output channels of one pixel, stored as one 8-byte
+// (bf16) or 16-byte (fp32) write straight from registers -- no staging.
+// 4 waves; wave w owns patch rows 4w..4w+3 (4 pixel fragments) x 64 channels.
+#include "conv_epilogue.h"
+
+namespace {
+
+constexpr int PH = 16, PW = 16;
+
+template <int KH, int KW>
+struct C8 {
+    static constexpr int TAPS = KH * KW, HWd = PW + KW - 1, HPIX = (PH + KH - 1) * HWd;
+    static constexpr int KS = (TAPS * 8 + 31) / 32;  // 32-deep K-steps
+    static constexpr int KP = KS * 32;
+    // weight row stride: KP*2 + 16 bytes keeps the 16 rows of a fragment read on
+    // distinct banks (row stride = 4 dwords mod 64 apart for KP*2 % 256 in {64, 192, 0})
+    static constexpr int WS = KP * 2 + 16;
+    static constexpr int HBYTES = HPIX * 16;
+    static constexpr int HPT = (HPIX + 255) / 256;   // halo pixels per thread
+    static constexpr int LDS = 64 * WS + 2 * HBYTES;
+    static_assert(LDS <= 80 * 1024, "two blocks per CU");
+};
+
+template <int KH, int KW>
+__global__ __launch_bounds__(256, 2) void conv_c8_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
+                                                         const bf16_t* __restrict__ w, const float* __restrict__ bias,
+                                                         void* __restrict__ y, int tpx, int tpy, int npatch) {
+    using G = C8<KH, KW>;
+    constexpr int TAPS = G::TAPS, HWd = G::HWd, HPIX = G::HPIX, KS = G::KS, KP = G::KP, WS = G::WS;
+    __shared__ __attribute__((aligned(16))) char smem[G::LDS];
+    char* const sW = smem;
+    char* const sH = smem + 64 * WS;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, c16 = lane & 15;
+    const bool reflect = d.pad_mode == IRGAN_PAD_REFLECT;
+    const bool out_f32 = d.out_dtype == IRGAN_F32;
+
+    // ---- weights: rows co < Cout, k < TAPS*8 from the packed [co][tap][8] rows (row
+    // stride rounded up to the 64-element K-tile, include/irgan.h); zero elsewhere
+    {
+        constexpr int Kw = (TAPS * 8 + 63) / 64 * 64;
+        for (int e = tid; e < 64 * (KP / 8); e += 256) {
+            const int co = e / (KP / 8), k8 = e - co * (KP / 8);
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (co < d.Cout && k8 * 8 < TAPS * 8) v = *(const uint4*)(w + (long)co * Kw + k8 * 8);
+            *(uint4*)(sW + co * WS + k8 * 16) = v;
+        }
+    }
+    // per-lane halo offset (pixels) of tap 4s + g; taps past the end read pixel 0
+    // (their weights are zero)
+    int toff[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+        const int t = s * 4 + g;
+        toff[s] = t < TAPS ? (t / KW) * HWd + t % KW : 0;
+    }
+
+    auto load_halo = [&](int p, uint4 (&hv)[G::HPT]) {
+        const int pxi = p % tpx, r = p / tpx, pyi = r % tpy, img = r / tpy;
+#pragma unroll
+        for (int u = 0; u < G::HPT; ++u) {
+            const int h = u * 256 + tid;
+            hv[u] = make_uint4(0u, 0u, 0u, 0u);
+            if (h < HPIX) {
+                const int hy = h / HWd, hx = h - hy * HWd;
+                int iy = pyi * PH + hy + d.c0y, ix = pxi * PW + hx + d.c0x;
+                if (reflect) {
+                    iy = reflect_idx(iy, d.H);
+                    ix = reflect_idx(ix, d.W);
+                }
+                if ((unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W)
+                    hv[u] = *(const uint4*)(x + (((long)img * d.H + iy) * d.W + ix) * d.ldx + d.xoff);
+            }
+        }
+    };
+    auto store_halo = [&](int buf, const uint4 (&hv)[G::HPT]) {
+#pragma unroll
+        for (int u = 0; u < G::HPT; ++u) {
+            const int h = u * 256 + tid;
+            if (h < HPIX) *(uint4*)(sH + buf * G::HBYTES + h * 16) = hv[u];
+        }
+    };
+
+    float bv[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int co = j * 16 + 4 * g + r;
+            bv[j][r] = (bias && co < d.Cout) ? bias[co] : 0.f;
+        }
+    const bool vec = d.ldy % 4 == 0 && d.yoff % 4 == 0;
+
+    uint4 hv[G::HPT];
+    int p = blockIdx.x;
+    if (p < npatch) {
+        load_halo(p, hv);
+        store_halo(0, hv);
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int it = 0; p < npatch; ++it, p += gridDim.x) {
+        const int pn = p + gridDim.x;
+        if (pn < npatch) load_halo(pn, hv);  // in flight under this patch's MFMAs
+        const char* H = sH + (it & 1) * G::HBYTES;
+        f32x4 acc[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            uint4 a[4], b[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) b[j] = *(const uint4*)(sW + (j * 16 + c16) * WS + s * 64 + g * 16);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[i] = *(const uint4*)(H + ((wid * 4 + i) * HWd + c16 + toff[s]) * 16);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, b[j]),
+                                                                        __builtin_bit_cast(bf16x8_t, a[i]),
+                                                                        acc[i][j], 0, 0, 0);
+        }
+        // ---- epilogue: pixel (row wid*4+i, column c16), channels j*16 + 4g + r
+        {
+            const int pxi = p % tpx, r0 = p / tpx, pyi = r0 % tpy, img = r0 / tpy;
+            const int ox = pxi * PW + c16;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int oy = pyi * PH + wid * 4 + i;
+                if (oy >= d.Ho || ox >= d.Wo) continue;
+                const long pix = ((long)img * d.OH + oy * d.omy + d.ooy) * d.OW + ox * d.omx + d.oox;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int co = j * 16 + 4 * g;
+                    if (co >= d.Cout) continue;
+                    float v[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = conv_act(acc[i][j][r] + bv[j][r], d.act);
+                    const bool full = co + 4 <= d.Cout;
+                    if (out_f32) {
+                        float* yp = (float*)y + pix * d.ldy + d.yoff + co;
+                        if (full && vec) {
+                            float4 o = make_float4(v[0], v[1], v[2], v[3]);
+                            if (d.accumulate) {
+                                const float4 q = *(const float4*)yp;
+                                o.x += q.x; o.y += q.y; o.z += q.z; o.w += q.w;
+                            }
+                            *(float4*)yp = o;
+                        } else {
+                            for (int r = 0; r < 4 && co + r < d.Cout; ++r) yp[r] = d.accumulate ? yp[r] + v[r] : v[r];
+                        }
+                    } else {
+                        bf16_t* yp = (bf16_t*)y + pix * d.ldy + d.yoff + co;
+                        if (full && vec) {
+                            if (d.accumulate) {
+                                const uint2 q = *(const uint2*)yp;
+                                v[0] += bf2f((bf16_t)(q.x & 0xffffu)); v[1] += bf2f((bf16_t)(q.x >> 16));
+                                v[2] += bf2f((bf16_t)(q.y & 0xffffu)); v[3] += bf2f((bf16_t)(q.y >> 16));
+                            }
+                            uint2 o;
+                            o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+                            o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+                            *(uint2*)yp = o;
+                        } else {
+                            for (int r = 0; r < 4 && co + r < d.Cout; ++r)
+                                yp[r] = f2bf(d.accumulate ? bf2f(yp[r]) + v[r] : v[r]);
+                        }
+                    }
+                }
+            }
+        }
+        if (pn < npatch) store_halo((it + 1) & 1, hv);
+        __syncthreads();
+    }
+}
+
+template <int KH, int KW>
+void launch_c8(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y, hipStream_t st) {
+    static int slots = 0;
+    if (!slots) {
+        int b = 0, dev = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, conv_c8_kernel<KH, KW>, 256, 0) != hipSuccess || b < 1)
+            b = 1;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+            cus = 256;
+        slots = b * cus;
+    }
+    const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH);
+    const int npatch = d->N * tpx * tpy;
+    const int grid = npatch < slots ? npatch : slots;
+    conv_c8_kernel<KH, KW><<<grid, 256, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, y, tpx, tpy, npatch);
+}
+
+}  // namespace
+
+// Preconditions: bf16 input and weights, Cin == 8, ldx % 8 == 0, xoff % 8 == 0,
+// sy = sx = 1, Cout <= 64, (KH, KW) in {(7,7), (4,4), (3,3)}, no mask.
+extern "C" int irgan_conv_fwd_c8(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
+                                 const void* mask, hipStream_t st) {
+    if ((long)d->N * d->Ho * d->Wo <= 0 || d->Cout <= 0) return 0;
+    if (d->dtype != IRGAN_BF16 || d->Cin != 8 || d->ldx % 8 || d->xoff % 8 || d->sy != 1 || d->sx != 1 ||
+        d->Cout > 64 || mask)
+        return IRGAN_EUNSUPPORTED;
+    if (d->KH == 7 && d->KW == 7) launch_c8<7, 7>(d, x, w, bias, y, st);
+    else if (d->KH == 4 && d->KW == 4) launch_c8<4, 4>(d, x, w, bias, y, st);
+    else if (d->KH == 3 && d->KW == 3) launch_c8<3, 3>(d, x, w, bias, y, st);
+    else return IRGAN_EUNSUPPORTED;
+    IRGAN_LAUNCH_CHECK();
+    return 0;
+}

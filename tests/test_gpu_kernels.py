@@ -54,6 +54,11 @@ CONV_CASES = [
     # multi-patch / ragged-edge cases for the halo kernel (16x16 output patches)
     (64, 3, 7, 1, 3, 1, 37),      # narrow-Cout kernel: G outc shape, several patches, ragged edge
     (512, 1, 4, 1, 1, 0, 31),     # narrow-Cout kernel, 8 chunks double-buffered: D's last layer
+    # 8-channel-input kernel (conv_c8.hip): 2 x 18 x 18 = 648 patches > the persistent grid
+    # (2 blocks x 256 CUs), ragged last patch row/column; fwd = inc / VGG conv1_1, dgrad = outc
+    (1, 64, 7, 1, 3, 1, 280),
+    (3, 64, 3, 1, 1, 0, 280),
+    (64, 3, 7, 1, 3, 1, 280),
     (128, 256, 3, 1, 1, 1, 37),
     (64, 64, 3, 1, 1, 0, 40),
     (128, 128, 4, 2, 1, 0, 34),
