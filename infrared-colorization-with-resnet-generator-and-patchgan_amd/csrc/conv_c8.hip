@@ -16,15 +16,18 @@
 // rows are 4 consecutive output channels of one pixel, stored as one 8-byte
 // (bf16) or 16-byte (fp32) write straight from registers -- no staging.
 // 4 waves; wave w owns patch rows 4w..4w+3 (4 pixel fragments) x 64 channels.
+// Stride 2 (D's first layer, 4x4): the halo is the 34x34 input span and output
+// pixel (r, c) of tap t reads span pixel (2r + ty, 2c + tx).
 #include "conv_epilogue.h"
 
 namespace {
 
 constexpr int PH = 16, PW = 16;
 
-template <int KH, int KW>
+template <int KH, int KW, int S>
 struct C8 {
-    static constexpr int TAPS = KH * KW, HWd = PW + KW - 1, HPIX = (PH + KH - 1) * HWd;
+    // stride S: the patch's input span is (16 S + K - S) pixels per axis
+    static constexpr int TAPS = KH * KW, HWd = PW * S + KW - S, HPIX = (PH * S + KH - S) * HWd;
     static constexpr int KS = (TAPS * 8 + 31) / 32;  // 32-deep K-steps
     static constexpr int KP = KS * 32;
     // weight row stride: KP*2 + 16 bytes keeps the 16 rows of a fragment read on
@@ -33,14 +36,15 @@ struct C8 {
     static constexpr int HBYTES = HPIX * 16;
     static constexpr int HPT = (HPIX + 255) / 256;   // halo pixels per thread
     static constexpr int LDS = 64 * WS + 2 * HBYTES;
-    static_assert(LDS <= 80 * 1024, "two blocks per CU");
+    // two resident blocks per CU (more spill: the 4x4 accumulator tile needs ~200 VGPRs)
+    static_assert(2 * LDS <= 160 * 1024, "resident blocks per CU");
 };
 
-template <int KH, int KW>
+template <int KH, int KW, int S>
 __global__ __launch_bounds__(256, 2) void conv_c8_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
                                                          const bf16_t* __restrict__ w, const float* __restrict__ bias,
                                                          void* __restrict__ y, int tpx, int tpy, int npatch) {
-    using G = C8<KH, KW>;
+    using G = C8<KH, KW, S>;
     constexpr int TAPS = G::TAPS, HWd = G::HWd, HPIX = G::HPIX, KS = G::KS, KP = G::KP, WS = G::WS;
     __shared__ __attribute__((aligned(16))) char smem[G::LDS];
     char* const sW = smem;
@@ -80,7 +84,7 @@ __global__ __launch_bounds__(256, 2) void conv_c8_kernel(const irgan_conv_desc d
             hv[u] = make_uint4(0u, 0u, 0u, 0u);
             if (h < HPIX) {
                 const int hy = h / HWd, hx = h - hy * HWd;
-                int iy = pyi * PH + hy + d.c0y, ix = pxi * PW + hx + d.c0x;
+                int iy = pyi * PH * S + hy + d.c0y, ix = pxi * PW * S + hx + d.c0x;
                 if (reflect) {
                     iy = reflect_idx(iy, d.H);
                     ix = reflect_idx(ix, d.W);
@@ -98,6 +102,7 @@ __global__ __launch_bounds__(256, 2) void conv_c8_kernel(const irgan_conv_desc d
         }
     };
 
+    const bool vec = d.ldy % 4 == 0 && d.yoff % 4 == 0;
     float bv[4][4];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -106,7 +111,6 @@ __global__ __launch_bounds__(256, 2) void conv_c8_kernel(const irgan_conv_desc d
             const int co = j * 16 + 4 * g + r;
             bv[j][r] = (bias && co < d.Cout) ? bias[co] : 0.f;
         }
-    const bool vec = d.ldy % 4 == 0 && d.yoff % 4 == 0;
 
     uint4 hv[G::HPT];
     int p = blockIdx.x;
@@ -131,7 +135,8 @@ __global__ __launch_bounds__(256, 2) void conv_c8_kernel(const irgan_conv_desc d
 #pragma unroll
             for (int j = 0; j < 4; ++j) b[j] = *(const uint4*)(sW + (j * 16 + c16) * WS + s * 64 + g * 16);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) a[i] = *(const uint4*)(H + ((wid * 4 + i) * HWd + c16 + toff[s]) * 16);
+            for (int i = 0; i < 4; ++i)
+                a[i] = *(const uint4*)(H + ((wid * 4 + i) * S * HWd + c16 * S + toff[s]) * 16);
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -194,12 +199,12 @@ __global__ __launch_bounds__(256, 2) void conv_c8_kernel(const irgan_conv_desc d
     }
 }
 
-template <int KH, int KW>
+template <int KH, int KW, int S>
 void launch_c8(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y, hipStream_t st) {
     static int slots = 0;
     if (!slots) {
         int b = 0, dev = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, conv_c8_kernel<KH, KW>, 256, 0) != hipSuccess || b < 1)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, conv_c8_kernel<KH, KW, S>, 256, 0) != hipSuccess || b < 1)
             b = 1;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
@@ -209,23 +214,31 @@ void launch_c8(const irgan_conv_desc* d, const void* x, const void* w, const flo
     const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH);
     const int npatch = d->N * tpx * tpy;
     const int grid = npatch < slots ? npatch : slots;
-    conv_c8_kernel<KH, KW><<<grid, 256, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, y, tpx, tpy, npatch);
+    conv_c8_kernel<KH, KW, S><<<grid, 256, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, y, tpx, tpy, npatch);
 }
 
 }  // namespace
 
 // Preconditions: bf16 input and weights, Cin == 8, ldx % 8 == 0, xoff % 8 == 0,
-// sy = sx = 1, Cout <= 64, (KH, KW) in {(7,7), (4,4), (3,3)}, no mask.
+// sy = sx = 1 with (KH, KW) in {(7,7), (4,4), (3,3)} or sy = sx = 2 with 4x4 (D's first
+// layer), Cout <= 64, no mask.
 extern "C" int irgan_conv_fwd_c8(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
                                  const void* mask, hipStream_t st) {
     if ((long)d->N * d->Ho * d->Wo <= 0 || d->Cout <= 0) return 0;
-    if (d->dtype != IRGAN_BF16 || d->Cin != 8 || d->ldx % 8 || d->xoff % 8 || d->sy != 1 || d->sx != 1 ||
-        d->Cout > 64 || mask)
+    if (d->dtype != IRGAN_BF16 || d->Cin != 8 || d->ldx % 8 || d->xoff % 8 || d->sy != d->sx || d->Cout > 64 ||
+        mask)
         return IRGAN_EUNSUPPORTED;
-    if (d->KH == 7 && d->KW == 7) launch_c8<7, 7>(d, x, w, bias, y, st);
-    else if (d->KH == 4 && d->KW == 4) launch_c8<4, 4>(d, x, w, bias, y, st);
-    else if (d->KH == 3 && d->KW == 3) launch_c8<3, 3>(d, x, w, bias, y, st);
-    else return IRGAN_EUNSUPPORTED;
+    if (d->sy == 2) {
+        if (d->KH == 4 && d->KW == 4) launch_c8<4, 4, 2>(d, x, w, bias, y, st);
+        else return IRGAN_EUNSUPPORTED;
+    } else if (d->sy == 1) {
+        if (d->KH == 7 && d->KW == 7) launch_c8<7, 7, 1>(d, x, w, bias, y, st);
+        else if (d->KH == 4 && d->KW == 4) launch_c8<4, 4, 1>(d, x, w, bias, y, st);
+        else if (d->KH == 3 && d->KW == 3) launch_c8<3, 3, 1>(d, x, w, bias, y, st);
+        else return IRGAN_EUNSUPPORTED;
+    } else {
+        return IRGAN_EUNSUPPORTED;
+    }
     IRGAN_LAUNCH_CHECK();
     return 0;
 }

@@ -59,6 +59,7 @@ CONV_CASES = [
     (1, 64, 7, 1, 3, 1, 280),
     (3, 64, 3, 1, 1, 0, 280),
     (64, 3, 7, 1, 3, 1, 280),
+    (4, 64, 4, 2, 1, 0, 530),     # stride-2 c8 (D's first layer): 2 x 17 x 17 patches, ragged
     (128, 256, 3, 1, 1, 1, 37),
     (64, 64, 3, 1, 1, 0, 40),
     (128, 128, 4, 2, 1, 0, 34),

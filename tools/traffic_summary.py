@@ -12,7 +12,8 @@ import json
 import os
 import sys
 
-FAMILIES = {"fwd": ("conv_pp_kernel<3, 3>",), "dgrad": ("conv_pp_kernel<3, 3>", "reflect_ring_kernel"),
+FAMILIES = {"fwd": ("conv_pp_kernel<3, 3, 256, false>",),
+            "dgrad": ("conv_pp_kernel<3, 3, 256, false>", "reflect_ring_kernel"),
             "wgrad": ("wgrad_halo_kernel<128, 3, 1",)}
 
 
