@@ -16,9 +16,9 @@
 //   column segments: band columns x (2p of them), rows y outside the band rows.
 //
 // The band is thin (~4 pixel rows per image for 3x3), so the launch is built
-// for parallelism rather than operand reuse: block = 32 band pixels x 64
-// output channels, 4 waves that split the K loop (term, tap, 32-channel step)
-// round-robin, each holding the full 32 x 64 tile (2 x 4 fragments of
+// for parallelism rather than operand reuse: block = NPIX band pixels x 64
+// output channels, 8 waves that split the K loop (term, tap, 32-channel step)
+// round-robin, each holding the full NPIX x 64 tile (NF x 4 fragments of
 // mfma_f32_16x16x32_bf16, weights as A: a lane's 4 accumulator rows are 4
 // consecutive channels of one pixel).  Operands come straight from L2 (no
 // LDS staging); the 4 partial tiles are summed through LDS in a fixed order
@@ -27,7 +27,11 @@
 
 namespace {
 
-constexpr int NPIX = 32;  // band pixels per block (2 fragments)
+// 64 band pixels per block: each block streams its (taps x Cin) weight slices from L2
+// once for 64 pixels instead of 32 -- the launch is bound by those L2 reads
+// (32-pixel blocks: ~440 MB per resblock dgrad ring, 35 us)
+constexpr int NPIX = 64;  // band pixels per block
+constexpr int NF = NPIX / 16;  // pixel fragments
 constexpr int NCO = 64;   // output channels per block (4 fragments)
 constexpr int NWV = 8;    // waves per block (K split)
 constexpr int MAXT = 160; // (term, tap) pairs: 3 terms x KH*KW (7x7: 147)
@@ -67,10 +71,10 @@ __global__ __launch_bounds__(NWV * 64) void reflect_ring_kernel(const irgan_conv
     const int co0 = blockIdx.y * NCO;
 
     // this lane's pixel in fragment f: index q = seg*NPIX + f*16 + (lane & 15) along the band line
-    int py[2], px[2];
-    bool pv[2];
+    int py[NF], px[NF];
+    bool pv[NF];
 #pragma unroll
-    for (int f = 0; f < 2; ++f) {
+    for (int f = 0; f < NF; ++f) {
         const int q = seg * NPIX + f * 16 + (lane & 15);
         if (rowseg) {
             py[f] = bpos;
@@ -90,9 +94,9 @@ __global__ __launch_bounds__(NWV * 64) void reflect_ring_kernel(const irgan_conv
     const int vby = rowseg ? mirror_pos(bpos, H, p) : 0;   // row segments: Vy (uniform)
     const int vbx = rowseg ? 0 : mirror_pos(bpos, W, p);   // column segments: Vx (uniform)
 
-    f32x4 acc[2][4];
+    f32x4 acc[NF][4];
 #pragma unroll
-    for (int f = 0; f < 2; ++f)
+    for (int f = 0; f < NF; ++f)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[f][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -115,9 +119,9 @@ __global__ __launch_bounds__(NWV * 64) void reflect_ring_kernel(const irgan_conv
     const int ntap = ntap_s;
 
     // mirrored column of fragment f's pixel (terms 1 and 2)
-    int mxf[2];
+    int mxf[NF];
 #pragma unroll
-    for (int f = 0; f < 2; ++f) mxf[f] = rowseg ? mirror_pos(px[f], W, p) : vbx;
+    for (int f = 0; f < NF; ++f) mxf[f] = rowseg ? mirror_pos(px[f], W, p) : vbx;
 
     const int kc = (lane >> 4) * 8;  // channel offset of this lane within a 32-deep k step
     const bf16_t* wrow[4];
@@ -130,7 +134,7 @@ __global__ __launch_bounds__(NWV * 64) void reflect_ring_kernel(const irgan_conv
     }
     const int nc = d.Cin / 32;
     const int total = ntap * nc;  // flattened K steps (tap, 32-channel step); wave wv takes s = wv mod NWV
-    auto load_step = [&](int q, uint4 (&a)[2], uint4 (&b)[4]) {
+    auto load_step = [&](int q, uint4 (&a)[NF], uint4 (&b)[4]) {
         const int tp = q / nc, c = q - tp * nc;
         const int e = tap_list[tp];
         const int term = e >> 8, ty = (e >> 4) & 15, tx = e & 15;
@@ -138,7 +142,7 @@ __global__ __launch_bounds__(NWV * 64) void reflect_ring_kernel(const irgan_conv
 #pragma unroll
         for (int j = 0; j < 4; ++j) b[j] = wok[j] ? *(const uint4*)(wrow[j] + wb) : uint4{0, 0, 0, 0};
 #pragma unroll
-        for (int f = 0; f < 2; ++f) {
+        for (int f = 0; f < NF; ++f) {
             // term 0: (Vy, x); term 1: (y, Vx); term 2: (Vy, Vx)  (term is wave-uniform)
             const int vy = term == 1 ? py[f] : vby;
             const int vx = term == 0 ? px[f] : mxf[f];
@@ -149,9 +153,9 @@ __global__ __launch_bounds__(NWV * 64) void reflect_ring_kernel(const irgan_conv
                       : uint4{0, 0, 0, 0};
         }
     };
-    auto mma = [&](const uint4 (&a)[2], const uint4 (&b)[4]) {
+    auto mma = [&](const uint4 (&a)[NF], const uint4 (&b)[4]) {
 #pragma unroll
-        for (int f = 0; f < 2; ++f)
+        for (int f = 0; f < NF; ++f)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
                 acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, b[j]),
@@ -159,7 +163,7 @@ __global__ __launch_bounds__(NWV * 64) void reflect_ring_kernel(const irgan_conv
                                                                     0, 0);
     };
     // two steps of operands in flight: step s+NWV loads while step s multiplies
-    uint4 a0[2], b0[4], a1[2], b1[4];
+    uint4 a0[NF], b0[4], a1[NF], b1[4];
     int ks = wv;
     if (ks < total) load_step(ks, a0, b0);
     while (ks < total) {
@@ -174,7 +178,7 @@ __global__ __launch_bounds__(NWV * 64) void reflect_ring_kernel(const irgan_conv
     }
     // partial tiles -> LDS: lane holds pixel f*16 + (lane & 15), channels j*16 + 4*(lane>>4) + r
 #pragma unroll
-    for (int f = 0; f < 2; ++f)
+    for (int f = 0; f < NF; ++f)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
             *(float4*)&red[wv][f * 16 + (lane & 15)][j * 16 + 4 * (lane >> 4)] =

@@ -262,14 +262,18 @@ def conv_dgrad(pc: PackedConv, dy: Feat, dx: Feat, accumulate=False, mask: Feat 
                     pad_mode=PAD_ZERO, act=0, dtype=pc.dtype, mask_act=0, ldm=0, moff=0)
         d = _desc(**base, Ho=H, Wo=W, ldy=dx.ld, yoff=dx.off, OH=H, OW=W, omy=1, ooy=0, omx=1, oox=0, sy=1, sx=1,
                   c0y=c0y + p, c0x=c0x + p, accumulate=int(accumulate), out_dtype=dx.dt)
-        TIMER.wrap(conv_tag("dgrad", s, (H, W), dx.N), lambda: _lib.call(
-            "irgan_conv_fwd", ctypes.byref(d), dy.ptr, P(buf), None, dx.ptr, None, stream()))
-        if p == 0:
-            return
-        if (pc.dtype == BF16 and RING_MFMA and pc.cout_eff % 32 == 0 and H >= 2 * p + 2 and W >= 2 * p + 2
-                and dy.ld % 8 == 0 and dy.off % 8 == 0):
-            # one launch: ring values of g by MFMA, added onto their mirrored border pixels
-            _lib.call("irgan_reflect_dgrad_ring", ctypes.byref(d), dy.ptr, P(buf), p, dx.ptr, stream())
+        ring_mfma = (p > 0 and pc.dtype == BF16 and RING_MFMA and pc.cout_eff % 32 == 0 and H >= 2 * p + 2
+                     and W >= 2 * p + 2 and dy.ld % 8 == 0 and dy.off % 8 == 0)
+
+        def launch():
+            _lib.call("irgan_conv_fwd", ctypes.byref(d), dy.ptr, P(buf), None, dx.ptr, None, stream())
+            if ring_mfma:
+                # one launch: ring values of g by MFMA, added onto their mirrored border pixels
+                _lib.call("irgan_reflect_dgrad_ring", ctypes.byref(d), dy.ptr, P(buf), p, dx.ptr, stream())
+
+        # the timed dgrad op is the whole backward-data: interior + ring
+        TIMER.wrap(conv_tag("dgrad", s, (H, W), dx.N), launch)
+        if p == 0 or ring_mfma:
             return
         # ring in split-K partials: rows[ks][N][2p][Wp][C], cols[ks][N][H][2p][C]
         rsz, csz = dx.N * 2 * p * Wp * s.cin, dx.N * H * 2 * p * s.cin
