@@ -133,6 +133,43 @@ class ParamStore:
     def zero_grad(self):
         self.grad.zero_()
 
+    def adam_state_dict(self, lr, betas=(0.5, 0.999), eps=1e-8, initial_lr=None):
+        """The Adam moments as a ``torch.optim.Adam.state_dict()`` (ir:1601-1609):
+        parameter indices follow the module's ``parameters()`` order (the
+        state_dict order without buffers), tensors in OIHW fp32 on the CPU, so the
+        file loads into the reference's optimizer unchanged."""
+        state = {}
+        if self.step_count > 0:
+            for i, k in enumerate(self.shapes):
+                state[i] = {"step": torch.tensor(float(self.step_count)),
+                            "exp_avg": self.oihw(k, self.m).detach().cpu().contiguous(),
+                            "exp_avg_sq": self.oihw(k, self.v).detach().cpu().contiguous()}
+        group = {"lr": lr, "betas": tuple(betas), "eps": eps, "weight_decay": 0, "amsgrad": False,
+                 "maximize": False, "foreach": None, "capturable": False, "differentiable": False, "fused": None,
+                 "params": list(range(len(self.shapes)))}
+        if initial_lr is not None:
+            group["initial_lr"] = initial_lr   # LambdaLR's key (ir:1606-1609)
+        return {"state": state, "param_groups": [group]}
+
+    @torch.no_grad()
+    def load_adam_state_dict(self, sd):
+        """Inverse of adam_state_dict (also accepts a reference optimizer file)."""
+        st = sd["state"]
+        if not st:
+            self.m.zero_()
+            self.v.zero_()
+            self.step_count = 0
+            return
+        steps = set()
+        for i, k in enumerate(self.shapes):
+            e = st[i]
+            self.oihw(k, self.m).copy_(e["exp_avg"].to(self.device, torch.float32))
+            self.oihw(k, self.v).copy_(e["exp_avg_sq"].to(self.device, torch.float32))
+            steps.add(int(float(e["step"])))
+        if len(steps) != 1:
+            raise RuntimeError(f"per-parameter Adam step counts differ: {sorted(steps)}")
+        self.step_count = steps.pop()
+
     def adam_step(self, lr, b1=0.5, b2=0.999, eps=1e-8):
         self.step_count += 1
         ops.adam(self.flat, self.grad, self.m, self.v, self.step_count, lr, b1, b2, eps)

@@ -584,6 +584,33 @@ class GANTrainer:
     def current_lr_G(self):
         return self.cfg.lr_G * self.core.lr_scale
 
+    # ---- full training state.  The reference checkpoints G only
+    # (ir:1708); this adds D, both Adams (torch.optim.Adam.state_dict() layout) and
+    # the LambdaLR position, so an interrupted run resumes bit-exactly.
+    def state_dict(self):
+        c, s = self.cfg, self.core
+        return {"netG": {k: v.detach().cpu().clone() for k, v in self.netG.store.state().items()},
+                "netD": {k: v.detach().cpu().clone() for k, v in self.netD.store.state().items()},
+                "optimizer_G": self.netG.store.adam_state_dict(c.lr_G * s.lr_scale, (c.beta1, c.beta2), 1e-8, c.lr_G),
+                "optimizer_D": self.netD.store.adam_state_dict(c.lr_D * s.lr_scale, (c.beta1, c.beta2), 1e-8, c.lr_D),
+                "epoch_index": self.epoch_index, "lr_scale": s.lr_scale}
+
+    def load_state_dict(self, sd):
+        self.netG.store.load(sd["netG"], strict=True)
+        self.netD.store.load(sd["netD"], strict=True)
+        self.netG.store.load_adam_state_dict(sd["optimizer_G"])
+        self.netD.store.load_adam_state_dict(sd["optimizer_D"])
+        self.epoch_index = int(sd["epoch_index"])
+        self.core.lr_scale = float(sd["lr_scale"])
+        for net in (self.netG, self.netD):
+            net.repack()
+
+    def save_checkpoint(self, path):
+        torch.save(self.state_dict(), path)
+
+    def load_checkpoint(self, path):
+        self.load_state_dict(torch.load(path, map_location="cpu", weights_only=True))
+
 
 @torch.no_grad()
 def _dp():

@@ -201,3 +201,64 @@ def test_kaist_native_resolution_512x640():
     for k in ("loss_D", "loss_G", "loss_G_L1", "loss_G_perc", "loss_G_ssim"):
         assert np.isfinite(l16[k]) and np.isfinite(l32[k]), k
         assert abs(l16[k] - l32[k]) <= 3e-2 * max(1.0, abs(l32[k])), (k, l16[k], l32[k])
+
+
+def _seeded_trainer(irc, seed_shift=0):
+    from oracle import step as O
+    cfg = irc.Config()
+    cfg.device = "cuda:0"
+    cfg.compute_dtype = "fp32"
+    tr = irc.GANTrainer(cfg)
+    tr.netG.store.load(O.seeded_params(O.g_param_shapes(), 1 + seed_shift, bias_std=0.02), strict=True)
+    tr.netD.store.load(O.seeded_params(O.d_param_shapes(), 2 + seed_shift, bias_std=0.02), strict=True)
+    tr.vgg.store.load(O.seeded_params(O.vgg_param_shapes(), 3, kaiming=True), strict=True)
+    for net in (tr.netG, tr.netD, tr.vgg):
+        net.repack()
+    return tr
+
+
+def test_full_state_checkpoint_resume_and_torch_adam(tmp_path):
+    """GANTrainer.save_checkpoint / load_checkpoint carry G, D, both
+    Adams and the LR position.  (1) A fresh trainer that loads the file after 2 steps
+    continues exactly as the original (same step 3, fp32 parity mode).  (2) The saved
+    optimizer_G is a torch.optim.Adam state: torch's own Adam, loaded with it and fed
+    step 3's gradient, reproduces the HIP Adam update (ir:1601-1609, 1681)."""
+    irc = pkg()
+    g = torch.Generator().manual_seed(21)
+    batches = [(torch.rand(2, 1, 32, 32, generator=g) * 2 - 1, torch.rand(2, 3, 32, 32, generator=g) * 2 - 1)
+               for _ in range(3)]
+    a = _seeded_trainer(irc)
+    for ir, rgb in batches[:2]:
+        a.step(ir.cuda(), rgb.cuda())
+    a.scheduler_step()
+    path = tmp_path / "full.pt"
+    a.save_checkpoint(path)
+    sd2 = torch.load(path, map_location="cpu", weights_only=True)
+    b = _seeded_trainer(irc, seed_shift=10)
+    b.load_checkpoint(path)
+    assert b.epoch_index == 1 and b.netG.store.step_count == 2 and b.netD.store.step_count == 2
+    La = a.losses(a.step(batches[2][0].cuda(), batches[2][1].cuda()))
+    Lb = b.losses(b.step(batches[2][0].cuda(), batches[2][1].cuda()))
+    for k in La:
+        assert abs(La[k] - Lb[k]) <= 1e-6 * max(1.0, abs(La[k])), (k, La[k], Lb[k])
+    lr = a.current_lr_G
+    for name in ("netG", "netD"):
+        sa, sb = getattr(a, name).store, getattr(b, name).store
+        for k in sa.shapes:
+            d = (sa.krsc(k) - sb.krsc(k)).abs().max().item()
+            assert d <= 2 * lr, (name, k, d)   # grads differ only by split-K atomics order
+    # torch.optim.Adam over the step-2 state and the step-3 gradient == the HIP update
+    st = a.netG.store
+    params = [torch.nn.Parameter(t.double().clone()) for t in sd2["netG"].values()]
+    for p, k in zip(params, st.shapes):
+        p.grad = st.oihw(k, st.grad).detach().cpu().double().clone()
+    opt = torch.optim.Adam(params, lr=lr, betas=(a.cfg.beta1, a.cfg.beta2))
+    osd = sd2["optimizer_G"]
+    osd["state"] = {i: {kk: (vv.double() if kk != "step" else vv) for kk, vv in e.items()}
+                    for i, e in osd["state"].items()}
+    opt.load_state_dict(osd)
+    opt.param_groups[0]["lr"] = lr
+    opt.step()
+    for p, k in zip(params, st.shapes):
+        got = st.oihw(k).detach().cpu().double()
+        assert (got - p.detach()).abs().max().item() <= 1e-6 * lr + 1e-7, k

@@ -106,3 +106,32 @@ def test_gpu_entry_points_fail_loudly_without_gpu():
     cfg = irc.Config()
     with pytest.raises(Exception):
         irc.IRColorizationModel(cfg)(torch.zeros(1, 1, 32, 32))
+
+
+def test_adam_state_dict_is_torch_optim_layout():
+    """ParamStore.adam_state_dict: torch.optim.Adam.state_dict()
+    layout over the reference's parameters() order, OIHW tensors; it loads into
+    torch.optim.Adam unchanged and round-trips through load_adam_state_dict."""
+    import importlib
+    import torch
+    engine = importlib.import_module(pkg().__name__ + ".engine")
+    shapes = engine.g_param_shapes(ngf=8, n_blocks=2)
+    st = engine.ParamStore(shapes, "cpu")
+    g = torch.Generator().manual_seed(3)
+    for buf in (st.flat, st.m, st.v):
+        buf.copy_(torch.rand(st.numel, generator=g))
+    st.step_count = 7
+    sd = st.adam_state_dict(2e-4, (0.5, 0.999), 1e-8, initial_lr=2e-4)
+    params = [torch.nn.Parameter(t.clone()) for t in st.state().values()]
+    assert [tuple(p.shape) for p in params] == [tuple(v) for k, v in shapes.items() if not k.endswith(".filt")]
+    opt = torch.optim.Adam(params, lr=2e-4, betas=(0.5, 0.999))
+    opt.load_state_dict(sd)
+    for i, (k, p) in enumerate(zip(st.shapes, params)):
+        s = opt.state[p]
+        assert float(s["step"]) == 7.0
+        assert torch.equal(s["exp_avg"], st.oihw(k, st.m)) and torch.equal(s["exp_avg_sq"], st.oihw(k, st.v))
+    st2 = engine.ParamStore(shapes, "cpu")
+    st2.load_adam_state_dict(opt.state_dict())
+    assert st2.step_count == 7
+    for k in st.shapes:   # per-tensor slices (the 64-element alignment padding is not state)
+        assert torch.equal(st2.krsc(k, st2.m), st.krsc(k, st.m)) and torch.equal(st2.krsc(k, st2.v), st.krsc(k, st.v))
