@@ -486,6 +486,42 @@ __global__ __launch_bounds__(256) void weight_pack_batch_kernel(const irgan_pack
     const int ka = q.kalign > 0 ? q.kalign : 1;
     const int Kp = (taps * Cp + ka - 1) / ka * ka;
     const long total = (long)R * Kp;
+    if (q.transpose) {
+        // backward-data pack dst[ci][tap*Cp + co] = src[co][ky][kx][ci]: per tap a 2-D
+        // transpose, staged through a 64x64 LDS tile so both the fp32 reads (along ci)
+        // and the stores (along co) are coalesced
+        __shared__ float tile[64][65];
+        const int ntc = (Cp + 63) / 64, ntr = (R + 63) / 64;
+        const long ntiles = (long)taps * ntc * ntr;
+        for (long t = blockIdx.x; t < ntiles; t += gridDim.x) {
+            const int rt = (int)(t % ntr);
+            const long t2 = t / ntr;
+            const int ct = (int)(t2 % ntc), tap = (int)(t2 / ntc);
+            const int a = tap / q.Ax, b = tap - a * q.Ax;
+            const int ky = q.tyr + q.s * (q.Ay - 1 - a), kx = q.txr + q.s * (q.Ax - 1 - b);
+            for (int e = threadIdx.x; e < 4096; e += 256) {
+                const int cc = e >> 6, rr = e & 63, c = ct * 64 + cc, row = rt * 64 + rr;
+                tile[cc][rr] = (c < Cr && row < R) ? q.src[(((long)c * q.KH + ky) * q.KW + kx) * q.Cin + row] : 0.f;
+            }
+            __syncthreads();
+            for (int e = threadIdx.x; e < 4096; e += 256) {
+                const int rr = e >> 6, cc = e & 63, c = ct * 64 + cc, row = rt * 64 + rr;
+                if (row < R && c < Cp) {
+                    const long o = (long)row * Kp + tap * Cp + c;
+                    if (q.dtype == IRGAN_BF16) ((bf16_t*)q.dst)[o] = f2bf(tile[cc][rr]);
+                    else ((float*)q.dst)[o] = tile[cc][rr];
+                }
+            }
+            __syncthreads();
+        }
+        const int tail = Kp - taps * Cp;  // K padding up to kalign: zeros
+        for (long idx = blockIdx.x * 256L + threadIdx.x; idx < (long)R * tail; idx += (long)gridDim.x * 256) {
+            const long o = (idx / tail) * Kp + taps * Cp + idx % tail;
+            if (q.dtype == IRGAN_BF16) ((bf16_t*)q.dst)[o] = 0;
+            else ((float*)q.dst)[o] = 0.f;
+        }
+        return;
+    }
     for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
         const int row = (int)(idx / Kp), k = (int)(idx - (long)row * Kp);
         const int tap = k / Cp, c = k - tap * Cp;
