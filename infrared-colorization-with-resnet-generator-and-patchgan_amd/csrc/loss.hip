@@ -189,27 +189,88 @@ __global__ __launch_bounds__(TPB) void ssim_h5_kernel(const float* __restrict__ 
     }
 }
 
-// vertical 11-tap pass over NM planar maps; blockIdx.y = n*H + y
-template <int NM>
+// Horizontal 11-tap pass, one image row per block: the row's NI input maps are
+// staged in LDS with coalesced loads (FIRST: a' = (a+1)/2 and b' = (b+1)/2, five
+// outputs mu1, mu2, E[a'^2], E[b'^2], E[a'b']; else NI = NO planar maps), then every
+// output element reads its 11 taps from LDS.  Same tap order as ssim_h5_kernel /
+// ssim_h_kernel (bit-identical results) without their stride-C global re-reads.
+template <int NI, int NO, bool FIRST>
+__global__ __launch_bounds__(TPB) void ssim_hrow_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                        const float* __restrict__ in, int W, int C, Win11 win,
+                                                        float* __restrict__ out, long S) {
+    extern __shared__ float rowm[];  // NI x W*C
+    const int WC = W * C;
+    const long rb = (long)blockIdx.x * WC;
+    for (int e = threadIdx.x; e < WC; e += TPB) {
+        if (FIRST) {
+            rowm[e] = (a[rb + e] + 1.f) * 0.5f;
+            rowm[WC + e] = (b[rb + e] + 1.f) * 0.5f;
+        } else {
+#pragma unroll
+            for (int m = 0; m < NI; ++m) rowm[m * WC + e] = in[m * S + rb + e];
+        }
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < WC; e += TPB) {
+        const int xw = e / C;
+        float acc[NO];
+#pragma unroll
+        for (int m = 0; m < NO; ++m) acc[m] = 0.f;
+#pragma unroll
+        for (int k = 0; k < 11; ++k) {
+            const int xx = xw + k - 5;
+            if (xx < 0 || xx >= W) continue;
+            const int j = e + (k - 5) * C;
+            const float gk = win.g[k];
+            if (FIRST) {
+                const float p = rowm[j], q = rowm[WC + j];
+                acc[0] += gk * p;
+                acc[1] += gk * q;
+                acc[2] += gk * p * p;
+                acc[3] += gk * q * q;
+                acc[4] += gk * p * q;
+            } else {
+#pragma unroll
+                for (int m = 0; m < NO; ++m) acc[m] += gk * rowm[m * WC + j];
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < NO; ++m) out[m * S + rb + e] = acc[m];
+    }
+}
+
+// vertical 11-tap pass over NM planar maps.  A thread owns one element (x*C + c)
+// of R consecutive rows: it loads the R + 10 input rows once into registers and
+// slides the window, so each input is read (R+10)/R times instead of 11 (the
+// pass was bound by those L2 re-reads).  blockIdx.y = n * ceil(H/R) + row block.
+template <int NM, int R>
 __global__ __launch_bounds__(TPB) void ssim_v_kernel(const float* __restrict__ in, int H, int W, int C, Win11 win,
                                                      float* __restrict__ out, long S) {
     const int e = blockIdx.x * TPB + threadIdx.x;  // element within the row (x*C + c)
     if (e >= W * C) return;
-    const int yh = blockIdx.y % H;
-    const long idx = (long)blockIdx.y * W * C + e;
-    float acc[NM];
+    const int hb = (H + R - 1) / R;
+    const int n = blockIdx.y / hb, y0 = (blockIdx.y - n * hb) * R;
+    const long WC = (long)W * C;
+    const long base = (long)n * H * WC + e;
+    float v[NM][R + 10];
 #pragma unroll
-    for (int m = 0; m < NM; ++m) acc[m] = 0.f;
+    for (int r = 0; r < R + 10; ++r) {
+        const int yy = y0 + r - 5;
+        const bool ok = yy >= 0 && yy < H;
 #pragma unroll
-    for (int k = 0; k < 11; ++k) {
-        const int yy = yh + k - 5;
-        if (yy < 0 || yy >= H) continue;
-        const long j = idx + (long)(k - 5) * W * C;
-#pragma unroll
-        for (int m = 0; m < NM; ++m) acc[m] += win.g[k] * in[m * S + j];
+        for (int m = 0; m < NM; ++m) v[m][r] = ok ? in[m * S + base + yy * WC] : 0.f;
     }
 #pragma unroll
-    for (int m = 0; m < NM; ++m) out[m * S + idx] = acc[m];
+    for (int r = 0; r < R; ++r) {
+        if (y0 + r >= H) break;
+#pragma unroll
+        for (int m = 0; m < NM; ++m) {
+            float acc = 0.f;
+#pragma unroll
+            for (int k = 0; k < 11; ++k) acc += win.g[k] * v[m][r + k];
+            out[m * S + base + (y0 + r) * WC] = acc;
+        }
+    }
 }
 
 // horizontal 11-tap pass over NM planar maps
@@ -361,12 +422,22 @@ extern "C" int irgan_ssim(const float* a, const float* b, int32_t N, int32_t H, 
     if (S <= 0) return 0;
     if ((long)N * H > 65535) return IRGAN_EUNSUPPORTED;
     const int nb = nblocks(S);
-    const dim3 gx(irgan_cdiv(W, TPB), N * H), ge(irgan_cdiv((long)W * C, TPB), N * H);
-    ssim_h5_kernel<<<gx, TPB, 0, st>>>(a, b, W, C, win, w0, S);
-    ssim_v_kernel<5><<<ge, TPB, 0, st>>>(w0, H, W, C, win, w1, S);
+    constexpr int VR = 8;  // rows per thread in the vertical passes
+    const dim3 gx(irgan_cdiv(W, TPB), N * H), ge(irgan_cdiv((long)W * C, TPB), N * irgan_cdiv(H, VR));
+    const size_t row5 = (size_t)W * C * 2 * sizeof(float), row3 = (size_t)W * C * 3 * sizeof(float);
+    if (row3 <= 64 * 1024) {  // row-staged horizontal passes (W*C <= 5461)
+        ssim_hrow_kernel<2, 5, true><<<N * H, TPB, row5, st>>>(a, b, nullptr, W, C, win, w0, S);
+    } else {
+        ssim_h5_kernel<<<gx, TPB, 0, st>>>(a, b, W, C, win, w0, S);
+    }
+    ssim_v_kernel<5, VR><<<ge, TPB, 0, st>>>(w0, H, W, C, win, w1, S);
     ssim_map_kernel<<<nblocks_red(S), TPB, 0, st>>>(w1, w, w0, loss, S);
-    ssim_h_kernel<3><<<gx, TPB, 0, st>>>(w0, W, C, win, w1, S);
-    ssim_v_kernel<3><<<ge, TPB, 0, st>>>(w1, H, W, C, win, w0, S);
+    if (row3 <= 64 * 1024) {
+        ssim_hrow_kernel<3, 3, false><<<N * H, TPB, row3, st>>>(nullptr, nullptr, w0, W, C, win, w1, S);
+    } else {
+        ssim_h_kernel<3><<<gx, TPB, 0, st>>>(w0, W, C, win, w1, S);
+    }
+    ssim_v_kernel<3, VR><<<ge, TPB, 0, st>>>(w1, H, W, C, win, w0, S);
     ssim_grad_kernel<<<nb, TPB, 0, st>>>(w0, a, b, g, S);
     IRGAN_LAUNCH_CHECK();
     return 0;
