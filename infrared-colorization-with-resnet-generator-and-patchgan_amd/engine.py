@@ -631,14 +631,15 @@ class VGGEngine:
 # ----------------------------------------------------------------------------
 
 def grad_allreduce(t: torch.Tensor, group=None) -> torch.Tensor:
-    """In-place mean of a flat gradient buffer over the data-parallel ranks.
+    """In-place mean of a flat gradient buffer over the data-parallel ranks, as
+    one blocking collective.
 
     Every loss of the step is a mean of per-sample terms and InstanceNorm is
     per-sample, so the mean of the per-rank grads over equal shards is the
-    global-batch gradient.  One collective per optimizer on the
-    whole flat buffer (D: 11 MB, G: 46 MB fp32): on xGMI a single large ring
-    all-reduce beats bucketing at this size.  RCCL averages natively; gloo
-    (the CPU test backend) sums and we scale.
+    global-batch gradient.  GANStep itself uses the overlapped
+    form (BucketedAllreduce); this whole-buffer helper is the reference
+    semantics the DP tests splice into the oracle step.  RCCL averages
+    natively; gloo (the CPU test backend) sums and we scale.
     """
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()):

@@ -644,7 +644,7 @@ def validate_kaist(model: IRColorizationModel, val_loader, device):
 def dp_loaders(train_ds, val_ds, batch_size, seed=0):
     """Train/val loaders (ir:1575-1581).  With world > 1 every rank gets an equal
     shard of whole per-rank batches (DistributedSampler, drop_last) so that the
-    gradient all-reduce (engine.grad_allreduce) averages equal-sized batch means:
+    gradient all-reduce (engine.BucketedAllreduce) averages equal-sized batch means:
     ``batch_size`` is per rank, the global batch is batch_size * world."""
     rank, world = _dp()
     if world == 1:
