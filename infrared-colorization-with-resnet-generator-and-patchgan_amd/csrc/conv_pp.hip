@@ -79,11 +79,12 @@ struct PP {
     static_assert(256 * RSB <= LDS && BN % 64 == 0 && WU * 8 * 1024 == BBYTES && NJ * 16 * CW == BN, "tile");
 };
 
-template <int KH, int KW, int BN, bool ACC>
+template <int KH, int KW, int BN, bool ACC, bool STATS = false>
 __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
                                                          const bf16_t* __restrict__ w, const float* __restrict__ bias,
                                                          void* __restrict__ y, const void* __restrict__ mask,
-                                                         int ntn, int tpx, int tpy, int swz) {
+                                                         int ntn, int tpx, int tpy, int swz,
+                                                         float2* __restrict__ part = nullptr) {
     constexpr int TAPS = KH * KW, HWd = PW + KW - 1, HROWS = (PH + KH - 1) * HWd, HP = (HROWS + 7) / 8;
     constexpr int BBYTES = PP<BN>::BBYTES, LDS = PP<BN>::LDS, NJ = PP<BN>::NJ, WU = PP<BN>::WU, RSB = PP<BN>::RSB;
     constexpr int MI = PP<BN>::MIW, RW = PP<BN>::RW;
@@ -339,6 +340,46 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
     __syncthreads();
     constexpr int LPP = PP<BN>::LPP;
     constexpr int PPASS = PP<BN>::PPASS;
+    if (STATS) {
+        // InstanceNorm statistics of the stored (bf16) outputs fused into the store
+        // pass: per-channel (sum, sum of squares) over this block's valid pixels, one
+        // float2 partial per (image, patch, channel) in the layout finalize_kernel
+        // (norm.hip) reduces.  Host guarantees Cout % BN == 0, LPP * PPASS == 512.
+        static_assert(!STATS || PP<BN>::LPP * PP<BN>::PPASS == 512, "all threads store");
+        const int c8 = (tid % LPP) * 8, co8 = n0 + c8;
+        float s1[8], s2[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.f;
+        for (int m = tid / LPP; m < 256; m += PPASS) {
+            const long pix = pix_of(m);
+            if (pix < 0) continue;
+            const uint4 v = *(const uint4*)(smem + m * RSB + c8 * 2);
+            *(uint4*)((bf16_t*)y + pix * d.ldy + d.yoff + co8) = v;
+            const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float lo = __uint_as_float(wv[k] << 16), hi = __uint_as_float(wv[k] & 0xffff0000u);
+                s1[2 * k] += lo; s2[2 * k] += lo * lo;
+                s1[2 * k + 1] += hi; s2[2 * k + 1] += hi * hi;
+            }
+        }
+        __syncthreads();  // staging reads done: reuse LDS for the cross-row reduction
+        float2* red = (float2*)smem;  // [PPASS][BN]
+#pragma unroll
+        for (int k = 0; k < 8; ++k) red[(tid / LPP) * BN + c8 + k] = make_float2(s1[k], s2[k]);
+        __syncthreads();
+        if (tid < BN) {
+            float a = 0.f, b = 0.f;
+            for (int r = 0; r < PPASS; ++r) {
+                const float2 e = red[r * BN + tid];
+                a += e.x;
+                b += e.y;
+            }
+            const long patch = (long)img * (tpx * tpy) + pyi * tpx + pxi;
+            part[patch * d.Cout + n0 + tid] = make_float2(a, b);
+        }
+        return;
+    }
     if (tid >= PPASS * LPP) return;
     const int c8 = (tid % LPP) * 8, co8 = n0 + c8;
     if (co8 >= d.Cout) return;
@@ -402,5 +443,38 @@ extern "C" int irgan_conv_fwd_pp(const irgan_conv_desc* d, const void* x, const 
         else launch_pp<4, 4, 64>(d, x, w, bias, y, mask, st, swz);
     }
     IRGAN_LAUNCH_CHECK();
+    return 0;
+}
+
+// Forward conv with the InstanceNorm statistics of its output fused into the
+// epilogue (replaces the separate irgan_in_stats pass over y; ir:154-165, 392, 417).
+// part: float2[N * nb * Cout] partials, nb (out) = 16x16 patches per image; reduce
+// them with irgan_in_finalize.  IRGAN_EUNSUPPORTED when the layer is not a plain
+// bf16 ping-pong conv with Cout % 256 == 0 (the caller then runs conv + in_stats).
+extern "C" int irgan_conv_fwd_stats(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
+                                    void* part, int32_t* nb, irgan_stream_t s) {
+    if (!d || !x || !w || !y || !part || !nb) return IRGAN_EINVAL;
+    const bool k33 = d->KH == 3 && d->KW == 3, k44 = d->KH == 4 && d->KW == 4;
+    if (d->dtype != IRGAN_BF16 || d->out_dtype != IRGAN_BF16 || d->accumulate || d->act != IRGAN_ACT_NONE ||
+        d->sy != 1 || d->sx != 1 || d->Cin % 64 || !(k33 || k44) || d->Cout % 256 || d->ldx % 8 || d->xoff % 8 ||
+        d->ldy % 8 || d->yoff % 8 || d->Ho != d->OH || d->Wo != d->OW || d->omy != 1 || d->omx != 1 || d->ooy ||
+        d->oox || (long)d->N * d->H * d->W * d->ldx >= (1L << 30) ||
+        (long)d->Cout * d->KH * d->KW * d->Cin >= (1L << 30) || getenv("IRGAN_NO_FUSED_STATS"))
+        return IRGAN_EUNSUPPORTED;
+    const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH);
+    if (tpx * tpy > IRGAN_IN_PARTS) return IRGAN_EUNSUPPORTED;
+    if ((long)d->N * d->Ho * d->Wo <= 0) return IRGAN_EUNSUPPORTED;
+    static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
+    const int ntn = d->Cout / 256;
+    const int blocks = d->N * tpy * tpx * ntn;
+    hipStream_t st = (hipStream_t)s;
+    if (k33)
+        conv_pp_kernel<3, 3, 256, false, true><<<blocks, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, y,
+                                                                       nullptr, ntn, tpx, tpy, swz, (float2*)part);
+    else
+        conv_pp_kernel<4, 4, 256, false, true><<<blocks, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, y,
+                                                                       nullptr, ntn, tpx, tpy, swz, (float2*)part);
+    IRGAN_LAUNCH_CHECK();
+    *nb = tpx * tpy;
     return 0;
 }

@@ -217,18 +217,35 @@ class INLayer:
     the reference's fp32 autograd produces rounding noise there.
     By default the exact zero is kept (no reduction, no atomics); set
     ``INLayer.sum_bias_grad = True`` to accumulate the fp32 sum of dx instead.
+    ``fused_stats``: take the forward statistics from the producing conv's epilogue
+    where a fused kernel exists (irgan_conv_fwd_stats) instead of a separate pass.
     """
+    fused_stats = True
     sum_bias_grad = False
 
     def __init__(self):
         self.mr = None
 
-    def fwd(self, bufs: Buffers, name: str, x: Feat, y: Feat, act, res: Feat = None, xhat=None):
+    def fwd(self, bufs: Buffers, name: str, x: Feat, y: Feat, act, res: Feat = None, xhat=None, nb=0):
+        """nb > 0: x's statistics partials are already in the shared work buffer
+        (written by the producing conv, conv_fwd); only the reduction runs."""
         N, C = x.N, x.C
         work = bufs.flat("in_work", ops.IN_PARTS * N * C, torch.float64)
         self.mr = bufs.get("mr_" + name, (N * C * 2,), torch.float32)
-        ops.in_stats(x, work, self.mr)
+        if nb:
+            ops.in_finalize(x, work, nb, self.mr)
+        else:
+            ops.in_stats(x, work, self.mr)
         ops.in_apply(x, self.mr, y, act=act, res=res, xhat=xhat)
+
+    def conv_fwd(self, bufs: Buffers, name: str, pc, x: Feat, z: Feat, y: Feat, act, res: Feat = None):
+        """z = conv(x) (kept for the backward), y = act(IN(z) [+ res]): the IN statistics
+        come from the conv's epilogue when it has a fused kernel (ops.conv_fwd_stats)."""
+        work = bufs.flat("in_work", ops.IN_PARTS * z.N * z.C, torch.float64)
+        nb = ops.conv_fwd_stats(pc, x, z, work) if INLayer.fused_stats else 0
+        if not nb:
+            ops.conv_fwd(pc, x, z)
+        self.fwd(bufs, name, z, y, act, res=res, nb=nb)
 
     def bwd(self, bufs: Buffers, dy: Feat, z: Feat, act, dx: Feat, db=None, dy2: Feat = None):
         """z: the PRE-norm input kept from forward; act: the activation after IN."""
@@ -328,19 +345,16 @@ class GeneratorEngine:
         else:
             z2 = Feat(g.get("z2", (B, H1, W1, c2), T))
             a2 = Feat(g.get("a2", (B, H1, W1, c2), T))
-            ops.conv_fwd(self.down2, x1, z2)
-            self.norms["down2"].fwd(g, "down2", z2, a2, ACT_RELU)
+            self.norms["down2"].conv_fwd(g, "down2", self.down2, x1, z2, a2, ACT_RELU)
             ops.blur_down(a2, h)
         # 9 ResnetBlocks  (ir:362-418, 485-490)
         for b, (p1, p2) in enumerate(self.res):
             r1 = Feat(g.get(f"r1_{b}", (B, H2, W2, c2), T))
             t = Feat(g.get(f"t{b}", (B, H2, W2, c2), T))
-            ops.conv_fwd(p1, h, r1)
-            self.norms[f"r{b}_1"].fwd(g, f"r{b}_1", r1, t, ACT_RELU)
+            self.norms[f"r{b}_1"].conv_fwd(g, f"r{b}_1", p1, h, r1, t, ACT_RELU)
             r2 = Feat(g.get(f"r2_{b}", (B, H2, W2, c2), T))
-            ops.conv_fwd(p2, t, r2)
             hn = Feat(g.get(f"h{b + 1}", (B, H2, W2, c2), T))
-            self.norms[f"r{b}_2"].fwd(g, f"r{b}_2", r2, hn, ACT_NONE, res=h)
+            self.norms[f"r{b}_2"].conv_fwd(g, f"r{b}_2", p2, t, r2, hn, ACT_NONE, res=h)
             h = hn
         # up1 -> cat with x1 -> conv/IN/ReLU  (ir:554-558)
         y1 = Feat(cat1, 0, c2)
@@ -512,8 +526,7 @@ class DiscriminatorEngine:
                 ops.conv_fwd(pc, x, y)
             else:
                 z = Feat(g.get(f"{tag}z{i}", (x.N, Ho, Wo, pc.spec.cout), T))
-                ops.conv_fwd(pc, x, z)
-                self.norms[i].fwd(g, f"{tag}n{i}", z, y, ACT_LRELU)
+                self.norms[i].conv_fwd(g, f"{tag}n{i}", pc, x, z, y, ACT_LRELU)
                 self.pre[i] = z
             self.acts.append(y)
             x = y

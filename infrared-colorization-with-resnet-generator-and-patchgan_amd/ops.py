@@ -236,6 +236,34 @@ def conv_fwd(pc: PackedConv, x: Feat, y: Feat, act=ACT_NONE, bias=True, accumula
         mask.ptr if mask else None, stream()))
 
 
+IRGAN_EUNSUPPORTED = 1002   # include/irgan.h
+
+
+def conv_fwd_stats(pc: PackedConv, x: Feat, y: Feat, part: torch.Tensor) -> int:
+    """conv_fwd (no activation) that also writes y's InstanceNorm partials into
+    ``part`` (irgan_conv_fwd_stats).  Returns the partials per image, or 0 when the
+    layer has no fused kernel -- then NOTHING ran and the caller does conv_fwd +
+    in_stats."""
+    s = pc.spec
+    if pc.dtype != BF16 or y.dt != BF16 or s.cout % 256 or s.stride != 1:
+        return 0
+    Ho, Wo = s.out_hw(x.H, x.W)
+    assert (y.H, y.W, y.C) == (Ho, Wo, s.cout) and x.C == pc.cin_eff and y.N == x.N, "conv_fwd shape mismatch"
+    d = _desc(N=x.N, H=x.H, W=x.W, Cin=pc.cin_eff, ldx=x.ld, xoff=x.off, Ho=Ho, Wo=Wo, Cout=s.cout, ldy=y.ld,
+              yoff=y.off, OH=Ho, OW=Wo, omy=1, ooy=0, omx=1, oox=0, KH=s.k, KW=s.k, sy=1, sx=1,
+              c0y=-s.pad, c0x=-s.pad, pad_mode=s.mode, act=ACT_NONE, accumulate=0, dtype=pc.dtype,
+              out_dtype=y.dt, mask_act=0, ldm=0, moff=0)
+    nb = ctypes.c_int32(0)
+    fn = getattr(_lib.load(), "irgan_conv_fwd_stats")
+    rc = TIMER.wrap(conv_tag("fwd", s, (x.H, x.W), x.N), lambda: fn(
+        ctypes.byref(d), x.ptr, P(pc.fwd), P(pc.bias), y.ptr, P(part), ctypes.byref(nb), stream()))
+    if rc == IRGAN_EUNSUPPORTED:
+        return 0
+    if rc != 0:
+        raise _lib.IrganError(f"irgan_conv_fwd_stats failed with code {rc}")
+    return int(nb.value)
+
+
 RING_MFMA = not os.environ.get("IRGAN_NO_RING_MFMA")
 
 
@@ -344,6 +372,11 @@ def _wgrad_ws(dev):
 
 def in_stats(x: Feat, work: torch.Tensor, mr: torch.Tensor):
     _lib.call("irgan_in_stats", x.ptr, x.dt, x.N, x.H * x.W, x.C, x.ld, x.off, P(work), P(mr), stream())
+
+
+def in_finalize(x: Feat, part: torch.Tensor, nb: int, mr: torch.Tensor):
+    """{mean, rstd} of x from the nb per-image partials irgan_conv_fwd_stats wrote."""
+    _lib.call("irgan_in_finalize", P(part), x.N, x.H * x.W, x.C, nb, P(mr), stream())
 
 
 def in_apply(x: Feat, mr, y: Feat, act=ACT_NONE, res: Feat = None, xhat: torch.Tensor = None):

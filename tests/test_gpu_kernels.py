@@ -302,3 +302,32 @@ def test_weight_pack_batch_matches_single_packs(ops, dtype):
         got = ([pc.fwd] if code == ops.BF16 else []) + [b for *_, b in pc.dg]
         for g, r in zip(got, ref):
             assert torch.equal(g, r)
+
+
+@pytest.mark.parametrize("case", [(256, 256, 3, 1, 64, 2), (128, 256, 3, 0, 37, 2), (256, 512, 4, 0, 31, 2)])
+def test_conv_fwd_fused_in_stats(ops, case):
+    """irgan_conv_fwd_stats (conv_pp epilogue writes the IN partials of its bf16
+    output) + irgan_in_finalize == irgan_conv_fwd + irgan_in_stats: same output bits,
+    (mean, rstd) equal to fp32 rounding (different summation order)."""
+    cin, cout, k, mode, H, N = case
+    torch.manual_seed(4)
+    spec = ops.ConvSpec(cin, cout, k, 1, 1, mode)
+    w = torch.randn(cout * k * k * cin, device=DEV) * (1.0 / (cin * k * k) ** 0.5)
+    b = torch.randn(cout, device=DEV) * 0.1
+    pc = ops.PackedConv(spec, w, b, ops.BF16)
+    pc.pack()
+    x = ops.Feat(torch.randn(N, H, H, cin, device=DEV).bfloat16())
+    Ho, Wo = spec.out_hw(H, H)
+    y0 = ops.Feat(torch.empty(N, Ho, Wo, cout, device=DEV, dtype=torch.bfloat16))
+    y1 = ops.Feat(torch.empty(N, Ho, Wo, cout, device=DEV, dtype=torch.bfloat16))
+    work = torch.empty(ops.IN_PARTS * N * cout, dtype=torch.float64, device=DEV)
+    mr0 = torch.empty(N * cout * 2, device=DEV)
+    mr1 = torch.empty(N * cout * 2, device=DEV)
+    ops.conv_fwd(pc, x, y0)
+    ops.in_stats(y0, work, mr0)
+    nb = ops.conv_fwd_stats(pc, x, y1, work)
+    assert nb == ((Ho + 15) // 16) * ((Wo + 15) // 16)
+    ops.in_finalize(y1, work, nb, mr1)
+    torch.cuda.synchronize()
+    assert torch.equal(y0.t, y1.t)
+    torch.testing.assert_close(mr1, mr0, rtol=2e-5, atol=1e-6)
