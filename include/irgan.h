@@ -63,11 +63,12 @@ typedef struct irgan_conv_desc {
 int irgan_conv_fwd(const irgan_conv_desc* d, const void* x, const void* w,
                    const float* bias, void* y, const void* mask, irgan_stream_t s);
 
-/* irgan_conv_fwd (bf16, stride 1, 3x3 / 4x4, Cout % 256 == 0, no activation) that
+/* irgan_conv_fwd (bf16, stride 1, 3x3 / 4x4, no activation) that
  * also writes the InstanceNorm statistics of its output -- the conv -> IN pairs of
  * ResnetBlock and the encoder / D (ir:386-392, 405-411, 468-470, 606-624) -- as
  * float2 (sum, sum of squares) partials part[n][b][c], b < *nb (16x16 patches per
- * image, <= IRGAN_IN_PARTS); irgan_in_finalize turns them into {mean, rstd}.
+ * image, <= IRGAN_IN_PARTS; Cout % 64 == 0 except 192); irgan_in_finalize turns them
+ * into {mean, rstd}.
  * Returns IRGAN_EUNSUPPORTED (nothing launched) for other layers. */
 int irgan_conv_fwd_stats(const irgan_conv_desc* d, const void* x, const void* w,
                          const float* bias, void* y, void* part, int32_t* nb, irgan_stream_t s);
@@ -121,7 +122,7 @@ int irgan_weight_pack_batch(const irgan_pack_desc* descs, int32_t n, irgan_strea
 /* ---- InstanceNorm (ir:154-165), per-(n,c) over H*W, eps 1e-5, no affine ---- */
 /* Reductions are two-level and atomic-free: <= IRGAN_IN_PARTS block partials per
  * (n, c) summed in fp64 in a fixed order. */
-enum { IRGAN_IN_PARTS = 128 };
+enum { IRGAN_IN_PARTS = 256 };
 /* mr[n][c] = {mean, rstd} from nb float2 (sum, sum of squares) partials per (n, c)
  * written by irgan_conv_fwd_stats (the reduction half of irgan_in_stats). */
 int irgan_in_finalize(const void* part, int32_t N, int32_t HW, int32_t C, int32_t nb, float* mr,

@@ -340,7 +340,7 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
     __syncthreads();
     constexpr int LPP = PP<BN>::LPP;
     constexpr int PPASS = PP<BN>::PPASS;
-    if (STATS) {
+    if constexpr (STATS) {
         // InstanceNorm statistics of the stored (bf16) outputs fused into the store
         // pass: per-channel (sum, sum of squares) over this block's valid pixels, one
         // float2 partial per (image, patch, channel) in the layout finalize_kernel
@@ -368,9 +368,28 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
 #pragma unroll
         for (int k = 0; k < 8; ++k) red[(tid / LPP) * BN + c8 + k] = make_float2(s1[k], s2[k]);
         __syncthreads();
+        // two-level fixed-order sum over the PPASS row groups: NR = 512 / BN threads per
+        // channel each add PPASS / NR rows, then one thread per channel adds the NR
+        constexpr int NR = 512 / BN, RPT = PPASS / NR;
+        static_assert(RPT * NR == PPASS, "row split");
+        float a = 0.f, b = 0.f;
+        {
+            const int c = tid % BN, r0 = tid / BN;
+#pragma unroll
+            for (int r = 0; r < RPT; ++r) {
+                const float2 e = red[(r0 * RPT + r) * BN + c];
+                a += e.x;
+                b += e.y;
+            }
+        }
+        __syncthreads();
+        red[tid] = make_float2(a, b);  // [NR][BN]
+        __syncthreads();
         if (tid < BN) {
-            float a = 0.f, b = 0.f;
-            for (int r = 0; r < PPASS; ++r) {
+            a = 0.f;
+            b = 0.f;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
                 const float2 e = red[r * BN + tid];
                 a += e.x;
                 b += e.y;
@@ -450,13 +469,15 @@ extern "C" int irgan_conv_fwd_pp(const irgan_conv_desc* d, const void* x, const 
 // epilogue (replaces the separate irgan_in_stats pass over y; ir:154-165, 392, 417).
 // part: float2[N * nb * Cout] partials, nb (out) = 16x16 patches per image; reduce
 // them with irgan_in_finalize.  IRGAN_EUNSUPPORTED when the layer is not a plain
-// bf16 ping-pong conv with Cout % 256 == 0 (the caller then runs conv + in_stats).
+// bf16 ping-pong conv with Cout % 64 == 0, Cout != 192 (the caller then runs conv +
+// in_stats).
 extern "C" int irgan_conv_fwd_stats(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
                                     void* part, int32_t* nb, irgan_stream_t s) {
     if (!d || !x || !w || !y || !part || !nb) return IRGAN_EINVAL;
     const bool k33 = d->KH == 3 && d->KW == 3, k44 = d->KH == 4 && d->KW == 4;
     if (d->dtype != IRGAN_BF16 || d->out_dtype != IRGAN_BF16 || d->accumulate || d->act != IRGAN_ACT_NONE ||
-        d->sy != 1 || d->sx != 1 || d->Cin % 64 || !(k33 || k44) || d->Cout % 256 || d->ldx % 8 || d->xoff % 8 ||
+        d->sy != 1 || d->sx != 1 || d->Cin % 64 || !(k33 || k44) || d->Cout % 64 || d->Cout == 192 || d->ldx % 8 ||
+        d->xoff % 8 ||
         d->ldy % 8 || d->yoff % 8 || d->Ho != d->OH || d->Wo != d->OW || d->omy != 1 || d->omx != 1 || d->ooy ||
         d->oox || (long)d->N * d->H * d->W * d->ldx >= (1L << 30) ||
         (long)d->Cout * d->KH * d->KW * d->Cin >= (1L << 30) || getenv("IRGAN_NO_FUSED_STATS"))
@@ -465,15 +486,19 @@ extern "C" int irgan_conv_fwd_stats(const irgan_conv_desc* d, const void* x, con
     if (tpx * tpy > IRGAN_IN_PARTS) return IRGAN_EUNSUPPORTED;
     if ((long)d->N * d->Ho * d->Wo <= 0) return IRGAN_EUNSUPPORTED;
     static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
-    const int ntn = d->Cout / 256;
+    const int bn = d->Cout % 256 == 0 ? 256 : (d->Cout % 128 == 0 ? 128 : 64);  // as irgan_conv_fwd_pp
+    const int ntn = d->Cout / bn;
     const int blocks = d->N * tpy * tpx * ntn;
     hipStream_t st = (hipStream_t)s;
-    if (k33)
-        conv_pp_kernel<3, 3, 256, false, true><<<blocks, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, y,
-                                                                       nullptr, ntn, tpx, tpy, swz, (float2*)part);
-    else
-        conv_pp_kernel<4, 4, 256, false, true><<<blocks, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, y,
-                                                                       nullptr, ntn, tpx, tpy, swz, (float2*)part);
+#define PPS(KHV, BNV)                                                                                              \
+    conv_pp_kernel<KHV, KHV, BNV, false, true><<<blocks, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, \
+                                                                       y, nullptr, ntn, tpx, tpy, swz, (float2*)part)
+    if (k33) {
+        if (bn == 256) PPS(3, 256); else if (bn == 128) PPS(3, 128); else PPS(3, 64);
+    } else {
+        if (bn == 256) PPS(4, 256); else if (bn == 128) PPS(4, 128); else PPS(4, 64);
+    }
+#undef PPS
     IRGAN_LAUNCH_CHECK();
     *nb = tpx * tpy;
     return 0;

@@ -16,7 +16,7 @@ namespace {
 
 constexpr int TPB = 256;
 constexpr int V = 8;          // channels per thread
-constexpr int IN_PARTS = 128; // max blocks (partials) per image; work = IN_PARTS*N*C doubles
+constexpr int IN_PARTS = 128; // max rows-kernel blocks (partials) per image (<= IRGAN_IN_PARTS, the work size)
 
 IRGAN_HD void ld8(const void* p, int dt, long i, float* o) {
     if (dt == IRGAN_BF16) {
@@ -516,7 +516,7 @@ extern "C" int irgan_in_stats(const void* x, int32_t dtype, int32_t N, int32_t H
 extern "C" int irgan_in_finalize(const void* part, int32_t N, int32_t HW, int32_t C, int32_t nb, float* mr,
                                  irgan_stream_t s) {
     if ((long)N * HW * C <= 0) return 0;
-    if (!part || !mr || nb < 1 || nb > IN_PARTS) return IRGAN_EINVAL;
+    if (!part || !mr || nb < 1 || nb > IRGAN_IN_PARTS) return IRGAN_EINVAL;
     finalize_kernel<<<dim3(irgan_cdiv(C, 32), N), 256, 0, (hipStream_t)s>>>((const float2*)part, mr, N, C, nb, HW, 0);
     IRGAN_LAUNCH_CHECK();
     return 0;

@@ -333,8 +333,7 @@ class GeneratorEngine:
         else:
             z1 = Feat(g.get("z1", (B, H, W, c1), T))
             a1 = Feat(g.get("a1", (B, H, W, c1), T))
-            ops.conv_fwd(self.down1, x0, z1)
-            self.norms["down1"].fwd(g, "down1", z1, a1, ACT_RELU)
+            self.norms["down1"].conv_fwd(g, "down1", self.down1, x0, z1, a1, ACT_RELU)
             ops.blur_down(a1, x1)
         # down2 (+ blur-down)  (ir:477-482)
         h = Feat(g.get("h0", (B, H2, W2, c2), T))
@@ -364,8 +363,7 @@ class GeneratorEngine:
             ops.upsample(h, y1)
         z3 = Feat(g.get("z3", (B, H1, W1, c1), T))
         a3 = Feat(g.get("a3", (B, H1, W1, c1), T))
-        ops.conv_fwd(self.up1, Feat(cat1), z3)
-        self.norms["up1"].fwd(g, "up1", z3, a3, ACT_RELU)
+        self.norms["up1"].conv_fwd(g, "up1", self.up1, Feat(cat1), z3, a3, ACT_RELU)
         # up2 -> cat with x0 -> conv/IN/ReLU  (ir:561-565)
         y2 = Feat(cat2, 0, c1)
         if self.no_aa_up:
@@ -374,8 +372,7 @@ class GeneratorEngine:
             ops.upsample(a3, y2)
         z4 = Feat(g.get("z4", (B, H, W, c0), T))
         a4 = Feat(g.get("a4", (B, H, W, c0), T))
-        ops.conv_fwd(self.up2, Feat(cat2), z4)
-        self.norms["up2"].fwd(g, "up2", z4, a4, ACT_RELU)
+        self.norms["up2"].conv_fwd(g, "up2", self.up2, Feat(cat2), z4, a4, ACT_RELU)
         # outc: reflect-pad 3, conv7x7 (+bias), tanh  (ir:527-531)
         fake = g.get("fake", (B, H, W, self.output_nc), torch.float32)
         ops.conv_fwd(self.outc, a4, Feat(fake), act=ACT_TANH)

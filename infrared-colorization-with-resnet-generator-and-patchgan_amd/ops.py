@@ -245,7 +245,7 @@ def conv_fwd_stats(pc: PackedConv, x: Feat, y: Feat, part: torch.Tensor) -> int:
     layer has no fused kernel -- then NOTHING ran and the caller does conv_fwd +
     in_stats."""
     s = pc.spec
-    if pc.dtype != BF16 or y.dt != BF16 or s.cout % 256 or s.stride != 1:
+    if pc.dtype != BF16 or y.dt != BF16 or s.cout % 64 or s.cout == 192 or s.stride != 1:
         return 0
     Ho, Wo = s.out_hw(x.H, x.W)
     assert (y.H, y.W, y.C) == (Ho, Wo, s.cout) and x.C == pc.cin_eff and y.N == x.N, "conv_fwd shape mismatch"

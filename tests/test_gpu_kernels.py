@@ -304,7 +304,8 @@ def test_weight_pack_batch_matches_single_packs(ops, dtype):
             assert torch.equal(g, r)
 
 
-@pytest.mark.parametrize("case", [(256, 256, 3, 1, 64, 2), (128, 256, 3, 0, 37, 2), (256, 512, 4, 0, 31, 2)])
+@pytest.mark.parametrize("case", [(256, 256, 3, 1, 64, 2), (128, 256, 3, 0, 37, 2), (256, 512, 4, 0, 31, 2),
+                                  (384, 128, 3, 0, 40, 2), (192, 64, 3, 0, 256, 1)])
 def test_conv_fwd_fused_in_stats(ops, case):
     """irgan_conv_fwd_stats (conv_pp epilogue writes the IN partials of its bf16
     output) + irgan_in_finalize == irgan_conv_fwd + irgan_in_stats: same output bits,
