@@ -49,42 +49,73 @@ def pmc_traffic(family):
         return None
 
 
-def cpu_baseline(H, W, batch=1, budget_s=20.0):
-    """The CPU oracle (fp32 PyTorch-CPU restatement of ir:1636-1681) on host cores."""
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def _time_oracle(O, G, D, V, ir, rgb, threads, budget_s, min_steps, max_steps):
+    """Median seconds per oracle step on `threads` torch CPU threads (1 warm-up)."""
+    import torch
+    torch.set_num_threads(threads)
+    oG, oD = O.AdamState(G), O.AdamState(D)
+    O.train_step(G, D, V, ir, rgb, oG, oD)  # warm-up (allocator, oneDNN primitives for these shapes)
+    times, t_start = [], time.perf_counter()
+    while len(times) < max_steps:
+        t0 = time.perf_counter()
+        O.train_step(G, D, V, ir, rgb, oG, oD)
+        times.append(time.perf_counter() - t0)
+        if len(times) >= min_steps and time.perf_counter() - t_start >= budget_s:
+            break
+    times.sort()
+    return times[len(times) // 2], len(times)
+
+
+def cpu_baseline(H, W, batch=16, budget_s=12.0):
+    """The CPU oracle (fp32 PyTorch-CPU restatement of ir:1636-1681, oracle/step.py)
+    at the bench's own config (batch, H x W), on ALL host CPUs (os.cpu_count()
+    torch threads) and, when the host has more, on 16 threads (the
+    per-GPU CPU share of the pool); the faster one is `value`, both are reported.
+    Median of the timed steps after one warm-up step each."""
     import torch
     from oracle import step as O
-    threads = min(os.cpu_count() or 1, 16)
-    torch.set_num_threads(threads)
     G = O.seeded_params(O.g_param_shapes(), 0)
     D = O.seeded_params(O.d_param_shapes(), 1)
     V = O.seeded_params(O.vgg_param_shapes(), 3, kaiming=True)
     g = torch.Generator().manual_seed(7)
     ir = torch.rand(batch, 1, H, W, generator=g) * 2 - 1
     rgb = torch.rand(batch, 3, H, W, generator=g) * 2 - 1
-    oG, oD = O.AdamState(G), O.AdamState(D)
-    O.train_step(G, D, V, ir, rgb, oG, oD)  # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
-        O.train_step(G, D, V, ir, rgb, oG, oD)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or n >= 60:
-            break
-    return {"value": round(n * batch / el, 4), "unit": "img/s", "cores": threads, "kind": "port",
-            "sample": f"{n} oracle steps of batch {batch} at {H}x{W} fp32 after 1 warm-up ({el:.1f}s, "
-                      f"torch CPU threads={threads}, {os.cpu_count()} host CPUs)"}
+    ncpu = os.cpu_count() or 1
+    runs = {}
+    for threads in sorted({ncpu, min(ncpu, 16)}, reverse=True):
+        med, n = _time_oracle(O, G, D, V, ir, rgb, threads, budget_s, 2, 10)
+        runs[threads] = {"img_per_s": round(batch / med, 4), "s_per_step_median": round(med, 3), "steps": n}
+    best = max(runs, key=lambda t: runs[t]["img_per_s"])
+    return {"value": runs[best]["img_per_s"], "unit": "img/s", "cores": best, "kind": "port",
+            "cpu_model": _cpu_model(), "nproc": ncpu, "torch_threads": best,
+            "by_threads": {str(t): r for t, r in runs.items()},
+            "sample": f"oracle/step.py train_step at batch {batch}, {H}x{W}, fp32 (the bench config): "
+                      f"median of {runs[best]['steps']} steps after 1 warm-up, {best} torch threads "
+                      f"on {ncpu} host CPUs ({_cpu_model()})"}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--batch", type=int, default=16, help="per-GPU batch")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds per CPU thread-count run")
     args = ap.parse_args()
 
     import torch
@@ -127,9 +158,13 @@ def main():
     torch.cuda.synchronize()
     ops.TIMER.tags = set(res_tags)
     ops.TIMER.enabled = True
+    # per-step HIP events (no host sync inside the timed region) for the median
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    evs[0].record()
+    for i in range(args.steps):
         L = tr.step(ir, rgb)
+        evs[i + 1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -141,6 +176,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t)
     timing = ops.TIMER.summary()
+    step_ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
+    median_ms = step_ms[len(step_ms) // 2]
     losses = tr.losses(L)
 
     if rank == 0:
@@ -162,7 +199,9 @@ def main():
         step_tflops = value * min_gflop_per_img(H, W) / 1e3 / world
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "img/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+            "warmup": args.warmup, "ms_per_step": round(ms, 3),
+            "ms_per_step_median": round(median_ms, 3), "img_per_s_median_step": round(B * world / median_ms * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (U(-1,1) IR/RGB pairs, seeded; random-init weights)",
             "config": {"workload": f"GAN train step {H}x{W}, batch {B}/GPU (BASELINE configs[1]"
                                    f"{' / [2]' if world > 1 else ''})", "global_batch": B * world,
@@ -178,7 +217,7 @@ def main():
             "losses": {k: round(v, 5) for k, v in losses.items()},
         }
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(H, W, 1, args.cpu_budget)
+            out["cpu_baseline"] = cpu_baseline(H, W, B, args.cpu_budget)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

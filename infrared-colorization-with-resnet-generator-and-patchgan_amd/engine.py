@@ -181,10 +181,17 @@ def _pc(store: ParamStore, key: str, spec: ConvSpec, dtype, need_dgrad=True, bia
 
 
 class Buffers:
-    """Static device buffers keyed by name (allocated once per shape)."""
+    """Device buffers keyed by name (allocated once per shape) plus the forward
+    state a backward needs (``state``: activation lists, the input shape).
+
+    The fused step reuses one long-lived set per engine.  The module API
+    (autograd.Function wrappers) gives every forward call a fresh set that its
+    ctx keeps until the backward, so interleaved calls -- netD(real), netD(fake),
+    then backward (ir:1642-1650) -- each back-propagate through their own
+    activations and InstanceNorm statistics."""
 
     def __init__(self, device):
-        self.device, self.d = device, {}
+        self.device, self.d, self.state = device, {}, {}
 
     def get(self, name, shape, dtype):
         t = self.d.get(name)
@@ -223,20 +230,18 @@ class INLayer:
     fused_stats = True
     sum_bias_grad = False
 
-    def __init__(self):
-        self.mr = None
-
     def fwd(self, bufs: Buffers, name: str, x: Feat, y: Feat, act, res: Feat = None, xhat=None, nb=0):
         """nb > 0: x's statistics partials are already in the shared work buffer
-        (written by the producing conv, conv_fwd); only the reduction runs."""
+        (written by the producing conv, conv_fwd); only the reduction runs.
+        The {mean, rstd} table stays in ``bufs`` under ``name`` for bwd()."""
         N, C = x.N, x.C
         work = bufs.flat("in_work", ops.IN_PARTS * N * C, torch.float64)
-        self.mr = bufs.get("mr_" + name, (N * C * 2,), torch.float32)
+        mr = bufs.get("mr_" + name, (N * C * 2,), torch.float32)
         if nb:
-            ops.in_finalize(x, work, nb, self.mr)
+            ops.in_finalize(x, work, nb, mr)
         else:
-            ops.in_stats(x, work, self.mr)
-        ops.in_apply(x, self.mr, y, act=act, res=res, xhat=xhat)
+            ops.in_stats(x, work, mr)
+        ops.in_apply(x, mr, y, act=act, res=res, xhat=xhat)
 
     def conv_fwd(self, bufs: Buffers, name: str, pc, x: Feat, z: Feat, y: Feat, act, res: Feat = None):
         """z = conv(x) (kept for the backward), y = act(IN(z) [+ res]): the IN statistics
@@ -247,12 +252,13 @@ class INLayer:
             ops.conv_fwd(pc, x, z)
         self.fwd(bufs, name, z, y, act, res=res, nb=nb)
 
-    def bwd(self, bufs: Buffers, dy: Feat, z: Feat, act, dx: Feat, db=None, dy2: Feat = None):
+    def bwd(self, bufs: Buffers, name: str, dy: Feat, z: Feat, act, dx: Feat, db=None, dy2: Feat = None):
         """z: the PRE-norm input kept from forward; act: the activation after IN."""
         N, C = z.N, z.C
         work = bufs.flat("in_work", ops.IN_PARTS * N * C, torch.float64)
         red = bufs.flat("in_red", 2 * N * C)
-        ops.in_backward(dy, z, act, self.mr, work, red, dx, db=db if INLayer.sum_bias_grad else None, dy2=dy2)
+        mr = bufs.d["mr_" + name]
+        ops.in_backward(dy, z, act, mr, work, red, dx, db=db if INLayer.sum_bias_grad else None, dy2=dy2)
 
 
 # ----------------------------------------------------------------------------
@@ -291,7 +297,6 @@ class GeneratorEngine:
                       [f"r{b}_{i}" for b in range(n_blocks) for i in (1, 2)]}
         assert len(self.norms) == n_in
         self.bufs = Buffers(store.device)
-        self.shape = None
 
     def pack(self):
         if self._pack_batch is None:
@@ -304,16 +309,14 @@ class GeneratorEngine:
         H2, W2 = (H1 - 1) // 2 + 1, (W1 - 1) // 2 + 1
         return H1, W1, H2, W2
 
-    def forward(self, ir_nchw: torch.Tensor, keep=True) -> torch.Tensor:
-        """ir (B, input_nc, H, W) fp32 in [-1,1] -> fake NHWC fp32 (B, H, W, 3)."""
+    def forward(self, ir_nchw: torch.Tensor, bufs: Buffers = None) -> torch.Tensor:
+        """ir (B, input_nc, H, W) fp32 in [-1,1] -> fake NHWC fp32 (B, H, W, 3).
+        Activations land in ``bufs`` (default: the engine's own set)."""
         B, _, H, W = ir_nchw.shape
-        if H % 4 or W % 4:
-            raise NotImplementedError("the HIP generator path needs H, W divisible by 4 "
-                                      "(the reference's odd-size resize fallback ir:555-556 is not ported)")
-        g, T = self.bufs, self.tdt
+        g, T = bufs or self.bufs, self.tdt
         c0, c1, c2 = self.ngf, 2 * self.ngf, 4 * self.ngf
         H1, W1, H2, W2 = self._dims(H, W)
-        self.shape = (B, H, W)
+        g.state["shape"] = (B, H, W)
         ir_buf = g.zeros("ir", (B, H, W, max(8, self.input_nc)), T)   # narrow input zero-padded to 8 ch
         ops.nchw_to_nhwc(ir_nchw.contiguous(), Feat(ir_buf, 0, self.input_nc))
         ir_t = Feat(ir_buf, 0, self.inc.cin_eff)
@@ -356,9 +359,12 @@ class GeneratorEngine:
             self.norms[f"r{b}_2"].conv_fwd(g, f"r{b}_2", p2, t, r2, hn, ACT_NONE, res=h)
             h = hn
         # up1 -> cat with x1 -> conv/IN/ReLU  (ir:554-558)
+        # (odd sizes: the up-sampled map is 2*H2 x 2*W2 != H1 x W1 and is resized to the
+        # skip's size, ir:555-556 -- folded into the UpsampleAA table, or a resize launch
+        # after the ConvTranspose2d)
         y1 = Feat(cat1, 0, c2)
         if self.no_aa_up:
-            ops.conv_dgrad(self.up1_up, h, y1, bias=True)
+            self._convt(self.up1_up, h, y1, g, "ut1")
         else:
             ops.upsample(h, y1)
         z3 = Feat(g.get("z3", (B, H1, W1, c1), T))
@@ -367,7 +373,7 @@ class GeneratorEngine:
         # up2 -> cat with x0 -> conv/IN/ReLU  (ir:561-565)
         y2 = Feat(cat2, 0, c1)
         if self.no_aa_up:
-            ops.conv_dgrad(self.up2_up, a3, y2, bias=True)
+            self._convt(self.up2_up, a3, y2, g, "ut2")
         else:
             ops.upsample(a3, y2)
         z4 = Feat(g.get("z4", (B, H, W, c0), T))
@@ -378,15 +384,38 @@ class GeneratorEngine:
         ops.conv_fwd(self.outc, a4, Feat(fake), act=ACT_TANH)
         return fake
 
-    def backward(self, dfake: torch.Tensor, ready=None):
+    def _convt(self, pc, x: Feat, y: Feat, g: Buffers, name: str):
+        """ConvTranspose2d(k3, s2, p1, op1) (ir:495-500) into y, through a 2H x 2W
+        temporary + bilinear resize when y's size is not 2x (ir:555-556)."""
+        if (y.H, y.W) == (2 * x.H, 2 * x.W):
+            ops.conv_dgrad(pc, x, y, bias=True)
+            return
+        t = Feat(g.get(name, (x.N, 2 * x.H, 2 * x.W, y.C), self.tdt))
+        ops.conv_dgrad(pc, x, t, bias=True)
+        ops.resize(t, y)
+
+    def _convt_bwd(self, pc, key, dy: Feat, x: Feat, dx: Feat, g: Buffers, name: str):
+        """Backward of _convt: bias grad, weight grad, and dx (the conv forward of the
+        transposed conv); dy is the gradient at the skip-sized output."""
+        S = self.store
+        if (dy.H, dy.W) != (2 * x.H, 2 * x.W):
+            t = Feat(g.get(name + "_d", (x.N, 2 * x.H, 2 * x.W, dy.C), self.tdt))
+            ops.resize_bwd(dy, t)
+            dy = t
+        ops.channel_sum(dy, S.krsc(key + ".bias", S.grad))
+        ops.conv_wgrad(pc.spec, dy, x, S.krsc(key + ".weight", S.grad), self.dtype)
+        ops.conv_fwd(pc, dy, dx, bias=False)
+
+    def backward(self, dfake: torch.Tensor, ready=None, bufs: Buffers = None):
         """dfake: dL/dfake, NHWC fp32 (B,H,W,3).  Accumulates into store.grad.
+        ``bufs``: the set the matching forward wrote (default: the engine's own).
 
         ``ready(key)``, if given, is called each time every gradient from parameter
         ``key`` to the end of the flat buffer is final (reverse layer order), so the
         caller can start reducing that tail while the rest of the backward runs."""
         ready = ready or (lambda key: None)
-        B, H, W = self.shape
-        g, T, S, dt = self.bufs, self.tdt, self.store, self.dtype
+        g, T, S, dt = bufs or self.bufs, self.tdt, self.store, self.dtype
+        B, H, W = g.state["shape"]
         c0, c1, c2 = self.ngf, 2 * self.ngf, 4 * self.ngf
         H1, W1, H2, W2 = self._dims(H, W)
         G = S.grad
@@ -408,7 +437,7 @@ class GeneratorEngine:
         da4 = Feat(g.get("da4", (B, H, W, c0), T))
         ops.conv_dgrad(self.outc, Feat(dzo_buf, 0, self.outc.cout_eff), da4, pad_buf=padbuf)
         # up2_conv
-        self.norms["up2"].bwd(g, da4, Feat(g.d["z4"]), ACT_RELU, da4, db=S.krsc("up2_conv.0.bias", G))
+        self.norms["up2"].bwd(g, "up2", da4, Feat(g.d["z4"]), ACT_RELU, da4, db=S.krsc("up2_conv.0.bias", G))
         wg(self.up2, "up2_conv.0", cat2, da4)
         dcat2 = Feat(g.get("dcat2", (B, H, W, c1 + c0), T))
         ops.conv_dgrad(self.up2, da4, dcat2)
@@ -417,13 +446,11 @@ class GeneratorEngine:
         da3 = Feat(g.get("da3", (B, H1, W1, c1), T))
         dy2 = dcat2.sl(0, c1)
         if self.no_aa_up:
-            ops.channel_sum(dy2, S.krsc("up2_up.bias", G))
-            wg(self.up2_up, "up2_up", dy2, a3)
-            ops.conv_fwd(self.up2_up, dy2, da3, bias=False)
+            self._convt_bwd(self.up2_up, "up2_up", dy2, a3, da3, g, "ut2")
         else:
             ops.upsample_bwd(dy2, da3)
         # up1_conv
-        self.norms["up1"].bwd(g, da3, Feat(g.d["z3"]), ACT_RELU, da3, db=S.krsc("up1_conv.0.bias", G))
+        self.norms["up1"].bwd(g, "up1", da3, Feat(g.d["z3"]), ACT_RELU, da3, db=S.krsc("up1_conv.0.bias", G))
         wg(self.up1, "up1_conv.0", cat1, da3)
         dcat1 = Feat(g.get("dcat1", (B, H1, W1, c2 + c1), T))
         ops.conv_dgrad(self.up1, da3, dcat1)
@@ -432,9 +459,7 @@ class GeneratorEngine:
         dh = Feat(g.get("dh", (B, H2, W2, c2), T))
         dy1 = dcat1.sl(0, c2)
         if self.no_aa_up:
-            ops.channel_sum(dy1, S.krsc("up1_up.bias", G))
-            wg(self.up1_up, "up1_up", dy1, h9)
-            ops.conv_fwd(self.up1_up, dy1, dh, bias=False)
+            self._convt_bwd(self.up1_up, "up1_up", dy1, h9, dh, g, "ut1")
         else:
             ops.upsample_bwd(dy1, dh)
         ready("up1_up.weight" if self.no_aa_up else "up1_conv.0.weight")
@@ -445,23 +470,23 @@ class GeneratorEngine:
             key = f"resblocks.{b}.conv_block."
             t, hb = Feat(g.d[f"t{b}"]), Feat(g.d[f"h{b}"])
             r1, r2 = Feat(g.d[f"r1_{b}"]), Feat(g.d[f"r2_{b}"])
-            self.norms[f"r{b}_2"].bwd(g, dh, r2, ACT_NONE, dt_, db=S.krsc(key + "5.bias", G))
+            self.norms[f"r{b}_2"].bwd(g, f"r{b}_2", dh, r2, ACT_NONE, dt_, db=S.krsc(key + "5.bias", G))
             wg(p2, key + "5", t, dt_)
             dr = Feat(g.get("dtmp2", (B, H2, W2, c2), T))
             ops.conv_dgrad(p2, dt_, dr, pad_buf=padbuf)
-            self.norms[f"r{b}_1"].bwd(g, dr, r1, ACT_RELU, dr, db=S.krsc(key + "1.bias", G))
+            self.norms[f"r{b}_1"].bwd(g, f"r{b}_1", dr, r1, ACT_RELU, dr, db=S.krsc(key + "1.bias", G))
             wg(p1, key + "1", hb, dr)
             ops.conv_dgrad(p1, dr, dh, accumulate=True, pad_buf=padbuf)
             ready(key + "1.weight")
         # down2 (+ blur-down)
         z2 = Feat(g.d["z2"])
         if self.no_aa:
-            self.norms["down2"].bwd(g, dh, z2, ACT_RELU, dh, db=S.krsc("down2.0.bias", G))
+            self.norms["down2"].bwd(g, "down2", dh, z2, ACT_RELU, dh, db=S.krsc("down2.0.bias", G))
             dz2 = dh
         else:
             dz2 = Feat(g.get("da2", (B, H1, W1, c2), T))
             ops.blur_down_bwd(dh, dz2)
-            self.norms["down2"].bwd(g, dz2, z2, ACT_RELU, dz2, db=S.krsc("down2.0.bias", G))
+            self.norms["down2"].bwd(g, "down2", dz2, z2, ACT_RELU, dz2, db=S.krsc("down2.0.bias", G))
         wg(self.down2, "down2.0", x1, dz2)
         dx1 = dcat1.sl(c2, c1)
         ops.conv_dgrad(self.down2, dz2, dx1, accumulate=True)  # x1 feeds down2 and the up1 concat
@@ -469,16 +494,16 @@ class GeneratorEngine:
         z1 = Feat(g.d["z1"])
         if self.no_aa:
             dz1 = Feat(g.get("da1", (B, H1, W1, c1), T))
-            self.norms["down1"].bwd(g, dx1, z1, ACT_RELU, dz1, db=S.krsc("down1.0.bias", G))
+            self.norms["down1"].bwd(g, "down1", dx1, z1, ACT_RELU, dz1, db=S.krsc("down1.0.bias", G))
         else:
             dz1 = Feat(g.get("da1", (B, H, W, c1), T))
             ops.blur_down_bwd(dx1, dz1)
-            self.norms["down1"].bwd(g, dz1, z1, ACT_RELU, dz1, db=S.krsc("down1.0.bias", G))
+            self.norms["down1"].bwd(g, "down1", dz1, z1, ACT_RELU, dz1, db=S.krsc("down1.0.bias", G))
         wg(self.down1, "down1.0", x0, dz1)
         dx0 = dcat2.sl(c1, c0)
         ops.conv_dgrad(self.down1, dz1, dx0, accumulate=True)
         # inc
-        self.norms["inc"].bwd(g, dx0, Feat(g.d["z0"]), ACT_RELU, dx0, db=S.krsc("inc.1.bias", G))
+        self.norms["inc"].bwd(g, "inc", dx0, Feat(g.d["z0"]), ACT_RELU, dx0, db=S.krsc("inc.1.bias", G))
         wg(self.inc, "inc.1", Feat(g.d["ir"]), dx0)
         ready("inc.1.weight")
 
@@ -507,12 +532,13 @@ class DiscriminatorEngine:
             self._pack_batch = ops.PackBatch(self.packs)
         self._pack_batch.run()
 
-    def forward(self, din: Feat, tag="") -> torch.Tensor:
-        """din: NHWC (NB, H, W, 4) compute-dtype -> patch logits (NB, h, w, 1) fp32."""
-        g, T = self.bufs, self.tdt
+    def forward(self, din: Feat, tag="", bufs: Buffers = None) -> torch.Tensor:
+        """din: NHWC (NB, H, W, 4) compute-dtype -> patch logits (NB, h, w, 1) fp32.
+        The activations are kept in ``bufs`` (default: the engine's own) under ``tag``."""
+        g, T = bufs or self.bufs, self.tdt
         x = din
-        self.acts = [din]
-        self.pre = {}
+        acts, pre = [din], {}
+        g.state[tag] = (acts, pre)
         for i, pc in enumerate(self.packs):
             Ho, Wo = pc.spec.out_hw(x.H, x.W)
             last = i == len(self.packs) - 1
@@ -524,15 +550,16 @@ class DiscriminatorEngine:
             else:
                 z = Feat(g.get(f"{tag}z{i}", (x.N, Ho, Wo, pc.spec.cout), T))
                 self.norms[i].conv_fwd(g, f"{tag}n{i}", pc, x, z, y, ACT_LRELU)
-                self.pre[i] = z
-            self.acts.append(y)
+                pre[i] = z
+            acts.append(y)
             x = y
         return x.t
 
-    def backward(self, dout: torch.Tensor, want_wgrad=True, want_dinput=False, tag=""):
+    def backward(self, dout: torch.Tensor, want_wgrad=True, want_dinput=False, tag="", bufs: Buffers = None):
         """dout: dL/dlogits fp32 (same shape as forward output).  Weight grads
         accumulate into store.grad; returns d input (fp32 NHWC) if asked."""
-        g, T, S = self.bufs, self.tdt, self.store
+        g, T, S = bufs or self.bufs, self.tdt, self.store
+        acts, pre = g.state[tag]
         G = S.grad
         n = len(self.packs)
         dbuf = g.zeros(f"{tag}dout_t", tuple(dout.shape[:3]) + (8,), T)   # 1-ch logits grad, padded to 8
@@ -540,12 +567,12 @@ class DiscriminatorEngine:
         dy = Feat(dbuf, 0, self.packs[-1].cout_eff)
         for i in reversed(range(n)):
             pc, key = self.packs[i], self.LAYERS[i][0]
-            x = self.acts[i]
+            x = acts[i]
             if i == n - 1:
                 if want_wgrad:
                     ops.channel_sum(Feat(dout), S.krsc(key + ".bias", G))
             elif self.norms[i] is not None:
-                self.norms[i].bwd(g, dy, self.pre[i], ACT_LRELU, dy,
+                self.norms[i].bwd(g, f"{tag}n{i}", dy, pre[i], ACT_LRELU, dy,
                                   db=S.krsc(key + ".bias", G) if want_wgrad else None)
             elif want_wgrad:  # layer 0: LReLU mask already folded into dy by the layer-1 dgrad
                 ops.channel_sum(dy, S.krsc(key + ".bias", G))
@@ -589,27 +616,27 @@ class VGGEngine:
             self._pack_batch = ops.PackBatch(self.packs)
         self._pack_batch.run()
 
-    def forward(self, vin: Feat) -> Feat:
-        g, T = self.bufs, self.tdt
+    def forward(self, vin: Feat, bufs: Buffers = None) -> Feat:
+        g, T = bufs or self.bufs, self.tdt
         x = vin
-        self.acts = [vin]
+        acts = g.state["acts"] = [vin]
         for j, pc in enumerate(self.packs):
             y = Feat(g.get(f"v{j}", (x.N, x.H, x.W, pc.spec.cout), T))
             ops.conv_fwd(pc, x, y, act=ACT_RELU)
-            self.acts.append(y)
+            acts.append(y)
             x = y
             if j in (1, 3):
                 p = Feat(g.get(f"p{j}", (x.N, x.H // 2, x.W // 2, x.C), T))
                 ops.maxpool(x, p)
-                self.acts.append(p)
+                acts.append(p)
                 x = p
         return x
 
-    def backward_input(self, dfeat: Feat, nb: int) -> Feat:
+    def backward_input(self, dfeat: Feat, nb: int, bufs: Buffers = None) -> Feat:
         """d(input) for the first nb images (frozen weights: backward-data only).
         dfeat = dL/d(relu3_3 output) for those images."""
-        g, T = self.bufs, self.tdt
-        acts = [a.batch(0, nb) for a in self.acts]
+        g, T = bufs or self.bufs, self.tdt
+        acts = [a.batch(0, nb) for a in g.state["acts"]]
         # acts: [vin, v0, v1, p1, v2, v3, p3, v4, v5, v6]
         out_of = {0: 1, 1: 2, 2: 4, 3: 5, 4: 7, 5: 8, 6: 9}     # conv j output index in acts
         in_of = {0: 0, 1: 1, 2: 3, 3: 4, 4: 6, 5: 7, 6: 8}      # conv j input index in acts
@@ -628,6 +655,8 @@ class VGGEngine:
                 ops.conv_dgrad(pc, dz, dp)
                 src = acts[prev - 1]
                 dzn = Feat(g.get(f"dz{j - 1}", (nb, src.H, src.W, src.C), T))
+                if src.H % 2 or src.W % 2:   # floor pooling: the last odd row / column gets no gradient
+                    dzn.t.zero_()
                 ops.maxpool_bwd(src, dp, dzn, relu_mask=True)
             else:  # input is a ReLU output: fold relu' into the dgrad epilogue
                 dzn = Feat(g.get(f"dz{j - 1}", (nb, xin.H, xin.W, xin.C), T))

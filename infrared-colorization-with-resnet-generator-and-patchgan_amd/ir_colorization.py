@@ -29,14 +29,14 @@ import torch
 import torch.nn as nn
 
 from . import ops
-from .engine import (DiscriminatorEngine, GANStep, GeneratorEngine, ParamStore, VGGEngine, d_param_shapes,
-                     g_param_shapes, vgg_param_shapes)
+from .engine import (Buffers, DiscriminatorEngine, GANStep, GeneratorEngine, ParamStore, VGGEngine,
+                     d_param_shapes, g_param_shapes, vgg_param_shapes)
 from .ops import BF16, F32, Feat
 
 __all__ = ["Config", "Identity", "get_norm_layer", "init_weights", "init_net", "get_lr_lambda", "get_filter",
            "ResnetUNetGenerator", "NLayerDiscriminator", "VGGPerceptual", "tv_loss", "ssim_loss_torch",
            "IRColorizationModel", "GANTrainer", "validate_kaist", "train_kaist", "SyntheticPairDataset",
-           "g_param_shapes", "d_param_shapes", "vgg_param_shapes", "seeded_state", "dp_loaders"]
+           "g_param_shapes", "d_param_shapes", "vgg_param_shapes", "seeded_state", "dp_loaders", "val_shard"]
 
 
 # =============================================================================
@@ -256,22 +256,30 @@ class _StoreModule(nn.Module):
 # 3-4) Generator (ir:425-569)
 # =============================================================================
 
+# Every autograd-recorded forward below runs on its OWN engine buffer set
+# (engine.Buffers), held by its ctx until the backward: the reference interleaves
+# calls before one backward (netD(real), netD(fake), loss_D.backward() ir:1642-1650;
+# vgg_perc(fake), vgg_perc(rgb) ir:1667-1668), so each call must back-propagate
+# through its own activations, ReLU/LReLU masks, maxpool argmaxes and IN statistics.
+
 class _GFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, mod, *params):
-        fake = mod.engine.forward(x.float())
-        ctx.mod = mod
+        bufs = Buffers(x.device)
+        fake = mod.engine.forward(x.float(), bufs=bufs)
+        ctx.mod, ctx.bufs = mod, bufs
         out = torch.empty(fake.shape[0], fake.shape[3], fake.shape[1], fake.shape[2], device=x.device)
         ops.nhwc_to_nchw(Feat(fake), out)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        mod = ctx.mod
+        mod, bufs = ctx.mod, ctx.bufs
+        ctx.bufs = None
         dnhwc = torch.empty(dout.shape[0], dout.shape[2], dout.shape[3], dout.shape[1], device=dout.device)
         ops.nchw_to_nhwc(dout.contiguous().float(), Feat(dnhwc))
         mod.store.zero_grad()
-        mod.engine.backward(dnhwc)
+        mod.engine.backward(dnhwc, bufs=bufs)
         grads = [mod.store.oihw(k, mod.store.grad).clone() for k, _ in mod.named_parameters()]
         return (None, None, *grads)
 
@@ -343,16 +351,18 @@ def _nhwc_input(x, pc, tdt, scale=None, shift=None):
 class _DFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, mod, *params):
-        out = mod.engine.forward(_nhwc_input(x, mod.engine.packs[0], mod.engine.tdt), tag="api")
-        ctx.mod = mod
+        bufs = Buffers(x.device)
+        out = mod.engine.forward(_nhwc_input(x, mod.engine.packs[0], mod.engine.tdt), tag="api", bufs=bufs)
+        ctx.mod, ctx.bufs = mod, bufs
         return out.permute(0, 3, 1, 2).contiguous()
 
     @staticmethod
     def backward(ctx, dout):
-        mod = ctx.mod
+        mod, bufs = ctx.mod, ctx.bufs
+        ctx.bufs = None
         mod.store.zero_grad()
         dn = dout.permute(0, 2, 3, 1).contiguous().float()
-        dx = mod.engine.backward(dn, want_wgrad=True, want_dinput=True, tag="api")
+        dx = mod.engine.backward(dn, want_wgrad=True, want_dinput=True, tag="api", bufs=bufs)
         B, H, W, C = dx.t.shape
         gx = torch.empty(B, C, H, W, device=dout.device)
         ops.nhwc_to_nchw(dx, gx)
@@ -393,16 +403,18 @@ class NLayerDiscriminator(_StoreModule):
 class _VFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, mod):
-        feat = mod._features(x)
-        ctx.mod = mod
+        bufs = Buffers(x.device)
+        feat = mod._features(x, bufs)
+        ctx.mod, ctx.bufs = mod, bufs
         ctx.n = x.shape[0]
         return feat.t.permute(0, 3, 1, 2).float().contiguous()
 
     @staticmethod
     def backward(ctx, dfeat):
-        mod = ctx.mod
+        mod, bufs = ctx.mod, ctx.bufs
+        ctx.bufs = None
         dn = dfeat.permute(0, 2, 3, 1).contiguous().to(mod.engine.tdt)
-        dv = mod.engine.backward_input(Feat(dn), ctx.n)
+        dv = mod.engine.backward_input(Feat(dn), ctx.n, bufs=bufs)
         dimg = torch.zeros(dv.N, dv.H, dv.W, dv.C, device=dfeat.device)
         ops.affine(dv, mod.engine.scale, None, Feat(dimg))
         out = torch.empty(dv.N, dv.C, dv.H, dv.W, device=dfeat.device)
@@ -439,11 +451,11 @@ class VGGPerceptual(_StoreModule):
         self.engine = VGGEngine(S, _dtype_code(compute_dtype))
         self._dirty = True
 
-    def _features(self, x):
+    def _features(self, x, bufs=None):
         _require_cuda(x, "VGGPerceptual")
         self._maybe_repack()
         vin = _nhwc_input(x, self.engine.packs[0], self.engine.tdt, self.engine.scale, self.engine.shift)
-        return self.engine.forward(vin)
+        return self.engine.forward(vin, bufs=bufs)
 
     def forward(self, x):
         if torch.is_grad_enabled() and x.requires_grad:
@@ -484,31 +496,43 @@ def tv_loss(x):
 
 class _SSIMFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, a, b):
+    def forward(ctx, a, b, size_average):
         # kernel takes [-1,1] images and maps (x+1)/2 itself; feed 2x-1 of the [0,1] inputs
         an, bn = _nhwc32(a * 2 - 1), _nhwc32(b * 2 - 1)
         g = torch.zeros_like(an)
-        loss = torch.zeros(1, dtype=torch.float64, device=a.device)
-        work = torch.empty(10 * an.numel(), device=a.device)
-        ops.ssim(Feat(an), Feat(bn), 1.0, g, loss, work)
+        if size_average:   # 1 - mean over B*C*H*W (ir:744-745): one launch over the batch
+            loss = torch.zeros(1, dtype=torch.float64, device=a.device)
+            work = torch.empty(10 * an.numel(), device=a.device)
+            ops.ssim(Feat(an), Feat(bn), 1.0, g, loss, work)
+        else:              # 1 - per-image mean over C*H*W (ir:746-747): one launch per image
+            B = an.shape[0]
+            loss = torch.zeros(B, dtype=torch.float64, device=a.device)
+            work = torch.empty(10 * an[0].numel(), device=a.device)
+            for i in range(B):
+                ops.ssim(Feat(an[i:i + 1]), Feat(bn[i:i + 1]), 1.0, g[i:i + 1], loss[i:i + 1], work)
         ctx.save_for_backward(g)
-        return loss.float()[0]
+        ctx.size_average = size_average
+        out = loss.float()
+        return out[0] if size_average else out
 
     @staticmethod
     def backward(ctx, gl):
         (g,) = ctx.saved_tensors
         out = torch.empty(g.shape[0], g.shape[3], g.shape[1], g.shape[2], device=g.device)
         ops.nhwc_to_nchw(Feat(g), out, scale=2.0)  # d/d(img01) = 2 * d/d(img[-1,1])
-        return out * gl, None
+        if not ctx.size_average:
+            gl = gl.view(-1, 1, 1, 1)
+        return out * gl, None, None
 
 
 def ssim_loss_torch(img1, img2, window_size=11, size_average=True):
-    """ir:714-750: 1 - SSIM of [0,1] images (11x11 Gaussian, sigma 1.5)."""
+    """ir:714-750: 1 - SSIM of [0,1] images (11x11 Gaussian, sigma 1.5); a scalar,
+    or with size_average=False the per-image vector (B,) of ir:746-747."""
     assert img1.shape == img2.shape, "SSIM images must have the same shape"
-    if window_size != 11 or not size_average:
-        raise NotImplementedError("HIP SSIM implements window_size=11, size_average=True (ir:1677)")
+    if window_size != 11:
+        raise NotImplementedError("HIP SSIM implements window_size=11 (the reference's default, ir:714)")
     _require_cuda(img1, "ssim_loss_torch")
-    return _SSIMFn.apply(img1, img2)
+    return _SSIMFn.apply(img1, img2, bool(size_average))
 
 
 # =============================================================================
@@ -612,7 +636,6 @@ class GANTrainer:
         self.load_state_dict(torch.load(path, map_location="cpu", weights_only=True))
 
 
-@torch.no_grad()
 def _dp():
     """(rank, world) of the data-parallel job, (0, 1) when not distributed."""
     import torch.distributed as dist
@@ -621,9 +644,11 @@ def _dp():
     return 0, 1
 
 
+@torch.no_grad()
 def validate_kaist(model: IRColorizationModel, val_loader, device):
-    """ir:1521-1542: batch-size-weighted mean L1 of G(ir) vs rgb.  Under data
-    parallelism each rank scores its val shard and (sum, count) is all-reduced."""
+    """ir:1521-1542 (under no_grad, ir:1532): batch-size-weighted mean L1 of G(ir)
+    vs rgb.  Under data parallelism each rank scores its val shard (disjoint, no
+    padding duplicates: dp_loaders) and (sum, count) is all-reduced."""
     total, count = 0.0, 0
     for batch in val_loader:
         ir = batch["ir"].to(device)
@@ -655,12 +680,19 @@ def dp_loaders(train_ds, val_ds, batch_size, seed=0):
         return tl, vl, None
     from torch.utils.data.distributed import DistributedSampler
     ts = DistributedSampler(train_ds, num_replicas=world, rank=rank, shuffle=True, seed=seed, drop_last=True)
-    vs = DistributedSampler(val_ds, num_replicas=world, rank=rank, shuffle=False, drop_last=False)
     tl = torch.utils.data.DataLoader(train_ds, batch_size=batch_size, sampler=ts, num_workers=0,
                                      pin_memory=True, drop_last=True)
-    vl = torch.utils.data.DataLoader(val_ds, batch_size=batch_size, sampler=vs, num_workers=0,
-                                     pin_memory=True, drop_last=False)
+    # validation: a strided, disjoint shard per rank WITHOUT DistributedSampler's
+    # padding duplicates, so the all-reduced (sum, count) is exactly the
+    # single-process val L1 (ir:1538-1542) whatever len(val) % world is
+    vl = torch.utils.data.DataLoader(val_shard(val_ds, rank, world), batch_size=batch_size, shuffle=False,
+                                     num_workers=0, pin_memory=True, drop_last=False)
     return tl, vl, ts
+
+
+def val_shard(val_ds, rank, world):
+    """Rank ``rank``'s disjoint strided share of the validation set (no padding)."""
+    return torch.utils.data.Subset(val_ds, list(range(rank, len(val_ds), world)))
 
 
 class SyntheticPairDataset(torch.utils.data.Dataset):

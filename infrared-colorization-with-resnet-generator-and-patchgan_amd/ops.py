@@ -428,27 +428,102 @@ TMAX = 8
 _TABLES = {}
 
 
-def resample_table(kind, n_in, p=0, transpose=False, device=None):
-    """Device (idx, w, rows) per-axis table of a separable resampling map, built by
-    the C ABI on the host (irgan_resample_table) and cached."""
+def _host_table(kind, n_in, p=0, transpose=False):
+    """Host (idx [rows][TMAX], w [rows][TMAX], rows) of a per-axis resampling map,
+    built by the C ABI (irgan_resample_table)."""
     import numpy as np
-    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    cap = 2 * n_in + 2 * p + 8
+    idx = np.zeros(cap * TMAX, np.int32)
+    w = np.zeros(cap * TMAX, np.float32)
+    rows = _lib.load().irgan_resample_table(kind, n_in, p, int(transpose), idx.ctypes.data_as(ctypes.c_void_p),
+                                              w.ctypes.data_as(ctypes.c_void_p), TMAX, cap)
+    if rows < 0:
+        raise _lib.IrganError(f"irgan_resample_table({kind}, {n_in}, {p}) failed: {rows}")
+    return idx[:rows * TMAX].reshape(rows, TMAX), w[:rows * TMAX].reshape(rows, TMAX), rows
+
+
+def _device_table(idx, w, rows, dev):
+    """Device copy of a table; each row's taps start at slot 0, so keep only the
+    widest row's tap count."""
+    import numpy as np
+    T = max(1, int((w != 0).sum(axis=1).max()))
+    return (torch.from_numpy(np.ascontiguousarray(idx[:, :T])).to(dev),
+            torch.from_numpy(np.ascontiguousarray(w[:, :T])).to(dev), rows, T)
+
+
+def _dev(device):
+    return torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+
+
+def resample_table(kind, n_in, p=0, transpose=False, device=None):
+    """Device (idx, w, rows, T) per-axis table of a separable resampling map, cached."""
+    dev = _dev(device)
     key = (kind, n_in, p, bool(transpose), dev)
     t = _TABLES.get(key)
     if t is None:
-        cap = 2 * n_in + 2 * p + 8
-        idx = np.zeros(cap * TMAX, np.int32)
-        w = np.zeros(cap * TMAX, np.float32)
-        rows = _lib.load().irgan_resample_table(kind, n_in, p, int(transpose), idx.ctypes.data_as(ctypes.c_void_p),
-                                                  w.ctypes.data_as(ctypes.c_void_p), TMAX, cap)
-        if rows < 0:
-            raise _lib.IrganError(f"irgan_resample_table({kind}, {n_in}, {p}) failed: {rows}")
-        # the table fills each row's taps from slot 0: keep only the widest row's count
-        idx, w = idx[:rows * TMAX].reshape(rows, TMAX), w[:rows * TMAX].reshape(rows, TMAX)
-        T = max(1, int((w != 0).sum(axis=1).max()))
-        t = (torch.from_numpy(np.ascontiguousarray(idx[:, :T])).to(dev),
-             torch.from_numpy(np.ascontiguousarray(w[:, :T])).to(dev), rows, T)
-        _TABLES[key] = t
+        t = _TABLES[key] = _device_table(*_host_table(kind, n_in, p, transpose), dev)
+    return t
+
+
+def bilinear_matrix(n_in, n_out):
+    """Dense (n_out x n_in) map of F.interpolate(mode='bilinear', align_corners=True)
+    along one axis (ir:555-556, 562-563): source coordinate o*(n_in-1)/(n_out-1),
+    linear weights between its two neighbours (ATen's upsample_bilinear2d)."""
+    import numpy as np
+    M = np.zeros((n_out, n_in), np.float64)
+    scale = (n_in - 1) / (n_out - 1) if n_out > 1 else 0.0
+    for o in range(n_out):
+        src = np.float32(np.float32(scale) * o) if n_out > 1 else 0.0
+        i0 = min(int(src), n_in - 1)
+        i1 = i0 + (1 if i0 < n_in - 1 else 0)
+        lam = float(src) - i0
+        M[o, i0] += 1.0 - lam
+        M[o, i1] += lam
+    return M
+
+
+def _dense(idx, w, rows, n_in):
+    import numpy as np
+    M = np.zeros((rows, n_in), np.float64)
+    for r in range(rows):
+        for t in range(idx.shape[1]):
+            if w[r, t] != 0:
+                M[r, idx[r, t]] += w[r, t]
+    return M
+
+
+def _table_from_dense(M):
+    """(idx, w, rows) table of a dense map (rows x n_in), taps packed from slot 0."""
+    import numpy as np
+    rows = M.shape[0]
+    nz = [np.nonzero(M[r])[0] for r in range(rows)]
+    T = max(1, max(len(z) for z in nz))
+    if T > TMAX:
+        raise _lib.IrganError(f"resampling map needs {T} taps per row (> {TMAX})")
+    idx = np.zeros((rows, TMAX), np.int32)
+    w = np.zeros((rows, TMAX), np.float32)
+    for r, z in enumerate(nz):
+        idx[r, :len(z)] = z
+        w[r, :len(z)] = M[r, z]
+    return idx, w, rows
+
+
+def resize_table(n_in, n_out, after_up=False, transpose=False, device=None):
+    """Per-axis table of the odd-size decoder fallback (ir:555-556, 562-563): the
+    bilinear align_corners resize from the up-sampled length to the skip's length.
+    after_up=True composes it with UpsampleAA (n_in -> 2*n_in -> n_out) into ONE
+    map, so the up-sample + resize is a single sep_resample launch."""
+    import numpy as np
+    dev = _dev(device)
+    key = ("resize", n_in, n_out, bool(after_up), bool(transpose), dev)
+    t = _TABLES.get(key)
+    if t is None:
+        if after_up:
+            M = bilinear_matrix(2 * n_in, n_out) @ _dense(*_host_table(RS_UP, n_in), n_in)
+        else:
+            M = bilinear_matrix(n_in, n_out)
+        M[np.abs(M) < 1e-12] = 0.0
+        t = _TABLES[key] = _device_table(*_table_from_dense(M.T.copy() if transpose else M), dev)
     return t
 
 
@@ -469,13 +544,29 @@ def blur_down_bwd(dy: Feat, dx: Feat, accumulate=False):
                  accumulate)
 
 
+def _up_axis(n_in, n_out, transpose):
+    if n_out == 2 * n_in:
+        return resample_table(RS_UP, n_in, transpose=transpose)
+    return resize_table(n_in, n_out, after_up=True, transpose=transpose)   # odd-size fallback folded in
+
+
 def upsample(x: Feat, y: Feat):
-    """UpsampleAA (ir:313-355)."""
-    sep_resample(x, y, resample_table(RS_UP, x.H), resample_table(RS_UP, x.W))
+    """UpsampleAA (ir:313-355); when y is not 2x (odd skip sizes) the reference's
+    bilinear resize to the skip's size (ir:555-556, 562-563) is folded into the map."""
+    sep_resample(x, y, _up_axis(x.H, y.H, False), _up_axis(x.W, y.W, False))
 
 
 def upsample_bwd(dy: Feat, dx: Feat, work=None, accumulate=False):
-    sep_resample(dy, dx, resample_table(RS_UP, dx.H, transpose=True), resample_table(RS_UP, dx.W, transpose=True),
+    sep_resample(dy, dx, _up_axis(dx.H, dy.H, True), _up_axis(dx.W, dy.W, True), accumulate)
+
+
+def resize(x: Feat, y: Feat, accumulate=False):
+    """F.interpolate(x, size=(y.H, y.W), mode='bilinear', align_corners=True)."""
+    sep_resample(x, y, resize_table(x.H, y.H), resize_table(x.W, y.W), accumulate)
+
+
+def resize_bwd(dy: Feat, dx: Feat, accumulate=False):
+    sep_resample(dy, dx, resize_table(dx.H, dy.H, transpose=True), resize_table(dx.W, dy.W, transpose=True),
                  accumulate)
 
 

@@ -1,0 +1,190 @@
+"""Tight parity for the bf16 kernels the benchmark actually runs.
+
+bf16 mode = bf16 operands, exact bf16 x bf16 products, fp32 accumulation.  So the
+HIP result is compared with an fp64 reference computed on the SAME bf16-quantised
+operands (x, w, dY), not with an unquantised fp32 conv:
+
+    |got - ref64| <= r_out * |ref64| + 2e-5 * absref   (every element)
+
+* ``absref`` is the same op on |x|, |w|, |dY| (the sum of |terms| of each output):
+  2e-5 of it bounds fp32 accumulation-order error with margin (sqrt(K) * eps32 is
+  3e-6 at K = 2304 and 5e-6 at K = 8192 pixels);
+* ``r_out`` = 2^-8 for bf16 outputs (the unit roundoff of an 8-bit significand),
+  0 for fp32.  The reflect-pad dgrad writes its interior first and folds the ring
+  onto the border band afterwards, so a bf16 border pixel is rounded twice: there
+  the bound is 2^-8 * (|ref| + |interior part|).
+
+A kernel that drops, duplicates or misplaces even one output element fails this,
+as do writes outside the output channel slice (checked separately).  Cases cover
+every family the dispatch reaches on the train step: conv_pp (BN 256/192/128/64,
+plain / accumulate / fused-IN-stats), the reflect ring, conv_c8 (incl. stride 2),
+conv_narrow, conv_halo, conv_glds (stride 2, per-phase dgrad), wgrad_halo (row
+segments, slab split-K), wgrad_glds and the generic fallbacks, with ragged tiles.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import pkg
+from test_gpu_kernels import CONV_CASES
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+R_BF16 = 2.0 ** -8
+R_ACC = 2e-5
+
+EXTRA_CASES = [
+    # cin, cout, k, s, p, mode, H : the G / D / VGG layers at odd sizes (ragged 16x16 patches)
+    (256, 256, 3, 1, 1, 1, 37),    # resblock: pp BN256 fwd, ring + pp dgrad
+    (128, 256, 3, 1, 1, 0, 33),    # down2: BN256 fwd, BN128 (accumulating) dgrad
+    (64, 128, 3, 1, 1, 0, 40),     # down1: BN128 fwd, BN64 dgrad
+    (384, 128, 3, 1, 1, 0, 24),    # up1_conv: BN128 fwd, 384-ch dgrad
+    (192, 64, 3, 1, 1, 0, 40),     # up2_conv: BN64 fwd, BN192 dgrad
+    (64, 64, 3, 1, 1, 0, 24),      # VGG conv1_2
+    (256, 512, 4, 1, 1, 0, 13),    # D model.8
+    (128, 256, 4, 2, 1, 0, 34),    # D model.5 (stride 2: glds fwd, per-phase dgrad)
+    (8, 64, 4, 2, 1, 0, 66),       # D model.0 with the 8-channel padded input
+]
+
+
+def q(t):
+    """bf16-representable copy (fp32 storage)."""
+    return t.bfloat16().float()
+
+
+def nhwc(x, dt=torch.bfloat16):
+    return x.permute(0, 2, 3, 1).contiguous().to(DEV, dt)
+
+
+def nchw64(x):
+    return x.double().cpu().permute(0, 3, 1, 2).contiguous()
+
+
+def ref_conv(x, w, b, k, s, p, mode):
+    if mode == 1:
+        x = F.pad(x, (p, p, p, p), mode="reflect")
+        p = 0
+    return F.conv2d(x, w, b, stride=s, padding=p)
+
+
+def references(x, w, b, gy, k, s, p, mode):
+    """fp64 y, dx, dw on the given operands, and the interior part of dx (reflect
+    mode: the padded-domain gradient before the ring is folded back; else dx)."""
+    xr, wr = x.double().requires_grad_(True), w.double().requires_grad_(True)
+    y = ref_conv(xr, wr, None if b is None else b.double(), k, s, p, mode)
+    y.backward(gy.double())
+    interior = xr.grad
+    if mode == 1:
+        xp = F.pad(x.double(), (p, p, p, p), mode="reflect").requires_grad_(True)
+        F.conv2d(xp, w.double(), stride=s).backward(gy.double())
+        interior = xp.grad[..., p:-p, p:-p]
+    return y.detach(), xr.grad, wr.grad, interior
+
+
+def check(got, ref, aref, r_out, what, partial=None):
+    """partial: an intermediate that a bf16 output is rounded to before the rest is
+    added (the reflect dgrad's interior, written before the ring is folded onto the
+    border band): its rounding enters the bound too."""
+    err = (got - ref).abs()
+    mag = ref.abs()
+    if partial is not None:   # pixels that received a ring term were rounded twice
+        twice = (partial - ref).abs() > 1e-9 * aref
+        mag = mag + torch.where(twice, partial.abs(), torch.zeros_like(mag))
+    bound = r_out * mag + R_ACC * aref + 1e-30
+    ratio = (err / bound).max().item()
+    assert ratio <= 1.0, f"{what}: worst |err|/bound = {ratio:.3g}, max |err| {err.max().item():.3g}"
+
+
+@pytest.fixture(scope="module")
+def ops():
+    return pkg().ops
+
+
+@pytest.mark.parametrize("case", CONV_CASES + EXTRA_CASES)
+def test_bf16_conv_family_tight(ops, case):
+    cin, cout, k, s, p, mode, H = case
+    torch.manual_seed(0)
+    N = 2
+    x = q(torch.randn(N, cin, H, H))
+    w = q(torch.randn(cout, cin, k, k) * (1.0 / (cin * k * k) ** 0.5))
+    b = torch.randn(cout) * 0.1
+    spec = ops.ConvSpec(cin, cout, k, s, p, mode)
+    Ho, Wo = spec.out_hw(H, H)
+    gy = q(torch.randn(N, cout, Ho, Wo))
+    y64, dx64, dw64, dxi = references(x, w, b, gy, k, s, p, mode)
+    ya, dxa, dwa, _ = references(x.abs(), w.abs(), b.abs(), gy.abs(), k, s, p, mode)
+
+    master = w.permute(0, 2, 3, 1).contiguous().reshape(-1).to(DEV)
+    pc = ops.PackedConv(spec, master, b.to(DEV), ops.BF16)
+    pc.pack()
+    xd = torch.zeros(N, H, H, pc.cin_eff, device=DEV, dtype=torch.bfloat16)
+    xd[..., :cin] = nhwc(x)
+
+    # forward, bf16 output into a channel slice (ld = cout + 8, off 8) -- the step's layout
+    yb = torch.zeros(N, Ho, Wo, cout + 8, device=DEV, dtype=torch.bfloat16)
+    ops.conv_fwd(pc, ops.Feat(xd), ops.Feat(yb, 8, cout))
+    check(nchw64(yb[..., 8:]), y64, ya, R_BF16, "fwd bf16")
+    assert not yb[..., :8].any(), "fwd wrote outside its channel slice"
+    # forward, fp32 output
+    yf = torch.zeros(N, Ho, Wo, cout, device=DEV, dtype=torch.float32)
+    ops.conv_fwd(pc, ops.Feat(xd), ops.Feat(yf))
+    check(nchw64(yf), y64, ya, 0.0, "fwd fp32")
+
+    # backward-data: dY zero-padded to cout_eff channels
+    gyd = torch.zeros(N, Ho, Wo, pc.cout_eff, device=DEV, dtype=torch.bfloat16)
+    gyd[..., :cout] = nhwc(gy)
+    pad = torch.empty(N * (H + 2 * p) ** 2 * cin, device=DEV) if mode == 1 else None
+    for out_dt, r_out in ((torch.float32, 0.0), (torch.bfloat16, R_BF16)):
+        dx = torch.zeros(N, H, H, cin, device=DEV, dtype=out_dt)
+        ops.conv_dgrad(pc, ops.Feat(gyd), ops.Feat(dx), pad_buf=pad)
+        check(nchw64(dx), dx64, dxa, r_out, f"dgrad {out_dt}", partial=dxi)
+    # backward-data accumulating onto another branch's gradient (bf16, the step's
+    # resblock / down2 / down1 skip paths), into a channel slice when aligned
+    sl = 8 if cin % 8 == 0 else 0
+    old = q(torch.randn(N, cin, H, H))
+    dxb = torch.zeros(N, H, H, cin + sl, device=DEV, dtype=torch.bfloat16)
+    dxb[..., sl:] = nhwc(old)
+    ops.conv_dgrad(pc, ops.Feat(gyd), ops.Feat(dxb, sl, cin), accumulate=True, pad_buf=pad)
+    check(nchw64(dxb[..., sl:]), dx64 + old.double(), dxa + old.double().abs(), R_BF16, "dgrad accumulate",
+          partial=dxi + old.double())
+    assert not dxb[..., :sl].any(), "dgrad wrote outside its channel slice"
+
+    # backward-weight (fp32, split-K slab workspace), accumulated onto an existing value
+    dw0 = torch.randn(cout * k * k * cin, device=DEV)
+    dw = dw0.clone()
+    ops.conv_wgrad(spec, ops.Feat(xd), ops.Feat(gyd, 0, cout), dw, ops.BF16)
+    got = (dw - dw0).view(cout, k, k, cin).permute(0, 3, 1, 2).double().cpu()
+    check(got, dw64, dwa + dw0.abs().max().item() * 1e-2, 0.0, "wgrad")
+
+
+@pytest.mark.parametrize("case", [(256, 256, 3, 1, 64, 2), (256, 256, 3, 1, 37, 2), (128, 256, 3, 0, 33, 2),
+                                  (64, 128, 3, 0, 40, 2), (384, 128, 3, 0, 24, 2), (256, 512, 4, 0, 13, 2),
+                                  (192, 64, 3, 0, 64, 1)])
+def test_bf16_fused_in_stats_tight(ops, case):
+    """conv_pp with the fused InstanceNorm-statistics epilogue: the bf16 output holds
+    the tight bound, and {mean, rstd} equal the fp64 statistics OF THAT bf16 OUTPUT
+    (which is what the IN apply normalises) to fp32 rounding."""
+    cin, cout, k, mode, H, N = case
+    torch.manual_seed(4)
+    spec = ops.ConvSpec(cin, cout, k, 1, 1, mode)
+    x = q(torch.randn(N, cin, H, H))
+    w = q(torch.randn(cout, cin, k, k) * (1.0 / (cin * k * k) ** 0.5))
+    b = torch.randn(cout) * 0.1
+    pc = ops.PackedConv(spec, w.permute(0, 2, 3, 1).contiguous().reshape(-1).to(DEV), b.to(DEV), ops.BF16)
+    pc.pack()
+    Ho, Wo = spec.out_hw(H, H)
+    y = ops.Feat(torch.empty(N, Ho, Wo, cout, device=DEV, dtype=torch.bfloat16))
+    work = torch.empty(ops.IN_PARTS * N * cout, dtype=torch.float64, device=DEV)
+    nb = ops.conv_fwd_stats(pc, ops.Feat(nhwc(x)), y, work)
+    assert nb > 0, "layer did not take the fused-statistics kernel"
+    mr = torch.empty(N * cout * 2, device=DEV)
+    ops.in_finalize(y, work, nb, mr)
+    y64 = ref_conv(x.double(), w.double(), b.double(), k, 1, 1, mode)
+    ya = ref_conv(x.abs().double(), w.abs().double(), b.abs().double(), k, 1, 1, mode)
+    yg = nchw64(y.t)
+    check(yg, y64, ya, R_BF16, "fwd+stats")
+    mean = yg.mean(dim=(2, 3))
+    rstd = (yg.var(dim=(2, 3), unbiased=False) + 1e-5).rsqrt()
+    got = mr.view(N, cout, 2).double().cpu()
+    torch.testing.assert_close(got[..., 0], mean, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(got[..., 1], rstd, rtol=1e-5, atol=1e-6)

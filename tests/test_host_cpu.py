@@ -135,3 +135,32 @@ def test_adam_state_dict_is_torch_optim_layout():
     assert st2.step_count == 7
     for k in st.shapes:   # per-tensor slices (the 64-element alignment padding is not state)
         assert torch.equal(st2.krsc(k, st2.m), st.krsc(k, st.m)) and torch.equal(st2.krsc(k, st2.v), st.krsc(k, st.v))
+
+
+def _table_dense(t, n_in):
+    idx, w, rows, T = t
+    M = np.zeros((rows, n_in), np.float64)
+    for r in range(rows):
+        for k in range(T):
+            M[r, int(idx[r, k])] += float(w[r, k])
+    return M
+
+
+@pytest.mark.parametrize("n_in,n_out", [(13, 25), (12, 23), (63, 125), (5, 9), (3, 1), (10, 21)])
+def test_odd_size_resize_tables_match_reference_ops(n_in, n_out):
+    """The decoder's odd-size fallback (ir:555-556, 562-563) as one per-axis map:
+    UpsampleAA (n_in -> 2 n_in) then F.interpolate(bilinear, align_corners=True) to
+    n_out, composed on the host; and the resize alone (ConvTranspose2d path).
+    Checked against the oracle's ops on a basis; transposes are the adjoints."""
+    ops = pkg().ops
+    filt = O.binomial_filter(3)[None, None].double()
+    X = torch.eye(n_in, dtype=torch.float64)[:, None, :, None] * torch.ones(1, 1, 1, n_in, dtype=torch.float64)
+    up = O.up_aa(X, filt)
+    ref = F.interpolate(up, size=(n_out, n_out), mode="bilinear", align_corners=True)[:, 0, :, 0].T.numpy()
+    M = _table_dense(ops.resize_table(n_in, n_out, after_up=True, device="cpu"), n_in)
+    assert np.allclose(M, ref, atol=1e-6)
+    Mt = _table_dense(ops.resize_table(n_in, n_out, after_up=True, transpose=True, device="cpu"), n_out)
+    assert np.allclose(Mt, M.T, atol=1e-7)
+    ref2 = F.interpolate(X, size=(n_out, n_out), mode="bilinear", align_corners=True)[:, 0, :, 0].T.numpy()
+    M2 = _table_dense(ops.resize_table(n_in, n_out, device="cpu"), n_in)
+    assert np.allclose(M2, ref2, atol=1e-6)
