@@ -13,7 +13,8 @@ import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 HEADER = os.path.join(os.path.dirname(HERE), "include", "irgan.h")
-LIB_PATH = os.path.join(HERE, "libirgan.so")
+# IRGAN_LIB: an alternative build of the same ABI (kernel A/B experiments, tools/)
+LIB_PATH = os.environ.get("IRGAN_LIB") or os.path.join(HERE, "libirgan.so")
 
 F32, BF16 = 0, 1
 PAD_ZERO, PAD_REFLECT = 0, 1

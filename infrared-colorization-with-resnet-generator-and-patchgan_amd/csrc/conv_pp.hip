@@ -42,6 +42,12 @@
 
 #include "conv_epilogue.h"
 
+#ifndef PP_EXP
+#define PP_EXP 0  // A/B timing experiments only (tools/build_variant.sh); 0 = the real kernel
+#endif
+// bits: 1 no MFMA, 2 no weight DMA in the loop, 4 no fragment reads, 8 no barriers in the loop, 16 no epilogue
+#define PPX(b) ((PP_EXP & (b)) != 0)
+
 namespace {
 
 IRGAN_HD int lds_off(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
@@ -50,7 +56,9 @@ IRGAN_HD void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
 // block barrier that the scheduler cannot move instructions across
 IRGAN_HD void phase_barrier() {
     sched_fence();
+#if !PPX(8)
     lds_barrier();
+#endif
     sched_fence();
 }
 IRGAN_HD void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
@@ -199,6 +207,7 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
                 const int bb = h ? bb1 : bb0;
                 int hbp = hb;
                 asm volatile("" : "+v"(hbp));  // per-phase base: the address adds stay here, not hoisted
+#if !PPX(4)
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) bfr[j] = *(const uint4*)(B + bb + j * 2048);
 #pragma unroll
@@ -206,7 +215,15 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
                     const int K = (i + ty) * HWd + tx;
                     af[i] = *(const uint4*)(sH + (hbp + (tsw[K & 7] ^ (h * 64))) + K * 128);
                 }
-                if (h == 0) {
+#else
+                if (k == 0 && h == 0) {
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j) bfr[j] = *(const uint4*)(B + bb + j * 2048);
+#pragma unroll
+                    for (int i = 0; i < MI; ++i) af[i] = *(const uint4*)(sH + hbp + i * 128);
+                }
+#endif
+                if (h == 0 && !PPX(2)) {
                     // W(k+1) (W(1) came with the prologue), then the next chunk's halo
                     if (k >= 1 && !last_k) {
                         if (tp + 1 < TAPS) issue_w(c, tp + 1, (k + 1) & 1);
@@ -221,7 +238,7 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
                 phase_barrier();
                 // ---- MFMA phase: C^T fragment (weights as A, pixels as B)
 #pragma unroll
-                for (int i = 0; i < MI; ++i)
+                for (int i = 0; i < MI * !PPX(1); ++i)
 #pragma unroll
                     for (int j = 0; j < NJ; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, bfr[j]),
@@ -234,6 +251,17 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
     }
     if (grp == 0) phase_barrier();  // match group 1's extra barrier
     __syncthreads();                // all operand reads done: LDS becomes the staging buffer
+#if PPX(16)
+    {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) s += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+        if (s == 123.f) *(float*)y = s;
+        return;
+    }
+#endif
 
     // ---- epilogue.  Fragment (i, j): pixel m = (prow + i)*16 + (lane & 15),
     // channels co = n0 + cb + j*16 + 4*(lane >> 4) + r, r = 0..3.

@@ -21,6 +21,12 @@
 // (split-K over segments).
 #include "common.h"
 
+#ifndef WG_EXP
+#define WG_EXP 0  // A/B timing experiments only (tools/build_variant.sh); 0 = the real kernel
+#endif
+// bits: 1 no MFMA, 2 no DMA in the loop, 4 no fragment reads, 8 no barrier in the loop, 16 no epilogue
+#define WGX(b) ((WG_EXP & (b)) != 0)
+
 namespace {
 
 __device__ __attribute__((aligned(4096))) bf16_t g_wgh_zero_page[2048];
@@ -149,14 +155,25 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void wgrad_halo_kernel(const irgan
         } else {
             wait_vmcnt<0>();
         }
+#if !WGX(8)
         lds_barrier();
-        if (kt + 2 < nk) issue(s_beg + kt + 2, (kt + 2) % STAGES);
+#endif
+        if (kt + 2 < nk && !WGX(2)) issue(s_beg + kt + 2, (kt + 2) % STAGES);
         const char* A = smem + (kt % STAGES) * STAGE;
         const char* X = A + APIECES * 1024;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {  // two 32-pixel MFMA k-steps per segment
             const int k_lo = 32 * h + 8 * g + q, k_hi = k_lo + 4;
             uint4 af[MI], bfr[NJ];
+#if WGX(4)
+            if (kt > 0) {
+#pragma unroll
+                for (int i = 0; i < MI; ++i) af[i] = make_uint4(kt, h, i, lane);
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) bfr[j] = make_uint4(kt, j, h, lane);
+            } else
+#endif
+            {
 #pragma unroll
             for (int i = 0; i < MI; ++i) {
                 const int col = (wm * MI + i) * 16 + 4 * p;
@@ -179,8 +196,9 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void wgrad_halo_kernel(const irgan
                 }
                 bfr[j] = tr_pair(X + img_off<128>(plo, col), X + img_off<128>(phi, col));
             }
+            }
 #pragma unroll
-            for (int i = 0; i < MI; ++i)
+            for (int i = 0; i < MI * !WGX(1); ++i)
 #pragma unroll
                 for (int j = 0; j < NJ; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[i]),
@@ -192,6 +210,17 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void wgrad_halo_kernel(const irgan
     // partials: plain stores into this split's slab (summed in a fixed order by
     // wgrad_slab_reduce) or, without a slab, fp32 atomics into dw.
     const int K = d.KH * KW * d.Cin;
+#if WGX(16)
+    {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) s += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+        if (s == 123.f) dw[0] = s;
+        return;
+    }
+#endif
     float* const dst = slab ? slab + (long)split * d.Cout * K : nullptr;
 #pragma unroll
     for (int i = 0; i < MI; ++i)

@@ -1,0 +1,360 @@
+// bf16 backward-weight convolution, producer/consumer form (3x3, stride 1,
+// Cout % 128 == 0, Cin % 64 == 0, Wo % 64 == 0): the ResnetBlock weight
+// gradients (ir:390, 411) and the encoder / decoder 3x3 convs that qualify
+// (down1, down2, up1_conv: ir:470, 478, 504).
+//
+//   dW[co][ty][tx][ci] += sum_p dY[p][co] * X[iy(p, ty)][ix(p, tx)][ci]
+//
+// Same work decomposition as conv_wgrad_halo.hip: a block owns (128-channel co
+// tile, 64-channel ci chunk, kernel row ty, all three tx taps) and walks 64-pixel
+// row segments of dY (split-K over segments); per segment the dY tile
+// [64 px][128 co] and ONE input row span [66][64 ci] sit in LDS and the three tx
+// taps are row shifts of the span.  What is different is who does what
+// (measured on the halo kernel: 5 VALU per MFMA, fragment reads and DMA issue
+// serialised with the MFMAs):
+//
+//  * 8 waves: waves 0-3 only compute (one per SIMD), waves 4-7 only load (one
+//    per SIMD).  A loader wave issues its ~6 LDS-DMA pieces per segment with
+//    precomputed per-lane offsets (dY: a lane-invariant offset + the segment's
+//    scalar soffset; X span: a few VALU per piece for the reflect / zero edge),
+//    so the compute waves issue no VMEM and almost no VALU;
+//  * 4-stage LDS ring (4 x 25 KiB), one s_barrier per segment, the DMA two
+//    segments ahead of its consumer: the loaders retire segment k+1 with a
+//    counted vmcnt before barrier k, then issue segment k+3 into the stage that
+//    segment k-1 (fully consumed before barrier k) used;
+//  * compute waves keep two fragment register sets: the reads of the next half
+//    segment (32 pixels) are issued before the MFMAs of the current one, and
+//    every fragment address is a precomputed per-lane offset plus the stage base
+//    (the read for pixel rows +4 / +32 is an immediate offset: the XOR swizzles
+//    below do not change over those steps).
+//
+// LDS images (conflict-free ds_read_b64_tr_b16, as conv_wgrad_halo.hip):
+//   dY, 256-B rows: 16-B chunk XOR 2*((r&3)|((r>>3&1)<<2));
+//   X span, 128-B rows: chunk XOR 2*((r>>1&1)|((r>>3&1)<<1)).
+// Split-K partials go to a caller slab (plain stores, ordered reduce) or, with
+// no slab, fp32 atomics into dW.
+#include "common.h"
+
+#ifndef PC_EXP
+#define PC_EXP 0  // A/B timing experiments only (tools/build_variant.sh); 0 = the real kernel
+#endif
+// bits: 1 loaders skip the in-loop vmcnt wait, 2 no DMA in the loop, 4 no fragment reads, 8 no barriers,
+// 16 compiler-scheduled reads (no sched_group_barrier), 32 s_setprio 1 on the compute waves
+#define PCX(b) ((PC_EXP & (b)) != 0)
+
+namespace {
+
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((address_space(3))) s16x4 lds_s4;
+
+IRGAN_HD int pc_t128(int r) { return ((r >> 1) & 1) | (((r >> 3) & 1) << 1); }
+IRGAN_HD int pc_t256(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
+
+constexpr int BMC = 128;                 // co tile
+constexpr int KW = 3;
+constexpr int APIECES = 64 * BMC * 2 / 1024;  // dY tile: 16 pieces of 4 pixel rows
+constexpr int XPOS = 66;                 // X span positions (63 + KW)
+constexpr int XPIECES = 9;               // 72 positions, 8 per piece
+constexpr int TP = APIECES + XPIECES;    // 25 pieces per segment
+constexpr int STAGE = TP * 1024;
+constexpr int STAGES = 4;
+constexpr int NJ = 3;                    // 3 (tx, 16-ci) fragments per compute wave
+constexpr int PPL = (TP + 3) / 4;        // max pieces per loader wave (7)
+// CW compute waves: 4 -> 128 co x 48 n per wave (1 per SIMD); 8 -> 64 co x 48 n (2 per SIMD)
+template <int CW>
+struct PC {
+    static constexpr int MI = BMC / 16 / (CW / 4);  // co fragments per compute wave
+    static constexpr int NT = (CW + 4) * 64;        // threads: CW compute + 4 loader waves
+};
+
+IRGAN_HD uint4 ld_tr_pair(const char* lo, const char* hi) {
+    const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)lo);
+    const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)hi);
+    uint4 out;
+    __builtin_memcpy(&out, &a, 8);
+    __builtin_memcpy((char*)&out + 8, &b, 8);
+    return out;
+}
+
+template <int MI>
+struct Frag {
+    uint4 a[MI], b[NJ];
+};
+
+template <int CW>
+__global__ __launch_bounds__(PC<CW>::NT, 1) void wgrad_pc_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
+                                                          const bf16_t* __restrict__ dy, float* __restrict__ dw,
+                                                          int segs_per_block, int nseg, int ntco, int nci, int swz,
+                                                          float* __restrict__ slab) {
+    __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    constexpr int MI = PC<CW>::MI;
+    const bool loader = wid >= CW;
+    const int tiles = ntco * nci * d.KH;
+    const int t = xcd_tile(blockIdx.x, gridDim.x, swz);
+    const int split = t / tiles;
+    int r = t - split * tiles;
+    const int ty = r % d.KH;
+    r /= d.KH;
+    const int cic = r % nci, cot = r / nci;
+    const int co0 = cot * BMC, ci0 = cic * 64;
+    const int s_beg = split * segs_per_block;
+    const int s_end = min(nseg, s_beg + segs_per_block);
+    if (s_beg >= s_end) return;  // block-uniform
+    const int nk = s_end - s_beg;
+    const int segs_row = d.Wo / 64;
+
+    if (loader) {
+        // ------------------------------------------------------------------
+        // loader wave l issues pieces j = l, l+4, ... (< TP) of every segment
+        const int l = wid - CW;
+        const int np = (TP - l + 3) / 4;  // 7 for l = 0, else 6
+        const bool reflect = d.pad_mode == IRGAN_PAD_REFLECT;
+        // dY: buffer base at dy + yoff + co0; lane offset fixed per piece, the
+        // segment's first pixel enters as the scalar soffset
+        const i32x4 rs_dy = make_rsrc(dy + d.yoff + co0,
+                                      (uint32_t)(((long)d.N * d.Ho * d.Wo * d.ldy - d.yoff - co0) * 2));
+        const i32x4 rs_x = make_rsrc(x + d.xoff + ci0, (uint32_t)(((long)d.N * d.H * d.W * d.ldx - d.xoff - ci0) * 2));
+        const int cout8 = (d.Cout + 7) / 8 * 8;
+        uint32_t voff[PPL];
+        int xpos[PPL], xc16[PPL];
+#pragma unroll
+        for (int u = 0; u < PPL; ++u) {
+            const int j = l + 4 * u;
+            voff[u] = IRGAN_OOB;
+            xpos[u] = 0;
+            xc16[u] = 0;
+            if (j < APIECES) {
+                const int pos = j * 4 + (lane >> 4), slot = lane & 15;
+                const int c16 = slot ^ (2 * pc_t256(pos));
+                if (co0 + c16 * 8 < cout8) voff[u] = (uint32_t)((pos * d.ldy + c16 * 8) * 2);
+            } else if (j < TP) {
+                const int pos = (j - APIECES) * 8 + (lane >> 3), slot = lane & 7;
+                xpos[u] = pos;
+                xc16[u] = (slot ^ (2 * pc_t128(pos))) * 16;  // byte offset of the lane's 16-B chunk
+            }
+        }
+        auto issue = [&](int s, int stage) {
+            const int rowi = s / segs_row, x0 = (s - rowi * segs_row) * 64;
+            const int n = rowi / d.Ho, oy = rowi - n * d.Ho;
+            int iy = oy * d.sy + ty + d.c0y;
+            if (reflect) iy = reflect_idx(iy, d.H);
+            const bool row_ok = (unsigned)iy < (unsigned)d.H;
+            const uint32_t dy_soff = (uint32_t)(((long)rowi * d.Wo + x0) * d.ldy * 2);
+            const long xrow = ((long)n * d.H + iy) * d.W;
+            char* base = smem + stage * STAGE;
+#pragma unroll
+            for (int u = 0; u < PPL; ++u) {
+                if (u >= np) break;
+                const int j = l + 4 * u;
+                if (j < APIECES) {
+                    blds16(rs_dy, voff[u], dy_soff, base + j * 1024);
+                } else {
+                    int ix = x0 + d.c0x + xpos[u];
+                    if (reflect) ix = reflect_idx(ix, d.W);
+                    const bool ok = row_ok & (xpos[u] < XPOS) & ((unsigned)ix < (unsigned)d.W);
+                    const uint32_t off = ok ? (uint32_t)((xrow + ix) * d.ldx * 2) + xc16[u] : IRGAN_OOB;
+                    blds16(rs_x, off, base + j * 1024);
+                }
+            }
+        };
+        // prologue: segments 0..2 in flight, retire segment 0
+        issue(s_beg, 0);
+        if (nk > 1) issue(s_beg + 1, 1);
+        if (nk > 2) issue(s_beg + 2, 2);
+        if (nk > 2) {
+            if (np == 7) wait_vmcnt<14>(); else wait_vmcnt<12>();
+        } else if (nk > 1) {
+            if (np == 7) wait_vmcnt<7>(); else wait_vmcnt<6>();
+        } else {
+            wait_vmcnt<0>();
+        }
+        lds_barrier();
+        for (int kt = 0; kt < nk; ++kt) {
+            // retire segment kt+1 (segment kt+2 may stay in flight), then barrier kt
+            if (kt + 1 < nk && !PCX(1)) {
+                if (kt + 2 < nk) {
+                    if (np == 7) wait_vmcnt<7>(); else wait_vmcnt<6>();
+                } else {
+                    wait_vmcnt<0>();
+                }
+            }
+#if !PCX(8)
+            lds_barrier();
+#endif
+            if (kt + 3 < nk && !PCX(2)) issue(s_beg + kt + 3, (kt + 3) % STAGES);
+        }
+        return;
+    }
+
+    // ----------------------------------------------------------------------
+    // compute wave wn: co 128 x n 48 (fragments jj = 3 wn + j: tx = jj >> 2,
+    // 16-ci group jj & 3), two 32-pixel k-steps per segment
+    const int wn = wid & 3, wm = wid >> 2;  // n group, co group (CW = 8)
+    const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+    const int k_lo = 8 * g + q;  // pixel row of the lane's low 4-row half (k-step 0)
+    // per-lane byte offsets inside a stage (k-step 0, low half); +1024 / +512 for
+    // the high half (rows +4), +8192 / +4096 for k-step 1 (rows +32)
+    int aoff[MI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+        const int col = (wm * MI + i) * 16 + 4 * p, c16 = col >> 3, within = (col & 7) * 2;
+        aoff[i] = k_lo * 256 + ((c16 ^ (2 * pc_t256(k_lo))) << 4) + within;
+    }
+    int boff[NJ][2];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int jj = wn * NJ + j, tx = jj >> 2, col = (jj & 3) * 16 + 4 * p;
+        const int c16 = col >> 3, within = (col & 7) * 2;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            const int pos = k_lo + 4 * hh + tx;
+            boff[j][hh] = APIECES * 1024 + pos * 128 + ((c16 ^ (2 * pc_t128(pos))) << 4) + within;
+        }
+    }
+    f32x4 acc[MI][NJ];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // MFMAs on `cur` with the 11 fragment-pair reads of `nxt` (stage, half h)
+    // interleaved one pair per MFMA: the first MFMA retires cur's reads with no
+    // newer read in flight, every later one needs no wait (lgkmcnt counts 15).
+    auto step = [&](const Frag<MI>& cur, Frag<MI>& nxt, int stage, int h) {
+        const char* S = smem + stage * STAGE + h * 8192;
+        const char* X = smem + stage * STAGE + h * 4096;
+#pragma unroll
+        for (int idx = 0; idx < MI * NJ; ++idx) {
+            const int i = idx / NJ, j = idx % NJ;
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, cur.a[i]),
+                                                                __builtin_bit_cast(bf16x8_t, cur.b[j]), acc[i][j], 0,
+                                                                0, 0);
+#if !PCX(4)
+            if (idx < MI) nxt.a[idx] = ld_tr_pair(S + aoff[idx], S + aoff[idx] + 1024);
+            else if (idx < MI + NJ) nxt.b[idx - MI] = ld_tr_pair(X + boff[idx - MI][0], X + boff[idx - MI][1]);
+#else
+            if (idx < MI) nxt.a[idx] = cur.a[idx] ^ make_uint4(idx, 1, 2, 3);
+            else if (idx < MI + NJ) nxt.b[idx - MI] = cur.b[idx - MI] ^ make_uint4(idx, 1, 2, 3);
+#endif
+        }
+#if !PCX(16)
+#pragma unroll
+        for (int k = 0; k < MI + NJ; ++k) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // 2 DS reads
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, MI * NJ - MI - NJ, 0);
+#endif
+    };
+    auto barrier = [] {
+        __builtin_amdgcn_sched_barrier(0);
+#if !PCX(8)
+        lds_barrier();
+#endif
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    Frag<MI> f0, f1;
+#if PCX(32)
+    __builtin_amdgcn_s_setprio(1);  // compute waves win issue arbitration over the loaders
+#endif
+    barrier();  // prologue barrier: segment 0 landed
+    {
+        const char* S = smem;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) f0.a[i] = ld_tr_pair(S + aoff[i], S + aoff[i] + 1024);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) f0.b[j] = ld_tr_pair(S + boff[j][0], S + boff[j][1]);
+    }
+    for (int kt = 0; kt < nk; ++kt) {
+        step(f0, f1, kt % STAGES, 1);        // segment kt, pixels 0-31 | read pixels 32-63
+        barrier();                           // barrier kt: segment kt+1 landed; segment kt-1 fully read
+        step(f1, f0, (kt + 1) % STAGES, 0);  // segment kt, pixels 32-63 | read segment kt+1, pixels 0-31
+    }                                        // (the last iteration's reads are unused)
+
+    // C[row = co][col = n]: co = co0 + i*16 + 4g + rr, n = jj*16 + (lane & 15)
+    const int K = d.KH * KW * d.Cin;
+    float* const dst = slab ? slab + (long)split * d.Cout * K : nullptr;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const int co = co0 + (wm * MI + i) * 16 + g * 4 + rr;
+            if (co >= d.Cout) continue;
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int jj = wn * NJ + j, tx = jj >> 2;
+                const int ci = ci0 + (jj & 3) * 16 + (lane & 15);
+                const long o = (long)co * K + (ty * KW + tx) * d.Cin + ci;
+                if (dst) dst[o] = acc[i][j][rr];
+                else atomicAdd(dw + o, acc[i][j][rr]);
+            }
+        }
+}
+
+__global__ __launch_bounds__(256) void wgrad_pc_reduce(const float* __restrict__ slab, int splits, long n,
+                                                        float* __restrict__ dw) {
+    const long n4 = n / 4;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+        float4 a = ((const float4*)dw)[i];
+        for (int s = 0; s < splits; ++s) {
+            const float4 v = ((const float4*)(slab + (long)s * n))[i];
+            a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+        }
+        ((float4*)dw)[i] = a;
+    }
+}
+
+}  // namespace
+
+// Preconditions (else IRGAN_EUNSUPPORTED, nothing launched): bf16 operands, KH x 3
+// taps with KW == 3, stride 1, Cout % 128 == 0, Cin % 64 == 0, Wo % 64 == 0, ldx, xoff,
+// ldy, yoff % 8 == 0, byte extents < 2^31.
+extern "C" int irgan_conv_wgrad_pc(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, int splitk,
+                                   float* ws, long ws_cap, hipStream_t st) {
+    if ((long)d->N * d->Ho * d->Wo <= 0) return 0;
+    if (getenv("IRGAN_NO_WGRAD_PC") || d->dtype != IRGAN_BF16 || d->KW != 3 || d->sx != 1 || d->sy != 1 ||
+        d->Cout % BMC || d->Cin % 64 || d->Wo % 64 || d->ldx % 8 || d->xoff % 8 || d->ldy % 8 || d->yoff % 8 ||
+        (long)d->N * d->H * d->W * d->ldx * 2 >= (1L << 31) || (long)d->N * d->Ho * d->Wo * d->ldy * 2 >= (1L << 31))
+        return IRGAN_EUNSUPPORTED;
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+            cus = 256;
+    }
+    static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
+    const int ntco = d->Cout / BMC, nci = d->Cin / 64;
+    const int tiles = ntco * nci * d->KH;
+    const int nseg = d->N * d->Ho * (d->Wo / 64);
+    if (splitk <= 0) {  // one block per CU: the largest split count whose grid fits one round
+        splitk = cus / tiles;
+        if (splitk < 1) splitk = 1;
+        const int maxs = irgan_cdiv(nseg, 4);  // >= 4 segments per split
+        if (splitk > maxs) splitk = maxs;
+        if (swz && (tiles * splitk) % 8) {
+            for (int s2 = splitk - 1; s2 >= 1 && s2 >= splitk - 8; --s2)
+                if ((tiles * s2) % 8 == 0) { splitk = s2; break; }
+        }
+    }
+    const int spb = irgan_cdiv(nseg, splitk);
+    splitk = irgan_cdiv(nseg, spb);
+    const long n = (long)d->Cout * d->KH * d->KW * d->Cin;
+    float* slab = (ws && splitk > 1 && n % 4 == 0 && (long)splitk * n <= ws_cap) ? ws : nullptr;
+    static const int cw = getenv("IRGAN_WGPC_CW4") ? 4 : 8;
+    if (cw == 8)
+        wgrad_pc_kernel<8><<<tiles * splitk, PC<8>::NT, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)dy, dw, spb, nseg,
+                                                                 ntco, nci, swz, slab);
+    else
+        wgrad_pc_kernel<4><<<tiles * splitk, PC<4>::NT, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)dy, dw, spb, nseg,
+                                                                 ntco, nci, swz, slab);
+    if (slab) {
+        const int blocks = (int)std::min<long>(irgan_cdiv(n / 4, 256), 2048);
+        wgrad_pc_reduce<<<blocks, 256, 0, st>>>(slab, splitk, n, dw);
+    } else if (splitk == 1) {
+        // (atomics with one split: still correct, dw accumulates)
+    }
+    IRGAN_LAUNCH_CHECK();
+    return 0;
+}

@@ -44,6 +44,11 @@ EXTRA_CASES = [
     (256, 512, 4, 1, 1, 0, 13),    # D model.8
     (128, 256, 4, 2, 1, 0, 34),    # D model.5 (stride 2: glds fwd, per-phase dgrad)
     (8, 64, 4, 2, 1, 0, 66),       # D model.0 with the 8-channel padded input
+    # Wo % 64 == 0, Cout % 128 == 0: the producer/consumer wgrad (conv_wgrad_pc.hip)
+    (128, 256, 3, 1, 1, 0, 64),    # down2 shape, zero pad, 2 co tiles
+    (384, 128, 3, 1, 1, 0, 64),    # up1_conv shape, 6 ci chunks
+    (64, 128, 3, 1, 1, 0, 128),    # down1 shape, 2 segments per row
+    (256, 256, 3, 1, 1, 1, 128),   # resblock conv, reflect, interior + edge segments
 ]
 
 
