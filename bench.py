@@ -61,17 +61,36 @@ def _cpu_model():
     return platform.processor() or "unknown"
 
 
+def cpu_share():
+    """CPUs this process may actually run on: the affinity mask, capped by the
+    cgroup CPU quota (a GPU box shows every host CPU in os.cpu_count() but grants
+    a share of them; oversubscribing the share makes torch's CPU threads crawl)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                n = min(n, max(1, int(q) // int(per)))
+        except (OSError, ValueError):
+            pass
+    return max(1, n)
+
+
 def _time_oracle(O, G, D, V, ir, rgb, threads, budget_s, min_steps, max_steps):
     """Median seconds per oracle step on `threads` torch CPU threads (1 warm-up)."""
     import torch
     torch.set_num_threads(threads)
     oG, oD = O.AdamState(G), O.AdamState(D)
+    t0 = time.perf_counter()
     O.train_step(G, D, V, ir, rgb, oG, oD)  # warm-up (allocator, oneDNN primitives for these shapes)
+    print(f"[cpu_baseline] warm-up step {time.perf_counter() - t0:.1f}s on {threads} threads", file=sys.stderr,
+          flush=True)
     times, t_start = [], time.perf_counter()
     while len(times) < max_steps:
         t0 = time.perf_counter()
         O.train_step(G, D, V, ir, rgb, oG, oD)
         times.append(time.perf_counter() - t0)
+        print(f"[cpu_baseline] step {len(times)}: {times[-1]:.1f}s", file=sys.stderr, flush=True)
         if len(times) >= min_steps and time.perf_counter() - t_start >= budget_s:
             break
     times.sort()
@@ -80,10 +99,10 @@ def _time_oracle(O, G, D, V, ir, rgb, threads, budget_s, min_steps, max_steps):
 
 def cpu_baseline(H, W, batch=16, budget_s=12.0):
     """The CPU oracle (fp32 PyTorch-CPU restatement of ir:1636-1681, oracle/step.py)
-    at the bench's own config (batch, H x W), on ALL host CPUs (os.cpu_count()
-    torch threads) and, when the host has more, on 16 threads (the
-    per-GPU CPU share of the pool); the faster one is `value`, both are reported.
-    Median of the timed steps after one warm-up step each."""
+    at the bench's own config (batch, H x W), on every CPU the process is granted
+    (cpu_share(): affinity mask and cgroup quota -- os.cpu_count() reports the
+    whole host) and, if that differs, on os.cpu_count() threads too when the host
+    is not shared; median of the timed steps after one warm-up step each."""
     import torch
     from oracle import step as O
     G = O.seeded_params(O.g_param_shapes(), 0)
@@ -93,17 +112,18 @@ def cpu_baseline(H, W, batch=16, budget_s=12.0):
     ir = torch.rand(batch, 1, H, W, generator=g) * 2 - 1
     rgb = torch.rand(batch, 3, H, W, generator=g) * 2 - 1
     ncpu = os.cpu_count() or 1
+    share = cpu_share()
     runs = {}
-    for threads in sorted({ncpu, min(ncpu, 16)}, reverse=True):
-        med, n = _time_oracle(O, G, D, V, ir, rgb, threads, budget_s, 2, 10)
+    for threads in sorted({share}, reverse=True):
+        med, n = _time_oracle(O, G, D, V, ir, rgb, threads, budget_s, 1, 10)
         runs[threads] = {"img_per_s": round(batch / med, 4), "s_per_step_median": round(med, 3), "steps": n}
     best = max(runs, key=lambda t: runs[t]["img_per_s"])
     return {"value": runs[best]["img_per_s"], "unit": "img/s", "cores": best, "kind": "port",
-            "cpu_model": _cpu_model(), "nproc": ncpu, "torch_threads": best,
+            "cpu_model": _cpu_model(), "nproc": ncpu, "cpu_share": share, "torch_threads": best,
             "by_threads": {str(t): r for t, r in runs.items()},
             "sample": f"oracle/step.py train_step at batch {batch}, {H}x{W}, fp32 (the bench config): "
-                      f"median of {runs[best]['steps']} steps after 1 warm-up, {best} torch threads "
-                      f"on {ncpu} host CPUs ({_cpu_model()})"}
+                      f"median of {runs[best]['steps']} steps after 1 warm-up, {best} torch threads = the CPUs "
+                      f"granted to the process ({ncpu} host CPUs, {_cpu_model()})"}
 
 
 def main():

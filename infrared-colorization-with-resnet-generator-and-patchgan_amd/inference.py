@@ -64,7 +64,7 @@ def colorize_u8(model, ir_bchw: torch.Tensor) -> torch.Tensor:
     conversion launch straight from the engine's NHWC fp32 output."""
     netG = getattr(model, "netG", model)
     netG._maybe_repack()
-    fake = netG.engine.forward(ir_bchw.float(), keep=False)
+    fake = netG.engine.forward(ir_bchw.float())
     return rgb_u8(Feat(fake))
 
 
