@@ -258,6 +258,26 @@ int irgan_to_rgb_u8(const float* x, int32_t N, int32_t H, int32_t W, int32_t C, 
 int irgan_image_metrics_u8(const void* pred, const void* gt, int32_t N, int64_t per_image,
                            double* work, int64_t work_cap, double* sums, irgan_stream_t s);
 
+/* ---- KAIST data pipeline (KAISTPairDataset ir:1132-1177) ---- */
+/* cv2.resize(..., INTER_AREA) of a batch of uint8 images src [N][Hin][Win][C]
+ * (C <= 4, image stride img_stride bytes) to out_u8 [N][C][Hout][Wout] (NCHW),
+ * as OpenCV's general area path computes it (resizeArea_: per destination
+ * pixel, source rows reduced horizontally with the x-table weights, then summed
+ * with the y-table weights, float32, round half to even, clamp).  Tables are
+ * CSR over destination indices: entries yptr[y]..yptr[y+1]-1 of (ysrc, yw), and
+ * the same for x (host: computeResizeAreaTab's recurrence).  flip (nullable,
+ * uint8 per image): 1 = horizontal flip (np.fliplr, ir:1166-1168).  img_max
+ * (nullable, zeroed int32 per image): max destination byte of each image. */
+int irgan_area_resize_u8(const void* src, int32_t N, int32_t Hin, int32_t Win, int32_t C, int64_t img_stride,
+                         const int32_t* yptr, const int32_t* ysrc, const float* yw, int32_t Hout,
+                         const int32_t* xptr, const int32_t* xsrc, const float* xw, int32_t Wout,
+                         const void* flip, void* out_u8, int32_t* img_max, irgan_stream_t s);
+/* out[n][i] = float32(in[n][i]) / 255 * 2 - 1 for per_image bytes per image (the
+ * [-1, 1] tensors of ir:1157, 1175-1176); max_rule = 1: the IR rule of ir:1142 --
+ * images whose img_max[n] <= 1 are not divided by 255. */
+int irgan_u8_to_unit(const void* in, int32_t N, int64_t per_image, const int32_t* img_max, int32_t max_rule,
+                     float* out, irgan_stream_t s);
+
 /* Version / capability probe (no GPU work). */
 int irgan_version(void);
 

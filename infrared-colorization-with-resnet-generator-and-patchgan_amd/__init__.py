@@ -23,3 +23,4 @@ except ImportError as _e:  # pragma: no cover - only while the API module is abs
 __all__ = ["_lib", "ops"] + list(_api_all)
 
 from . import inference  # noqa: E402,F401  -- batched test-mode path
+from . import data  # noqa: E402,F401  -- KAIST pipeline, device resize

@@ -171,8 +171,18 @@ class ParamStore:
         self.step_count = steps.pop()
 
     def adam_step(self, lr, b1=0.5, b2=0.999, eps=1e-8):
+        self.adam_begin(lr, b1, b2, eps)(0, self.numel)
+
+    def adam_begin(self, lr, b1=0.5, b2=0.999, eps=1e-8):
+        """Count one optimizer step and return apply(start, end), the Adam update of
+        the flat slice [start, end): a step may be applied bucket by bucket as each
+        bucket's gradient all-reduce completes (BucketedAllreduce.finish)."""
         self.step_count += 1
-        ops.adam(self.flat, self.grad, self.m, self.v, self.step_count, lr, b1, b2, eps)
+        t = self.step_count
+
+        def apply(a, b):
+            ops.adam(self.flat[a:b], self.grad[a:b], self.m[a:b], self.v[a:b], t, lr, b1, b2, eps)
+        return apply
 
 
 def _pc(store: ParamStore, key: str, spec: ConvSpec, dtype, need_dgrad=True, bias=True):
@@ -726,7 +736,7 @@ class BucketedAllreduce:
             return
         t = self.store.grad[start:self.end]
         op = dist.ReduceOp.AVG if self.avg else dist.ReduceOp.SUM
-        self.works.append((dist.all_reduce(t, op=op, group=self.group, async_op=True), t))
+        self.works.append((dist.all_reduce(t, op=op, group=self.group, async_op=True), t, start, self.end))
         self.end = start
 
     def start(self):
@@ -741,14 +751,24 @@ class BucketedAllreduce:
         if (self.end - start) * 4 >= self.bucket_bytes:
             self._launch(start)
 
-    def finish(self):
+    def finish(self, apply=None):
+        """Reduce the remainder, then per bucket (in issue order, tail-first): make the
+        compute stream wait for that bucket only and call ``apply(start, end)`` -- the
+        optimizer update of the bucket is queued behind its own collective and runs
+        while the later buckets are still being reduced (the G-Adam of
+        bucket k overlaps the all-reduce of bucket k+1).  Each element of the flat
+        buffer lies in exactly one bucket, so this is the whole-buffer mean + update."""
         if not self.active:
+            if apply is not None:
+                apply(0, self.store.numel)
             return
         self._launch(0)
-        for w, t in self.works:
+        for w, t, a, b in self.works:
             w.wait()
             if not self.avg:
                 t.div_(self.world)
+            if apply is not None:
+                apply(a, b)
         self.works, self.end = [], self.store.numel
 
 
@@ -823,8 +843,7 @@ class GANStep:
         ops.tv(Feat(fake), cfg.lambda_tv, dfake, L[4:5])
         ssim_work = b.flat("ssim_work", 10 * fake.numel())
         ops.ssim(Feat(fake), Feat(rgb_h), cfg.lambda_ssim, dfake, L[5:6], ssim_work)
-        self.d_reduce.finish()
-        self.D.adam_step(cfg.lr_D * self.lr_scale, cfg.beta1, cfg.beta2)
+        self.d_reduce.finish(self.D.adam_begin(cfg.lr_D * self.lr_scale, cfg.beta1, cfg.beta2))
         self.dis.pack()
         # GAN term through the updated D (ir:1659-1662)
         dinf = Feat(b.zeros("din1", (B, H, W, dpad), T), 0, self.dis.packs[0].cin_eff)
@@ -835,8 +854,7 @@ class GANStep:
         dd = self.dis.backward(dpg, want_wgrad=False, want_dinput=True, tag="g")
         ops.axpby(dd.sl(cin, cout), 1.0, Feat(dfake), 1.0)
         self.gen.backward(dfake, ready=self.g_reduce.ready)
-        self.g_reduce.finish()
-        self.G.adam_step(cfg.lr_G * self.lr_scale, cfg.beta1, cfg.beta2)
+        self.g_reduce.finish(self.G.adam_begin(cfg.lr_G * self.lr_scale, cfg.beta1, cfg.beta2))
         self.gen.pack()
         return L
 

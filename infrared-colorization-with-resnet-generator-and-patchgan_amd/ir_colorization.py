@@ -711,31 +711,51 @@ class SyntheticPairDataset(torch.utils.data.Dataset):
         return {"ir": self.ir[i], "rgb": self.rgb[i]}
 
 
-def train_kaist(cfg: Config, dataset=None, log=print):
-    """ir:1549-1723 with the fused HIP step.  ``dataset`` defaults to the KAIST
-    pair dataset, which needs cv2 + the dataset on disk; pass any dataset
-    yielding {'ir','rgb'} (e.g. SyntheticPairDataset) otherwise."""
+def train_kaist(cfg: Config, dataset=None, log=print, trainer_hook=None):
+    """ir:1549-1723 with the fused HIP step.  ``dataset=None`` trains on the KAIST
+    pairs under ``cfg.train_roots`` (data.KAISTPairDataset: decode on the host,
+    INTER_AREA resize + paired flip + normalisation on the device); any dataset
+    yielding {'ir','rgb'} (e.g. SyntheticPairDataset) may be passed instead.
+    ``trainer_hook(trainer)`` (optional) runs once after the networks are built
+    (e.g. to load D / VGG weights from files)."""
     device = torch.device(cfg.device)
     log(f"[TRAIN] Device: {device}")
     log(f"KAIST root (V000, V001, ...): {cfg.kaist_root}")
+    rank, world = _dp()
     if dataset is None:
-        raise RuntimeError("KAIST data loading (cv2) is outside the MI355X hot path; pass dataset=...")
-    N = len(dataset)
+        from .data import KAISTPairDataset, kaist_loader
+        N = len(KAISTPairDataset(cfg.train_roots, img_size=cfg.img_size, augment=False, verbose=rank == 0))
+    else:
+        N = len(dataset)
     val_size = max(1, int(N * cfg.val_ratio))
     train_size = N - val_size
     log(f"Total pairs: {N}, train: {train_size}, val: {val_size}")
     idxs = list(range(N))
     random.seed(42)
     random.shuffle(idxs)
-    train_ds = torch.utils.data.Subset(dataset, idxs[:train_size])
-    val_ds = torch.utils.data.Subset(dataset, idxs[train_size:])
-    train_loader, val_loader, sampler = dp_loaders(train_ds, val_ds, cfg.batch_size)
-    rank, _ = _dp()
+    if dataset is None:
+        train_ds = KAISTPairDataset(cfg.train_roots, img_size=cfg.img_size, augment=True, indices=idxs[:train_size],
+                                    verbose=rank == 0)
+        val_ds = KAISTPairDataset(cfg.train_roots, img_size=cfg.img_size, augment=False,
+                                  indices=idxs[train_size:][rank::world], verbose=rank == 0)
+        sampler = None
+        if world > 1:
+            from torch.utils.data.distributed import DistributedSampler
+            sampler = DistributedSampler(train_ds, num_replicas=world, rank=rank, shuffle=True, seed=0, drop_last=True)
+        train_loader = kaist_loader(train_ds, cfg.batch_size, device, shuffle=True, drop_last=True,
+                                    num_workers=cfg.num_workers, sampler=sampler)
+        val_loader = kaist_loader(val_ds, cfg.batch_size, device, num_workers=cfg.num_workers)
+    else:
+        train_ds = torch.utils.data.Subset(dataset, idxs[:train_size])
+        val_ds = torch.utils.data.Subset(dataset, idxs[train_size:])
+        train_loader, val_loader, sampler = dp_loaders(train_ds, val_ds, cfg.batch_size)
     model = IRColorizationModel(cfg)
     if cfg.init_G_weights is not None and os.path.isfile(cfg.init_G_weights):
         log(f"Initializing generator from: {cfg.init_G_weights}")
         model.load_weights(cfg.init_G_weights)
     trainer = GANTrainer(cfg, model=model)
+    if trainer_hook is not None:
+        trainer_hook(trainer)
     if rank == 0:
         os.makedirs(cfg.save_dir, exist_ok=True)
     best_val = float("inf")

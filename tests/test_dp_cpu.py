@@ -9,6 +9,7 @@ between backward and Adam) and the val-L1 (sum, count) reduction
 equal shards reproduce the single-process step on the union batch.  In fp64
 the only difference is summation order, so the tolerance is 1e-9 relative.
 """
+import math
 import os
 import socket
 
@@ -170,3 +171,54 @@ def test_bucketed_allreduce_matches_whole_buffer_mean(tmp_path):
     assert res[0]["buckets"] >= 4           # genuinely bucketed, not one collective at the end
     for r in res:
         torch.testing.assert_close(r["grad"], want, rtol=1e-6, atol=1e-7)
+
+
+def _adam_slice(store, a, b, step, lr=2e-4, b1=0.5, b2=0.999, eps=1e-8):
+    """torch.optim.Adam's update on the flat slice [a, b) (test-side reference)."""
+    g = store.grad[a:b]
+    store.m[a:b].mul_(b1).add_(g, alpha=1 - b1)
+    store.v[a:b].mul_(b2).addcmul_(g, g, value=1 - b2)
+    denom = (store.v[a:b].sqrt() / math.sqrt(1 - b2 ** step)).add_(eps)
+    store.flat[a:b].addcdiv_(store.m[a:b], denom, value=-lr / (1 - b1 ** step))
+
+
+def _overlap_worker(rank, port, out):
+    import importlib
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    engine = importlib.import_module(pkg().__name__ + ".engine")
+    res = {}
+    for mode in ("bucketed", "whole"):
+        store = engine.ParamStore(engine.g_param_shapes(), "cpu")
+        store.flat.copy_(torch.randn(store.numel, generator=torch.Generator().manual_seed(3)))
+        store.grad.copy_(torch.randn(store.numel, generator=torch.Generator().manual_seed(100 + rank)))
+        calls = []
+        if mode == "bucketed":
+            red = engine.BucketedAllreduce(store, bucket_bytes=4 << 20)
+            for k in ["up1_conv.0.weight"] + [f"resblocks.{b}.conv_block.1.weight" for b in reversed(range(9))]:
+                red.ready(k)
+            red.finish(lambda a, b: (calls.append((a, b)), _adam_slice(store, a, b, 1)))
+        else:
+            engine.grad_allreduce(store.grad)
+            _adam_slice(store, 0, store.numel, 1)
+        res[mode] = {"flat": store.flat.clone(), "calls": calls}
+    torch.save(res, os.path.join(out, f"o{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_bucketed_adam_overlap_equals_whole_buffer_update(tmp_path):
+    """GANStep's G update: BucketedAllreduce.finish(apply) runs the
+    Adam of each bucket right after that bucket's collective (tail-first), while
+    later buckets are still in flight.  Two gloo ranks: the result equals one
+    whole-buffer all-reduce followed by one whole-buffer Adam, bit for bit, every
+    element is updated exactly once, and the update really is split (>= 4 buckets)."""
+    mp.spawn(_overlap_worker, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True)
+    res = [torch.load(tmp_path / f"o{r}.pt", weights_only=True) for r in range(WORLD)]
+    for r in res:
+        calls = r["bucketed"]["calls"]
+        assert len(calls) >= 4
+        assert calls[0][1] == max(b for _, b in calls) and calls[-1][0] == 0      # tail first, head last
+        cov = sorted(calls)
+        assert cov[0][0] == 0 and all(cov[i][1] == cov[i + 1][0] for i in range(len(cov) - 1))
+        assert torch.equal(r["bucketed"]["flat"], r["whole"]["flat"])
+    assert torch.equal(res[0]["bucketed"]["flat"], res[1]["bucketed"]["flat"])
