@@ -278,6 +278,14 @@ int irgan_area_resize_u8(const void* src, int32_t N, int32_t Hin, int32_t Win, i
 int irgan_u8_to_unit(const void* in, int32_t N, int64_t per_image, const int32_t* img_max, int32_t max_rule,
                      float* out, irgan_stream_t s);
 
+/* The SSIM of compute_metrics (ir:1208-1213): skimage.metrics.structural_similarity(
+ * gt, pred, data_range=1.0, channel_axis=2) for N uint8 image pairs [N][H][W][C]
+ * standing for v / 255 -- per channel 7x7 uniform windows, sample covariance,
+ * C1 = 0.01^2, C2 = 0.03^2, map averaged over pixels >= 3 from the border, then over
+ * channels; fp64.  ssim[n] out.  work: >= N doubles (more = more blocks). */
+int irgan_ssim_eval_u8(const void* pred, const void* gt, int32_t N, int32_t H, int32_t W, int32_t C,
+                       double* work, int64_t work_cap, double* ssim, irgan_stream_t s);
+
 /* Version / capability probe (no GPU work). */
 int irgan_version(void);
 

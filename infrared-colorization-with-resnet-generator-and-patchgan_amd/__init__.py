@@ -24,3 +24,4 @@ __all__ = ["_lib", "ops"] + list(_api_all)
 
 from . import inference  # noqa: E402,F401  -- batched test-mode path
 from . import data  # noqa: E402,F401  -- KAIST pipeline, device resize
+from . import evaluation  # noqa: E402,F401  -- run_test, metrics CSV, Top-K

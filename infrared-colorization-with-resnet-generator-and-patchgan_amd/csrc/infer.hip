@@ -111,7 +111,83 @@ __global__ void metrics_finalize_kernel(const double* __restrict__ partials, int
     sums[2 * n + 1] = q;
 }
 
+// skimage.metrics.structural_similarity(gt, pred, data_range=1, channel_axis=2)
+// (compute_metrics, ir:1208-1213) on uint8 images that stand for float32(v / 255)
+// (run_test, ir:1412-1413; scikit-image then casts to float64): per channel, 7x7
+// uniform windows, sample covariance (49/48), C1 = 0.01^2, C2 = 0.03^2, the SSIM
+// map averaged over the pixels >= 3 from every border, then over the channels.
+// fp64 like scikit-image.  grid (blocks, N): partials[(n*gridDim.x + b)] = sum of
+// the block's SSIM map values.
+__global__ __launch_bounds__(TPB) void ssim_eval_kernel(const uint8_t* __restrict__ pred,
+                                                        const uint8_t* __restrict__ gt, int H, int W, int C,
+                                                        double* __restrict__ partials) {
+    __shared__ double red[TPB];
+    __shared__ double lut[256];  // float32(k / 255) widened, the reference's input values
+    lut[threadIdx.x] = (double)((float)threadIdx.x / 255.0f);
+    __syncthreads();
+    const int n = blockIdx.y;
+    const long per = (long)H * W * C;
+    const uint8_t* a = gt + n * per;    // im1 = gt (ir:1210)
+    const uint8_t* b = pred + n * per;  // im2 = pred
+    const int Hv = H - 6, Wv = W - 6;
+    const long total = (long)Hv * Wv * C;
+    const double inv = 1.0 / 49.0, cov = 49.0 / 48.0;
+    const double C1 = 0.01 * 0.01, C2 = 0.03 * 0.03;
+    double acc = 0.0;
+    for (long e = blockIdx.x * (long)TPB + threadIdx.x; e < total; e += (long)gridDim.x * TPB) {
+        const int c = (int)(e % C);
+        const long q = e / C;
+        const int y = (int)(q / Wv) + 3, x = (int)(q % Wv) + 3;
+        double sa = 0, sb = 0, saa = 0, sbb = 0, sab = 0;
+        for (int dy = -3; dy <= 3; ++dy) {
+            const long row = ((long)(y + dy) * W + x) * C + c;
+#pragma unroll
+            for (int dx = -3; dx <= 3; ++dx) {
+                const double va = lut[a[row + dx * C]], vb = lut[b[row + dx * C]];
+                sa += va; sb += vb; saa += va * va; sbb += vb * vb; sab += va * vb;
+            }
+        }
+        const double ux = sa * inv, uy = sb * inv;
+        const double vx = cov * (saa * inv - ux * ux), vy = cov * (sbb * inv - uy * uy);
+        const double vxy = cov * (sab * inv - ux * uy);
+        const double A1 = 2.0 * ux * uy + C1, A2 = 2.0 * vxy + C2;
+        const double B1 = ux * ux + uy * uy + C1, B2 = vx + vy + C2;
+        acc += (A1 * A2) / (B1 * B2);
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int w = TPB / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partials[(long)n * gridDim.x + blockIdx.x] = red[0];
+}
+
+__global__ void ssim_eval_finalize(const double* __restrict__ partials, int nb, int N, double denom,
+                                   double* __restrict__ out) {
+    const int n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= N) return;
+    double s = 0.0;
+    for (int b = 0; b < nb; ++b) s += partials[(long)n * nb + b];
+    out[n] = s / denom;
+}
+
 }  // namespace
+
+extern "C" int irgan_ssim_eval_u8(const void* pred, const void* gt, int32_t N, int32_t H, int32_t W, int32_t C,
+                                  double* work, int64_t work_cap, double* ssim, irgan_stream_t s) {
+    if (!pred || !gt || !work || !ssim || C < 1) return IRGAN_EINVAL;
+    if (N <= 0) return 0;
+    if (H < 7 || W < 7) return IRGAN_EINVAL;  // skimage: win_size exceeds image extent
+    const long total = (long)(H - 6) * (W - 6) * C;
+    int nb = (int)std::min<long>(256, std::max<long>(1, irgan_cdiv(total, TPB)));
+    if ((long)nb * N > work_cap) nb = (int)std::max<long>(1, work_cap / N);
+    if ((long)nb * N > work_cap || N > 65535) return IRGAN_EINVAL;
+    ssim_eval_kernel<<<dim3(nb, N), TPB, 0, (hipStream_t)s>>>((const uint8_t*)pred, (const uint8_t*)gt, H, W, C, work);
+    ssim_eval_finalize<<<irgan_cdiv(N, 64), 64, 0, (hipStream_t)s>>>(work, nb, N, (double)total, ssim);
+    IRGAN_LAUNCH_CHECK();
+    return 0;
+}
 
 extern "C" int irgan_to_rgb_u8(const float* x, int32_t N, int32_t H, int32_t W, int32_t C, int32_t ldx, int32_t xoff,
                                void* out, irgan_stream_t s) {

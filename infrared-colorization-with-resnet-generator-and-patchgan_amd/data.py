@@ -306,15 +306,26 @@ class DeviceResizer:
             t = self._tabs[n] = tuple(torch.from_numpy(a).to(self.device) for a in area_table(n, self.size))
         return t
 
-    def _one(self, u8, C, flip, max_rule):
+    def resize_u8(self, u8, C, flip=None, img_max=None):
+        """(B,H,W[,C]) uint8 device batch -> (B,C,S,S) uint8 (cv2.resize INTER_AREA,
+        optional per-image horizontal flip)."""
+        if u8.dtype != torch.uint8 or not u8.is_cuda:
+            raise ValueError("resize_u8 takes a uint8 device tensor")
+        u8 = u8.contiguous()
         B, H, W = u8.shape[:3]
         S = self.size
         yp, ys, yw = self._tab(H)
         xp, xs, xw = self._tab(W)
         out8 = torch.empty(B, C, S, S, dtype=torch.uint8, device=self.device)
-        mx = torch.zeros(B, dtype=torch.int32, device=self.device)
         _lib.call("irgan_area_resize_u8", P(u8), B, H, W, C, ctypes.c_int64(H * W * C), P(yp), P(ys), P(yw), S,
-                  P(xp), P(xs), P(xw), S, P(flip), P(out8), P(mx), stream())
+                  P(xp), P(xs), P(xw), S, P(flip) if flip is not None else None, P(out8),
+                  P(img_max) if img_max is not None else None, stream())
+        return out8
+
+    def _one(self, u8, C, flip, max_rule):
+        B, S = u8.shape[0], self.size
+        mx = torch.zeros(B, dtype=torch.int32, device=self.device)
+        out8 = self.resize_u8(u8, C, flip, mx)
         out = torch.empty(B, C, S, S, dtype=torch.float32, device=self.device)
         _lib.call("irgan_u8_to_unit", P(out8), B, ctypes.c_int64(C * S * S), P(mx), int(max_rule), P(out), stream())
         return out

@@ -7,8 +7,9 @@ ir:865-876: ``.cpu().numpy()``, then numpy float32 ops) and computes MAE / MSE
 through one G forward, one ``irgan_to_rgb_u8`` launch (NHWC fp32 -> uint8
 HxWx3, the reference's exact float32 pipeline) and one
 ``irgan_image_metrics_u8`` launch; only the uint8 images (or 2 doubles per
-image) cross PCIe.  SSIM of compute_metrics needs scikit-image (ir:1208-1213),
-which is optional in the reference too; it is reported as None here.
+image) cross PCIe.  SSIM of compute_metrics (scikit-image's structural_similarity, ir:1208-1213)
+runs on the device too (``irgan_ssim_eval_u8``), pinned to scikit-image 0.18.3
+outputs (tests/golden/ssim_eval.npz).
 """
 from __future__ import annotations
 
@@ -68,22 +69,29 @@ def colorize_u8(model, ir_bchw: torch.Tensor) -> torch.Tensor:
     return rgb_u8(Feat(fake))
 
 
-def image_metrics_u8(pred_u8: torch.Tensor, gt_u8: torch.Tensor):
-    """Per-image (mae, mse, psnr, None) of compute_metrics (ir:1184-1206) on
-    uint8 (B,H,W,C) device batches, as run_test forms them (pred_u8/255 against
-    load_rgb_image's gt_u8/255, ir:1412-1415)."""
+def image_metrics_u8(pred_u8: torch.Tensor, gt_u8: torch.Tensor, with_ssim=True):
+    """Per-image (mae, mse, psnr, ssim) of compute_metrics (ir:1184-1217) on uint8
+    (B,H,W,C) device batches, as run_test forms them (pred_u8/255 against
+    load_rgb_image's gt_u8/255, ir:1412-1415).  SSIM is scikit-image's
+    structural_similarity(gt, pred, data_range=1, channel_axis=2) computed on the
+    device (irgan_ssim_eval_u8); None for images smaller than its 7x7 window."""
     assert pred_u8.shape == gt_u8.shape and pred_u8.dtype == gt_u8.dtype == torch.uint8
-    B = pred_u8.shape[0]
+    pred_u8, gt_u8 = pred_u8.contiguous(), gt_u8.contiguous()
+    B, H, W, C = pred_u8.shape
     per = pred_u8[0].numel()
-    work = torch.empty(128 * B, dtype=torch.float64, device=pred_u8.device)
+    work = torch.empty(256 * B, dtype=torch.float64, device=pred_u8.device)
     sums = torch.empty(2 * B, dtype=torch.float64, device=pred_u8.device)
-    _lib.call("irgan_image_metrics_u8", P(pred_u8.contiguous()), P(gt_u8.contiguous()), B, per, P(work),
-              work.numel(), P(sums), stream())
+    _lib.call("irgan_image_metrics_u8", P(pred_u8), P(gt_u8), B, per, P(work), work.numel(), P(sums), stream())
+    ssim = [None] * B
+    if with_ssim and H >= 7 and W >= 7:
+        sv = torch.empty(B, dtype=torch.float64, device=pred_u8.device)
+        _lib.call("irgan_ssim_eval_u8", P(pred_u8), P(gt_u8), B, H, W, C, P(work), work.numel(), P(sv), stream())
+        ssim = sv.cpu().tolist()
     out = []
-    for s, q in sums.view(B, 2).cpu().tolist():
+    for (s, q), sv_ in zip(sums.view(B, 2).cpu().tolist(), ssim):
         mae, mse = s / per, q / per
         psnr = float("inf") if mse == 0 else 20.0 * math.log10(1.0) - 10.0 * math.log10(mse + 1e-12)
-        out.append((mae, mse, psnr, None))
+        out.append((mae, mse, psnr, sv_))
     return out
 
 

@@ -7,7 +7,10 @@ path and the pieces a train/test driver touches:
     (ir:168-209), get_lr_lambda (ir:212), get_filter (ir:240),
     ResnetUNetGenerator (ir:425), NLayerDiscriminator (ir:576),
     VGGPerceptual (ir:642), tv_loss (ir:686), ssim_loss_torch (ir:714),
-    IRColorizationModel (ir:757), validate_kaist (ir:1521), train_kaist (ir:1549)
+    IRColorizationModel (ir:757), validate_kaist (ir:1521), train_kaist (ir:1549),
+    and the test-mode names re-exported from inference.py / evaluation.py:
+    ir_to_tensor, tensor_to_rgb_image, compute_metrics, save_best_k_outputs,
+    make_comparison_collage, save_comparison_image, run_test (ir:855-1514)
 
 Modules keep the reference ``state_dict`` keys and OIHW shapes (checkpoints
 ``netG_*.pth`` load unchanged), but their parameters are views into flat
@@ -36,7 +39,9 @@ from .ops import BF16, F32, Feat
 __all__ = ["Config", "Identity", "get_norm_layer", "init_weights", "init_net", "get_lr_lambda", "get_filter",
            "ResnetUNetGenerator", "NLayerDiscriminator", "VGGPerceptual", "tv_loss", "ssim_loss_torch",
            "IRColorizationModel", "GANTrainer", "validate_kaist", "train_kaist", "SyntheticPairDataset",
-           "g_param_shapes", "d_param_shapes", "vgg_param_shapes", "seeded_state", "dp_loaders", "val_shard"]
+           "g_param_shapes", "d_param_shapes", "vgg_param_shapes", "seeded_state", "dp_loaders", "val_shard",
+           "compute_metrics", "save_best_k_outputs", "run_test", "make_comparison_collage", "save_comparison_image",
+           "float01_to_uint8_rgb", "save_rgb", "ir_to_tensor", "tensor_to_rgb_image", "HAVE_SKIMAGE", "main"]
 
 
 # =============================================================================
@@ -93,6 +98,7 @@ class Config:
         self.vgg_weights = None          # local path to vgg16 features weights (ImageNet); None -> seeded synthetic
         self.vgg_seed = 3
         self.log_every = 50
+        self.test_batch = 16             # run_test: frames per generator call (the reference runs one)
 
 
 # =============================================================================
@@ -802,3 +808,23 @@ def train_kaist(cfg: Config, dataset=None, log=print, trainer_hook=None):
 def _cpu_state(net):
     """state_dict in the reference layout: contiguous OIHW fp32 (ir:1708)."""
     return type(net.state_dict())((k, v.detach().contiguous().cpu()) for k, v in net.state_dict().items())
+
+
+# test-mode names (ir:855-1514); evaluation imports this module lazily, so bind them last
+from .evaluation import (HAVE_SKIMAGE, float01_to_uint8_rgb, make_comparison_collage, run_test,  # noqa: E402
+                         save_best_k_outputs, save_comparison_image, save_rgb)
+from .inference import compute_metrics, ir_to_tensor, tensor_to_rgb_image  # noqa: E402
+
+
+def main(cfg: Config = None, log=print):
+    """ir:1730-1752: train or test according to cfg.mode (``python -m <package>``)."""
+    cfg = cfg or Config()
+    log(f"Config mode: {cfg.mode}")
+    log(f"SAVE_DIR: {cfg.save_dir}")
+    log(f"OUTPUT_DIR: {cfg.output_dir}")
+    log(f"TEST_G_WEIGHTS: {cfg.test_G_weights}")
+    if cfg.mode == "train":
+        return train_kaist(cfg, log=log)
+    if cfg.mode == "test":
+        return run_test(cfg, log=log)
+    raise ValueError("cfg.mode must be 'train' or 'test'")

@@ -6,6 +6,8 @@
 * irgan_image_metrics_u8 vs the reference's compute_metrics (ir:1184-1206) --
   MAE/MSE within 1e-6 relative (the reference averages in numpy float32
   pairwise sums, the kernel in fp64), PSNR within 1e-5 dB, inf for equal images;
+  the SSIM (irgan_ssim_eval_u8) within 1e-9 of the oracle's scikit-image
+  restatement (test_gpu_eval.py pins it to scikit-image's own outputs);
 * colorize_u8 (batched G forward + conversion) vs the reference's
   IRColorizationModel.forward + tensor_to_rgb_image at 32x32 in fp32 mode: the
   G output within 1e-4 abs, so a uint8 code may move by one where the output
@@ -66,8 +68,9 @@ def test_image_metrics_match_reference_golden(fx, inf):
     p = torch.from_numpy(fx["met_pred_u8"]).to(DEV)
     q = torch.from_numpy(fx["met_gt_u8"]).to(DEV)
     got = inf.image_metrics_u8(p, q)
-    for (mae, mse, psnr, ssim), want in zip(got, fx["met_out"]):
-        assert ssim is None
+    for i, ((mae, mse, psnr, ssim), want) in enumerate(zip(got, fx["met_out"])):
+        ref_ssim = OI.structural_similarity(fx["met_gt_u8"][i] / 255.0, fx["met_pred_u8"][i] / 255.0)
+        assert abs(ssim - ref_ssim) < 1e-9
         assert abs(mae - want[0]) <= 1e-6 * max(want[0], 1e-12) + 1e-12
         assert abs(mse - want[1]) <= 1e-6 * max(want[1], 1e-12) + 1e-12
         assert (np.isinf(psnr) and np.isinf(want[2])) or abs(psnr - want[2]) < 1e-5

@@ -110,3 +110,19 @@ def test_infer_oracle_matches_reference_golden():
     # the generator's test-mode output converts to the stored uint8 images
     for i in range(fx["g_fake"].shape[0]):
         assert np.array_equal(OI.tensor_to_rgb_image(fx["g_fake"][i:i + 1]), fx["g_u8"][i])
+
+
+def test_ssim_oracle_matches_skimage_golden():
+    """oracle/infer.structural_similarity against scikit-image 0.18.3 itself
+    (tests/golden/make_ssim_golden.py -> ssim_eval.npz): fp64 round-off."""
+    import os
+    from conftest import GOLDEN
+    from oracle import infer as OI
+    fx = dict(np.load(os.path.join(GOLDEN, "ssim_eval.npz")))
+    k = 0
+    while f"ssim{k}" in fx:
+        for p, g, want in zip(fx[f"pred{k}"], fx[f"gt{k}"], fx[f"ssim{k}"]):
+            got = OI.structural_similarity(g.astype(np.float32) / 255.0, p.astype(np.float32) / 255.0)
+            assert abs(got - want) < 1e-12, (k, got, want)
+        k += 1
+    assert k == 3 and fx["ssim0"][1] == 1.0
