@@ -28,6 +28,7 @@ PKG = "infrared-colorization-with-resnet-generator-and-patchgan_amd"
 METRIC = "GAN train-step img/s (G+D fwd/bwd) at 256×256, 1/2/4/8 MI355X"
 MIN_GFLOP_PER_IMG_256 = 534.85   # minimal-step algorithmic FLOPs per image at 256^2
 BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+FP8_DENSE_PEAK_TFLOPS = 5000.0   # MI355X dense fp8 (block-scaled f8f6f4 MFMA, MI355X_MICROARCH.md)
 FP32_MFMA_PEAK_TFLOPS = 157.3
 
 
@@ -133,7 +134,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--batch", type=int, default=16, help="per-GPU batch")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp8"],
+                    help="fp8: BASELINE configs[4] -- the ResnetBlock convs on e4m3 operands (use --batch 32)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds per CPU thread-count run")
     args = ap.parse_args()
@@ -169,7 +171,7 @@ def main():
 
     # dominant kernel for the live roofline: the resblock 3x3 conv (256->256 @ H/4)
     res_tags = [ops.conv_tag(k, ops.ConvSpec(256, 256, 3, 1, 1, ops.PAD_REFLECT), (H // 4, W // 4), B)
-                for k in ("fwd", "dgrad", "wgrad")]
+                for k in (("fwd8", "dgrad8", "wgrad") if args.dtype == "fp8" else ("fwd", "dgrad", "wgrad"))]
     for _ in range(args.warmup):
         tr.step(ir, rgb)
     torch.cuda.synchronize()
@@ -206,15 +208,19 @@ def main():
         ms = el / args.steps * 1e3
         # roofline of the dominant kernel family: algorithmic FLOPs per launch / mean launch time
         res_flop = 2.0 * B * (H // 4) * (W // 4) * 256 * 256 * 9
-        peak = BF16_DENSE_PEAK_TFLOPS if args.dtype == "bf16" else FP32_MFMA_PEAK_TFLOPS
+        def peak_of(tag):
+            if args.dtype == "fp32":
+                return FP32_MFMA_PEAK_TFLOPS
+            return FP8_DENSE_PEAK_TFLOPS if tag.split(":")[0].endswith("8") else BF16_DENSE_PEAK_TFLOPS
         kern = {}
         for tg in res_tags:
             if tg in timing:
                 n, mean_ms = timing[tg]
                 kern[tg] = {"launches": n, "mean_ms": round(mean_ms, 4),
-                            "tflops": round(res_flop / (mean_ms * 1e-3) / 1e12, 2)}
+                            "tflops": round(res_flop / (mean_ms * 1e-3) / 1e12, 2), "peak": peak_of(tg)}
         dom = max(kern, key=lambda k: kern[k]["launches"] * kern[k]["mean_ms"]) if kern else None
         achieved = kern[dom]["tflops"] if dom else None
+        peak = peak_of(dom) if dom else BF16_DENSE_PEAK_TFLOPS
         traffic = pmc_traffic(dom.split(":")[0]) if (dom and H == 256 and B == 16 and args.dtype == "bf16") else None
         step_tflops = value * min_gflop_per_img(H, W) / 1e3 / world
         out = {
@@ -223,8 +229,10 @@ def main():
             "ms_per_step_median": round(median_ms, 3), "img_per_s_median_step": round(B * world / median_ms * 1e3, 3),
             "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (U(-1,1) IR/RGB pairs, seeded; random-init weights)",
-            "config": {"workload": f"GAN train step {H}x{W}, batch {B}/GPU (BASELINE configs[1]"
-                                   f"{' / [2]' if world > 1 else ''})", "global_batch": B * world,
+            "config": {"workload": (f"GAN train step {H}x{W}, batch {B}/GPU, ResnetBlock convs on fp8 e4m3 "
+                                    f"operands (BASELINE configs[4])") if args.dtype == "fp8" else
+                                   (f"GAN train step {H}x{W}, batch {B}/GPU (BASELINE configs[1]"
+                                    f"{' / [2]' if world > 1 else ''})"), "global_batch": B * world,
                        "img_size": H, "parallelism": f"dp{world}",
                        "min_gflop_per_img": round(min_gflop_per_img(H, W), 2),
                        "step_tflops_per_gpu": round(step_tflops, 2),

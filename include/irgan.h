@@ -29,7 +29,7 @@ extern "C" {
 
 typedef void* irgan_stream_t;
 
-enum { IRGAN_F32 = 0, IRGAN_BF16 = 1 };
+enum { IRGAN_F32 = 0, IRGAN_BF16 = 1, IRGAN_FP8 = 2 };  /* FP8: OCP e4m3 (e4m3fn) */
 enum { IRGAN_PAD_ZERO = 0, IRGAN_PAD_REFLECT = 1 };
 /* forward activations (epilogues / IN apply) */
 enum { IRGAN_ACT_NONE = 0, IRGAN_ACT_RELU = 1, IRGAN_ACT_LRELU = 2, IRGAN_ACT_TANH = 3 };
@@ -51,7 +51,7 @@ typedef struct irgan_conv_desc {
     int32_t pad_mode;                     /* IRGAN_PAD_* */
     int32_t act;                          /* IRGAN_ACT_* applied in the epilogue */
     int32_t accumulate;                   /* 1: y += result (fp32 output only) */
-    int32_t dtype;                        /* input/weight dtype IRGAN_F32|IRGAN_BF16 */
+    int32_t dtype;                        /* input/weight dtype IRGAN_F32|IRGAN_BF16|IRGAN_FP8 */
     int32_t out_dtype;                    /* output dtype */
     int32_t mask_act;                     /* backward mask: 0 none, 1 relu, 2 lrelu(0.2) */
     int32_t ldm, moff;                    /* mask slice (same pixel grid as output) */
@@ -72,6 +72,41 @@ int irgan_conv_fwd(const irgan_conv_desc* d, const void* x, const void* w,
  * Returns IRGAN_EUNSUPPORTED (nothing launched) for other layers. */
 int irgan_conv_fwd_stats(const irgan_conv_desc* d, const void* x, const void* w,
                          const float* bias, void* y, void* part, int32_t* nb, irgan_stream_t s);
+
+/* irgan_conv_fwd_stats / irgan_conv_fwd on fp8 operands (BASELINE config 5): x and
+ * w OCP e4m3 (d->dtype = IRGAN_FP8; x NHWC with ldx, xoff % 16 == 0, w the packed
+ * [Cout][3][3][Cin] image), 3x3, stride 1, Cin % 128 == 0, Cout % 64 == 0 (not
+ * 192), bf16 output y = act(conv * dqx[0] * dqw[0] + bias) -- the dequantisation
+ * multipliers of the per-tensor scales, read on the device.  part != NULL: also the
+ * InstanceNorm partials of y (as irgan_conv_fwd_stats; act none, no accumulate).
+ * Replaces the ResnetBlock convs (ir:386-411) forward and backward-data in the fp8
+ * path.  IRGAN_EUNSUPPORTED (nothing launched) for other layers. */
+int irgan_conv_fwd_fp8(const irgan_conv_desc* d, const void* x, const void* w, const float* dqx,
+                       const float* dqw, const float* bias, void* y, void* part, int32_t* nb,
+                       irgan_stream_t s);
+
+/* fp8 quantisation of an NHWC slice: y[p][yoff + c] = e4m3(clamp(x * q[0], +-448))
+ * (round to nearest even; x bf16 or fp32 by dt; C, ld, off % 8 == 0), and
+ * atomicMax(amax, bits(max |x|)) when amax != NULL.  y == NULL: the max only.
+ * q == NULL: q = 1. */
+int irgan_fp8_quant(const void* x, int32_t dt, int64_t P, int32_t C, int32_t ldx, int32_t xoff,
+                    void* y, int32_t ldy, int32_t yoff, const float* q, uint32_t* amax,
+                    irgan_stream_t s);
+/* Per-tensor scales from recorded maxima, for n slots: q = 2^floor(log2(448 / amax))
+ * (1 if amax is 0), dq = 1 / q; reset != 0 clears amax afterwards. */
+int irgan_fp8_scale(uint32_t* amax, int32_t n, float* q, float* dq, int32_t reset, irgan_stream_t s);
+/* A table of njobs irgan_fp8_job records (device memory; n % 8 == 0, bf16 src,
+ * n <= max_n): amax != NULL -> atomicMax(amax[slot], max |src|) only; otherwise
+ * dst = e4m3(clamp(src * q[slot], +-448)).  The per-step re-quantisation of the
+ * packed fp8 weights: one amax launch, irgan_fp8_scale, one quantise launch. */
+typedef struct irgan_fp8_job {
+    const void* src;
+    void* dst;
+    int64_t n;
+    int32_t slot, reserved;
+} irgan_fp8_job;
+int irgan_fp8_quant_batch(const void* jobs, int32_t njobs, int64_t max_n, const float* q,
+                          uint32_t* amax, irgan_stream_t s);
 
 /* Split-K partial sums of irgan_conv_fwd (fp32 out; no bias, activation, mask or
  * accumulate): the K range is cut into ksplit parts and part ks lands at

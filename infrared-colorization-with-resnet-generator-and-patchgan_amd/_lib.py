@@ -16,7 +16,7 @@ HEADER = os.path.join(os.path.dirname(HERE), "include", "irgan.h")
 # IRGAN_LIB: an alternative build of the same ABI (kernel A/B experiments, tools/)
 LIB_PATH = os.environ.get("IRGAN_LIB") or os.path.join(HERE, "libirgan.so")
 
-F32, BF16 = 0, 1
+F32, BF16, FP8 = 0, 1, 2
 PAD_ZERO, PAD_REFLECT = 0, 1
 ACT_NONE, ACT_RELU, ACT_LRELU, ACT_TANH = 0, 1, 2, 3
 
@@ -41,7 +41,7 @@ class ConvDesc(ctypes.Structure):
 
 
 _CTYPES = {
-    "int32_t": ctypes.c_int32, "int64_t": ctypes.c_int64, "float": ctypes.c_float,
+    "int32_t": ctypes.c_int32, "int64_t": ctypes.c_int64, "float": ctypes.c_float, "uint32_t": ctypes.c_uint32,
     "irgan_stream_t": ctypes.c_void_p, "void": None,
 }
 

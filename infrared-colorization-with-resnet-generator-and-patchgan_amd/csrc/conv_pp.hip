@@ -34,6 +34,18 @@
 // window may overwrite that stage; every other READ is consumed by the same
 // wave's MFMA phase before any DMA can target its buffer.
 //
+// fp8 (F8, irgan_conv_fwd_fp8): the same kernel on OCP e4m3 operands.  A K-step
+// is one tap x 128 channels (a 128-byte halo / weight row, so every DMA, LDS
+// image and barrier window is byte-for-byte the bf16 schedule); its MFMA is
+// mfma_scale_f32_16x16x128_f8f6f4 (unit block scales: 2x the bf16 rate), a
+// fragment is 32 bytes (chunks g and g+4 of the row for lane group g, the same
+// channels for both operands), and the sub-steps of a K-step split the wave's
+// pixel fragments instead of the channels (sub-step 0 also reads the weight
+// fragments, which stay in registers for the others); at 8 pixel fragments a
+// K-step has 4 sub-steps (8 barrier windows), so the operand registers stay at
+// the bf16 kernel's 48.  The per-tensor
+// scales are undone in the epilogue: y = acc * (dqx[0] * dqw[0]) + bias.
+//
 // Preconditions (checked by irgan_conv_fwd_pp): bf16, sy = sx = 1, Cin % 64 == 0,
 // (KH, KW) in {(3,3), (4,4)}, ldx, xoff % 8 == 0, Cout % 256 == 0 (channel
 // tiles of 256), no tanh epilogue, input slice and weights < 2^30 elements (byte offsets
@@ -87,15 +99,26 @@ struct PP {
     static_assert(256 * RSB <= LDS && BN % 64 == 0 && WU * 8 * 1024 == BBYTES && NJ * 16 * CW == BN, "tile");
 };
 
-template <int KH, int KW, int BN, bool ACC, bool STATS = false>
+typedef int v8i_t __attribute__((ext_vector_type(8)));
+IRGAN_HD v8i_t cat8(i32x4 a, i32x4 b) { return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7); }
+
+template <int KH, int KW, int BN, bool ACC, bool STATS = false, bool F8 = false>
 __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
                                                          const bf16_t* __restrict__ w, const float* __restrict__ bias,
                                                          void* __restrict__ y, const void* __restrict__ mask,
                                                          int ntn, int tpx, int tpy, int swz,
-                                                         float2* __restrict__ part = nullptr) {
+                                                         float2* __restrict__ part = nullptr,
+                                                         const float* __restrict__ dqx = nullptr,
+                                                         const float* __restrict__ dqw = nullptr) {
+    constexpr int ESZ = F8 ? 1 : 2, CHN = 128 / ESZ;  // operand bytes, channels per 128-byte chunk
+    const char* const xb = (const char*)x;
+    const char* const wb = (const char*)w;
     constexpr int TAPS = KH * KW, HWd = PW + KW - 1, HROWS = (PH + KH - 1) * HWd, HP = (HROWS + 7) / 8;
     constexpr int BBYTES = PP<BN>::BBYTES, LDS = PP<BN>::LDS, NJ = PP<BN>::NJ, WU = PP<BN>::WU, RSB = PP<BN>::RSB;
     constexpr int MI = PP<BN>::MIW, RW = PP<BN>::RW;
+    // sub-steps per K-step: bf16 2 (32 channels each); fp8 splits the pixel fragments,
+    // MS per sub-step (4 sub-steps at MI = 8 keep the operand registers at the bf16 48)
+    constexpr int HS = F8 && MI >= 8 ? 4 : 2, MS = F8 ? MI / HS : MI;
     static_assert(HP <= HPMAX && HP > 40 && TAPS >= 2, "halo pieces per wave are 5 or 6");
     __shared__ __attribute__((aligned(1024))) char smem[LDS];
     char* const sH = smem;
@@ -116,14 +139,14 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
     const int py0 = pyi * PH, px0 = pxi * PW, n0 = nt * BN;
     const int nh = (HP - wid + 7) >> 3;  // halo pieces this wave loads: wid, wid+8, ... (5 or 6)
     const int Kw = TAPS * d.Cin;
-    const int nchunk = d.Cin / 64;
+    const int nchunk = d.Cin / CHN;
     const int sub = lane >> 3;
     const int chunk = (lane & 7) ^ sub;  // source chunk for this lane's LDS slot (row & 7 == sub)
     const bool reflect = d.pad_mode == IRGAN_PAD_REFLECT;
 
     // DMA sources as byte offsets into buffer resources (out-of-range offsets
     // arrive as zeros: padding and Cout tails cost no address math in the loop)
-    const uint32_t xbytes = (uint32_t)((long)d.N * d.H * d.W * d.ldx * 2);
+    const uint32_t xbytes = (uint32_t)((long)d.N * d.H * d.W * d.ldx * ESZ);
     // byte offset of this lane's row of halo piece (u*8 + wid) (computed at issue
     // time, once per chunk: keeping six offsets live costs registers the MFMA
     // tile needs)
@@ -136,15 +159,15 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
             ix = reflect_idx(ix, d.W);
         }
         const bool ok = (h < HROWS) & ((unsigned)iy < (unsigned)d.H) & ((unsigned)ix < (unsigned)d.W);
-        return ok ? (uint32_t)((((img * d.H + iy) * d.W + ix) * d.ldx + d.xoff + ((lane & 7) ^ lsub) * 8) * 2)
+        return ok ? (uint32_t)((((img * d.H + iy) * d.W + ix) * d.ldx + d.xoff) * ESZ + ((lane & 7) ^ lsub) * 16)
                   : IRGAN_OOB;
     };
     // weight rows co >= Cout lie beyond num_records: they arrive as zeros
-    const uint32_t wbytes = (uint32_t)((long)d.Cout * Kw * 2);
-    const uint32_t b_off = (uint32_t)(((n0 + wid * WU * 8 + sub) * Kw + chunk * 8) * 2);  // piece u: + u*16*Kw
+    const uint32_t wbytes = (uint32_t)((long)d.Cout * Kw * ESZ);
+    const uint32_t b_off = (uint32_t)((n0 + wid * WU * 8 + sub) * Kw * ESZ + chunk * 16);  // piece u (8 rows): + u*8*Kw*ESZ
     auto issue_halo = [&](int c) {
         char* dst = sH + (c & 1) * HBYTES;
-        const i32x4 rs = make_rsrc(x + c * 64, xbytes - c * 128);
+        const i32x4 rs = make_rsrc(xb + c * 128, xbytes - c * 128);
         int lsub = sub;
         asm volatile("" : "+v"(lsub));  // recompute the offsets here instead of hoisting them out of the loop
 #pragma unroll
@@ -152,11 +175,11 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
             if (u < nh) blds16(rs, halo_off(u, lsub), dst + (u * 8 + wid) * 1024);
     };
     auto issue_w = [&](int c, int tp, int stage) {
-        const int kcol = tp * d.Cin + c * 64;
-        const i32x4 rs = make_rsrc(w + kcol, wbytes - kcol * 2);
+        const int kcol = tp * d.Cin + c * CHN;
+        const i32x4 rs = make_rsrc(wb + kcol * ESZ, wbytes - kcol * ESZ);
         char* dst = sB + stage * BBYTES + wid * WU * 1024;
 #pragma unroll
-        for (int u = 0; u < WU; ++u) blds16(rs, b_off, (uint32_t)(u * 16 * Kw), dst + u * 1024);
+        for (int u = 0; u < WU; ++u) blds16(rs, b_off, (uint32_t)(u * 8 * Kw * ESZ), dst + u * 1024);
     };
     // W(k+1) landed; the halo issued at step k (after W(k+1)) may stay in flight
     auto retire = [&](bool halo_now) {
@@ -171,7 +194,7 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     uint4 af[MI], bfr[NJ];
-
+    v8i_t af8[MS], bf8[NJ];  // fp8: 32-byte fragments (chunks g, g + 4)
     // prologue: W(0), halo(0), W(1); retire the first two
     issue_w(0, 0, 0);
     issue_halo(0);
@@ -186,10 +209,15 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
     // ds_read immediate K * 128: one VALU add per fragment read.
     const int arow0 = prow * HWd + (lane & 15);  // halo row of fragment 0 at tap (0,0)
     const int brow0 = cb + (lane & 15);          // weight row of fragment 0 (rows +16j share the XOR)
-    const int bb0 = lds_off(brow0, lane >> 4), bb1 = lds_off(brow0, 4 + (lane >> 4));
-    int tsw[8];  // h = 1 flips chunk bit 2: tsw ^ 64 (v_xad_u32)
+    // bf16: sub-step h reads chunk (lane >> 4) + 4h; fp8: a fragment is chunks (lane >> 4) and
+    // (lane >> 4) + 4 (the same byte <-> channel map for both operands)
+    const int g0 = lane >> 4;
+    const int bb0 = lds_off(brow0, g0), bb1 = lds_off(brow0, 4 + g0);
+    int tsw[F8 ? 1 : 8];  // h = 1 / the second fp8 chunk flips chunk bit 2: tsw ^ 64 (v_xad_u32)
+    if constexpr (!F8) {
 #pragma unroll
-    for (int k8 = 0; k8 < 8; ++k8) tsw[k8] = ((lane >> 4) ^ ((arow0 + k8) & 7)) << 4;
+        for (int k8 = 0; k8 < 8; ++k8) tsw[k8] = (g0 ^ ((arow0 + k8) & 7)) << 4;
+    }
 #pragma unroll 1
     for (int c = 0; c < nchunk; ++c) {
         const int hb = arow0 * 128 + (c & 1) * HBYTES;
@@ -202,11 +230,26 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
             const bool last_k = !more && tp == TAPS - 1;
             const bool halo_now = tp == 0 && more;
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
+            for (int h = 0; h < HS; ++h) {
                 // ---- READ phase (group 0: even windows, group 1: odd)
                 const int bb = h ? bb1 : bb0;
                 int hbp = hb;
                 asm volatile("" : "+v"(hbp));  // per-phase base: the address adds stay here, not hoisted
+                if constexpr (F8) {
+                    if (h == 0) {
+#pragma unroll
+                        for (int j = 0; j < NJ; ++j)
+                            bf8[j] = cat8(*(const i32x4*)(B + bb0 + j * 2048), *(const i32x4*)(B + bb1 + j * 2048));
+                    }
+#pragma unroll
+                    for (int ii = 0; ii < MS; ++ii) {
+                        const int K = (h * MS + ii + ty) * HWd + tx;
+                        // the swizzle term from arow0 on the fly (fp8 has no registers to spare)
+                        const int sw = (g0 ^ ((arow0 + K) & 7)) << 4;
+                        af8[ii] = cat8(*(const i32x4*)(sH + (hbp + sw) + K * 128),
+                                       *(const i32x4*)(sH + (hbp + (sw ^ 64)) + K * 128));
+                    }
+                } else {
 #if !PPX(4)
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) bfr[j] = *(const uint4*)(B + bb + j * 2048);
@@ -223,6 +266,7 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
                     for (int i = 0; i < MI; ++i) af[i] = *(const uint4*)(sH + hbp + i * 128);
                 }
 #endif
+                }
                 if (h == 0 && !PPX(2)) {
                     // W(k+1) (W(1) came with the prologue), then the next chunk's halo
                     if (k >= 1 && !last_k) {
@@ -231,20 +275,35 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
                     }
                     if (halo_now) issue_halo(c + 1);
                 }
-                if (h == 1 && grp == 1) {  // window 4k+3: last reads of step k, then retire
+                if (h == HS - 1 && grp == 1) {  // last window of step k (4k+3 in bf16): last reads, then retire
                     wait_lgkm0();
                     if (!last_k) retire(halo_now);
                 }
                 phase_barrier();
                 // ---- MFMA phase: C^T fragment (weights as A, pixels as B)
+                if constexpr (F8) {
 #pragma unroll
-                for (int i = 0; i < MI * !PPX(1); ++i)
+                    for (int ii = 0; ii < MS; ++ii)
 #pragma unroll
-                    for (int j = 0; j < NJ; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, bfr[j]),
-                                                                            __builtin_bit_cast(bf16x8_t, af[i]),
-                                                                            acc[i][j], 0, 0, 0);
-                if (h == 1 && grp == 0 && !last_k) retire(halo_now);  // window 4k+3
+                        for (int j = 0; j < NJ; ++j)
+                            acc[h * MS + ii][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                                bf8[j], af8[ii], acc[h * MS + ii][j], 0, 0, 0, 127, 0, 127);
+                    // pin the scaled MFMAs inside this phase: hipcc otherwise sinks them past the
+                    // barriers to the end of the chunk, keeping every tap's fragments live (spills)
+#pragma unroll
+                    for (int ii = 0; ii < MS; ++ii)
+#pragma unroll
+                        for (int j = 0; j < NJ; ++j) asm volatile("" : "+v"(acc[h * MS + ii][j]));
+                } else {
+#pragma unroll
+                    for (int i = 0; i < MI * !PPX(1); ++i)
+#pragma unroll
+                        for (int j = 0; j < NJ; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                                __builtin_bit_cast(bf16x8_t, bfr[j]), __builtin_bit_cast(bf16x8_t, af[i]), acc[i][j],
+                                0, 0, 0);
+                }
+                if (h == HS - 1 && grp == 0 && !last_k) retire(halo_now);  // last window of step k
                 phase_barrier();
             }
         }
@@ -266,6 +325,7 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
     // ---- epilogue.  Fragment (i, j): pixel m = (prow + i)*16 + (lane & 15),
     // channels co = n0 + cb + j*16 + 4*(lane >> 4) + r, r = 0..3.
     const int cl0 = cb + 4 * (lane >> 4);  // block-local channel of r = 0, j = 0
+    const float osc = F8 ? *dqx * *dqw : 1.f;  // fp8: 1 / (x scale * w scale), powers of two
     float4 b4[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
@@ -317,6 +377,12 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
                 const int cl = cl0 + j * 16, co = n0 + cl;
                 const float4 b = b4[j];
                 float v[4] = {acc[i][j][0] + b.x, acc[i][j][1] + b.y, acc[i][j][2] + b.z, acc[i][j][3] + b.w};
+                if constexpr (F8) {
+                    v[0] = acc[i][j][0] * osc + b.x;
+                    v[1] = acc[i][j][1] * osc + b.y;
+                    v[2] = acc[i][j][2] * osc + b.z;
+                    v[3] = acc[i][j][3] * osc + b.w;
+                }
 #pragma unroll
                 for (int r = 0; r < 4; ++r) v[r] = conv_act(v[r], A);
                 const bool full = co + 4 <= d.Cout;
@@ -529,5 +595,44 @@ extern "C" int irgan_conv_fwd_stats(const irgan_conv_desc* d, const void* x, con
 #undef PPS
     IRGAN_LAUNCH_CHECK();
     *nb = tpx * tpy;
+    return 0;
+}
+
+// fp8 e4m3 operands (x: NHWC, w: the packed [Cout][taps][Cin] image, both OCP
+// e4m3 with per-tensor scales): y = act(conv(x, w) * dqx[0] * dqw[0] + bias), bf16
+// out, and with part != NULL the InstanceNorm partials of y as irgan_conv_fwd_stats.
+extern "C" int irgan_conv_fwd_fp8(const irgan_conv_desc* d, const void* x, const void* w, const float* dqx,
+                                  const float* dqw, const float* bias, void* y, void* part, int32_t* nb,
+                                  irgan_stream_t s) {
+    if (!d || !x || !w || !dqx || !dqw || !y || (part && !nb)) return IRGAN_EINVAL;
+    if ((long)d->N * d->Ho * d->Wo <= 0 || d->Cout <= 0) return 0;
+    const bool k33 = d->KH == 3 && d->KW == 3;
+    if (d->dtype != IRGAN_FP8 || d->out_dtype != IRGAN_BF16 || d->act == IRGAN_ACT_TANH || d->sy != 1 || d->sx != 1 ||
+        d->Cin % 128 || !k33 || d->Cout % 64 || d->Cout == 192 || d->ldx % 16 || d->xoff % 16 || d->mask_act ||
+        (long)d->N * d->H * d->W * d->ldx >= (1L << 30) || (long)d->Cout * 9 * d->Cin >= (1L << 30))
+        return IRGAN_EUNSUPPORTED;
+    if (part && (d->accumulate || d->act != IRGAN_ACT_NONE || d->ldy % 8 || d->yoff % 8 || d->Ho != d->OH ||
+                 d->Wo != d->OW || d->omy != 1 || d->omx != 1 || d->ooy || d->oox))
+        return IRGAN_EUNSUPPORTED;
+    const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH);
+    if (part && tpx * tpy > IRGAN_IN_PARTS) return IRGAN_EUNSUPPORTED;
+    static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
+    const int bn = d->Cout % 256 == 0 ? 256 : (d->Cout % 128 == 0 ? 128 : 64);
+    const int ntn = d->Cout / bn;
+    const int blocks = d->N * tpy * tpx * ntn;
+    hipStream_t st = (hipStream_t)s;
+#define PP8(BNV, ACCV, STV)                                                                                        \
+    conv_pp_kernel<3, 3, BNV, ACCV, STV, true><<<blocks, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, \
+                                                                       y, nullptr, ntn, tpx, tpy, swz, (float2*)part, dqx, dqw)
+    if (part) {
+        if (bn == 256) PP8(256, false, true); else if (bn == 128) PP8(128, false, true); else PP8(64, false, true);
+        *nb = tpx * tpy;
+    } else if (d->accumulate) {
+        if (bn == 256) PP8(256, true, false); else if (bn == 128) PP8(128, true, false); else PP8(64, true, false);
+    } else {
+        if (bn == 256) PP8(256, false, false); else if (bn == 128) PP8(128, false, false); else PP8(64, false, false);
+    }
+#undef PP8
+    IRGAN_LAUNCH_CHECK();
     return 0;
 }

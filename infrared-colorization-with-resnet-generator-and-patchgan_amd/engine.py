@@ -253,6 +253,13 @@ class INLayer:
             ops.in_stats(x, work, mr)
         ops.in_apply(x, mr, y, act=act, res=res, xhat=xhat)
 
+    def conv_fwd8(self, bufs: Buffers, name: str, pc, w8, dqw, x8: Feat, dqx, z: Feat, y: Feat, act,
+                  res: Feat = None):
+        """conv_fwd on fp8 operands (ops.conv_fwd_fp8) with the fused statistics."""
+        work = bufs.flat("in_work", ops.IN_PARTS * z.N * z.C, torch.float64)
+        nb = ops.conv_fwd_fp8(pc, w8, dqw, x8, dqx, z, part=work)
+        self.fwd(bufs, name, z, y, act, res=res, nb=nb)
+
     def conv_fwd(self, bufs: Buffers, name: str, pc, x: Feat, z: Feat, y: Feat, act, res: Feat = None):
         """z = conv(x) (kept for the backward), y = act(IN(z) [+ res]): the IN statistics
         come from the conv's epilogue when it has a fused kernel (ops.conv_fwd_stats)."""
@@ -279,8 +286,15 @@ class GeneratorEngine:
     _pack_batch = None  # ops.PackBatch of self.packs, built on the first pack()
 
     def __init__(self, store: ParamStore, dtype=BF16, ngf=64, input_nc=1, output_nc=3, n_blocks=9,
-                 no_antialias=False, no_antialias_up=False):
+                 no_antialias=False, no_antialias_up=False, fp8=False):
+        """fp8: the ResnetBlock convs (forward and the backward-data interior) run on
+        OCP e4m3 operands (BASELINE config 5): per-tensor power-of-two scales, current
+        scaling for the re-packed weights, delayed scaling for the activations and
+        gradients they read; everything else (and every weight gradient) stays bf16."""
         self.store, self.dtype, self.ngf = store, dtype, ngf
+        self.fp8 = bool(fp8)
+        if self.fp8 and (dtype != BF16 or 4 * ngf % 128):
+            raise ValueError("the fp8 path runs on the bf16 engine with 4*ngf % 128 == 0")
         self.input_nc, self.output_nc, self.n_blocks = input_nc, output_nc, n_blocks
         self.no_aa, self.no_aa_up = no_antialias, no_antialias_up
         self.tdt = ops.TORCH_DT[dtype]
@@ -302,6 +316,13 @@ class GeneratorEngine:
         self.outc = _pc(S, "outc.1", ConvSpec(c0, output_nc, 7, 1, 3, PAD_REFLECT), dtype)
         self.packs = [self.inc, self.down1, self.down2, self.up1, self.up2, self.outc] + \
             [p for pr in self.res for p in pr] + ([self.up1_up, self.up2_up] if no_antialias_up else [])
+        if self.fp8:
+            # weight images 4b..4b+3: conv1 fwd, conv1 dgrad, conv2 fwd, conv2 dgrad of block b;
+            # activation slots: forward inputs 2b (conv1), 2b+1 (conv2); backward-data inputs
+            # 2n+2b (conv2's dY), 2n+2b+1 (conv1's dY)
+            self.f8w = ops.Fp8Weights([im for p1, p2 in self.res for im in (p1.fwd, p1.dg[0][2], p2.fwd,
+                                                                             p2.dg[0][2])], store.device)
+            self.f8a = ops.Fp8Acts(4 * n_blocks, store.device)
         n_in = 5 + 2 * n_blocks
         self.norms = {k: INLayer() for k in ["inc", "down1", "down2", "up1", "up2"] +
                       [f"r{b}_{i}" for b in range(n_blocks) for i in (1, 2)]}
@@ -312,6 +333,11 @@ class GeneratorEngine:
         if self._pack_batch is None:
             self._pack_batch = ops.PackBatch(self.packs)
         self._pack_batch.run()
+        if self.fp8:
+            self.f8w.run()
+
+    def _w8(self, k):
+        return self.f8w.dst[k], ops.Pi(self.f8w.dq, k)
 
     # -- shapes
     def _dims(self, H, W):
@@ -360,14 +386,27 @@ class GeneratorEngine:
             self.norms["down2"].conv_fwd(g, "down2", self.down2, x1, z2, a2, ACT_RELU)
             ops.blur_down(a2, h)
         # 9 ResnetBlocks  (ir:362-418, 485-490)
+        x8 = Feat(g.get("x8", (B, H2, W2, c2), torch.float8_e4m3fn)) if self.fp8 else None
         for b, (p1, p2) in enumerate(self.res):
             r1 = Feat(g.get(f"r1_{b}", (B, H2, W2, c2), T))
             t = Feat(g.get(f"t{b}", (B, H2, W2, c2), T))
-            self.norms[f"r{b}_1"].conv_fwd(g, f"r{b}_1", p1, h, r1, t, ACT_RELU)
+            if self.fp8:
+                self.f8a.quant(2 * b, h, x8)
+                self.norms[f"r{b}_1"].conv_fwd8(g, f"r{b}_1", p1, *self._w8(4 * b), x8,
+                                                ops.Pi(self.f8a.dq, 2 * b), r1, t, ACT_RELU)
+            else:
+                self.norms[f"r{b}_1"].conv_fwd(g, f"r{b}_1", p1, h, r1, t, ACT_RELU)
             r2 = Feat(g.get(f"r2_{b}", (B, H2, W2, c2), T))
             hn = Feat(g.get(f"h{b + 1}", (B, H2, W2, c2), T))
-            self.norms[f"r{b}_2"].conv_fwd(g, f"r{b}_2", p2, t, r2, hn, ACT_NONE, res=h)
+            if self.fp8:
+                self.f8a.quant(2 * b + 1, t, x8)
+                self.norms[f"r{b}_2"].conv_fwd8(g, f"r{b}_2", p2, *self._w8(4 * b + 2), x8,
+                                                ops.Pi(self.f8a.dq, 2 * b + 1), r2, hn, ACT_NONE, res=h)
+            else:
+                self.norms[f"r{b}_2"].conv_fwd(g, f"r{b}_2", p2, t, r2, hn, ACT_NONE, res=h)
             h = hn
+        if self.fp8:
+            self.f8a.update(0, 2 * self.n_blocks)   # next step's forward scales
         # up1 -> cat with x1 -> conv/IN/ReLU  (ir:554-558)
         # (odd sizes: the up-sampled map is 2*H2 x 2*W2 != H1 x W1 and is resized to the
         # skip's size, ir:555-556 -- folded into the UpsampleAA table, or a resize launch
@@ -475,6 +514,8 @@ class GeneratorEngine:
         ready("up1_up.weight" if self.no_aa_up else "up1_conv.0.weight")
         # resblocks, reversed: dh holds d h_{b+1}; becomes d h_b in place
         dt_ = Feat(g.get("dtmp", (B, H2, W2, c2), T))
+        nb2 = 2 * self.n_blocks
+        dy8 = Feat(g.get("dy8", (B, H2, W2, c2), torch.float8_e4m3fn)) if self.fp8 else None
         for b in reversed(range(self.n_blocks)):
             p1, p2 = self.res[b]
             key = f"resblocks.{b}.conv_block."
@@ -483,11 +524,22 @@ class GeneratorEngine:
             self.norms[f"r{b}_2"].bwd(g, f"r{b}_2", dh, r2, ACT_NONE, dt_, db=S.krsc(key + "5.bias", G))
             wg(p2, key + "5", t, dt_)
             dr = Feat(g.get("dtmp2", (B, H2, W2, c2), T))
-            ops.conv_dgrad(p2, dt_, dr, pad_buf=padbuf)
+            if self.fp8:
+                self.f8a.quant(nb2 + 2 * b, dt_, dy8)
+                ops.conv_dgrad_fp8(p2, *self._w8(4 * b + 3), dy8, ops.Pi(self.f8a.dq, nb2 + 2 * b), dt_, dr)
+            else:
+                ops.conv_dgrad(p2, dt_, dr, pad_buf=padbuf)
             self.norms[f"r{b}_1"].bwd(g, f"r{b}_1", dr, r1, ACT_RELU, dr, db=S.krsc(key + "1.bias", G))
             wg(p1, key + "1", hb, dr)
-            ops.conv_dgrad(p1, dr, dh, accumulate=True, pad_buf=padbuf)
+            if self.fp8:
+                self.f8a.quant(nb2 + 2 * b + 1, dr, dy8)
+                ops.conv_dgrad_fp8(p1, *self._w8(4 * b + 1), dy8, ops.Pi(self.f8a.dq, nb2 + 2 * b + 1), dr, dh,
+                                   accumulate=True)
+            else:
+                ops.conv_dgrad(p1, dr, dh, accumulate=True, pad_buf=padbuf)
             ready(key + "1.weight")
+        if self.fp8:
+            self.f8a.update(nb2, nb2)   # next step's backward-data scales
         # down2 (+ blur-down)
         z2 = Feat(g.d["z2"])
         if self.no_aa:
@@ -783,7 +835,8 @@ class GANStep:
         self.G, self.D, self.V, self.cfg, self.dtype = G, D, V, cfg, dtype
         self.tdt = ops.TORCH_DT[dtype]
         self.gen = gen or GeneratorEngine(G, dtype, ngf=cfg.ngf, input_nc=cfg.input_nc, output_nc=cfg.output_nc,
-                                          no_antialias=cfg.no_antialias, no_antialias_up=cfg.no_antialias_up)
+                                          no_antialias=cfg.no_antialias, no_antialias_up=cfg.no_antialias_up,
+                                          fp8=getattr(cfg, "compute_dtype", "bf16") == "fp8")
         self.dis = dis or DiscriminatorEngine(D, dtype, input_nc=cfg.input_nc + cfg.output_nc)
         self.vgg = vgg or VGGEngine(V, dtype)
         self.bufs = Buffers(G.device)

@@ -94,7 +94,8 @@ class Config:
         self.topk = 50
         self.best50_dirname = "Best_50_colored_images"
         # --- MI355X additions (new names only; nothing above is renamed)
-        self.compute_dtype = "bf16"      # "bf16" (MFMA bf16, fp32 accumulate) or "fp32" (exact parity mode)
+        self.compute_dtype = "bf16"      # "bf16" (MFMA bf16, fp32 accumulate), "fp8" (bf16 + e4m3 ResnetBlock
+                                         # convs, BASELINE config 5) or "fp32" (exact parity mode)
         self.vgg_weights = None          # local path to vgg16 features weights (ImageNet); None -> seeded synthetic
         self.vgg_seed = 3
         self.log_every = 50
@@ -203,7 +204,9 @@ def _require_cuda(t: torch.Tensor, what: str):
 
 
 def _dtype_code(name):
-    return {"bf16": BF16, "fp32": F32, "f32": F32}[name]
+    """compute_dtype -> engine dtype.  "fp8": the bf16 engines with the generator's
+    ResnetBlock convs on e4m3 operands (GeneratorEngine(fp8=True))."""
+    return {"bf16": BF16, "fp8": BF16, "fp32": F32, "f32": F32}[name]
 
 
 # =============================================================================
@@ -327,7 +330,7 @@ class ResnetUNetGenerator(_StoreModule):
         self.outc = _seq(None, _Slot(S, "outc.1"), None)
         self.engine = GeneratorEngine(S, _dtype_code(compute_dtype), ngf=ngf, input_nc=input_nc,
                                       output_nc=output_nc, n_blocks=n_blocks, no_antialias=no_antialias,
-                                      no_antialias_up=no_antialias_up)
+                                      no_antialias_up=no_antialias_up, fp8=compute_dtype == "fp8")
         self._dirty = True
 
     def forward(self, x, layers=None, encode_only=False):

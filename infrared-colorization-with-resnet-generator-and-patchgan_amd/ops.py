@@ -13,9 +13,10 @@ import os
 import torch
 
 from . import _lib
-from ._lib import ACT_LRELU, ACT_NONE, ACT_RELU, ACT_TANH, BF16, F32, IN_PARTS, PAD_REFLECT, PAD_ZERO  # noqa: F401
+from ._lib import (ACT_LRELU, ACT_NONE, ACT_RELU, ACT_TANH, BF16, F32, FP8, IN_PARTS, PAD_REFLECT,  # noqa: F401
+                   PAD_ZERO)
 
-TORCH_DT = {F32: torch.float32, BF16: torch.bfloat16}
+TORCH_DT = {F32: torch.float32, BF16: torch.bfloat16, FP8: torch.float8_e4m3fn}
 
 
 def dt_code(t: torch.Tensor) -> int:
@@ -23,6 +24,8 @@ def dt_code(t: torch.Tensor) -> int:
         return F32
     if t.dtype == torch.bfloat16:
         return BF16
+    if t.dtype == torch.float8_e4m3fn:
+        return FP8
     raise TypeError(f"unsupported dtype {t.dtype}")
 
 
@@ -32,6 +35,11 @@ def stream():
 
 def P(t):
     return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+def Pi(t, i):
+    """Pointer to element i of a contiguous device tensor (a scale / amax slot)."""
+    return ctypes.c_void_p(t.data_ptr() + i * t.element_size())
 
 
 class LaunchTimer:
@@ -636,3 +644,118 @@ def adam(p, g, m, v, step: int, lr: float, b1: float, b2: float, eps: float):
     bc2 = 1 - b2 ** step
     _lib.call("irgan_adam", P(p), P(g), P(m), P(v), p.numel(), ctypes.c_float(lr / bc1), ctypes.c_float(b1),
               ctypes.c_float(b2), ctypes.c_float(math.sqrt(bc2)), ctypes.c_float(eps), stream())
+
+
+# ----------------------------------------------------------------------------
+# fp8 (OCP e4m3) operands: BASELINE config 5
+# ----------------------------------------------------------------------------
+
+def fp8_quant(x: Feat, y: Feat = None, q=None, amax=None):
+    """y = e4m3(clamp(x * q, +-448)); amax = max(amax, max|x|) (irgan_fp8_quant).
+    q / amax: ctypes pointers to one float / uint32 slot (Pi), or None."""
+    assert y is None or (y.dt == FP8 and (y.N, y.H, y.W, y.C) == (x.N, x.H, x.W, x.C))
+    _lib.call("irgan_fp8_quant", x.ptr, x.dt, x.P, x.C, x.ld, x.off, y.ptr if y is not None else None,
+              y.ld if y is not None else 0, y.off if y is not None else 0, q, amax, stream())
+
+
+def fp8_scale(amax: torch.Tensor, q: torch.Tensor, dq: torch.Tensor, reset=True, start=0, n=None):
+    """Slots [start, start+n): q = 2^floor(log2(448 / amax)), dq = 1 / q (irgan_fp8_scale)."""
+    n = amax.numel() - start if n is None else n
+    _lib.call("irgan_fp8_scale", Pi(amax, start), n, Pi(q, start), Pi(dq, start), int(reset), stream())
+
+
+class Fp8Job(ctypes.Structure):
+    """irgan_fp8_job (include/irgan.h)."""
+    _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("n", ctypes.c_int64),
+                ("slot", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class Fp8Weights:
+    """fp8 copies of bf16 packed weight images, re-quantised after every re-pack with
+    per-tensor current scaling: one amax launch, irgan_fp8_scale, one quantise launch
+    for all of them.  ``dst[k]`` / slot k belongs to the k-th (src) image."""
+
+    def __init__(self, srcs, device):
+        self.srcs = list(srcs)
+        self.dst = [torch.empty(t.numel(), dtype=torch.float8_e4m3fn, device=device) for t in self.srcs]
+        n = len(self.srcs)
+        self.amax = torch.zeros(n, dtype=torch.int32, device=device)
+        self.q = torch.ones(n, dtype=torch.float32, device=device)
+        self.dq = torch.ones(n, dtype=torch.float32, device=device)
+        jobs = (Fp8Job * n)(*[Fp8Job(s.data_ptr(), d.data_ptr(), s.numel(), k, 0)
+                              for k, (s, d) in enumerate(zip(self.srcs, self.dst))])
+        assert all(s.numel() % 8 == 0 and s.dtype == torch.bfloat16 and s.is_contiguous() for s in self.srcs)
+        self.table = torch.frombuffer(bytearray(bytes(jobs)), dtype=torch.uint8).to(device)
+        self.max_n = max(s.numel() for s in self.srcs)
+
+    def run(self):
+        n = len(self.srcs)
+        _lib.call("irgan_fp8_quant_batch", P(self.table), n, self.max_n, None, P(self.amax), stream())
+        fp8_scale(self.amax, self.q, self.dq, reset=True)
+        _lib.call("irgan_fp8_quant_batch", P(self.table), n, self.max_n, P(self.q), None, stream())
+
+
+class Fp8Acts:
+    """Per-tensor scales of fp8 activation operands with delayed scaling: a slot's
+    tensor is quantised with the q made from the amax it had at the previous step
+    (its first use calibrates from its own amax).  update() turns the recorded maxima
+    into the next step's q / dq."""
+
+    def __init__(self, n, device):
+        self.amax = torch.zeros(n, dtype=torch.int32, device=device)
+        self.q = torch.ones(n, dtype=torch.float32, device=device)
+        self.dq = torch.ones(n, dtype=torch.float32, device=device)
+        self.seen = [False] * n
+
+    def quant(self, slot, x: Feat, y: Feat):
+        if not self.seen[slot]:
+            fp8_quant(x, None, None, Pi(self.amax, slot))
+            fp8_scale(self.amax, self.q, self.dq, reset=False, start=slot, n=1)
+            self.seen[slot] = True
+        fp8_quant(x, y, Pi(self.q, slot), Pi(self.amax, slot))
+
+    def update(self, start=0, n=None):
+        fp8_scale(self.amax, self.q, self.dq, reset=True, start=start, n=n)
+
+
+def conv_fwd_fp8(pc: PackedConv, w8: torch.Tensor, dqw, x8: Feat, dqx, y: Feat, part: torch.Tensor = None,
+                 act=ACT_NONE, bias=True, accumulate=False) -> int:
+    """conv_fwd on fp8 operands (irgan_conv_fwd_fp8): x8 e4m3 NHWC, w8 the e4m3 copy
+    of pc.fwd; dqx / dqw: pointers to the dequantisation multipliers.  With ``part``
+    also the InstanceNorm partials of y; returns their count per image (else 0)."""
+    s = pc.spec
+    Ho, Wo = s.out_hw(x8.H, x8.W)
+    assert (y.H, y.W, y.C) == (Ho, Wo, s.cout) and x8.C == s.cin and y.N == x8.N and x8.dt == FP8
+    d = _desc(N=x8.N, H=x8.H, W=x8.W, Cin=s.cin, ldx=x8.ld, xoff=x8.off, Ho=Ho, Wo=Wo, Cout=s.cout, ldy=y.ld,
+              yoff=y.off, OH=Ho, OW=Wo, omy=1, ooy=0, omx=1, oox=0, KH=s.k, KW=s.k, sy=s.stride, sx=s.stride,
+              c0y=-s.pad, c0x=-s.pad, pad_mode=s.mode, act=act, accumulate=int(accumulate), dtype=FP8,
+              out_dtype=y.dt, mask_act=0, ldm=0, moff=0)
+    nb = ctypes.c_int32(0)
+    TIMER.wrap(conv_tag("fwd8", s, (x8.H, x8.W), x8.N), lambda: _lib.call(
+        "irgan_conv_fwd_fp8", ctypes.byref(d), x8.ptr, P(w8), dqx, dqw, P(pc.bias if bias else None), y.ptr,
+        P(part), ctypes.byref(nb), stream()))
+    return int(nb.value)
+
+
+def conv_dgrad_fp8(pc: PackedConv, wd8: torch.Tensor, dqw, dy8: Feat, dqx, dy: Feat, dx: Feat, accumulate=False):
+    """Backward-data of a reflect-padded stride-1 3x3 layer: the interior on fp8
+    operands (dy8 = e4m3(dy), wd8 = e4m3 copy of the flipped image pc.dg[0]), the
+    padded ring from the bf16 dy by irgan_reflect_dgrad_ring (as conv_dgrad)."""
+    s = pc.spec
+    assert pc.reflect and s.stride == 1 and dy.dt == BF16 and dy8.dt == FP8 and dx.C == s.cin
+    p = s.pad
+    H, W = dx.H, dx.W
+    (_, _, ay, c0y), (_, _, ax, c0x), buf = pc.dg[0]
+    base = dict(N=dy.N, H=dy.H, W=dy.W, Cin=pc.cout_eff, Cout=s.cin, KH=ay, KW=ax, pad_mode=PAD_ZERO, act=0,
+                mask_act=0, ldm=0, moff=0, Ho=H, Wo=W, ldy=dx.ld, yoff=dx.off, OH=H, OW=W, omy=1, ooy=0, omx=1,
+                oox=0, sy=1, sx=1, c0y=c0y + p, c0x=c0x + p, accumulate=int(accumulate), out_dtype=dx.dt)
+    d8 = _desc(**base, ldx=dy8.ld, xoff=dy8.off, dtype=FP8)
+    d = _desc(**base, ldx=dy.ld, xoff=dy.off, dtype=BF16)
+    nb = ctypes.c_int32(0)
+
+    def launch():
+        _lib.call("irgan_conv_fwd_fp8", ctypes.byref(d8), dy8.ptr, P(wd8), dqx, dqw, None, dx.ptr, None,
+                  ctypes.byref(nb), stream())
+        if p > 0:
+            _lib.call("irgan_reflect_dgrad_ring", ctypes.byref(d), dy.ptr, P(buf), p, dx.ptr, stream())
+    TIMER.wrap(conv_tag("dgrad8", s, (H, W), dx.N), launch)

@@ -21,7 +21,7 @@ __all__ = [
     "binomial_filter", "g_param_shapes", "d_param_shapes", "vgg_param_shapes",
     "seeded_params", "g_forward", "d_forward", "vgg_features", "tv_loss",
     "ssim_loss", "adam_update", "AdamState", "train_step", "PRE_IN_BIAS_G",
-    "PRE_IN_BIAS_D", "pre_in_bias_keys", "lr_lambda",
+    "PRE_IN_BIAS_D", "pre_in_bias_keys", "lr_lambda", "fp8_q",
 ]
 
 IN_EPS = 1e-5                       # nn.InstanceNorm2d default (ir:161)
@@ -159,8 +159,49 @@ def up_aa(x, filt):
     return F.conv2d(_rpad(y, 1), filt, stride=1, groups=x.shape[1])
 
 
-def g_forward(P, x, no_antialias=False, no_antialias_up=False, n_blocks=9, acts=None):
-    """ResnetUNetGenerator.forward (ir:533-569); returns the tanh image."""
+def fp8_q(t):
+    """Per-tensor e4m3 fake-quantisation with the product's power-of-two scale rule
+    (csrc/fp8.hip): q = 2^floor(log2(448 / max|t|)), e4m3(clamp(t * q)) / q."""
+    a = float(t.detach().abs().max())
+    q = 2.0 ** math.floor(math.log2(448.0 / a)) if a > 0 else 1.0
+    return (t.detach() * q).clamp(-448.0, 448.0).to(torch.float8_e4m3fn).to(t.dtype) / q
+
+
+class _Fp8ResConv(torch.autograd.Function):
+    """The fp8 path's ResnetBlock conv (reflect pad 1, 3x3; GeneratorEngine(fp8=True)):
+    forward on e4m3(x), e4m3(bf16(w)); backward-data on e4m3(dY) x e4m3(bf16(w)) over
+    the padded interior, the reflect ring folded from the unquantised dY and bf16(w);
+    the weight / bias gradients on the unquantised x and dY.  Not a reference
+    function: the emulation the fp8 step is checked against (ir:390-411 otherwise)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        wb = w.to(torch.bfloat16).to(w.dtype)
+        ctx.save_for_backward(x, w, wb)
+        return F.conv2d(_rpad(fp8_q(x), 1), fp8_q(wb), b)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, wb = ctx.saved_tensors
+        with torch.enable_grad():
+            xr = x.detach().requires_grad_(True)
+            wr = w.detach().requires_grad_(True)
+            y = F.conv2d(_rpad(xr, 1), wr)
+            dx_exact, dw = torch.autograd.grad(y, (xr, wr), gy)
+        H, W = x.shape[-2:]
+        xp = torch.zeros(x.shape[0], x.shape[1], H + 2, W + 2, dtype=x.dtype)
+        g8 = torch.nn.grad.conv2d_input(xp.shape, fp8_q(wb), fp8_q(gy))
+        gb = torch.nn.grad.conv2d_input(xp.shape, wb, gy)
+        xf = torch.zeros_like(x, requires_grad=True)
+        with torch.enable_grad():
+            ring = torch.autograd.grad(_rpad(xf, 1), xf, gb)[0] - gb[..., 1:-1, 1:-1]
+        del dx_exact
+        return g8[..., 1:-1, 1:-1] + ring, dw, gy.sum(dim=(0, 2, 3))
+
+
+def g_forward(P, x, no_antialias=False, no_antialias_up=False, n_blocks=9, acts=None, fp8=False):
+    """ResnetUNetGenerator.forward (ir:533-569); returns the tanh image.
+    fp8=True: the ResnetBlock convs as the fp8 path computes them (_Fp8ResConv)."""
     def rec(name, t):
         if acts is not None:
             acts[name] = t
@@ -177,8 +218,12 @@ def g_forward(P, x, no_antialias=False, no_antialias_up=False, n_blocks=9, acts=
     h = rec("x2", x2)
     for b in range(n_blocks):
         pre = f"resblocks.{b}.conv_block."
-        t = F.relu(_inorm(F.conv2d(_rpad(h, 1), P[pre + "1.weight"], P[pre + "1.bias"])))
-        t = _inorm(F.conv2d(_rpad(t, 1), P[pre + "5.weight"], P[pre + "5.bias"]))
+        if fp8:
+            t = F.relu(_inorm(_Fp8ResConv.apply(h, P[pre + "1.weight"], P[pre + "1.bias"])))
+            t = _inorm(_Fp8ResConv.apply(t, P[pre + "5.weight"], P[pre + "5.bias"]))
+        else:
+            t = F.relu(_inorm(F.conv2d(_rpad(h, 1), P[pre + "1.weight"], P[pre + "1.bias"])))
+            t = _inorm(F.conv2d(_rpad(t, 1), P[pre + "5.weight"], P[pre + "5.bias"]))
         h = h + t                                              # ir:417-418
     rec("x3", h)
     if no_antialias_up:
@@ -304,7 +349,7 @@ def _trainable(P):
 
 
 def train_step(G, D, V, ir, rgb, optG, optD, lam=None, no_antialias=False,
-               no_antialias_up=False, n_blocks=9, grad_hook=None):
+               no_antialias_up=False, n_blocks=9, grad_hook=None, fp8=False):
     """One train step, minimal form of ir:1636-1681.
 
     D step: hinge on D(cat[ir,rgb]) and D(cat[ir,G(ir)]) (G detached), D Adam.
@@ -320,7 +365,7 @@ def train_step(G, D, V, ir, rgb, optG, optD, lam=None, no_antialias=False,
     lam = dict(LAMBDAS, **(lam or {}))
     out = {}
     gk = {k: G[k].detach().clone().requires_grad_(k in _trainable(G)) for k in G}
-    fake = g_forward(gk, ir, no_antialias, no_antialias_up, n_blocks)
+    fake = g_forward(gk, ir, no_antialias, no_antialias_up, n_blocks, fp8=fp8)
     out["fake"] = fake.detach().clone()
 
     # ---- D step (ir:1636-1651)
