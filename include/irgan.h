@@ -85,18 +85,24 @@ int irgan_conv_fwd_fp8(const irgan_conv_desc* d, const void* x, const void* w, c
                        const float* dqw, const float* bias, void* y, void* part, int32_t* nb,
                        irgan_stream_t s);
 
+/* fp8 amax slots: each slot is IRGAN_FP8_AMAX_PARTS uint32 partial maxima (bits of
+ * non-negative floats); a kernel's block b raises part b % IRGAN_FP8_AMAX_PARTS of
+ * the slot it records into, irgan_fp8_scale takes the max over the parts. */
+enum { IRGAN_FP8_AMAX_PARTS = 256 };
+
 /* fp8 quantisation of an NHWC slice: y[p][yoff + c] = e4m3(clamp(x * q[0], +-448))
- * (round to nearest even; x bf16 or fp32 by dt; C, ld, off % 8 == 0), and
- * atomicMax(amax, bits(max |x|)) when amax != NULL.  y == NULL: the max only.
+ * (round to nearest even; x bf16 or fp32 by dt; C, ld, off % 8 == 0), and the
+ * max |x| recorded into the amax slot when amax != NULL.  y == NULL: the max only.
  * q == NULL: q = 1. */
 int irgan_fp8_quant(const void* x, int32_t dt, int64_t P, int32_t C, int32_t ldx, int32_t xoff,
                     void* y, int32_t ldy, int32_t yoff, const float* q, uint32_t* amax,
                     irgan_stream_t s);
-/* Per-tensor scales from recorded maxima, for n slots: q = 2^floor(log2(448 / amax))
- * (1 if amax is 0), dq = 1 / q; reset != 0 clears amax afterwards. */
+/* Per-tensor scales from recorded maxima, for n slots (amax: n x IRGAN_FP8_AMAX_PARTS):
+ * q = 2^floor(log2(448 / amax)) (1 if amax is 0), dq = 1 / q; reset != 0 clears the
+ * slots afterwards. */
 int irgan_fp8_scale(uint32_t* amax, int32_t n, float* q, float* dq, int32_t reset, irgan_stream_t s);
 /* A table of njobs irgan_fp8_job records (device memory; n % 8 == 0, bf16 src,
- * n <= max_n): amax != NULL -> atomicMax(amax[slot], max |src|) only; otherwise
+ * n <= max_n): amax != NULL -> max |src| into amax slot `slot` only; otherwise
  * dst = e4m3(clamp(src * q[slot], +-448)).  The per-step re-quantisation of the
  * packed fp8 weights: one amax launch, irgan_fp8_scale, one quantise launch. */
 typedef struct irgan_fp8_job {
@@ -185,6 +191,21 @@ int irgan_in_bwd_apply(const void* dy, int32_t dy_dtype, int32_t lddy, int32_t d
                        int32_t N, int32_t HW, int32_t C, const float* mr, const float* red,
                        void* dx, int32_t dx_dtype, int32_t lddx, int32_t dxoff, float* db,
                        irgan_stream_t s);
+
+/* irgan_in_apply (bf16 x, res, y) / irgan_in_bwd_apply (bf16, no db) that also
+ * write y8 = e4m3(clamp(bf16(y) * q[0], +-448)) (an NHWC fp8 slice) and record
+ * max |bf16(y)| into the amax slot (IRGAN_FP8_AMAX_PARTS partials): the producers
+ * of the fp8 path's ResnetBlock conv operands, so no separate quantise pass runs.
+ * IRGAN_EUNSUPPORTED when C, the strides or offsets are not multiples of 8. */
+int irgan_in_apply_fp8(const void* x, int32_t N, int32_t HW, int32_t C, int32_t ldx, int32_t xoff,
+                       const float* mr, int32_t act, const void* res, int32_t ldr, int32_t roff, void* y,
+                       int32_t ldy, int32_t yoff, void* y8, int32_t ld8, int32_t off8, const float* q,
+                       uint32_t* amax, irgan_stream_t s);
+int irgan_in_bwd_apply_fp8(const void* dy, int32_t lddy, int32_t dyoff, const void* dy2, int32_t lddy2,
+                           int32_t dy2off, const void* x, int32_t ldx, int32_t xoff, int32_t act, int32_t N,
+                           int32_t HW, int32_t C, const float* mr, const float* red, void* dx, int32_t lddx,
+                           int32_t dxoff, void* y8, int32_t ld8, int32_t off8, const float* q,
+                           uint32_t* amax, irgan_stream_t s);
 /* db[c] += sum over pixels of g[p][c] (bias gradient), g slice (dtype, ld, off).
  * work: IRGAN_IN_PARTS*C doubles of scratch. */
 int irgan_channel_sum(const void* g, int32_t dtype, int32_t P, int32_t C, int32_t ld,

@@ -21,7 +21,11 @@ PAD_ZERO, PAD_REFLECT = 0, 1
 ACT_NONE, ACT_RELU, ACT_LRELU, ACT_TANH = 0, 1, 2, 3
 
 
-IN_PARTS = int(re.search(r"IRGAN_IN_PARTS\s*=\s*(\d+)", open(HEADER).read()).group(1))
+def header_enum(name: str) -> int:
+    return int(re.search(name + r"\s*=\s*(\d+)", open(HEADER).read()).group(1))
+
+
+IN_PARTS = header_enum("IRGAN_IN_PARTS")
 
 
 def _desc_fields():

@@ -4,42 +4,24 @@
 //  * fp8_quant_kernel: y = e4m3(clamp(x * q, +-448)) for an NHWC slice (bf16 or
 //    fp32 in, dense or strided fp8 out; round to nearest even, the hardware
 //    v_cvt_pk_fp8_f32 = torch's float8_e4m3fn conversion), and the max |x| of
-//    what it read recorded into amax (uint32 bits of a non-negative float, so an
-//    integer max orders them).  One HBM pass: read 2 B, write 1 B per element.
+//    what it read recorded into the slot's IRGAN_FP8_AMAX_PARTS partial maxima
+//    (uint32 bits of a non-negative float, so an integer max orders them; block b
+//    updates part b % PARTS, so the atomics do not pile up on one address).  One
+//    HBM pass: read 2 B, write 1 B per element.
 //  * fp8_amax_kernel: the max only (first use of a tensor, weights).
-//  * fp8_scale_kernel: per slot, q = 2^floor(log2(448 / amax)) (1 when amax is 0
-//    or not finite), dq = 1 / q; optionally clears amax for the next step.  A
+//  * fp8_scale_kernel: per slot, amax = max of its partials, q =
+//    2^floor(log2(448 / amax)) (1 when amax is 0 or not finite), dq = 1 / q;
+//    optionally clears the partials for the next step.  A
 //    tensor quantised at step t uses the q made from its step t-1 amax (delayed
 //    scaling); values beyond 448 / q saturate.
 //  * the *_batch kernels run a table of jobs (the per-step weight re-quantisation
 //    of every fp8 layer in two launches).
 // Byte streams, no LDS beyond the block max, no MFMA.
-#include "common.h"
+#include "fp8_util.h"
 
 namespace {
 
 constexpr int TPB = 256;
-
-IRGAN_HD uint32_t pack4_fp8(float a, float b, float c, float d, float q) {
-    a = __builtin_amdgcn_fmed3f(a * q, 448.f, -448.f);
-    b = __builtin_amdgcn_fmed3f(b * q, 448.f, -448.f);
-    c = __builtin_amdgcn_fmed3f(c * q, 448.f, -448.f);
-    d = __builtin_amdgcn_fmed3f(d * q, 448.f, -448.f);
-    int v = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
-    v = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, v, true);
-    return (uint32_t)v;
-}
-
-__device__ void block_amax(float m, uint32_t* amax) {
-    __shared__ float red[TPB / 64];
-    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int k = 1; k < TPB / 64; ++k) m = fmaxf(m, red[k]);
-        if (m > 0.f) atomicMax(amax, __float_as_uint(m));
-    }
-}
 
 // 8 channels per thread-item; C % 8 == 0, ld / off % 8 == 0 (bf16) or % 4 (fp32).
 template <typename T>
@@ -69,26 +51,27 @@ __global__ __launch_bounds__(TPB) void fp8_quant_kernel(const T* __restrict__ x,
 #pragma unroll
         for (int k = 0; k < 8; ++k) m = fmaxf(m, fabsf(v[k]));
         if (y) {
-            uint2 o;
-            o.x = pack4_fp8(v[0], v[1], v[2], v[3], qs);
-            o.y = pack4_fp8(v[4], v[5], v[6], v[7], qs);
-            *(uint2*)(y + p * ldy + yoff + c) = o;
+            *(uint2*)(y + p * ldy + yoff + c) = pack8_fp8(v, qs);
         }
     }
-    if (amax) block_amax(m, amax);
+    if (amax) fp8_block_amax(m, amax, blockIdx.x);
 }
 
 __global__ void fp8_scale_kernel(uint32_t* __restrict__ amax, int n, float* __restrict__ q, float* __restrict__ dq,
                                  int reset) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const float a = __uint_as_float(amax[i]);
+    uint32_t* ap = amax + (long)i * IRGAN_FP8_AMAX_PARTS;
+    uint32_t mb = 0;
+    for (int k = 0; k < IRGAN_FP8_AMAX_PARTS; ++k) mb = ap[k] > mb ? ap[k] : mb;
+    const float a = __uint_as_float(mb);
     float s = 1.f;
     if (a > 0.f && a <= 3.0e38f) s = exp2f(floorf(log2f(448.f / a)));
     s = fminf(fmaxf(s, 0x1p-100f), 0x1p100f);
     q[i] = s;
     dq[i] = 1.f / s;  // exact: s is a power of two
-    if (reset) amax[i] = 0u;
+    if (reset)
+        for (int k = 0; k < IRGAN_FP8_AMAX_PARTS; ++k) ap[k] = 0u;
 }
 
 // job table: {src, dst, n, slot}; src bf16 contiguous, dst fp8 contiguous, n % 8 == 0
@@ -118,13 +101,10 @@ __global__ __launch_bounds__(TPB) void fp8_batch_kernel(const QJob* __restrict__
 #pragma unroll
             for (int k = 0; k < 8; ++k) m = fmaxf(m, fabsf(v[k]));
         } else {
-            uint2 o;
-            o.x = pack4_fp8(v[0], v[1], v[2], v[3], qs);
-            o.y = pack4_fp8(v[4], v[5], v[6], v[7], qs);
-            *(uint2*)(j.dst + e * 8) = o;
+            *(uint2*)(j.dst + e * 8) = pack8_fp8(v, qs);
         }
     }
-    if (amax) block_amax(m, amax + j.slot);
+    if (amax) fp8_block_amax(m, amax + (long)j.slot * IRGAN_FP8_AMAX_PARTS, blockIdx.x);
 }
 
 int grid_for(long items) { return (int)std::max<long>(1, std::min<long>(irgan_cdiv(items, TPB), 2048)); }

@@ -10,9 +10,19 @@
 // (<= IN_PARTS blocks per image), and the finalize launch sums the partials of
 // each (n, c) in fp64, in a fixed order (deterministic), into fp32 (mean, rstd)
 // or (mean g, mean g*xhat).
-#include "common.h"
+#include "fp8_util.h"
 
 namespace {
+
+// optional fp8 copy of a pass's bf16 output (the fp8 path's conv operands,
+// GeneratorEngine(fp8=True)): y8 = e4m3(clamp(bf16(y) * q[0])), max |bf16(y)|
+// into the amax slot -- the same bytes irgan_fp8_quant makes from the stored y
+struct Q8 {
+    uint8_t* p;
+    int ld, off;
+    const float* q;
+    uint32_t* amax;
+};
 
 constexpr int TPB = 256;
 constexpr int V = 8;          // channels per thread
@@ -275,13 +285,15 @@ IRGAN_HD void block_partials8(float* a0, float* a1, const Lay& L, bool on, int c
 // batch, unconverted, before using any; tail rows of the last batch re-load a
 // valid row and are masked.  dx may alias dy (no __restrict__ on either): a
 // thread stores only rows it has already loaded.
-template <int MODE, int U>
+template <int MODE, int U, bool F8 = false>
 __global__ __launch_bounds__(TPB) void rows8_kernel(const bf16_t* x, int ldx, int xoff, const bf16_t* dy, int lddy,
                                                     int dyoff, const bf16_t* dy2, int lddy2, int dy2off, int act,
                                                     const float* __restrict__ mr, const float* __restrict__ red,
                                                     bf16_t* dx, int lddx, int dxoff, int HW, int C, int rows_per_block,
-                                                    float2* __restrict__ part) {
+                                                    float2* __restrict__ part, Q8 q8 = Q8{}) {
     __shared__ float s0[TPB * 8], s1[TPB * 8];
+    const float qs = F8 ? *q8.q : 1.f;
+    float amx = 0.f;
     const int n = blockIdx.y;
     const int r0 = blockIdx.x * rows_per_block;
     const int r1 = min(HW, r0 + rows_per_block);
@@ -360,6 +372,13 @@ __global__ __launch_bounds__(TPB) void rows8_kernel(const bf16_t* x, int ldx, in
                         w.z = (uint32_t)f2bf(o[4]) | ((uint32_t)f2bf(o[5]) << 16);
                         w.w = (uint32_t)f2bf(o[6]) | ((uint32_t)f2bf(o[7]) << 16);
                         *(uint4*)(dx + (pb + r + u * L.RP) * lddx + dxoff + c) = w;
+                        if constexpr (F8) {
+                            float vb[8];
+                            bf8f(w, vb);
+#pragma unroll
+                            for (int k = 0; k < 8; ++k) amx = fmaxf(amx, fabsf(vb[k]));
+                            *(uint2*)(q8.p + (pb + r + u * L.RP) * q8.ld + q8.off + c) = pack8_fp8(vb, qs);
+                        }
                     }
                 }
             }
@@ -367,6 +386,7 @@ __global__ __launch_bounds__(TPB) void rows8_kernel(const bf16_t* x, int ldx, in
         if (MODE == 2) continue;  // uniform across the block
         block_partials8(a0, a1, L, on, cb, c, C, n, s0, s1, part);
     }
+    if constexpr (F8) fp8_block_amax(amx, q8.amax, blockIdx.y * gridDim.x + blockIdx.x);
 }
 
 // fp64 sum of the nb block partials of each (n, c).  Block (32 channels x 8
@@ -409,11 +429,13 @@ __global__ __launch_bounds__(256) void finalize_kernel(const float2* __restrict_
     }
 }
 
-template <int VW>
+template <int VW, bool F8 = false>
 __global__ __launch_bounds__(TPB) void apply_kernel(Slice X, int HW, int C, const float* __restrict__ mr, int act,
                                                     Slice R, void* __restrict__ y, int ldy, int yoff,
-                                                    void* __restrict__ xhat, long total) {
+                                                    void* __restrict__ xhat, long total, Q8 q8 = Q8{}) {
     const int CV = C / VW;
+    const float qs = F8 ? *q8.q : 1.f;
+    float amx = 0.f;
     for (long idx = blockIdx.x * (long)TPB + threadIdx.x; idx < total; idx += (long)gridDim.x * TPB) {
         const long p = idx / CV;
         const int c = (int)(idx - p * CV) * VW;
@@ -442,7 +464,17 @@ __global__ __launch_bounds__(TPB) void apply_kernel(Slice X, int HW, int C, cons
             for (int k = 0; k < VW; ++k) v[k] += rv[k];
         }
         stv_<VW>(y, X.dt, p * ldy + yoff + c, v);
+        if constexpr (F8) {  // bf16 output, VW == 8
+            float vb[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                vb[k] = bf2f(f2bf(v[k]));
+                amx = fmaxf(amx, fabsf(vb[k]));
+            }
+            *(uint2*)(q8.p + p * q8.ld + q8.off + c) = pack8_fp8(vb, qs);
+        }
     }
+    if constexpr (F8) fp8_block_amax(amx, q8.amax, blockIdx.x);
 }
 
 bool vec_ok(int C, std::initializer_list<int> lds) {
@@ -470,7 +502,8 @@ int blocks_per_image(long HW, int N, int RP) {
 
 template <int MODE>
 int launch_rows(Slice X, Slice DY, Slice DY2, int act, const float* mr, const float* red, void* dx, int dxdt, int lddx,
-                int dxoff, int N, int HW, int C, float2* part, float* db, bool vec, hipStream_t st, int* nb_out) {
+                int dxoff, int N, int HW, int C, float2* part, float* db, bool vec, hipStream_t st, int* nb_out,
+                const Q8* q8 = nullptr) {
     const int VW = vec ? V : 1;
     int nb = blocks_per_image(HW, N, rp_of(C, VW));
     const int rows = irgan_cdiv(HW, nb);
@@ -479,9 +512,13 @@ int launch_rows(Slice X, Slice DY, Slice DY2, int act, const float* mr, const fl
     static const bool fast = !getenv("IRGAN_NO_ROWS8");
     const bool bf = X.dt == IRGAN_BF16 && (MODE == 0 || (DY.dt == IRGAN_BF16 && (!DY2.p || DY2.dt == IRGAN_BF16))) &&
                     (MODE != 2 || (dxdt == IRGAN_BF16 && !db));
-    if (fast && vec && bf && MODE <= 2) {
+    if (q8 && !(vec && bf && MODE == 2)) return IRGAN_EUNSUPPORTED;
+    if ((fast || q8) && vec && bf && MODE <= 2) {
         const bf16_t *xp = (const bf16_t*)X.p, *gp = (const bf16_t*)DY.p, *hp = (const bf16_t*)DY2.p;
-        if (MODE == 0)
+        if (MODE == 2 && q8)
+            rows8_kernel<2, 4, true><<<g, TPB, 0, st>>>(xp, X.ld, X.off, gp, DY.ld, DY.off, hp, DY2.ld, DY2.off, act, mr,
+                                                        red, (bf16_t*)dx, lddx, dxoff, HW, C, rows, part, *q8);
+        else if (MODE == 0)
             rows8_kernel<0, 8><<<g, TPB, 0, st>>>(xp, X.ld, X.off, nullptr, 0, 0, nullptr, 0, 0, act, mr, red, nullptr,
                                                   0, 0, HW, C, rows, part);
         else
@@ -585,6 +622,42 @@ extern "C" int irgan_channel_sum(const void* g, int32_t dtype, int32_t P, int32_
     launch_rows<0>(X, Z, Z, 0, nullptr, nullptr, nullptr, 0, 0, 0, 1, P, C, (float2*)work, nullptr,
                    vec_ok(C, {ld, off}), st, &nb);
     colsum_finalize_kernel<<<irgan_cdiv(C, 256), 256, 0, st>>>((const float2*)work, db, nb, C);
+    IRGAN_LAUNCH_CHECK();
+    return 0;
+}
+
+// irgan_in_apply / irgan_in_bwd_apply that also write the fp8 copy of their bf16
+// output (Q8 above): the producers of the fp8 path's ResnetBlock conv operands.
+extern "C" int irgan_in_apply_fp8(const void* x, int32_t N, int32_t HW, int32_t C, int32_t ldx, int32_t xoff,
+                                  const float* mr, int32_t act, const void* res, int32_t ldr, int32_t roff, void* y,
+                                  int32_t ldy, int32_t yoff, void* y8, int32_t ld8, int32_t off8, const float* q,
+                                  uint32_t* amax, irgan_stream_t s) {
+    if (!x || !mr || !y || !y8 || !q || !amax) return IRGAN_EINVAL;
+    if (!vec_ok(C, {ldx, xoff, ldy, yoff, ld8, off8}) || (res && !vec_ok(C, {ldr, roff}))) return IRGAN_EUNSUPPORTED;
+    const long total = (long)N * HW * (C / V);
+    if (total <= 0) return 0;
+    const int blocks = (int)std::min<long>((total + TPB - 1) / TPB, 16384);
+    Slice X{x, IRGAN_BF16, ldx, xoff}, R{res, IRGAN_BF16, ldr, roff};
+    apply_kernel<V, true><<<blocks, TPB, 0, (hipStream_t)s>>>(X, HW, C, mr, act, R, y, ldy, yoff, nullptr, total,
+                                                               Q8{(uint8_t*)y8, ld8, off8, q, amax});
+    IRGAN_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int irgan_in_bwd_apply_fp8(const void* dy, int32_t lddy, int32_t dyoff, const void* dy2, int32_t lddy2,
+                                      int32_t dy2off, const void* x, int32_t ldx, int32_t xoff, int32_t act, int32_t N,
+                                      int32_t HW, int32_t C, const float* mr, const float* red, void* dx, int32_t lddx,
+                                      int32_t dxoff, void* y8, int32_t ld8, int32_t off8, const float* q,
+                                      uint32_t* amax, irgan_stream_t s) {
+    if (!dy || !x || !mr || !red || !dx || !y8 || !q || !amax) return IRGAN_EINVAL;
+    if ((long)N * HW * C <= 0) return 0;
+    const bool vec = vec_ok(C, {lddy, dyoff, ldx, xoff, lddx, dxoff, ld8, off8}) && (!dy2 || vec_ok(C, {lddy2, dy2off}));
+    if (!vec) return IRGAN_EUNSUPPORTED;
+    Slice X{x, IRGAN_BF16, ldx, xoff}, DY{dy, IRGAN_BF16, lddy, dyoff}, DY2{dy2, IRGAN_BF16, lddy2, dy2off};
+    const Q8 q8{(uint8_t*)y8, ld8, off8, q, amax};
+    const int rc = launch_rows<2>(X, DY, DY2, act, mr, red, dx, IRGAN_BF16, lddx, dxoff, N, HW, C, nullptr, nullptr,
+                                  true, (hipStream_t)s, nullptr, &q8);
+    if (rc) return rc;
     IRGAN_LAUNCH_CHECK();
     return 0;
 }

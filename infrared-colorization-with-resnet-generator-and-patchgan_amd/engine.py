@@ -240,10 +240,11 @@ class INLayer:
     fused_stats = True
     sum_bias_grad = False
 
-    def fwd(self, bufs: Buffers, name: str, x: Feat, y: Feat, act, res: Feat = None, xhat=None, nb=0):
+    def fwd(self, bufs: Buffers, name: str, x: Feat, y: Feat, act, res: Feat = None, xhat=None, nb=0, q8=None):
         """nb > 0: x's statistics partials are already in the shared work buffer
         (written by the producing conv, conv_fwd); only the reduction runs.
-        The {mean, rstd} table stays in ``bufs`` under ``name`` for bwd()."""
+        The {mean, rstd} table stays in ``bufs`` under ``name`` for bwd().
+        q8: also write y's fp8 copy (ops.in_apply)."""
         N, C = x.N, x.C
         work = bufs.flat("in_work", ops.IN_PARTS * N * C, torch.float64)
         mr = bufs.get("mr_" + name, (N * C * 2,), torch.float32)
@@ -251,14 +252,14 @@ class INLayer:
             ops.in_finalize(x, work, nb, mr)
         else:
             ops.in_stats(x, work, mr)
-        ops.in_apply(x, mr, y, act=act, res=res, xhat=xhat)
+        ops.in_apply(x, mr, y, act=act, res=res, xhat=xhat, q8=q8)
 
     def conv_fwd8(self, bufs: Buffers, name: str, pc, w8, dqw, x8: Feat, dqx, z: Feat, y: Feat, act,
-                  res: Feat = None):
+                  res: Feat = None, q8=None):
         """conv_fwd on fp8 operands (ops.conv_fwd_fp8) with the fused statistics."""
         work = bufs.flat("in_work", ops.IN_PARTS * z.N * z.C, torch.float64)
         nb = ops.conv_fwd_fp8(pc, w8, dqw, x8, dqx, z, part=work)
-        self.fwd(bufs, name, z, y, act, res=res, nb=nb)
+        self.fwd(bufs, name, z, y, act, res=res, nb=nb, q8=q8)
 
     def conv_fwd(self, bufs: Buffers, name: str, pc, x: Feat, z: Feat, y: Feat, act, res: Feat = None):
         """z = conv(x) (kept for the backward), y = act(IN(z) [+ res]): the IN statistics
@@ -269,13 +270,15 @@ class INLayer:
             ops.conv_fwd(pc, x, z)
         self.fwd(bufs, name, z, y, act, res=res, nb=nb)
 
-    def bwd(self, bufs: Buffers, name: str, dy: Feat, z: Feat, act, dx: Feat, db=None, dy2: Feat = None):
-        """z: the PRE-norm input kept from forward; act: the activation after IN."""
+    def bwd(self, bufs: Buffers, name: str, dy: Feat, z: Feat, act, dx: Feat, db=None, dy2: Feat = None, q8=None):
+        """z: the PRE-norm input kept from forward; act: the activation after IN.
+        q8: also write dx's fp8 copy (ops.in_backward)."""
         N, C = z.N, z.C
         work = bufs.flat("in_work", ops.IN_PARTS * N * C, torch.float64)
         red = bufs.flat("in_red", 2 * N * C)
         mr = bufs.d["mr_" + name]
-        ops.in_backward(dy, z, act, mr, work, red, dx, db=db if INLayer.sum_bias_grad else None, dy2=dy2)
+        ops.in_backward(dy, z, act, mr, work, red, dx, db=db if INLayer.sum_bias_grad else None, dy2=dy2,
+                        q8=q8 if not INLayer.sum_bias_grad else None)
 
 
 # ----------------------------------------------------------------------------
@@ -386,22 +389,30 @@ class GeneratorEngine:
             self.norms["down2"].conv_fwd(g, "down2", self.down2, x1, z2, a2, ACT_RELU)
             ops.blur_down(a2, h)
         # 9 ResnetBlocks  (ir:362-418, 485-490)
+        # fp8: one e4m3 operand buffer, written by the producer of each conv input (the
+        # IN passes, fused; h_0 from blur-down by a quantise launch) and read by the conv
         x8 = Feat(g.get("x8", (B, H2, W2, c2), torch.float8_e4m3fn)) if self.fp8 else None
+        A = self.f8a if self.fp8 else None
+        if self.fp8:
+            A.quant(0, h, x8)
+        nres = len(self.res)
         for b, (p1, p2) in enumerate(self.res):
             r1 = Feat(g.get(f"r1_{b}", (B, H2, W2, c2), T))
             t = Feat(g.get(f"t{b}", (B, H2, W2, c2), T))
             if self.fp8:
-                self.f8a.quant(2 * b, h, x8)
-                self.norms[f"r{b}_1"].conv_fwd8(g, f"r{b}_1", p1, *self._w8(4 * b), x8,
-                                                ops.Pi(self.f8a.dq, 2 * b), r1, t, ACT_RELU)
+                self.norms[f"r{b}_1"].conv_fwd8(g, f"r{b}_1", p1, *self._w8(4 * b), x8, A.dqp(2 * b), r1, t,
+                                                ACT_RELU, q8=A.spec(2 * b + 1, x8))
+                A.ensure(2 * b + 1, t, x8)
             else:
                 self.norms[f"r{b}_1"].conv_fwd(g, f"r{b}_1", p1, h, r1, t, ACT_RELU)
             r2 = Feat(g.get(f"r2_{b}", (B, H2, W2, c2), T))
             hn = Feat(g.get(f"h{b + 1}", (B, H2, W2, c2), T))
             if self.fp8:
-                self.f8a.quant(2 * b + 1, t, x8)
-                self.norms[f"r{b}_2"].conv_fwd8(g, f"r{b}_2", p2, *self._w8(4 * b + 2), x8,
-                                                ops.Pi(self.f8a.dq, 2 * b + 1), r2, hn, ACT_NONE, res=h)
+                nxt = 2 * b + 2 if b + 1 < nres else None   # the next block's conv1 input
+                self.norms[f"r{b}_2"].conv_fwd8(g, f"r{b}_2", p2, *self._w8(4 * b + 2), x8, A.dqp(2 * b + 1), r2,
+                                                hn, ACT_NONE, res=h, q8=A.spec(nxt, x8) if nxt else None)
+                if nxt:
+                    A.ensure(nxt, hn, x8)
             else:
                 self.norms[f"r{b}_2"].conv_fwd(g, f"r{b}_2", p2, t, r2, hn, ACT_NONE, res=h)
             h = hn
@@ -521,20 +532,23 @@ class GeneratorEngine:
             key = f"resblocks.{b}.conv_block."
             t, hb = Feat(g.d[f"t{b}"]), Feat(g.d[f"h{b}"])
             r1, r2 = Feat(g.d[f"r1_{b}"]), Feat(g.d[f"r2_{b}"])
-            self.norms[f"r{b}_2"].bwd(g, f"r{b}_2", dh, r2, ACT_NONE, dt_, db=S.krsc(key + "5.bias", G))
+            A = self.f8a if self.fp8 else None
+            s2, s1 = nb2 + 2 * b, nb2 + 2 * b + 1
+            self.norms[f"r{b}_2"].bwd(g, f"r{b}_2", dh, r2, ACT_NONE, dt_, db=S.krsc(key + "5.bias", G),
+                                      q8=A.spec(s2, dy8) if self.fp8 else None)
             wg(p2, key + "5", t, dt_)
             dr = Feat(g.get("dtmp2", (B, H2, W2, c2), T))
             if self.fp8:
-                self.f8a.quant(nb2 + 2 * b, dt_, dy8)
-                ops.conv_dgrad_fp8(p2, *self._w8(4 * b + 3), dy8, ops.Pi(self.f8a.dq, nb2 + 2 * b), dt_, dr)
+                A.ensure(s2, dt_, dy8)
+                ops.conv_dgrad_fp8(p2, *self._w8(4 * b + 3), dy8, A.dqp(s2), dt_, dr)
             else:
                 ops.conv_dgrad(p2, dt_, dr, pad_buf=padbuf)
-            self.norms[f"r{b}_1"].bwd(g, f"r{b}_1", dr, r1, ACT_RELU, dr, db=S.krsc(key + "1.bias", G))
+            self.norms[f"r{b}_1"].bwd(g, f"r{b}_1", dr, r1, ACT_RELU, dr, db=S.krsc(key + "1.bias", G),
+                                      q8=A.spec(s1, dy8) if self.fp8 else None)
             wg(p1, key + "1", hb, dr)
             if self.fp8:
-                self.f8a.quant(nb2 + 2 * b + 1, dr, dy8)
-                ops.conv_dgrad_fp8(p1, *self._w8(4 * b + 1), dy8, ops.Pi(self.f8a.dq, nb2 + 2 * b + 1), dr, dh,
-                                   accumulate=True)
+                A.ensure(s1, dr, dy8)
+                ops.conv_dgrad_fp8(p1, *self._w8(4 * b + 1), dy8, A.dqp(s1), dr, dh, accumulate=True)
             else:
                 ops.conv_dgrad(p1, dr, dh, accumulate=True, pad_buf=padbuf)
             ready(key + "1.weight")

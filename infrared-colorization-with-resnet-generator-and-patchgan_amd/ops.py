@@ -387,15 +387,25 @@ def in_finalize(x: Feat, part: torch.Tensor, nb: int, mr: torch.Tensor):
     _lib.call("irgan_in_finalize", P(part), x.N, x.H * x.W, x.C, nb, P(mr), stream())
 
 
-def in_apply(x: Feat, mr, y: Feat, act=ACT_NONE, res: Feat = None, xhat: torch.Tensor = None):
+def in_apply(x: Feat, mr, y: Feat, act=ACT_NONE, res: Feat = None, xhat: torch.Tensor = None, q8=None):
+    """y = act(IN(x)) [+ res].  q8 = (y8 Feat, q ptr, amax ptr): also the fp8 copy of y
+    (irgan_in_apply_fp8; bf16, no xhat)."""
     assert x.dt == y.dt
+    if q8 is not None:
+        y8, qp, ap = q8
+        assert xhat is None and x.dt == BF16 and y8.dt == FP8 and (y8.N, y8.H, y8.W, y8.C) == (y.N, y.H, y.W, y.C)
+        _lib.call("irgan_in_apply_fp8", x.ptr, x.N, x.H * x.W, x.C, x.ld, x.off, P(mr), act,
+                  res.ptr if res else None, res.ld if res else 0, res.off if res else 0, y.ptr, y.ld, y.off,
+                  y8.ptr, y8.ld, y8.off, qp, ap, stream())
+        return
     _lib.call("irgan_in_apply", x.ptr, x.dt, x.N, x.H * x.W, x.C, x.ld, x.off, P(mr), act,
               res.ptr if res else None, res.ld if res else 0, res.off if res else 0, y.ptr, y.ld, y.off, P(xhat),
               stream())
 
 
-def in_bwd_parts(dy: Feat, x: Feat, act: int, mr, work, red, dx: Feat, db=None, dy2: Feat = None):
-    """(reduce, apply) launch closures of in_backward (also used for per-pass timing)."""
+def in_bwd_parts(dy: Feat, x: Feat, act: int, mr, work, red, dx: Feat, db=None, dy2: Feat = None, q8=None):
+    """(reduce, apply) launch closures of in_backward (also used for per-pass timing).
+    q8 = (y8 Feat, q ptr, amax ptr): the apply also writes the fp8 copy of dx."""
     N, HW, C = x.N, x.H * x.W, x.C
     d2 = (dy2.ptr, dy2.dt, dy2.ld, dy2.off) if dy2 is not None else (None, 0, 0, 0)
 
@@ -404,14 +414,20 @@ def in_bwd_parts(dy: Feat, x: Feat, act: int, mr, work, red, dx: Feat, db=None, 
                   P(mr), P(work), P(red), stream())
 
     def apply():
+        if q8 is not None:
+            y8, qp, ap = q8
+            assert db is None and y8.dt == FP8 and dx.dt == BF16 and (y8.N, y8.H, y8.W, y8.C) == (dx.N, dx.H, dx.W, C)
+            _lib.call("irgan_in_bwd_apply_fp8", dy.ptr, dy.ld, dy.off, d2[0], d2[2], d2[3], x.ptr, x.ld, x.off, act,
+                      N, HW, C, P(mr), P(red), dx.ptr, dx.ld, dx.off, y8.ptr, y8.ld, y8.off, qp, ap, stream())
+            return
         _lib.call("irgan_in_bwd_apply", dy.ptr, dy.dt, dy.ld, dy.off, *d2, x.ptr, x.dt, x.ld, x.off, act, N, HW, C,
                   P(mr), P(red), dx.ptr, dx.dt, dx.ld, dx.off, P(db), stream())
     return reduce, apply
 
 
-def in_backward(dy: Feat, x: Feat, act: int, mr, work, red, dx: Feat, db=None, dy2: Feat = None):
+def in_backward(dy: Feat, x: Feat, act: int, mr, work, red, dx: Feat, db=None, dy2: Feat = None, q8=None):
     """dx = backward of act(IN(x)) applied to (dy [+ dy2]); x = PRE-norm input."""
-    reduce, apply = in_bwd_parts(dy, x, act, mr, work, red, dx, db, dy2)
+    reduce, apply = in_bwd_parts(dy, x, act, mr, work, red, dx, db, dy2, q8)
     reduce()
     apply()
 
@@ -658,10 +674,22 @@ def fp8_quant(x: Feat, y: Feat = None, q=None, amax=None):
               y.ld if y is not None else 0, y.off if y is not None else 0, q, amax, stream())
 
 
+FP8_AMAX_PARTS = _lib.header_enum("IRGAN_FP8_AMAX_PARTS")
+
+
+def amax_slots(n, device):
+    """n amax slots of FP8_AMAX_PARTS partial maxima each (irgan.h)."""
+    return torch.zeros(n * FP8_AMAX_PARTS, dtype=torch.int32, device=device)
+
+
+def amax_ptr(amax: torch.Tensor, slot: int):
+    return Pi(amax, slot * FP8_AMAX_PARTS)
+
+
 def fp8_scale(amax: torch.Tensor, q: torch.Tensor, dq: torch.Tensor, reset=True, start=0, n=None):
     """Slots [start, start+n): q = 2^floor(log2(448 / amax)), dq = 1 / q (irgan_fp8_scale)."""
-    n = amax.numel() - start if n is None else n
-    _lib.call("irgan_fp8_scale", Pi(amax, start), n, Pi(q, start), Pi(dq, start), int(reset), stream())
+    n = q.numel() - start if n is None else n
+    _lib.call("irgan_fp8_scale", amax_ptr(amax, start), n, Pi(q, start), Pi(dq, start), int(reset), stream())
 
 
 class Fp8Job(ctypes.Structure):
@@ -679,7 +707,7 @@ class Fp8Weights:
         self.srcs = list(srcs)
         self.dst = [torch.empty(t.numel(), dtype=torch.float8_e4m3fn, device=device) for t in self.srcs]
         n = len(self.srcs)
-        self.amax = torch.zeros(n, dtype=torch.int32, device=device)
+        self.amax = amax_slots(n, device)
         self.q = torch.ones(n, dtype=torch.float32, device=device)
         self.dq = torch.ones(n, dtype=torch.float32, device=device)
         jobs = (Fp8Job * n)(*[Fp8Job(s.data_ptr(), d.data_ptr(), s.numel(), k, 0)
@@ -702,17 +730,31 @@ class Fp8Acts:
     into the next step's q / dq."""
 
     def __init__(self, n, device):
-        self.amax = torch.zeros(n, dtype=torch.int32, device=device)
+        self.amax = amax_slots(n, device)
         self.q = torch.ones(n, dtype=torch.float32, device=device)
         self.dq = torch.ones(n, dtype=torch.float32, device=device)
         self.seen = [False] * n
 
     def quant(self, slot, x: Feat, y: Feat):
+        """Standalone quantisation of x into y (irgan_fp8_quant)."""
         if not self.seen[slot]:
-            fp8_quant(x, None, None, Pi(self.amax, slot))
+            fp8_quant(x, None, None, amax_ptr(self.amax, slot))
             fp8_scale(self.amax, self.q, self.dq, reset=False, start=slot, n=1)
             self.seen[slot] = True
-        fp8_quant(x, y, Pi(self.q, slot), Pi(self.amax, slot))
+        fp8_quant(x, y, Pi(self.q, slot), amax_ptr(self.amax, slot))
+
+    def spec(self, slot, y: Feat):
+        """The (y8, q, amax) side output for a producer that writes the fp8 copy itself
+        (in_apply / in_backward q8=), or None before the slot is calibrated -- then the
+        caller runs ensure() on the produced tensor."""
+        return (y, Pi(self.q, slot), amax_ptr(self.amax, slot)) if self.seen[slot] else None
+
+    def ensure(self, slot, x: Feat, y: Feat):
+        if not self.seen[slot]:
+            self.quant(slot, x, y)
+
+    def dqp(self, slot):
+        return Pi(self.dq, slot)
 
     def update(self, start=0, n=None):
         fp8_scale(self.amax, self.q, self.dq, reset=True, start=start, n=n)

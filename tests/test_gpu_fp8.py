@@ -39,12 +39,12 @@ def test_quant_bit_exact_and_amax(ops):
     xd = x.to(DEV)
     for qv in (1.0, 4.0, 2.0 ** -3, 2.0 ** 6):
         qt = torch.tensor([qv], device=DEV)
-        amax = torch.zeros(1, dtype=torch.int32, device=DEV)
+        amax = ops.amax_slots(1, DEV)
         y = torch.empty(x.shape, dtype=torch.float8_e4m3fn, device=DEV)
-        ops.fp8_quant(ops.Feat(xd), ops.Feat(y), ops.Pi(qt, 0), ops.Pi(amax, 0))
+        ops.fp8_quant(ops.Feat(xd), ops.Feat(y), ops.Pi(qt, 0), ops.amax_ptr(amax, 0))
         want = e4m3(x.float() * qv)
         assert torch.equal(y.cpu().view(torch.uint8), want.view(torch.uint8)), qv
-        assert amax.cpu().view(torch.float32).item() == x.float().abs().max().item()
+        assert amax.cpu().view(torch.float32).max().item() == x.float().abs().max().item()
     # channel slice in, channel slice out (the step quantises NHWC slices)
     xs = torch.randn(2, 5, 7, 48).bfloat16().to(DEV)
     ys = torch.zeros(2, 5, 7, 40, dtype=torch.float8_e4m3fn, device=DEV)
@@ -55,13 +55,58 @@ def test_quant_bit_exact_and_amax(ops):
 
 def test_scale_rule(ops):
     vals = [0.0, 1.0, 448.0, 500.0, 1e-3, 3.0]
-    amax = torch.tensor(vals, dtype=torch.float32).view(torch.int32).to(DEV)
+    amax = ops.amax_slots(len(vals), DEV)
+    part = torch.tensor(vals, dtype=torch.float32).view(torch.int32)
+    amax.view(len(vals), -1)[:, 7] = part.to(DEV)          # one partial per slot holds the max
+    amax.view(len(vals), -1)[:, 3] = (part.view(torch.float32) * 0.5).view(torch.int32).to(DEV)
     qt = torch.zeros(len(vals), device=DEV)
     dq = torch.zeros(len(vals), device=DEV)
     ops.fp8_scale(amax, qt, dq, reset=True)
     want = [1.0, 256.0, 1.0, 0.5, 2.0 ** 18, 128.0]
     assert qt.cpu().tolist() == want and dq.cpu().tolist() == [1.0 / v for v in want]
     assert not amax.any()
+
+
+def test_in_passes_emit_fp8_copy(ops):
+    """The IN forward apply (ReLU, and + residual) and the IN backward apply write the
+    same fp8 bytes and amax as irgan_fp8_quant of the bf16 tensor they store."""
+    torch.manual_seed(5)
+    N, HW, C = 2, 12 * 10, 256
+    Fe = ops.Feat
+    z = torch.randn(N, 12, 10, C).bfloat16().to(DEV)
+    res = torch.randn(N, 12, 10, C).bfloat16().to(DEV)
+    mr = torch.empty(N * C * 2, device=DEV)
+    work = torch.empty(ops.IN_PARTS * N * C, dtype=torch.float64, device=DEV)
+    ops.in_stats(Fe(z), work, mr)
+    qt = torch.tensor([8.0], device=DEV)
+
+    def same(y, y8, amax):
+        ref8 = torch.empty_like(y8)
+        ra = ops.amax_slots(1, DEV)
+        ops.fp8_quant(Fe(y), Fe(ref8), ops.Pi(qt, 0), ops.amax_ptr(ra, 0))
+        assert torch.equal(y8.view(torch.uint8), ref8.view(torch.uint8))
+        assert amax.max().item() == ra.max().item() > 0
+
+    for act, r in ((ops.ACT_RELU, None), (ops.ACT_NONE, res)):
+        y = torch.empty_like(z)
+        y8 = torch.empty(z.shape, dtype=torch.float8_e4m3fn, device=DEV)
+        amax = ops.amax_slots(1, DEV)
+        ops.in_apply(Fe(z), mr, Fe(y), act=act, res=Fe(r) if r is not None else None,
+                     q8=(Fe(y8), ops.Pi(qt, 0), ops.amax_ptr(amax, 0)))
+        y2 = torch.empty_like(z)
+        ops.in_apply(Fe(z), mr, Fe(y2), act=act, res=Fe(r) if r is not None else None)
+        assert torch.equal(y, y2)
+        same(y, y8, amax)
+    dy = torch.randn(N, 12, 10, C).bfloat16().to(DEV)
+    red = torch.empty(2 * N * C, device=DEV)
+    dx, dx2 = torch.empty_like(z), torch.empty_like(z)
+    y8 = torch.empty(z.shape, dtype=torch.float8_e4m3fn, device=DEV)
+    amax = ops.amax_slots(1, DEV)
+    ops.in_backward(Fe(dy), Fe(z), ops.ACT_RELU, mr, work, red, Fe(dx), q8=(Fe(y8), ops.Pi(qt, 0),
+                                                                            ops.amax_ptr(amax, 0)))
+    ops.in_backward(Fe(dy), Fe(z), ops.ACT_RELU, mr, work, red, Fe(dx2))
+    assert torch.equal(dx, dx2)
+    same(dx, y8, amax)
 
 
 def _weights(ops, spec, w, b):
