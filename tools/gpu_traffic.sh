@@ -11,5 +11,5 @@ for K in fwd dgrad wgrad; do
 done
 python tools/traffic_summary.py $O > $O/traffic.json
 cat $O/traffic.json
-timeout -k 10 300 python -u -m pytest tests/test_gpu_infer.py -x -v --timeout 120 --timeout-method thread > $O/pytest_infer.log 2>&1
+
 echo ALLDONE

@@ -12,9 +12,9 @@ import json
 import os
 import sys
 
-FAMILIES = {"fwd": ("conv_pp_kernel<3, 3, 256, false>",),
-            "dgrad": ("conv_pp_kernel<3, 3, 256, false>", "reflect_ring_kernel"),
-            "wgrad": ("wgrad_halo_kernel<128, 3, 1",)}
+FAMILIES = {"fwd": ("conv_pp_kernel<3, 3, 256, false, false, false>",),
+            "dgrad": ("conv_pp_kernel<3, 3, 256, false, false, false>", "reflect_ring_kernel"),
+            "wgrad": ("wgrad_pc_kernel<8>", "wgrad_pc_reduce")}
 
 
 def per_kernel(d, counter):
