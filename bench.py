@@ -42,7 +42,7 @@ def pmc_traffic(family):
     from the committed rocprofv3 --pmc passes of tools/gpu_traffic.sh (FETCH_SIZE
     doubled per the gfx950 correction, plus WRITE_SIZE).  PMC counters cannot be
     collected inside this process, so the measured figure is read, not recomputed."""
-    p = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+    p = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
     try:
         with open(p) as f:
             return json.load(f)[family]["hbm_bytes"]
@@ -240,7 +240,7 @@ def main():
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4) if achieved else None, "traffic": traffic,
                          "traffic_unit": "HBM bytes per launch (rocprofv3 PMC: 2*FETCH_SIZE + WRITE_SIZE, "
-                                         "profiles/r01_pmc_traffic.json)",
+                                         "profiles/r02_pmc_traffic.json)",
                          "flop_per_launch": res_flop, "per_kernel": kern},
             "losses": {k: round(v, 5) for k, v in losses.items()},
         }

@@ -28,6 +28,8 @@ extern "C" int irgan_conv_wgrad_halo(const irgan_conv_desc* d, const void* x, co
                                      float* ws, long ws_cap, hipStream_t st);
 extern "C" int irgan_conv_wgrad_pc(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, int splitk,
                                    float* ws, long ws_cap, hipStream_t st);
+extern "C" int irgan_conv_wgrad_narrow(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, float* ws,
+                                       long ws_cap, hipStream_t st);
 extern "C" int irgan_conv_wgrad_glds(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, int splitk,
                                      hipStream_t st);
 
@@ -601,6 +603,10 @@ int launch_wgrad(const irgan_conv_desc* d, const void* x, const void* dy, float*
     const bool fa = (d->Cout % EPC == 0) && (d->ldy % EPC == 0) && (d->yoff % EPC == 0);
     const bool fb = (d->Cin % 64 == 0) && (d->ldx % EPC == 0) && (d->xoff % EPC == 0);
     if constexpr (sizeof(T) == 2) {
+        {   // 8-channel inputs (G inc, D model.0): conv_wgrad_narrow.hip
+            const int rc = irgan_conv_wgrad_narrow(d, x, dy, dw, ws, ws_cap, st);
+            if (rc != IRGAN_EUNSUPPORTED) return rc;
+        }
         {   // 3x3 stride-1, Cout % 128: producer/consumer row-segment kernel (conv_wgrad_pc.hip)
             const int rc = irgan_conv_wgrad_pc(d, x, dy, dw, splitk, ws, ws_cap, st);
             if (rc != IRGAN_EUNSUPPORTED) return rc;

@@ -19,7 +19,8 @@ as do writes outside the output channel slice (checked separately).  Cases cover
 every family the dispatch reaches on the train step: conv_pp (BN 256/192/128/64,
 plain / accumulate / fused-IN-stats), the reflect ring, conv_c8 (incl. stride 2),
 conv_narrow, conv_halo, conv_glds (stride 2, per-phase dgrad), wgrad_halo (row
-segments, slab split-K), wgrad_glds and the generic fallbacks, with ragged tiles.
+segments, slab split-K), wgrad_pc, wgrad_narrow (8-channel inputs), wgrad_glds and the
+generic fallbacks, with ragged tiles.
 """
 import pytest
 import torch
@@ -44,6 +45,10 @@ EXTRA_CASES = [
     (256, 512, 4, 1, 1, 0, 13),    # D model.8
     (128, 256, 4, 2, 1, 0, 34),    # D model.5 (stride 2: glds fwd, per-phase dgrad)
     (8, 64, 4, 2, 1, 0, 66),       # D model.0 with the 8-channel padded input
+    # 8-channel-input weight gradient (conv_wgrad_narrow.hip): inc 7x7 reflect, D model.0 s2, ragged rows
+    (1, 64, 7, 1, 3, 1, 37),
+    (1, 64, 7, 1, 3, 1, 130),
+    (4, 64, 4, 2, 1, 0, 258),
     # Wo % 64 == 0, Cout % 128 == 0: the producer/consumer wgrad (conv_wgrad_pc.hip)
     (128, 256, 3, 1, 1, 0, 64),    # down2 shape, zero pad, 2 co tiles
     (384, 128, 3, 1, 1, 0, 64),    # up1_conv shape, 6 ci chunks
