@@ -389,18 +389,20 @@ __global__ __launch_bounds__(TPB) void rows8_kernel(const bf16_t* x, int ldx, in
     if constexpr (F8) fp8_block_amax(amx, q8.amax, blockIdx.y * gridDim.x + blockIdx.x);
 }
 
-// fp64 sum of the nb block partials of each (n, c).  Block (32 channels x 8
-// partial lanes) per (image, channel group): loads are 256-byte rows of
-// consecutive channels, the 8 lanes of a channel combine through LDS in a fixed
-// order (deterministic).
+// fp64 sum of the nb block partials of each (n, c).  Block (FC channels x FS
+// partial lanes) per (image, channel group): a lane adds partials sub, sub + FS,
+// ... (at most nb / FS dependent loads: the launch is latency-bound, so the
+// partial lanes are many and the channel groups narrow), then the FS lanes of a
+// channel combine through LDS in a fixed order (deterministic).
+constexpr int FC = 8, FS = 32;
 __global__ __launch_bounds__(256) void finalize_kernel(const float2* __restrict__ part, float* __restrict__ mr, int N,
                                                        int C, int nb, int HW, int mode) {
-    __shared__ double s0[8][32], s1[8][32];
-    const int n = blockIdx.y, cl = threadIdx.x & 31, sub = threadIdx.x >> 5;
-    const int c = blockIdx.x * 32 + cl;
+    __shared__ double s0[FS][FC], s1[FS][FC];
+    const int n = blockIdx.y, cl = threadIdx.x % FC, sub = threadIdx.x / FC;
+    const int c = blockIdx.x * FC + cl;
     double s = 0.0, q = 0.0;
     if (c < C) {
-        for (int b = sub; b < nb; b += 8) {
+        for (int b = sub; b < nb; b += FS) {
             const float2 v = part[((long)n * nb + b) * C + c];
             s += v.x;
             q += v.y;
@@ -412,7 +414,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(const float2* __restrict_
     if (sub != 0 || c >= C) return;
     s = 0.0;
     q = 0.0;
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < FS; ++k) {
         s += s0[k][cl];
         q += s1[k][cl];
     }
@@ -545,7 +547,7 @@ extern "C" int irgan_in_stats(const void* x, int32_t dtype, int32_t N, int32_t H
     int nb = 1;
     launch_rows<0>(X, Z, Z, 0, nullptr, nullptr, nullptr, 0, 0, 0, N, HW, C, (float2*)work, nullptr,
                    vec_ok(C, {ld, off}), st, &nb);
-    finalize_kernel<<<dim3(irgan_cdiv(C, 32), N), 256, 0, st>>>((const float2*)work, mr, N, C, nb, HW, 0);
+    finalize_kernel<<<dim3(irgan_cdiv(C, FC), N), 256, 0, st>>>((const float2*)work, mr, N, C, nb, HW, 0);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }
@@ -554,7 +556,7 @@ extern "C" int irgan_in_finalize(const void* part, int32_t N, int32_t HW, int32_
                                  irgan_stream_t s) {
     if ((long)N * HW * C <= 0) return 0;
     if (!part || !mr || nb < 1 || nb > IRGAN_IN_PARTS) return IRGAN_EINVAL;
-    finalize_kernel<<<dim3(irgan_cdiv(C, 32), N), 256, 0, (hipStream_t)s>>>((const float2*)part, mr, N, C, nb, HW, 0);
+    finalize_kernel<<<dim3(irgan_cdiv(C, FC), N), 256, 0, (hipStream_t)s>>>((const float2*)part, mr, N, C, nb, HW, 0);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }
@@ -586,7 +588,7 @@ extern "C" int irgan_in_bwd_reduce(const void* dy, int32_t dy_dtype, int32_t ldd
     Slice X{x, x_dtype, ldx, xoff}, DY{dy, dy_dtype, lddy, dyoff}, DY2{dy2, dy2_dtype, lddy2, dy2off};
     int nb = 1;
     launch_rows<1>(X, DY, DY2, act, mr, nullptr, nullptr, 0, 0, 0, N, HW, C, (float2*)work, nullptr, vec, st, &nb);
-    finalize_kernel<<<dim3(irgan_cdiv(C, 32), N), 256, 0, st>>>((const float2*)work, red, N, C, nb, HW, 1);
+    finalize_kernel<<<dim3(irgan_cdiv(C, FC), N), 256, 0, st>>>((const float2*)work, red, N, C, nb, HW, 1);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }
