@@ -102,8 +102,11 @@ struct PP {
 typedef int v8i_t __attribute__((ext_vector_type(8)));
 IRGAN_HD v8i_t cat8(i32x4 a, i32x4 b) { return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7); }
 
-template <int KH, int KW, int BN, bool ACC, bool STATS = false, bool F8 = false>
-__global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
+// ONE: the input has a single channel chunk (Cin == 64 in bf16), so one halo buffer
+// suffices; at BN = 64 the block then fits twice per CU (LDS 62 KiB, <= 128 VGPRs),
+// and one block's prologue / epilogue overlaps the other's MFMA loop.
+template <int KH, int KW, int BN, bool ACC, bool STATS = false, bool F8 = false, bool ONE = false>
+__global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
                                                          const bf16_t* __restrict__ w, const float* __restrict__ bias,
                                                          void* __restrict__ y, const void* __restrict__ mask,
                                                          int ntn, int tpx, int tpy, int swz,
@@ -114,7 +117,9 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
     const char* const xb = (const char*)x;
     const char* const wb = (const char*)w;
     constexpr int TAPS = KH * KW, HWd = PW + KW - 1, HROWS = (PH + KH - 1) * HWd, HP = (HROWS + 7) / 8;
-    constexpr int BBYTES = PP<BN>::BBYTES, LDS = PP<BN>::LDS, NJ = PP<BN>::NJ, WU = PP<BN>::WU, RSB = PP<BN>::RSB;
+    constexpr int BBYTES = PP<BN>::BBYTES, NJ = PP<BN>::NJ, WU = PP<BN>::WU, RSB = PP<BN>::RSB;
+    constexpr int LDS = ONE ? HBYTES + 2 * BBYTES : PP<BN>::LDS;
+    static_assert(!ONE || (BN <= 128 && 256 * RSB <= LDS && !F8), "single-chunk variant: staging must fit");
     constexpr int MI = PP<BN>::MIW, RW = PP<BN>::RW;
     // sub-steps per K-step: bf16 2 (32 channels each); fp8 splits the pixel fragments,
     // MS per sub-step (4 sub-steps at MI = 8 keep the operand registers at the bf16 48)
@@ -122,7 +127,7 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const irgan_conv_desc d
     static_assert(HP <= HPMAX && HP > 40 && TAPS >= 2, "halo pieces per wave are 5 or 6");
     __shared__ __attribute__((aligned(1024))) char smem[LDS];
     char* const sH = smem;
-    char* const sB = smem + 2 * HBYTES;
+    char* const sB = smem + (ONE ? 1 : 2) * HBYTES;
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -516,6 +521,18 @@ void launch_pp(const irgan_conv_desc* d, const void* x, const void* w, const flo
     const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH);
     const int ntn = irgan_cdiv(d->Cout, BN);
     const int nb = d->N * tpy * tpx * ntn;
+    static const bool one_ok = !getenv("IRGAN_NO_PP_ONE");
+    if constexpr (BN == 64) {
+        if (one_ok && d->Cin == 64) {  // single input chunk: two blocks per CU
+            if (d->accumulate)
+                conv_pp_kernel<KH, KW, BN, true, false, false, true><<<nb, 512, 0, st>>>(
+                    *d, (const bf16_t*)x, (const bf16_t*)w, bias, y, mask, ntn, tpx, tpy, swz);
+            else
+                conv_pp_kernel<KH, KW, BN, false, false, false, true><<<nb, 512, 0, st>>>(
+                    *d, (const bf16_t*)x, (const bf16_t*)w, bias, y, mask, ntn, tpx, tpy, swz);
+            return;
+        }
+    }
     if (d->accumulate)
         conv_pp_kernel<KH, KW, BN, true><<<nb, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, y, mask, ntn,
                                                              tpx, tpy, swz);
