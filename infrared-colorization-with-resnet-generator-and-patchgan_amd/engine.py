@@ -18,7 +18,9 @@ gradient buffers (RCCL) before each Adam.
 from __future__ import annotations
 
 import math
+import os
 from collections import OrderedDict
+from contextlib import nullcontext as _nullcontext
 
 import torch
 
@@ -859,6 +861,12 @@ class GANStep:
         self.g_reduce = BucketedAllreduce(G, process_group)
         self.d_reduce = BucketedAllreduce(D, process_group)
         self.lr_scale = 1.0
+        # the D step (D forward/backward on [real; fake] and its all-reduce) runs on a
+        # side stream, concurrently with the G-step terms that do not read D (L1,
+        # VGG, TV, SSIM); IRGAN_NO_D_OVERLAP=1 keeps everything on one stream
+        self.side = None
+        if G.device.type == "cuda" and not os.environ.get("IRGAN_NO_D_OVERLAP"):
+            self.side = torch.cuda.Stream(device=G.device)
         self.vgg.pack()
         self.gen.pack()
         self.dis.pack()
@@ -881,17 +889,21 @@ class GANStep:
         ir_t = Feat(self.gen.bufs.d["ir"])
         rgb_h = b.get("rgb_nhwc", (B, H, W, cout), torch.float32)
         ops.nchw_to_nhwc(rgb.contiguous(), Feat(rgb_h))
-        # ---- D step on [real; fake] as one 2B batch (ir:1636-1651)
-        self.D.zero_grad()
+        # ---- D step on [real; fake] as one 2B batch (ir:1636-1651), on the side stream
         dpad = max(8, cin + cout)   # D input zero-padded to 8 channels (narrow-input conv path)
         din = Feat(b.zeros("din2", (2 * B, H, W, dpad), T), 0, self.dis.packs[0].cin_eff)
-        self._din(ir_t, rgb_h, din.batch(0, B))
-        self._din(ir_t, fake, din.batch(B, B))
-        pred = self.dis.forward(din, tag="d")
-        dpred = b.get("dpred", tuple(pred.shape), torch.float32)
-        ops.hinge(pred, pred[:B].numel(), 0, 1.0, dpred, L[0:1])
-        self.dis.backward(dpred, want_wgrad=True, want_dinput=False, tag="d")
-        self.d_reduce.start()
+        main = torch.cuda.current_stream() if self.side is not None else None
+        if main is not None:
+            self.side.wait_stream(main)           # G output, rgb, the zeroed losses
+        with torch.cuda.stream(self.side) if main is not None else _nullcontext():
+            self.D.zero_grad()
+            self._din(ir_t, rgb_h, din.batch(0, B))
+            self._din(ir_t, fake, din.batch(B, B))
+            pred = self.dis.forward(din, tag="d")
+            dpred = b.get("dpred", tuple(pred.shape), torch.float32)
+            ops.hinge(pred, pred[:B].numel(), 0, 1.0, dpred, L[0:1])
+            self.dis.backward(dpred, want_wgrad=True, want_dinput=False, tag="d")
+            self.d_reduce.start()
         # ---- G step (ir:1656-1681).  The terms that do not read D (L1, VGG, TV, SSIM)
         # go first so they overlap the D-grad all-reduce; the GAN term follows D Adam.
         self.G.zero_grad()
@@ -910,6 +922,8 @@ class GANStep:
         ops.tv(Feat(fake), cfg.lambda_tv, dfake, L[4:5])
         ssim_work = b.flat("ssim_work", 10 * fake.numel())
         ops.ssim(Feat(fake), Feat(rgb_h), cfg.lambda_ssim, dfake, L[5:6], ssim_work)
+        if main is not None:
+            main.wait_stream(self.side)           # D grads (and their all-reduce launch) are in
         self.d_reduce.finish(self.D.adam_begin(cfg.lr_D * self.lr_scale, cfg.beta1, cfg.beta2))
         self.dis.pack()
         # GAN term through the updated D (ir:1659-1662)

@@ -366,11 +366,13 @@ _WGRAD_WS = {}
 
 
 def _wgrad_ws(dev):
-    """Per-device fp32 workspace for the wgrad split-K partials (irgan_conv_wgrad_ws):
-    plain-store slabs + an ordered reduce instead of fp32 atomics into dw."""
-    w = _WGRAD_WS.get(dev)
+    """Per-(device, stream) fp32 workspace for the wgrad split-K partials
+    (irgan_conv_wgrad_ws): plain-store slabs + an ordered reduce instead of fp32
+    atomics into dw.  One per stream, so concurrent streams never share it."""
+    key = (dev, torch.cuda.current_stream(dev).cuda_stream)
+    w = _WGRAD_WS.get(key)
     if w is None:
-        w = _WGRAD_WS[dev] = torch.empty(WGRAD_WS_FLOATS, dtype=torch.float32, device=dev)
+        w = _WGRAD_WS[key] = torch.empty(WGRAD_WS_FLOATS, dtype=torch.float32, device=dev)
     return w
 
 
@@ -436,7 +438,7 @@ _CS_WORK = {}
 
 
 def channel_sum(g: Feat, db: torch.Tensor):
-    key = (db.device, g.C)
+    key = (db.device, g.C, torch.cuda.current_stream(db.device).cuda_stream)
     w = _CS_WORK.get(key)
     if w is None:
         w = _CS_WORK[key] = torch.empty(IN_PARTS * g.C, dtype=torch.float64, device=db.device)
