@@ -694,18 +694,22 @@ class VGGEngine:
             self._pack_batch = ops.PackBatch(self.packs)
         self._pack_batch.run()
 
-    def forward(self, vin: Feat, bufs: Buffers = None) -> Feat:
+    def forward(self, vin: Feat, bufs: Buffers = None, part=None) -> Feat:
+        """relu3_3 features of vin.  part = (b0, nb): compute only images [b0, b0+nb)
+        into the full-batch activation buffers (the step runs the real and the fake
+        half on different streams)."""
         g, T = bufs or self.bufs, self.tdt
         x = vin
         acts = g.state["acts"] = [vin]
+        sl = (lambda f: f) if part is None else (lambda f: f.batch(*part))  # noqa: E731
         for j, pc in enumerate(self.packs):
             y = Feat(g.get(f"v{j}", (x.N, x.H, x.W, pc.spec.cout), T))
-            ops.conv_fwd(pc, x, y, act=ACT_RELU)
+            ops.conv_fwd(pc, sl(x), sl(y), act=ACT_RELU)
             acts.append(y)
             x = y
             if j in (1, 3):
                 p = Feat(g.get(f"p{j}", (x.N, x.H // 2, x.W // 2, x.C), T))
-                ops.maxpool(x, p)
+                ops.maxpool(sl(x), sl(p))
                 acts.append(p)
                 x = p
         return x
@@ -884,18 +888,32 @@ class GANStep:
         cin, cout = cfg.input_nc, cfg.output_nc
         self.losses.zero_()
         L = self.losses
+        main = torch.cuda.current_stream() if self.side is not None else None
+        side_ctx = (lambda: torch.cuda.stream(self.side)) if main is not None else _nullcontext  # noqa: E731
+        rgb_h = b.get("rgb_nhwc", (B, H, W, cout), torch.float32)
+        ops.nchw_to_nhwc(rgb.contiguous(), Feat(rgb_h))
+        # ---- VGG features of the real images (ir:1668) need nothing from G: side stream,
+        # concurrent with the G forward
+        vin = Feat(b.zeros("vin", (2 * B, H, W, max(8, cout)), T), 0, self.vgg.packs[0].cin_eff)
+        vgg_side = main is not None and not os.environ.get("IRGAN_NO_VGG_OVERLAP")
+        if vgg_side:
+            self.side.wait_stream(main)
+        with side_ctx() if vgg_side else _nullcontext():
+            ops.affine(Feat(rgb_h), self.vgg.scale, self.vgg.shift, vin.batch(B, B))
+            self.vgg.forward(vin, part=(B, B))
+        ev_vgg = None
+        if vgg_side:
+            ev_vgg = torch.cuda.Event()
+            ev_vgg.record(self.side)
         # ---- G forward once (ir:1638 / 1657 compute the same image)
         fake = self.gen.forward(ir)
         ir_t = Feat(self.gen.bufs.d["ir"])
-        rgb_h = b.get("rgb_nhwc", (B, H, W, cout), torch.float32)
-        ops.nchw_to_nhwc(rgb.contiguous(), Feat(rgb_h))
         # ---- D step on [real; fake] as one 2B batch (ir:1636-1651), on the side stream
         dpad = max(8, cin + cout)   # D input zero-padded to 8 channels (narrow-input conv path)
         din = Feat(b.zeros("din2", (2 * B, H, W, dpad), T), 0, self.dis.packs[0].cin_eff)
-        main = torch.cuda.current_stream() if self.side is not None else None
         if main is not None:
-            self.side.wait_stream(main)           # G output, rgb, the zeroed losses
-        with torch.cuda.stream(self.side) if main is not None else _nullcontext():
+            self.side.wait_stream(main)           # G output, the zeroed losses
+        with side_ctx():
             self.D.zero_grad()
             self._din(ir_t, rgb_h, din.batch(0, B))
             self._din(ir_t, fake, din.batch(B, B))
@@ -904,17 +922,27 @@ class GANStep:
             ops.hinge(pred, pred[:B].numel(), 0, 1.0, dpred, L[0:1])
             self.dis.backward(dpred, want_wgrad=True, want_dinput=False, tag="d")
             self.d_reduce.start()
-        # ---- G step (ir:1656-1681).  The terms that do not read D (L1, VGG, TV, SSIM)
-        # go first so they overlap the D-grad all-reduce; the GAN term follows D Adam.
+            # D Adam, then the G-step GAN term through the updated D (ir:1651, 1659-1662),
+            # still on the side stream: the main stream meanwhile runs the G-step terms
+            # that do not read D (L1, VGG, TV, SSIM)
+            self.d_reduce.finish(self.D.adam_begin(cfg.lr_D * self.lr_scale, cfg.beta1, cfg.beta2))
+            self.dis.pack()
+            dinf = Feat(b.zeros("din1", (B, H, W, dpad), T), 0, self.dis.packs[0].cin_eff)
+            self._din(ir_t, fake, dinf)
+            predg = self.dis.forward(dinf, tag="g")
+            dpg = b.get("dpredg", tuple(predg.shape), torch.float32)
+            ops.hinge(predg, predg.numel(), 1, cfg.lambda_gan, dpg, L[1:2])
+            dd = self.dis.backward(dpg, want_wgrad=False, want_dinput=True, tag="g")
+        # ---- G step (ir:1656-1681)
         self.G.zero_grad()
         dfake = b.get("dfake", (B, H, W, cout), torch.float32)
         dfake.zero_()
         ops.l1(fake, rgb_h, cfg.lambda_L1, dfake, L[2:3], accumulate=True)
-        # perceptual: VGG on [fake; rgb] as one 2B batch (ir:1667-1669)
-        vin = Feat(b.zeros("vin", (2 * B, H, W, max(8, cout)), T), 0, self.vgg.packs[0].cin_eff)
+        # perceptual (ir:1667-1669): VGG on the fake half; the real half ran on the side stream
         ops.affine(Feat(fake), self.vgg.scale, self.vgg.shift, vin.batch(0, B))
-        ops.affine(Feat(rgb_h), self.vgg.scale, self.vgg.shift, vin.batch(B, B))
-        feat = self.vgg.forward(vin)
+        feat = self.vgg.forward(vin, part=(0, B))
+        if ev_vgg is not None:
+            main.wait_event(ev_vgg)
         dfeat = b.get("dfeat", (B, feat.H, feat.W, feat.C), T)
         ops.l1(feat.t[:B], feat.t[B:], cfg.lambda_perc, dfeat, L[3:4])
         dv = self.vgg.backward_input(Feat(dfeat), B)
@@ -923,16 +951,7 @@ class GANStep:
         ssim_work = b.flat("ssim_work", 10 * fake.numel())
         ops.ssim(Feat(fake), Feat(rgb_h), cfg.lambda_ssim, dfake, L[5:6], ssim_work)
         if main is not None:
-            main.wait_stream(self.side)           # D grads (and their all-reduce launch) are in
-        self.d_reduce.finish(self.D.adam_begin(cfg.lr_D * self.lr_scale, cfg.beta1, cfg.beta2))
-        self.dis.pack()
-        # GAN term through the updated D (ir:1659-1662)
-        dinf = Feat(b.zeros("din1", (B, H, W, dpad), T), 0, self.dis.packs[0].cin_eff)
-        self._din(ir_t, fake, dinf)
-        predg = self.dis.forward(dinf, tag="g")
-        dpg = b.get("dpredg", tuple(predg.shape), torch.float32)
-        ops.hinge(predg, predg.numel(), 1, cfg.lambda_gan, dpg, L[1:2])
-        dd = self.dis.backward(dpg, want_wgrad=False, want_dinput=True, tag="g")
+            main.wait_stream(self.side)           # the GAN term's d fake
         ops.axpby(dd.sl(cin, cout), 1.0, Feat(dfake), 1.0)
         self.gen.backward(dfake, ready=self.g_reduce.ready)
         self.g_reduce.finish(self.G.adam_begin(cfg.lr_G * self.lr_scale, cfg.beta1, cfg.beta2))
