@@ -102,9 +102,12 @@ struct PP {
 typedef int v8i_t __attribute__((ext_vector_type(8)));
 IRGAN_HD v8i_t cat8(i32x4 a, i32x4 b) { return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7); }
 
-// ONE: the input has a single channel chunk (Cin == 64 in bf16), so one halo buffer
-// suffices; at BN = 64 the block then fits twice per CU (LDS 62 KiB, <= 128 VGPRs),
-// and one block's prologue / epilogue overlaps the other's MFMA loop.
+// ONE: a single halo buffer, so at BN = 64 the block fits twice per CU (LDS 62 KiB,
+// <= 128 VGPRs) and one block's halo loads / epilogue overlap the other's MFMA loop
+// (BN = 128 would need 159 VGPRs: at 128 it spills 30 and runs slower than two BN-64
+// tiles, profiles/r02_s5_pp_one_ab.txt).  With more than one channel chunk the next chunk's halo cannot be
+// prefetched: after the last window that reads chunk c (4k+3 of its last tap) every
+// wave issues its pieces of chunk c+1, retires them and meets at one extra barrier.
 template <int KH, int KW, int BN, bool ACC, bool STATS = false, bool F8 = false, bool ONE = false>
 __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
                                                          const bf16_t* __restrict__ w, const float* __restrict__ bias,
@@ -119,7 +122,7 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
     constexpr int TAPS = KH * KW, HWd = PW + KW - 1, HROWS = (PH + KH - 1) * HWd, HP = (HROWS + 7) / 8;
     constexpr int BBYTES = PP<BN>::BBYTES, NJ = PP<BN>::NJ, WU = PP<BN>::WU, RSB = PP<BN>::RSB;
     constexpr int LDS = ONE ? HBYTES + 2 * BBYTES : PP<BN>::LDS;
-    static_assert(!ONE || (BN <= 128 && 256 * RSB <= LDS && !F8), "single-chunk variant: staging must fit");
+    static_assert(!ONE || (BN == 64 && 256 * RSB <= LDS && !F8), "single-halo variant: staging must fit");
     constexpr int MI = PP<BN>::MIW, RW = PP<BN>::RW;
     // sub-steps per K-step: bf16 2 (32 channels each); fp8 splits the pixel fragments,
     // MS per sub-step (4 sub-steps at MI = 8 keep the operand registers at the bf16 48)
@@ -171,7 +174,7 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
     const uint32_t wbytes = (uint32_t)((long)d.Cout * Kw * ESZ);
     const uint32_t b_off = (uint32_t)((n0 + wid * WU * 8 + sub) * Kw * ESZ + chunk * 16);  // piece u (8 rows): + u*8*Kw*ESZ
     auto issue_halo = [&](int c) {
-        char* dst = sH + (c & 1) * HBYTES;
+        char* dst = sH + (ONE ? 0 : (c & 1) * HBYTES);
         const i32x4 rs = make_rsrc(xb + c * 128, xbytes - c * 128);
         int lsub = sub;
         asm volatile("" : "+v"(lsub));  // recompute the offsets here instead of hoisting them out of the loop
@@ -185,6 +188,13 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
         char* dst = sB + stage * BBYTES + wid * WU * 1024;
 #pragma unroll
         for (int u = 0; u < WU; ++u) blds16(rs, b_off, (uint32_t)(u * 8 * Kw * ESZ), dst + u * 1024);
+    };
+    // ONE: chunk c's halo after the barrier closing its last reading window (the same
+    // barrier instance for both groups), landed before anyone reads it
+    auto reload_halo = [&](int c) {
+        issue_halo(c);
+        wait_vmcnt<0>();
+        phase_barrier();
     };
     // W(k+1) landed; the halo issued at step k (after W(k+1)) may stay in flight
     auto retire = [&](bool halo_now) {
@@ -225,7 +235,7 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
     }
 #pragma unroll 1
     for (int c = 0; c < nchunk; ++c) {
-        const int hb = arow0 * 128 + (c & 1) * HBYTES;
+        const int hb = arow0 * 128 + (ONE ? 0 : (c & 1) * HBYTES);
         const bool more = c + 1 < nchunk;
 #pragma unroll
         for (int tp = 0; tp < TAPS; ++tp) {
@@ -233,7 +243,8 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
             const int k = c * TAPS + tp;  // K-step
             const char* B = sB + (k & 1) * BBYTES;
             const bool last_k = !more && tp == TAPS - 1;
-            const bool halo_now = tp == 0 && more;
+            const bool halo_now = tp == 0 && more && !ONE;
+            const bool reload = ONE && more && tp == TAPS - 1;  // single buffer: chunk c+1 after window 4k+3
 #pragma unroll
             for (int h = 0; h < HS; ++h) {
                 // ---- READ phase (group 0: even windows, group 1: odd)
@@ -285,6 +296,7 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
                     if (!last_k) retire(halo_now);
                 }
                 phase_barrier();
+                if (reload && h == HS - 1 && grp == 1) reload_halo(c + 1);
                 // ---- MFMA phase: C^T fragment (weights as A, pixels as B)
                 if constexpr (F8) {
 #pragma unroll
@@ -310,6 +322,7 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
                 }
                 if (h == HS - 1 && grp == 0 && !last_k) retire(halo_now);  // last window of step k
                 phase_barrier();
+                if (reload && h == HS - 1 && grp == 0) reload_halo(c + 1);
             }
         }
     }
@@ -515,15 +528,38 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
     }
 }
 
+// single-halo-buffer policy for BN-64 tiles (A/B knobs: IRGAN_NO_PP_ONE,
+// IRGAN_PP_ONE_MAXCH = the most input channel chunks that take it; default: all)
+bool use_one(int cin) {
+    static int mx = -1;
+    if (mx < 0) {
+        mx = getenv("IRGAN_NO_PP_ONE") ? 0 : 1 << 20;
+        if (const char* e = getenv("IRGAN_PP_ONE_MAXCH")) mx = atoi(e);
+    }
+    return cin / 64 <= mx;
+}
+
+// Cout % 128 (not % 256) layers with at most this many input chunks run as BN-64
+// single-halo tiles (IRGAN_PP_SPLIT128, default: all): two blocks per CU beat one
+// BN-128 block on every such layer of the step (down1 / up1 / VGG conv2,
+// profiles/r02_s5_pp_one_ab.txt)
+bool split128(int cin) {
+    static int mx = -1;
+    if (mx < 0) {
+        mx = 1 << 20;
+        if (const char* e = getenv("IRGAN_PP_SPLIT128")) mx = atoi(e);
+    }
+    return cin / 64 <= mx;
+}
+
 template <int KH, int KW, int BN>
 void launch_pp(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y, const void* mask,
                hipStream_t st, int swz) {
     const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH);
     const int ntn = irgan_cdiv(d->Cout, BN);
     const int nb = d->N * tpy * tpx * ntn;
-    static const bool one_ok = !getenv("IRGAN_NO_PP_ONE");
     if constexpr (BN == 64) {
-        if (one_ok && d->Cin == 64) {  // single input chunk: two blocks per CU
+        if (use_one(d->Cin)) {  // single halo buffer: two blocks per CU
             if (d->accumulate)
                 conv_pp_kernel<KH, KW, BN, true, false, false, true><<<nb, 512, 0, st>>>(
                     *d, (const bf16_t*)x, (const bf16_t*)w, bias, y, mask, ntn, tpx, tpy, swz);
@@ -559,11 +595,12 @@ extern "C" int irgan_conv_fwd_pp(const irgan_conv_desc* d, const void* x, const 
     if (d->Cout % 256 == 0) {
         if (k33) launch_pp<3, 3, 256>(d, x, w, bias, y, mask, st, swz);
         else launch_pp<4, 4, 256>(d, x, w, bias, y, mask, st, swz);
-    } else if (d->Cout % 128 == 0) {
+    } else if (d->Cout % 128 == 0 && !split128(d->Cin)) {
         if (!pp128) return IRGAN_EUNSUPPORTED;
         if (k33) launch_pp<3, 3, 128>(d, x, w, bias, y, mask, st, swz);
         else launch_pp<4, 4, 128>(d, x, w, bias, y, mask, st, swz);
-    } else if (d->Cout == 192) {  // up2_conv backward-data (dx = [up | skip] = 128 + 64 channels)
+    } else if (d->Cout == 192 && getenv("IRGAN_PP_NOSPLIT192")) {  // up2_conv backward-data (dx = [up | skip] = 128 + 64 channels)
+        // (default: three BN-64 single-halo tiles, 350 -> 323 us)
         if (!pp192) return IRGAN_EUNSUPPORTED;
         if (k33) launch_pp<3, 3, 192>(d, x, w, bias, y, mask, st, swz);
         else launch_pp<4, 4, 192>(d, x, w, bias, y, mask, st, swz);
@@ -597,17 +634,22 @@ extern "C" int irgan_conv_fwd_stats(const irgan_conv_desc* d, const void* x, con
     if (tpx * tpy > IRGAN_IN_PARTS) return IRGAN_EUNSUPPORTED;
     if ((long)d->N * d->Ho * d->Wo <= 0) return IRGAN_EUNSUPPORTED;
     static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
-    const int bn = d->Cout % 256 == 0 ? 256 : (d->Cout % 128 == 0 ? 128 : 64);  // as irgan_conv_fwd_pp
+    const int bn = d->Cout % 256 == 0 ? 256 : (d->Cout % 128 == 0 && !split128(d->Cin) ? 128 : 64);  // as irgan_conv_fwd_pp
     const int ntn = d->Cout / bn;
     const int blocks = d->N * tpy * tpx * ntn;
     hipStream_t st = (hipStream_t)s;
-#define PPS(KHV, BNV)                                                                                              \
-    conv_pp_kernel<KHV, KHV, BNV, false, true><<<blocks, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, \
-                                                                       y, nullptr, ntn, tpx, tpy, swz, (float2*)part)
+#define PPS(KHV, BNV, ONEV)                                                                                        \
+    conv_pp_kernel<KHV, KHV, BNV, false, true, false, ONEV><<<blocks, 512, 0, st>>>(                                 \
+        *d, (const bf16_t*)x, (const bf16_t*)w, bias, y, nullptr, ntn, tpx, tpy, swz, (float2*)part)
+    const bool one = bn == 64 && use_one(d->Cin);
     if (k33) {
-        if (bn == 256) PPS(3, 256); else if (bn == 128) PPS(3, 128); else PPS(3, 64);
+        if (bn == 256) PPS(3, 256, false);
+        else if (bn == 128) PPS(3, 128, false);
+        else { if (one) PPS(3, 64, true); else PPS(3, 64, false); }
     } else {
-        if (bn == 256) PPS(4, 256); else if (bn == 128) PPS(4, 128); else PPS(4, 64);
+        if (bn == 256) PPS(4, 256, false);
+        else if (bn == 128) PPS(4, 128, false);
+        else { if (one) PPS(4, 64, true); else PPS(4, 64, false); }
     }
 #undef PPS
     IRGAN_LAUNCH_CHECK();
