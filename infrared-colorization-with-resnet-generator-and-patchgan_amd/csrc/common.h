@@ -11,11 +11,13 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 #define IRGAN_HD __device__ __forceinline__
 
 IRGAN_HD float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
-IRGAN_HD bf16_t f2bf(float f) {
-    uint32_t u = __float_as_uint(f);
-    if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40);  // keep NaN a NaN
-    u += 0x7fffu + ((u >> 16) & 1u);                                          // round to nearest even
-    return (bf16_t)(u >> 16);
+// fp32 -> bf16, round to nearest even (NaN stays NaN): gfx950's v_cvt_pk_bf16_f32
+IRGAN_HD bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
+// two values -> one packed word (lo in bits 0..15): ONE v_cvt_pk_bf16_f32
+IRGAN_HD uint32_t pk_bf16(float lo, float hi) {
+    typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+    const bf16x2_t v = {(__bf16)lo, (__bf16)hi};
+    return __builtin_bit_cast(uint32_t, v);
 }
 
 // typed scalar load/store through a dtype code (IRGAN_F32 / IRGAN_BF16)

@@ -183,8 +183,8 @@ __global__ __launch_bounds__(256, 2) void conv_c8_kernel(const irgan_conv_desc d
                                 v[2] += bf2f((bf16_t)(q.y & 0xffffu)); v[3] += bf2f((bf16_t)(q.y >> 16));
                             }
                             uint2 o;
-                            o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-                            o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+                            o.x = pk_bf16(v[0], v[1]);
+                            o.y = pk_bf16(v[2], v[3]);
                             *(uint2*)yp = o;
                         } else {
                             for (int r = 0; r < 4 && co + r < d.Cout; ++r)

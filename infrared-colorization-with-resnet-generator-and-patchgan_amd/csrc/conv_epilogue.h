@@ -56,10 +56,10 @@ IRGAN_HD void conv_store8(const irgan_conv_desc& d, float (&v)[8], long pix, int
                 }
             }
             uint4 o;
-            o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-            o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-            o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
-            o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+            o.x = pk_bf16(v[0], v[1]);
+            o.y = pk_bf16(v[2], v[3]);
+            o.z = pk_bf16(v[4], v[5]);
+            o.w = pk_bf16(v[6], v[7]);
             *yp = o;
         }
     } else {

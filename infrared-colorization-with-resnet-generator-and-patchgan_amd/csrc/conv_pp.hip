@@ -60,6 +60,13 @@
 // bits: 1 no MFMA, 2 no weight DMA in the loop, 4 no fragment reads, 8 no barriers in the loop, 16 no epilogue
 #define PPX(b) ((PP_EXP & (b)) != 0)
 
+// conv_res64.hip: the resident-weight persistent kernel for one input chunk (Cin == 64)
+namespace irgan_res64 {
+bool ok(const irgan_conv_desc* d);
+void launch(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y, const void* mask,
+            float2* part, hipStream_t st);
+}  // namespace irgan_res64
+
 namespace {
 
 IRGAN_HD int lds_off(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
@@ -436,8 +443,8 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
                             if (full || co + r < d.Cout) v[r] += bf2f(yp[r]);
                     }
                     uint2 pk;
-                    pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-                    pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+                    pk.x = pk_bf16(v[0], v[1]);
+                    pk.y = pk_bf16(v[2], v[3]);
                     *(uint2*)(smem + m * RSB + cl * 2) = pk;
                 }
             }
@@ -592,6 +599,11 @@ extern "C" int irgan_conv_fwd_pp(const irgan_conv_desc* d, const void* x, const 
     // measured (profiles/r01_s7_pp_ab.txt): up2 dgrad (Cout 192) 539 -> 351 us, Cout-64 layers +6 %
     static const bool pp192 = !getenv("IRGAN_NO_PP192");
     static const bool pp64 = !getenv("IRGAN_NO_PP64");
+    if (irgan_res64::ok(d) && (!mask || (d->ldm % 4 == 0 && d->moff % 4 == 0))) {  // one input chunk: resident weights
+        irgan_res64::launch(d, x, w, bias, y, mask, nullptr, st);
+        IRGAN_LAUNCH_CHECK();
+        return 0;
+    }
     if (d->Cout % 256 == 0) {
         if (k33) launch_pp<3, 3, 256>(d, x, w, bias, y, mask, st, swz);
         else launch_pp<4, 4, 256>(d, x, w, bias, y, mask, st, swz);
@@ -638,6 +650,12 @@ extern "C" int irgan_conv_fwd_stats(const irgan_conv_desc* d, const void* x, con
     const int ntn = d->Cout / bn;
     const int blocks = d->N * tpy * tpx * ntn;
     hipStream_t st = (hipStream_t)s;
+    if (irgan_res64::ok(d)) {
+        irgan_res64::launch(d, x, w, bias, y, nullptr, (float2*)part, st);
+        IRGAN_LAUNCH_CHECK();
+        *nb = tpx * tpy;
+        return 0;
+    }
 #define PPS(KHV, BNV, ONEV)                                                                                        \
     conv_pp_kernel<KHV, KHV, BNV, false, true, false, ONEV><<<blocks, 512, 0, st>>>(                                 \
         *d, (const bf16_t*)x, (const bf16_t*)w, bias, y, nullptr, ntn, tpx, tpy, swz, (float2*)part)

@@ -1,0 +1,321 @@
+// Resident-weight persistent conv for one 64-channel input chunk (3x3, stride 1):
+// VGG conv1_2 / conv2_1 forward, down1 forward (+ fused InstanceNorm statistics) and every
+// backward-data conv whose dY has 64 channels (VGG conv1_2, up2_conv).  Entered from
+// irgan_conv_fwd_pp / irgan_conv_fwd_stats (conv_pp.hip), which own the C ABI.
+#include <type_traits>
+
+#include "conv_epilogue.h"
+
+namespace {
+
+IRGAN_HD int lds_off(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+constexpr int PH = 16, PW = 16;  // output patch
+
+// ---- resident-weight persistent variant: 3x3 stride 1, Cin == 64 --------------------
+// With one 64-channel input chunk a conv_pp block does only 9 K-steps per 16x16 patch, so
+// its fixed cost (first DMA latency, per-window barriers, LDS-staged epilogue) outweighs
+// the MFMA work: VGG conv1_2 / down1 / up2-dgrad ran at 0.16-0.32 of peak.  Here one
+// block per CU loops over the patches of one 64-channel output tile:
+//  * all 9 taps x 64 x 64 weights stay in LDS (72 KiB, loaded once per block);
+//  * the input halo is double-buffered: patch i+2's halo is DMA'd (buffer_load ... lds)
+//    into the buffer patch i just released, so it lands under patch i+1's MFMA loop;
+//  * the K loop has no barrier at all (nothing is written into LDS it reads): 8 waves,
+//    2 patch rows x 64 channels each, 18 sub-steps of 8 mfma_f32_16x16x32_bf16;
+//  * epilogue straight from the C^T accumulators (4 consecutive channels of one pixel
+//    per lane: bias, activation, mask, accumulate, one 8-byte store), so a wave that
+//    finishes its MFMAs stores while the others still multiply; STATS: per-wave channel
+//    sums by a 4-step reduce-scatter across the 16 pixel lanes, 8 wave rows summed in
+//    fixed order into the same per-(image, patch, channel) partials as conv_pp;
+//  * two barriers per patch: halo landed (counted vmcnt: the next patch's pieces are
+//    the only younger loads) and halo released.
+// LDS: 73728 (weights) + 2 x 41984 (halos) + 4096 (stats rows) = 161792 bytes.
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+// s_waitcnt vmcnt(n) for a wave-uniform n in [0, 31] (the immediate is an encoding field)
+IRGAN_HD void wait_vm_dyn(int n) {
+    switch (n) {
+#define WV(k) case k: wait_vmcnt<k>(); break;
+        WV(0) WV(1) WV(2) WV(3) WV(4) WV(5) WV(6) WV(7) WV(8) WV(9) WV(10) WV(11) WV(12) WV(13) WV(14) WV(15)
+        WV(16) WV(17) WV(18) WV(19) WV(20) WV(21) WV(22) WV(23) WV(24) WV(25) WV(26) WV(27) WV(28) WV(29) WV(30)
+#undef WV
+        default: wait_vmcnt<31>(); break;
+    }
+}
+constexpr int R64_HP = 41;               // halo pieces: 18 x 18 rows of 128 B
+constexpr int R64_HB = R64_HP * 1024;
+constexpr int R64_WB = 9 * 64 * 128;
+constexpr int R64_LDS = R64_WB + 2 * R64_HB + 8 * 64 * 8;
+
+template <bool ACC, bool STATS>
+__global__ __launch_bounds__(512, 1) void conv_res64_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
+                                                           const bf16_t* __restrict__ w,
+                                                           const float* __restrict__ bias, bf16_t* __restrict__ y,
+                                                           const bf16_t* __restrict__ mask, int ntn, int tpx,
+                                                           int tpy, float2* __restrict__ part) {
+    constexpr int TAPS = 9, HWd = PW + 2, HROWS = (PH + 2) * HWd, MI = 2, NJ = 4, Kw = TAPS * 64;
+    static_assert(HROWS <= R64_HP * 8 && R64_HP * 8 - HROWS < 8, "halo pieces");
+    __shared__ __attribute__((aligned(1024))) char smem[R64_LDS];
+    char* const sW = smem;
+    char* const sH = smem + R64_WB;
+    float2* const sR = (float2*)(smem + R64_WB + 2 * R64_HB);  // [8 waves][64 channels]
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nt = blockIdx.x % ntn, q0 = blockIdx.x / ntn, qs = gridDim.x / ntn;
+    const int P = d.N * tpy * tpx;
+    const int n0 = nt * 64;
+    const int nh = (R64_HP - wid + 7) >> 3;  // halo pieces of this wave: 6 (wave 0) or 5
+    const int sub = lane >> 3;
+    const bool reflect = d.pad_mode == IRGAN_PAD_REFLECT;
+    const i32x4 xr = make_rsrc(x, (uint32_t)((long)d.N * d.H * d.W * d.ldx * 2));
+
+    auto issue_halo = [&](int p, int buf) {
+        const int pxi = p % tpx, pyi = (p / tpx) % tpy, img = p / (tpx * tpy);
+        const int py0 = pyi * PH + d.c0y, px0 = pxi * PW + d.c0x;
+        char* dst = sH + buf * R64_HB;
+        int lsub = sub;
+        asm volatile("" : "+v"(lsub));
+#pragma unroll
+        for (int u = 0; u < 6; ++u) {
+            if (u < nh) {
+                const int h = (u * 8 + wid) * 8 + lsub;
+                const int hy = h / HWd, hx = h - hy * HWd;
+                int iy = py0 + hy, ix = px0 + hx;
+                if (reflect) {
+                    iy = reflect_idx(iy, d.H);
+                    ix = reflect_idx(ix, d.W);
+                }
+                const bool ok = (h < HROWS) & ((unsigned)iy < (unsigned)d.H) & ((unsigned)ix < (unsigned)d.W);
+                const uint32_t off = ok ? (uint32_t)((((img * d.H + iy) * d.W + ix) * d.ldx + d.xoff) * 2 +
+                                                     ((lane & 7) ^ lsub) * 16)
+                                        : IRGAN_OOB;
+                blds16(xr, off, dst + (u * 8 + wid) * 1024);
+            }
+        }
+    };
+
+    // prologue: the block's weight tile (piece u*8 + wid = tap u, channels wid*8 .. +8),
+    // then the first two halos
+    {
+        const i32x4 wr = make_rsrc(w, (uint32_t)((long)d.Cout * Kw * 2));
+        const uint32_t off = (uint32_t)((n0 + wid * 8 + sub) * Kw * 2 + ((lane & 7) ^ sub) * 16);
+#pragma unroll
+        for (int u = 0; u < TAPS; ++u) blds16(wr, off, (uint32_t)(u * 128), sW + (u * 8 + wid) * 1024);
+    }
+    if (q0 < P) issue_halo(q0, 0);
+    if (q0 + qs < P) issue_halo(q0 + qs, 1);
+
+    const int prow = wid * 2;
+    const int g0 = lane >> 4;
+    const int arow0 = prow * HWd + (lane & 15);
+    const int bb0 = lds_off(lane & 15, g0), bb1 = lds_off(lane & 15, 4 + g0);
+    int tsw[8];
+#pragma unroll
+    for (int k8 = 0; k8 < 8; ++k8) tsw[k8] = (g0 ^ ((arow0 + k8) & 7)) << 4;
+    const int cl0 = 4 * g0;  // tile-local channel of r = 0, j = 0
+    float4 b4[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+        b4[j] = bias ? *(const float4*)(bias + n0 + cl0 + j * 16) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const bool vmask = mask != nullptr;
+
+    // output through a raw buffer resource: exactly MI * NJ store instructions per wave and
+    // patch (a pixel outside the image gets the out-of-range offset and is dropped), so the
+    // counted vmcnt at the top of the loop knows how many of its ops are younger than a halo
+    const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(
+        y, (short)0, (int)((long)d.N * d.OH * d.OW * d.ldy * 2), 0x00020000);
+    constexpr int NST = MI * NJ;
+    int it = 0;
+#pragma unroll 1
+    for (int p = q0; p < P; p += qs, ++it) {
+        const int buf = it & 1;
+        // VMEM ops issued after this patch's halo, in issue order: (it >= 2) the stats
+        // store of patch it-2 (made at the top of it-1), the stores of patch it-1, the halo
+        // of patch it+1 (it == 0: only that halo)
+        {
+            const int nxt = p + qs < P ? nh : 0;
+            const int younger = it == 0 ? nxt : (it == 1 ? NST + nxt : (STATS ? 1 : 0) + NST + nxt);
+            wait_vm_dyn(__builtin_amdgcn_readfirstlane(younger));
+        }
+        lds_barrier();  // every wave's pieces of this patch's halo (and the weights) landed
+        if constexpr (STATS) {
+            // patch it-1's partials: its 8 wave rows are complete (written before this barrier)
+            if (it > 0 && lane < 8) {
+                const int c = wid * 8 + lane;
+                float a = 0.f, b = 0.f;
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    const float2 e = sR[r * 64 + c];
+                    a += e.x;
+                    b += e.y;
+                }
+                part[(long)(p - qs) * d.Cout + n0 + c] = make_float2(a, b);
+            }
+        }
+
+        f32x4 acc[MI][NJ];
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int hb = arow0 * 128 + buf * R64_HB;
+#pragma unroll
+        for (int tp = 0; tp < TAPS; ++tp) {
+            const int ty = tp / 3, tx = tp % 3;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                uint4 af[MI], bfr[NJ];
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) bfr[j] = *(const uint4*)(sW + tp * 8192 + (h ? bb1 : bb0) + j * 2048);
+#pragma unroll
+                for (int i = 0; i < MI; ++i) {
+                    const int K = (i + ty) * HWd + tx;
+                    af[i] = *(const uint4*)(sH + (hb + (tsw[K & 7] ^ (h * 64))) + K * 128);
+                }
+#pragma unroll
+                for (int i = 0; i < MI; ++i)
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, bfr[j]),
+                                                                            __builtin_bit_cast(bf16x8_t, af[i]),
+                                                                            acc[i][j], 0, 0, 0);
+            }
+        }
+        lds_barrier();  // every wave is done with this halo buffer; the stats rows were read
+
+        // ---- epilogue from the accumulators
+        const int pxi = p % tpx, pyi = (p / tpx) % tpy, img = p / (tpx * tpy);
+        float st[2 * NJ * 4];  // STATS: (sum, sum of squares) of channel (j, r) at [2 (4j + r) + {0, 1}]
+#pragma unroll
+        for (int k = 0; k < 2 * NJ * 4; ++k) st[k] = 0.f;
+        auto body = [&](auto actc) {
+            constexpr int A = decltype(actc)::value;
+#pragma unroll
+            for (int i = 0; i < MI; ++i) {
+                const int oy = pyi * PH + prow + i, ox = pxi * PW + (lane & 15);
+                const bool ok = oy < d.Ho && ox < d.Wo;
+                const long pix = ok ? ((long)img * d.OH + oy * d.omy + d.ooy) * d.OW + ox * d.omx + d.oox : 0;
+                uint2 old[NJ], mk[NJ];
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                    const int co = n0 + cl0 + j * 16;
+                    old[j] = mk[j] = make_uint2(0u, 0u);
+                    if (ACC && ok) old[j] = *(const uint2*)(y + pix * d.ldy + d.yoff + co);
+                    if (vmask && ok) mk[j] = *(const uint2*)(mask + pix * d.ldm + d.moff + co);
+                }
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                    const int co = n0 + cl0 + j * 16;
+                    const float bb[4] = {b4[j].x, b4[j].y, b4[j].z, b4[j].w};
+                    float v[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        v[r] = conv_act(acc[i][j][r] + bb[r], A);
+                        if (vmask) {
+                            const uint32_t mw = r < 2 ? mk[j].x : mk[j].y;
+                            v[r] *= mask_mul(__uint_as_float((r & 1) ? (mw & 0xffff0000u) : (mw << 16)), d.mask_act);
+                        }
+                        if (ACC) {
+                            const uint32_t ow = r < 2 ? old[j].x : old[j].y;
+                            v[r] += __uint_as_float((r & 1) ? (ow & 0xffff0000u) : (ow << 16));
+                        }
+                    }
+                    u32x2_t pk;
+                    pk.x = pk_bf16(v[0], v[1]);
+                    pk.y = pk_bf16(v[2], v[3]);
+                    const int off = ok ? (int)((pix * d.ldy + d.yoff + co) * 2) : (int)IRGAN_OOB;
+                    __builtin_amdgcn_raw_buffer_store_b64(pk, yr, off, 0, 0);
+                    if constexpr (STATS) {
+                        if (ok) {
+                            const float q[4] = {__uint_as_float(pk.x << 16), __uint_as_float(pk.x & 0xffff0000u),
+                                                __uint_as_float(pk.y << 16), __uint_as_float(pk.y & 0xffff0000u)};
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                st[2 * (4 * j + r)] += q[r];
+                                st[2 * (4 * j + r) + 1] += q[r] * q[r];
+                            }
+                        }
+                    }
+                }
+            }
+        };
+        switch (d.act) {
+            case IRGAN_ACT_RELU: body(std::integral_constant<int, IRGAN_ACT_RELU>()); break;
+            case IRGAN_ACT_LRELU: body(std::integral_constant<int, IRGAN_ACT_LRELU>()); break;
+            default: body(std::integral_constant<int, IRGAN_ACT_NONE>()); break;
+        }
+        if constexpr (STATS) {
+            // reduce-scatter over the 16 pixel lanes (lane & 15): 32 values -> 2 per lane;
+            // lane (g0, k) ends with channel (j, r) = (k >> 2, k & 3) of its lane group
+#pragma unroll
+            for (int lv = 0; lv < 4; ++lv) {
+                const int m = 8 >> lv, n = 32 >> lv;  // xor distance, values held
+                const bool hi = (lane & m) != 0;
+#pragma unroll
+                for (int k = 0; k < n / 2; ++k) {
+                    const float keep = hi ? st[n / 2 + k] : st[k];
+                    const float send = hi ? st[k] : st[n / 2 + k];
+                    st[k] = keep + __shfl_xor(send, m, 64);
+                }
+            }
+            const int k = lane & 15;
+            sR[wid * 64 + (k >> 2) * 16 + cl0 + (k & 3)] = make_float2(st[0], st[1]);
+        }
+        if (p + 2 * qs < P) issue_halo(p + 2 * qs, buf);
+    }
+    if constexpr (STATS) {
+        lds_barrier();  // the last patch's stats rows
+        if (lane < 8) {
+            const int c = wid * 8 + lane;
+            float a = 0.f, b = 0.f;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const float2 e = sR[r * 64 + c];
+                a += e.x;
+                b += e.y;
+            }
+            part[(long)(q0 + (it - 1) * qs) * d.Cout + n0 + c] = make_float2(a, b);
+        }
+    }
+    wait_vmcnt<0>();
+}
+
+}  // namespace
+
+namespace irgan_res64 {
+
+bool ok(const irgan_conv_desc* d) {
+    static const bool on = !getenv("IRGAN_NO_RES64");
+    return on && d->Cin == 64 && d->KH == 3 && d->KW == 3 && d->sy == 1 && d->sx == 1 && d->Cout % 64 == 0 &&
+           d->dtype == IRGAN_BF16 && d->out_dtype == IRGAN_BF16 && d->act != IRGAN_ACT_TANH && d->ldy % 4 == 0 &&
+           d->yoff % 4 == 0 && d->ldx % 8 == 0 && d->xoff % 8 == 0 && (long)d->N * d->H * d->W * d->ldx < (1L << 30) &&
+           (long)d->N * d->OH * d->OW * d->ldy * 2 < (1L << 31);
+}
+
+static int grid_for(int ntn, int tiles) {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+    }
+    const int g = (cus / ntn) * ntn;
+    return g < tiles ? (g > 0 ? g : ntn) : tiles;
+}
+
+// mask: NULL or the bf16 backward mask (8-byte aligned slices: checked by the caller)
+void launch(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y, const void* mask,
+            float2* part, hipStream_t st) {
+    const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH), ntn = d->Cout / 64;
+    const int grid = grid_for(ntn, d->N * tpx * tpy * ntn);
+#define R64(ACCV, STV)                                                                                    \
+    conv_res64_kernel<ACCV, STV><<<grid, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, (bf16_t*)y, \
+                                                       (const bf16_t*)mask, ntn, tpx, tpy, part)
+    if (part) R64(false, true);
+    else if (d->accumulate) R64(true, false);
+    else R64(false, false);
+#undef R64
+}
+
+}  // namespace irgan_res64
+

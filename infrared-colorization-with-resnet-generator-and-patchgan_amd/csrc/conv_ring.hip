@@ -224,7 +224,7 @@ __global__ __launch_bounds__(NWV * 64) void reflect_ring_kernel(const irgan_conv
             for (int k = 0; k < 4; ++k) {
                 const float a = __uint_as_float(wds[k] << 16) + v[2 * k];
                 const float b = __uint_as_float(wds[k] & 0xffff0000u) + v[2 * k + 1];
-                wds[k] = (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+                wds[k] = pk_bf16(a, b);
             }
             *(uint4*)yp = uint4{wds[0], wds[1], wds[2], wds[3]};
         } else {

@@ -75,10 +75,10 @@ template <typename T>
 IRGAN_HD void st8t(T* p, long i, const float* v) {
     if constexpr (sizeof(T) == 2) {
         uint4 u;
-        u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-        u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-        u.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
-        u.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+        u.x = pk_bf16(v[0], v[1]);
+        u.y = pk_bf16(v[2], v[3]);
+        u.z = pk_bf16(v[4], v[5]);
+        u.w = pk_bf16(v[6], v[7]);
         *(uint4*)(p + i) = u;
     } else {
         *(float4*)(p + i) = make_float4(v[0], v[1], v[2], v[3]);

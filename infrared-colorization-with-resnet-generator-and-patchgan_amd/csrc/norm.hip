@@ -45,10 +45,10 @@ IRGAN_HD void ld8(const void* p, int dt, long i, float* o) {
 IRGAN_HD void st8(void* p, int dt, long i, const float* v) {
     if (dt == IRGAN_BF16) {
         uint4 u;
-        u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-        u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-        u.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
-        u.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+        u.x = pk_bf16(v[0], v[1]);
+        u.y = pk_bf16(v[2], v[3]);
+        u.z = pk_bf16(v[4], v[5]);
+        u.w = pk_bf16(v[6], v[7]);
         *(uint4*)((bf16_t*)p + i) = u;
     } else {
         *(float4*)((float*)p + i) = make_float4(v[0], v[1], v[2], v[3]);
@@ -367,10 +367,10 @@ __global__ __launch_bounds__(TPB) void rows8_kernel(const bf16_t* x, int ldx, in
                     }
                     if (MODE == 2) {
                         uint4 w;
-                        w.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
-                        w.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
-                        w.z = (uint32_t)f2bf(o[4]) | ((uint32_t)f2bf(o[5]) << 16);
-                        w.w = (uint32_t)f2bf(o[6]) | ((uint32_t)f2bf(o[7]) << 16);
+                        w.x = pk_bf16(o[0], o[1]);
+                        w.y = pk_bf16(o[2], o[3]);
+                        w.z = pk_bf16(o[4], o[5]);
+                        w.w = pk_bf16(o[6], o[7]);
                         *(uint4*)(dx + (pb + r + u * L.RP) * lddx + dxoff + c) = w;
                         if constexpr (F8) {
                             float vb[8];

@@ -54,6 +54,11 @@ EXTRA_CASES = [
     (384, 128, 3, 1, 1, 0, 64),    # up1_conv shape, 6 ci chunks
     (64, 128, 3, 1, 1, 0, 128),    # down1 shape, 2 segments per row
     (256, 256, 3, 1, 1, 1, 128),   # resblock conv, reflect, interior + edge segments
+    # one 64-channel input chunk: the resident-weight persistent kernel (conv_res64) takes the
+    # bf16 forward and every dgrad whose dY has 64 channels (ragged patches, reflect, 3 co tiles)
+    (64, 64, 3, 1, 1, 1, 37),
+    (192, 64, 3, 1, 1, 1, 21),
+    (64, 192, 3, 1, 1, 0, 50),
 ]
 
 
@@ -169,7 +174,7 @@ def test_bf16_conv_family_tight(ops, case):
 
 @pytest.mark.parametrize("case", [(256, 256, 3, 1, 64, 2), (256, 256, 3, 1, 37, 2), (128, 256, 3, 0, 33, 2),
                                   (64, 128, 3, 0, 40, 2), (384, 128, 3, 0, 24, 2), (256, 512, 4, 0, 13, 2),
-                                  (192, 64, 3, 0, 64, 1)])
+                                  (192, 64, 3, 0, 64, 1), (64, 64, 3, 1, 37, 3), (64, 128, 3, 0, 64, 2)])
 def test_bf16_fused_in_stats_tight(ops, case):
     """conv_pp with the fused InstanceNorm-statistics epilogue: the bf16 output holds
     the tight bound, and {mean, rstd} equal the fp64 statistics OF THAT bf16 OUTPUT
@@ -198,3 +203,31 @@ def test_bf16_fused_in_stats_tight(ops, case):
     got = mr.view(N, cout, 2).double().cpu()
     torch.testing.assert_close(got[..., 0], mean, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(got[..., 1], rstd, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("cout,H,mode", [(64, 37, 1), (192, 24, 0), (128, 16, 0)])
+def test_bf16_res64_act_mask_tight(ops, cout, H, mode):
+    """The Cin = 64 resident-weight kernel's epilogue: ReLU / LeakyReLU activations and the
+    backward ReLU / LeakyReLU masks (VGG conv1_2 / conv2_1, ir:664) on the bf16 path, into a
+    channel slice, held to the tight bf16 bound."""
+    torch.manual_seed(7)
+    N, cin = 2, 64
+    spec = ops.ConvSpec(cin, cout, 3, 1, 1, mode)
+    x = q(torch.randn(N, cin, H, H))
+    w = q(torch.randn(cout, cin, 3, 3) * (1.0 / (cin * 9) ** 0.5))
+    b = torch.randn(cout) * 0.1
+    m = q(torch.randn(N, cout, H, H))
+    pc = ops.PackedConv(spec, w.permute(0, 2, 3, 1).contiguous().reshape(-1).to(DEV), b.to(DEV), ops.BF16)
+    pc.pack()
+    y64 = ref_conv(x.double(), w.double(), b.double(), 3, 1, 1, mode)
+    ya = ref_conv(x.abs().double(), w.abs().double(), b.abs().double(), 3, 1, 1, mode)
+    for act, fn in ((ops.ACT_RELU, F.relu), (ops.ACT_LRELU, lambda t: F.leaky_relu(t, 0.2))):
+        y = torch.zeros(N, H, H, cout + 8, device=DEV, dtype=torch.bfloat16)
+        ops.conv_fwd(pc, ops.Feat(nhwc(x)), ops.Feat(y, 8, cout), act=act)
+        check(nchw64(y[..., 8:]), fn(y64), ya, R_BF16, f"act {act}")
+        assert not y[..., :8].any()
+    for mact, slope in ((1, 0.0), (2, 0.2)):
+        y = torch.zeros(N, H, H, cout, device=DEV, dtype=torch.bfloat16)
+        ops.conv_fwd(pc, ops.Feat(nhwc(x)), ops.Feat(y), mask=ops.Feat(nhwc(m)), mask_act=mact)
+        mm = torch.where(m > 0, 1.0, slope).double()
+        check(nchw64(y), y64 * mm, ya, R_BF16, f"mask {mact}")
