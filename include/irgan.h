@@ -247,6 +247,16 @@ int irgan_sep_resample(const void* in, int32_t in_dtype, int32_t N, int32_t Hin,
                        int32_t Hout, int32_t Wout, int32_t ldo, int32_t offo, const int32_t* ty,
                        const float* wy, int32_t Ty, const int32_t* tx, const float* wx,
                        int32_t Tx, int32_t accumulate, irgan_stream_t s);
+/* irgan_sep_resample (no accumulate) of act(InstanceNorm(in)): mr = the per-(n, c)
+ * {mean, rstd} pairs of in (irgan_in_finalize / irgan_in_stats), act IRGAN_ACT_*.
+ * The IN apply + ReLU of down1 / down2 / up1_conv (ir:469-482, 557-558) fused into the
+ * Downsample / UpsampleAA that consumes it.  IRGAN_EUNSUPPORTED unless 8-channel-aligned
+ * slices and at most 8 taps per axis (then apply + resample separately). */
+int irgan_sep_resample_in(const void* in, int32_t in_dtype, int32_t N, int32_t Hin, int32_t Win,
+                          int32_t C, int32_t ldi, int32_t offi, const float* mr, int32_t act,
+                          void* out, int32_t out_dtype, int32_t Hout, int32_t Wout, int32_t ldo,
+                          int32_t offo, const int32_t* ty, const float* wy, int32_t Ty,
+                          const int32_t* tx, const float* wx, int32_t Tx, irgan_stream_t s);
 /* 2x2 max pool (VGG features) forward / backward (first max wins, as ATen). */
 int irgan_maxpool_fwd(const void* x, int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t C,
                       void* y, irgan_stream_t s);

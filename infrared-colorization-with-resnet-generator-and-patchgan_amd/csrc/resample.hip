@@ -107,20 +107,37 @@ __global__ __launch_bounds__(TPB) void sep_kernel(const void* __restrict__ in, i
 // compile-time bound TM (tables are compacted to their widest row on the host),
 // so a thread's loads are issued back to back.  Global loads per output drop
 // from Ty*Tx (sep_kernel) to about Ty*Win/Wout.
+//
+// NORM (irgan_sep_resample_in): the input is a pre-InstanceNorm tensor z and every
+// loaded value becomes act((z - mean[n][c]) * rstd[n][c]) before the vertical taps --
+// the InstanceNorm apply + ReLU of down1 / down2 / up1_conv (ir:469-482, 557) fused into
+// the Downsample / UpsampleAA that consumes it, so the normalised tensor is never stored.
+// LTPB % G == 0, so a thread's channel group (and its 8 (mean, rstd) pairs) is fixed.
 constexpr int LTPB = 1024;
-template <int TM>
+template <int TM, bool NORM = false>
 __global__ __launch_bounds__(LTPB) void sep_lds_kernel(const void* __restrict__ in, int idt, int Hin, int Win,
                                                        int ldi, int offi, void* __restrict__ out, int odt, int Hout,
                                                        int Wout, int ldo, int offo, const int* __restrict__ ty,
                                                        const float* __restrict__ wy, int Ty,
                                                        const int* __restrict__ tx, const float* __restrict__ wx,
-                                                       int Tx, int accumulate, int CB) {
+                                                       int Tx, int accumulate, int CB,
+                                                       const float* __restrict__ mr = nullptr, int C = 0,
+                                                       int act = 0) {
     extern __shared__ float4 sm4[];
     float* const sm = (float*)sm4;
     const int row = blockIdx.x;
     const int n = row / Hout, oy = row - n * Hout;
     const int c0 = blockIdx.y * CB;
     const int G = CB >> 3;  // 8-channel groups
+    float nm[NORM ? 8 : 1], nr[NORM ? 8 : 1];
+    if constexpr (NORM) {
+        const float4* m4 = (const float4*)(mr + 2 * ((long)n * C + c0 + (threadIdx.x % G) * 8));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float4 t = m4[k];
+            nm[2 * k] = t.x; nr[2 * k] = t.y; nm[2 * k + 1] = t.z; nr[2 * k + 1] = t.w;
+        }
+    }
     float wyv[TM];
     long rb[TM];
 #pragma unroll
@@ -138,6 +155,13 @@ __global__ __launch_bounds__(LTPB) void sep_lds_kernel(const void* __restrict__ 
             if (wyv[i] == 0.f) continue;
             float xv[8];
             ldvec<8>(in, idt, (rb[i] + col) * ldi + offi + c0 + g * 8, xv);
+            if constexpr (NORM) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const float h = (xv[k] - nm[k]) * nr[k];
+                    xv[k] = act == IRGAN_ACT_RELU ? fmaxf(h, 0.f) : (act == IRGAN_ACT_LRELU && h < 0.f ? 0.2f * h : h);
+                }
+            }
 #pragma unroll
             for (int k = 0; k < 8; ++k) acc[k] += wyv[i] * xv[k];
         }
@@ -493,6 +517,39 @@ extern "C" int irgan_sep_resample(const void* in, int32_t in_dtype, int32_t N, i
     else
         sep_kernel<1><<<g, TPB, 0, (hipStream_t)s>>>(in, in_dtype, Hin, Win, C, ldi, offi, out, out_dtype, Hout, Wout,
                                                      ldo, offo, ty, wy, Ty, tx, wx, Tx, accumulate);
+    IRGAN_LAUNCH_CHECK();
+    return 0;
+}
+
+// out = (Wy (x) Wx) act(IN(in)) with IN's per-(n, c) {mean, rstd} table mr (the
+// InstanceNorm apply fused into the resample that consumes it); the LDS form only
+// (IRGAN_EUNSUPPORTED otherwise: the caller applies the norm itself, then resamples).
+extern "C" int irgan_sep_resample_in(const void* in, int32_t in_dtype, int32_t N, int32_t Hin, int32_t Win,
+                                     int32_t C, int32_t ldi, int32_t offi, const float* mr, int32_t act, void* out,
+                                     int32_t out_dtype, int32_t Hout, int32_t Wout, int32_t ldo, int32_t offo,
+                                     const int32_t* ty, const float* wy, int32_t Ty, const int32_t* tx,
+                                     const float* wx, int32_t Tx, irgan_stream_t s) {
+    if (!mr) return IRGAN_EINVAL;
+    const bool vec = (C % 8 == 0) && (ldi % 8 == 0) && (offi % 8 == 0) && (ldo % 8 == 0) && (offo % 8 == 0);
+    if ((long)N * Hout * Wout * C <= 0) return 0;
+    if (Ty < 1 || Tx < 1) return IRGAN_EINVAL;
+    const int TM = Ty > Tx ? Ty : Tx;
+    if (!vec || TM > 8 || getenv("IRGAN_NO_SEP_LDS") || getenv("IRGAN_NO_IN_RESAMPLE")) return IRGAN_EUNSUPPORTED;
+    int CB = 0;
+    for (int cb = 128; cb >= 8 && !CB; cb >>= 1)
+        if (C % cb == 0 && (long)Win * cb <= 16384) CB = cb;
+    if (!CB) return IRGAN_EUNSUPPORTED;
+    dim3 g(N * Hout, C / CB);
+    const size_t sh = (size_t)Win * CB * 4;
+    hipStream_t st = (hipStream_t)s;
+#define SEPN(T)                                                                                                   \
+    sep_lds_kernel<T, true><<<g, LTPB, sh, st>>>(in, in_dtype, Hin, Win, ldi, offi, out, out_dtype, Hout, Wout, ldo, \
+                                                 offo, ty, wy, Ty, tx, wx, Tx, 0, CB, mr, C, act)
+    if (TM <= 2) SEPN(2);
+    else if (TM <= 4) SEPN(4);
+    else if (TM <= 6) SEPN(6);
+    else SEPN(8);
+#undef SEPN
     IRGAN_LAUNCH_CHECK();
     return 0;
 }

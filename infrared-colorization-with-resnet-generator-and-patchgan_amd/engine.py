@@ -240,6 +240,7 @@ class INLayer:
     where a fused kernel exists (irgan_conv_fwd_stats) instead of a separate pass.
     """
     fused_stats = True
+    fused_resample = not os.environ.get("IRGAN_NO_IN_RESAMPLE")
     sum_bias_grad = False
 
     def fwd(self, bufs: Buffers, name: str, x: Feat, y: Feat, act, res: Feat = None, xhat=None, nb=0, q8=None):
@@ -271,6 +272,29 @@ class INLayer:
         if not nb:
             ops.conv_fwd(pc, x, z)
         self.fwd(bufs, name, z, y, act, res=res, nb=nb)
+
+    def conv_stats(self, bufs: Buffers, name: str, pc, x: Feat, z: Feat):
+        """z = conv(x) and z's {mean, rstd} table (returned, kept for bwd()) -- no apply:
+        the consumer normalises on load (ops.blur_down_in / ops.upsample_in)."""
+        work = bufs.flat("in_work", ops.IN_PARTS * z.N * z.C, torch.float64)
+        mr = bufs.get("mr_" + name, (z.N * z.C * 2,), torch.float32)
+        nb = ops.conv_fwd_stats(pc, x, z, work) if INLayer.fused_stats else 0
+        if nb:
+            ops.in_finalize(z, work, nb, mr)
+        else:
+            ops.conv_fwd(pc, x, z)
+            ops.in_stats(z, work, mr)
+        return mr
+
+    def resample_fwd(self, bufs: Buffers, name: str, pc, x: Feat, z: Feat, a_name: str, act, y: Feat, fused, plain):
+        """y = resample(act(IN(conv(x)))): the IN apply fused into the resample when
+        ``fused(z, mr, act, y)`` takes the shapes, else apply into bufs[a_name] + ``plain``."""
+        mr = self.conv_stats(bufs, name, pc, x, z)
+        if INLayer.fused_resample and fused(z, mr, act, y):
+            return
+        a = Feat(bufs.get(a_name, (z.N, z.H, z.W, z.C), z.t.dtype))
+        ops.in_apply(z, mr, a, act=act)
+        plain(a, y)
 
     def bwd(self, bufs: Buffers, name: str, dy: Feat, z: Feat, act, dx: Feat, db=None, dy2: Feat = None, q8=None):
         """z: the PRE-norm input kept from forward; act: the activation after IN.
@@ -376,9 +400,8 @@ class GeneratorEngine:
             self.norms["down1"].fwd(g, "down1", z1, x1, ACT_RELU)
         else:
             z1 = Feat(g.get("z1", (B, H, W, c1), T))
-            a1 = Feat(g.get("a1", (B, H, W, c1), T))
-            self.norms["down1"].conv_fwd(g, "down1", self.down1, x0, z1, a1, ACT_RELU)
-            ops.blur_down(a1, x1)
+            self.norms["down1"].resample_fwd(g, "down1", self.down1, x0, z1, "a1", ACT_RELU, x1, ops.blur_down_in,
+                                             ops.blur_down)
         # down2 (+ blur-down)  (ir:477-482)
         h = Feat(g.get("h0", (B, H2, W2, c2), T))
         if self.no_aa:
@@ -387,9 +410,8 @@ class GeneratorEngine:
             self.norms["down2"].fwd(g, "down2", z2, h, ACT_RELU)
         else:
             z2 = Feat(g.get("z2", (B, H1, W1, c2), T))
-            a2 = Feat(g.get("a2", (B, H1, W1, c2), T))
-            self.norms["down2"].conv_fwd(g, "down2", self.down2, x1, z2, a2, ACT_RELU)
-            ops.blur_down(a2, h)
+            self.norms["down2"].resample_fwd(g, "down2", self.down2, x1, z2, "a2", ACT_RELU, h, ops.blur_down_in,
+                                             ops.blur_down)
         # 9 ResnetBlocks  (ir:362-418, 485-490)
         # fp8: one e4m3 operand buffer, written by the producer of each conv input (the
         # IN passes, fused; h_0 from blur-down by a quantise launch) and read by the conv
@@ -430,14 +452,15 @@ class GeneratorEngine:
         else:
             ops.upsample(h, y1)
         z3 = Feat(g.get("z3", (B, H1, W1, c1), T))
-        a3 = Feat(g.get("a3", (B, H1, W1, c1), T))
-        self.norms["up1"].conv_fwd(g, "up1", self.up1, Feat(cat1), z3, a3, ACT_RELU)
         # up2 -> cat with x0 -> conv/IN/ReLU  (ir:561-565)
         y2 = Feat(cat2, 0, c1)
         if self.no_aa_up:
+            a3 = Feat(g.get("a3", (B, H1, W1, c1), T))   # also the ConvTranspose2d's weight-gradient input
+            self.norms["up1"].conv_fwd(g, "up1", self.up1, Feat(cat1), z3, a3, ACT_RELU)
             self._convt(self.up2_up, a3, y2, g, "ut2")
         else:
-            ops.upsample(a3, y2)
+            self.norms["up1"].resample_fwd(g, "up1", self.up1, Feat(cat1), z3, "a3", ACT_RELU, y2, ops.upsample_in,
+                                           ops.upsample)
         z4 = Feat(g.get("z4", (B, H, W, c0), T))
         a4 = Feat(g.get("a4", (B, H, W, c0), T))
         self.norms["up2"].conv_fwd(g, "up2", self.up2, Feat(cat2), z4, a4, ACT_RELU)
@@ -504,11 +527,10 @@ class GeneratorEngine:
         dcat2 = Feat(g.get("dcat2", (B, H, W, c1 + c0), T))
         ops.conv_dgrad(self.up2, da4, dcat2)
         # up2_up
-        a3 = Feat(g.d["a3"])
         da3 = Feat(g.get("da3", (B, H1, W1, c1), T))
         dy2 = dcat2.sl(0, c1)
         if self.no_aa_up:
-            self._convt_bwd(self.up2_up, "up2_up", dy2, a3, da3, g, "ut2")
+            self._convt_bwd(self.up2_up, "up2_up", dy2, Feat(g.d["a3"]), da3, g, "ut2")
         else:
             ops.upsample_bwd(dy2, da3)
         # up1_conv

@@ -560,9 +560,30 @@ def sep_resample(x: Feat, y: Feat, ytab, xtab, accumulate=False):
               P(ty), P(wy), Ty, P(tx), P(wx), Tx, int(accumulate), stream())
 
 
+def sep_resample_in(z: Feat, mr: torch.Tensor, act, y: Feat, ytab, xtab) -> bool:
+    """y = resample(act(InstanceNorm(z))) with z's {mean, rstd} table ``mr``
+    (irgan_sep_resample_in: the IN apply fused into the resample's loads).  False when
+    the kernel does not take the shapes -- then NOTHING ran."""
+    (ty, wy, ry, Ty), (tx, wx, rx, Tx) = ytab, xtab
+    assert (ry, rx) == (y.H, y.W) and z.C == y.C and z.N == y.N, "sep_resample_in shape mismatch"
+    rc = getattr(_lib.load(), "irgan_sep_resample_in")(
+        z.ptr, z.dt, z.N, z.H, z.W, z.C, z.ld, z.off, P(mr), act, y.ptr, y.dt, y.H, y.W, y.ld, y.off,
+        P(ty), P(wy), Ty, P(tx), P(wx), Tx, stream())
+    if rc == IRGAN_EUNSUPPORTED:
+        return False
+    if rc != 0:
+        raise _lib.IrganError(f"irgan_sep_resample_in failed with code {rc}")
+    return True
+
+
 def blur_down(x: Feat, y: Feat):
     """Downsample (ir:269-310)."""
     sep_resample(x, y, resample_table(RS_DOWN, x.H), resample_table(RS_DOWN, x.W))
+
+
+def blur_down_in(z: Feat, mr: torch.Tensor, act, y: Feat) -> bool:
+    """Downsample of act(IN(z)) (ir:469-482) without storing the normalised tensor."""
+    return sep_resample_in(z, mr, act, y, resample_table(RS_DOWN, z.H), resample_table(RS_DOWN, z.W))
 
 
 def blur_down_bwd(dy: Feat, dx: Feat, accumulate=False):
@@ -580,6 +601,11 @@ def upsample(x: Feat, y: Feat):
     """UpsampleAA (ir:313-355); when y is not 2x (odd skip sizes) the reference's
     bilinear resize to the skip's size (ir:555-556, 562-563) is folded into the map."""
     sep_resample(x, y, _up_axis(x.H, y.H, False), _up_axis(x.W, y.W, False))
+
+
+def upsample_in(z: Feat, mr: torch.Tensor, act, y: Feat) -> bool:
+    """UpsampleAA of act(IN(z)) (ir:557-561) without storing the normalised tensor."""
+    return sep_resample_in(z, mr, act, y, _up_axis(z.H, y.H, False), _up_axis(z.W, y.W, False))
 
 
 def upsample_bwd(dy: Feat, dx: Feat, work=None, accumulate=False):
