@@ -73,6 +73,18 @@ int irgan_conv_fwd(const irgan_conv_desc* d, const void* x, const void* w,
 int irgan_conv_fwd_stats(const irgan_conv_desc* d, const void* x, const void* w,
                          const float* bias, void* y, void* part, int32_t* nb, irgan_stream_t s);
 
+/* Backward-data of a reflect-padded 3x3 stride-1 ResnetBlock conv (ir:381-392, 401-411:
+ * the interior by the bf16 conv_pp kernel, then the reflect-pad ring as
+ * irgan_reflect_dgrad_ring; d = the interior descriptor ops.conv_dgrad builds, p = 1) that
+ * also writes the InstanceNorm-backward partials (sum g, sum g*xhat) of its bf16 output
+ * dx for the IN that produced the forward input of this conv's layer: z = that IN's
+ * pre-norm input, mr its {mean, rstd}, act the activation after it; g = dx * act'(xhat).
+ * *nb (out) = partial rows per image; reduce with irgan_in_bwd_finalize.  Replaces the
+ * separate irgan_in_bwd_reduce pass over dx.  IRGAN_EUNSUPPORTED (nothing launched)
+ * unless bf16, Cout % 256 == 0, 8-aligned slices, an output the size of the input. */
+int irgan_conv_dgrad_in_stats(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p,
+                              void* dx, const void* z, int32_t ldz, int32_t zoff, const float* mr,
+                              int32_t act, void* part, int32_t* nb, irgan_stream_t s);
 /* irgan_conv_fwd_stats / irgan_conv_fwd on fp8 operands (BASELINE config 5): x and
  * w OCP e4m3 (d->dtype = IRGAN_FP8; x NHWC with ldx, xoff % 16 == 0, w the packed
  * [Cout][3][3][Cin] image), 3x3, stride 1, Cin % 128 == 0, Cout % 64 == 0 (not
@@ -168,6 +180,10 @@ enum { IRGAN_IN_PARTS = 256 };
  * written by irgan_conv_fwd_stats (the reduction half of irgan_in_stats). */
 int irgan_in_finalize(const void* part, int32_t N, int32_t HW, int32_t C, int32_t nb, float* mr,
                       irgan_stream_t s);
+/* red[n][c] = {mean g, mean g*xhat} from nb per-image partial rows (the reduce half of
+ * irgan_in_bwd_reduce) written by irgan_conv_dgrad_in_stats. */
+int irgan_in_bwd_finalize(const void* part, int32_t N, int32_t HW, int32_t C, int32_t nb, float* red,
+                          irgan_stream_t s);
 /* mr[n][c] = {mean, rstd}; work: IRGAN_IN_PARTS*N*C doubles of scratch. */
 int irgan_in_stats(const void* x, int32_t dtype, int32_t N, int32_t HW, int32_t C,
                    int32_t ld, int32_t off, double* work, float* mr, irgan_stream_t s);

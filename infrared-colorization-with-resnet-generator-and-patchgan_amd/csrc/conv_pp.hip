@@ -109,6 +109,22 @@ struct PP {
 typedef int v8i_t __attribute__((ext_vector_type(8)));
 IRGAN_HD v8i_t cat8(i32x4 a, i32x4 b) { return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7); }
 
+// InstanceNorm-backward statistics in the STATS epilogue (irgan_conv_dgrad_in_stats):
+// with z set, the partials of the stored output v are (sum g, sum g*xhat) with
+// xhat = (z - mean) * rstd and g = v * act'(xhat) -- the reduce half of the IN backward
+// of the layer whose gradient this dgrad produces -- instead of (sum v, sum v^2).
+// pstride: partial rows per image (0: the patch count; > it leaves slots for the ring).
+struct InBwdStats {
+    const bf16_t* z;
+    int ldz, zoff, act, pstride;
+    const float* mr;
+};
+IRGAN_HD float in_act_grad(float xh, int act) {  // as norm.hip's act_grad
+    if (act == IRGAN_ACT_RELU) return xh > 0.f ? 1.f : 0.f;
+    if (act == IRGAN_ACT_LRELU) return xh > 0.f ? 1.f : 0.2f;
+    return 1.f;
+}
+
 // ONE: a single halo buffer, so at BN = 64 the block fits twice per CU (LDS 62 KiB,
 // <= 128 VGPRs) and one block's halo loads / epilogue overlap the other's MFMA loop
 // (BN = 128 would need 159 VGPRs: at 128 it spills 30 and runs slower than two BN-64
@@ -122,7 +138,8 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
                                                          int ntn, int tpx, int tpy, int swz,
                                                          float2* __restrict__ part = nullptr,
                                                          const float* __restrict__ dqx = nullptr,
-                                                         const float* __restrict__ dqw = nullptr) {
+                                                         const float* __restrict__ dqw = nullptr,
+                                                         const InBwdStats ib = InBwdStats{}) {
     constexpr int ESZ = F8 ? 1 : 2, CHN = 128 / ESZ;  // operand bytes, channels per 128-byte chunk
     const char* const xb = (const char*)x;
     const char* const wb = (const char*)w;
@@ -469,17 +486,41 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
         float s1[8], s2[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.f;
+        const bool bw = ib.z != nullptr;  // IN-backward statistics (block-uniform)
+        float mn[8], rs[8];
+        if (bw) {
+            const float4* m4 = (const float4*)(ib.mr + 2 * ((long)img * d.Cout + co8));
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float4 t4 = m4[k];
+                mn[2 * k] = t4.x; rs[2 * k] = t4.y; mn[2 * k + 1] = t4.z; rs[2 * k + 1] = t4.w;
+            }
+        }
         for (int m = tid / LPP; m < 256; m += PPASS) {
             const long pix = pix_of(m);
             if (pix < 0) continue;
             const uint4 v = *(const uint4*)(smem + m * RSB + c8 * 2);
             *(uint4*)((bf16_t*)y + pix * d.ldy + d.yoff + co8) = v;
             const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+            if (bw) {
+                const uint4 zz = *(const uint4*)(ib.z + pix * ib.ldz + ib.zoff + co8);
+                const uint32_t zw[4] = {zz.x, zz.y, zz.z, zz.w};
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float lo = __uint_as_float(wv[k] << 16), hi = __uint_as_float(wv[k] & 0xffff0000u);
-                s1[2 * k] += lo; s2[2 * k] += lo * lo;
-                s1[2 * k + 1] += hi; s2[2 * k + 1] += hi * hi;
+                for (int k = 0; k < 8; ++k) {
+                    const float f = __uint_as_float((k & 1) ? (wv[k / 2] & 0xffff0000u) : (wv[k / 2] << 16));
+                    const float zf = __uint_as_float((k & 1) ? (zw[k / 2] & 0xffff0000u) : (zw[k / 2] << 16));
+                    const float xh = (zf - mn[k]) * rs[k];
+                    const float g = f * in_act_grad(xh, ib.act);
+                    s1[k] += g;
+                    s2[k] += g * xh;
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float lo = __uint_as_float(wv[k] << 16), hi = __uint_as_float(wv[k] & 0xffff0000u);
+                    s1[2 * k] += lo; s2[2 * k] += lo * lo;
+                    s1[2 * k + 1] += hi; s2[2 * k + 1] += hi * hi;
+                }
             }
         }
         __syncthreads();  // staging reads done: reuse LDS for the cross-row reduction
@@ -513,7 +554,7 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
                 a += e.x;
                 b += e.y;
             }
-            const long patch = (long)img * (tpx * tpy) + pyi * tpx + pxi;
+            const long patch = (long)img * (ib.pstride > 0 ? ib.pstride : tpx * tpy) + pyi * tpx + pxi;
             part[patch * d.Cout + n0 + tid] = make_float2(a, b);
         }
         return;
@@ -672,6 +713,51 @@ extern "C" int irgan_conv_fwd_stats(const irgan_conv_desc* d, const void* x, con
 #undef PPS
     IRGAN_LAUNCH_CHECK();
     *nb = tpx * tpy;
+    return 0;
+}
+
+// Reflect-padded resblock backward-data (interior conv_pp + the ring, as ops.conv_dgrad)
+// that also writes the InstanceNorm-backward partials of its bf16 output for the layer
+// whose gradient it is: z / mr / act of that IN (ir:386-392, 401-411).  The interior's
+// partials fill rows [0, tpx*tpy) of each image, the ring kernel (irgan_reflect_dgrad_ring_in)
+// adds the change it makes to the border pixels in rows [tpx*tpy, *nb).  Reduce them with
+// irgan_in_bwd_finalize.  IRGAN_EUNSUPPORTED (nothing launched) unless BN-256 tiles.
+int ring_in_launch(const irgan_conv_desc* d, const void* dy, const void* w, int p, void* dx, const void* z, int ldz,
+                   int zoff, const float* mr, int act, void* part, int pstride, int slot0, hipStream_t st);
+int ring_in_slots(const irgan_conv_desc* d, int p);
+
+extern "C" int irgan_conv_dgrad_in_stats(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p, void* dx,
+                                         const void* z, int32_t ldz, int32_t zoff, const float* mr, int32_t act,
+                                         void* part, int32_t* nb, irgan_stream_t s) {
+    if (!d || !dy || !w || !dx || !z || !mr || !part || !nb) return IRGAN_EINVAL;
+    if (d->dtype != IRGAN_BF16 || d->out_dtype != IRGAN_BF16 || d->act != IRGAN_ACT_NONE || d->KH != 3 ||
+        d->KW != 3 || d->sy != 1 || d->sx != 1 || d->Cin % 64 || d->Cout % 256 || d->ldx % 8 || d->xoff % 8 ||
+        d->ldy % 8 || d->yoff % 8 || ldz % 8 || zoff % 8 || d->Ho != d->OH || d->Wo != d->OW || d->omy != 1 ||
+        d->omx != 1 || d->ooy || d->oox || p != 1 || d->Ho != d->H || d->Wo != d->W ||
+        (long)d->N * d->H * d->W * d->ldx >= (1L << 30) || (long)d->Cout * 9 * d->Cin >= (1L << 30) ||
+        getenv("IRGAN_NO_FUSED_IN_BWD"))
+        return IRGAN_EUNSUPPORTED;
+    const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH);
+    const int nr = ring_in_slots(d, p);
+    if (nr <= 0 || tpx * tpy + nr > IRGAN_IN_PARTS) return IRGAN_EUNSUPPORTED;
+    if ((long)d->N * d->Ho * d->Wo <= 0) return IRGAN_EUNSUPPORTED;
+    static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
+    const int ntn = d->Cout / 256;
+    const int blocks = d->N * tpy * tpx * ntn;
+    const int pstride = tpx * tpy + nr;
+    hipStream_t st = (hipStream_t)s;
+    const InBwdStats ib{(const bf16_t*)z, ldz, zoff, act, pstride, mr};
+#define PPB(ACCV)                                                                                                 \
+    conv_pp_kernel<3, 3, 256, ACCV, true, false, false><<<blocks, 512, 0, st>>>(                                   \
+        *d, (const bf16_t*)dy, (const bf16_t*)w, nullptr, dx, nullptr, ntn, tpx, tpy, swz, (float2*)part, nullptr, \
+        nullptr, ib)
+    if (d->accumulate) PPB(true);
+    else PPB(false);
+#undef PPB
+    IRGAN_LAUNCH_CHECK();
+    const int rc = ring_in_launch(d, dy, w, p, dx, z, ldz, zoff, mr, act, part, pstride, tpx * tpy, st);
+    if (rc) return rc;
+    *nb = pstride;
     return 0;
 }
 

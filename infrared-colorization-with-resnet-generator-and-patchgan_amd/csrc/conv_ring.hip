@@ -42,9 +42,27 @@ IRGAN_HD int mirror_pos(int i, int n, int p) {  // virtual position folding onto
     return -0x40000000;
 }
 
+// IN-backward statistics of the band pixels this launch changes (irgan_conv_dgrad_in_stats):
+// with part set, block (image n, segment slot s, channel tile) writes the sums over its
+// pixels of (delta g, delta g * xhat), delta = the stored bf16 value after the add minus
+// the one before, g and xhat as conv_pp's InBwdStats -- so the interior partials plus
+// these equal the partials of the final tensor.  Row n*pstride + slot0 + s of part.
+struct RingInStats {
+    const bf16_t* z;
+    int ldz, zoff, act, pstride, slot0;
+    const float* mr;
+    float2* part;
+};
+IRGAN_HD float ring_act_grad(float xh, int act) {  // as norm.hip's act_grad
+    if (act == IRGAN_ACT_RELU) return xh > 0.f ? 1.f : 0.f;
+    if (act == IRGAN_ACT_LRELU) return xh > 0.f ? 1.f : 0.2f;
+    return 1.f;
+}
+
 __global__ __launch_bounds__(NWV * 64) void reflect_ring_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ dy,
                                                            const bf16_t* __restrict__ w, int p, void* __restrict__ dx,
-                                                           int segs_row, int segs_col) {
+                                                           int segs_row, int segs_col,
+                                                           const RingInStats is = RingInStats{}) {
     __shared__ __attribute__((aligned(16))) float red[NWV][NPIX][NCO + 4];  // +4: conflict-free row writes
     __shared__ int tap_list[MAXT];
     __shared__ int ntap_s;
@@ -185,13 +203,16 @@ __global__ __launch_bounds__(NWV * 64) void reflect_ring_kernel(const irgan_conv
                 make_float4(acc[f][j][0], acc[f][j][1], acc[f][j][2], acc[f][j][3]);
     __syncthreads();
     // thread -> (pixel, 8 channels): sum the NWV partials in order, add into dx
-    if (threadIdx.x >= NPIX * NCO / 8) return;
+    static_assert(NPIX * NCO / 8 == NWV * 64, "one (pixel, 8 channels) per thread");
     const int pix_l = threadIdx.x >> 3, cg = (threadIdx.x & 7) * 8;
     const int q = seg * NPIX + pix_l;
     const int yy = rowseg ? bpos : q, xx = rowseg ? q : bpos;
     const bool own = rowseg ? q < W : (q < H && mirror_pos(q, H, p) == -0x40000000);
     const int co = co0 + cg;
-    if (!own || co >= d.Cout) return;
+    float st1[8], st2[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) st1[k] = st2[k] = 0.f;
+    if (own && co < d.Cout) {
     float v[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = 0.f;
@@ -220,20 +241,73 @@ __global__ __launch_bounds__(NWV * 64) void reflect_ring_kernel(const irgan_conv
         if (full && (o & 7) == 0) {
             uint4 u = *(uint4*)yp;
             uint32_t wds[4] = {u.x, u.y, u.z, u.w};
+            float dlt[8];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const float a = __uint_as_float(wds[k] << 16) + v[2 * k];
-                const float b = __uint_as_float(wds[k] & 0xffff0000u) + v[2 * k + 1];
-                wds[k] = pk_bf16(a, b);
+                const float o0 = __uint_as_float(wds[k] << 16), o1 = __uint_as_float(wds[k] & 0xffff0000u);
+                wds[k] = pk_bf16(o0 + v[2 * k], o1 + v[2 * k + 1]);
+                dlt[2 * k] = __uint_as_float(wds[k] << 16) - o0;
+                dlt[2 * k + 1] = __uint_as_float(wds[k] & 0xffff0000u) - o1;
             }
             *(uint4*)yp = uint4{wds[0], wds[1], wds[2], wds[3]};
+            if (is.part) {  // host guarantees the aligned bf16 path for every owned pixel
+                const uint4 zz = *(const uint4*)(is.z + pix * is.ldz + is.zoff + co);
+                const uint32_t zw[4] = {zz.x, zz.y, zz.z, zz.w};
+                const float4* m4 = (const float4*)(is.mr + 2 * ((long)n * d.Cout + co));
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float4 t4 = m4[k];
+                    const float x0 = (__uint_as_float(zw[k] << 16) - t4.x) * t4.y;
+                    const float x1 = (__uint_as_float(zw[k] & 0xffff0000u) - t4.z) * t4.w;
+                    const float g0 = dlt[2 * k] * ring_act_grad(x0, is.act);
+                    const float g1 = dlt[2 * k + 1] * ring_act_grad(x1, is.act);
+                    st1[2 * k] = g0; st2[2 * k] = g0 * x0;
+                    st1[2 * k + 1] = g1; st2[2 * k + 1] = g1 * x1;
+                }
+            }
         } else {
             for (int k = 0; k < 8 && co + k < d.Cout; ++k) yp[k] = f2bf(bf2f(yp[k]) + v[k]);
         }
     }
+    }
+    if (!is.part) return;
+    // per-channel sums over the block's NPIX pixels, fixed order (deterministic)
+    __syncthreads();  // every wave is done reading red[][][]
+    float2* sr = (float2*)&red[0][0][0];  // [NPIX][NCO]
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sr[pix_l * NCO + cg + k] = make_float2(st1[k], st2[k]);
+    __syncthreads();
+    if (threadIdx.x < NCO && co0 + (int)threadIdx.x < d.Cout) {
+        float a = 0.f, b = 0.f;
+        for (int r = 0; r < NPIX; ++r) {
+            const float2 e = sr[r * NCO + threadIdx.x];
+            a += e.x;
+            b += e.y;
+        }
+        const int slot = blockIdx.x - n * per_img;
+        is.part[((long)n * is.pstride + is.slot0 + slot) * d.Cout + co0 + threadIdx.x] = make_float2(a, b);
+    }
 }
 
 }  // namespace
+
+// conv_pp.hip's irgan_conv_dgrad_in_stats: the ring partial rows per image, and the
+// ring launch that writes them (bf16 output, Cout % 64 == 0, 8-aligned slices: checked there)
+int ring_in_slots(const irgan_conv_desc* d, int p) {
+    return 2 * p * (irgan_cdiv(d->Wo, NPIX) + irgan_cdiv(d->Ho, NPIX));
+}
+int ring_in_launch(const irgan_conv_desc* d, const void* dy, const void* w, int p, void* dx, const void* z, int ldz,
+                   int zoff, const float* mr, int act, void* part, int pstride, int slot0, hipStream_t st) {
+    if (d->dtype != IRGAN_BF16 || d->Cin % 32 || d->Cout % NCO || d->H < 2 * p + 2 || d->W < 2 * p + 2)
+        return IRGAN_EUNSUPPORTED;
+    const int segs_row = irgan_cdiv(d->Wo, NPIX), segs_col = irgan_cdiv(d->Ho, NPIX);
+    dim3 grid(d->N * 2 * p * (segs_row + segs_col), irgan_cdiv(d->Cout, NCO));
+    const RingInStats is{(const bf16_t*)z, ldz, zoff, act, pstride, slot0, mr, (float2*)part};
+    reflect_ring_kernel<<<grid, NWV * 64, 0, st>>>(*d, (const bf16_t*)dy, (const bf16_t*)w, p, dx, segs_row, segs_col,
+                                                   is);
+    IRGAN_LAUNCH_CHECK();
+    return 0;
+}
 
 extern "C" int irgan_reflect_dgrad_ring(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p, void* dx,
                                         irgan_stream_t s) {

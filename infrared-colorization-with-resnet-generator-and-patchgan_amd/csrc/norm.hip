@@ -561,6 +561,15 @@ extern "C" int irgan_in_finalize(const void* part, int32_t N, int32_t HW, int32_
     return 0;
 }
 
+extern "C" int irgan_in_bwd_finalize(const void* part, int32_t N, int32_t HW, int32_t C, int32_t nb, float* red,
+                                     irgan_stream_t s) {
+    if ((long)N * HW * C <= 0) return 0;
+    if (!part || !red || nb < 1 || nb > IRGAN_IN_PARTS) return IRGAN_EINVAL;
+    finalize_kernel<<<dim3(irgan_cdiv(C, FC), N), 256, 0, (hipStream_t)s>>>((const float2*)part, red, N, C, nb, HW, 1);
+    IRGAN_LAUNCH_CHECK();
+    return 0;
+}
+
 extern "C" int irgan_in_apply(const void* x, int32_t dtype, int32_t N, int32_t HW, int32_t C, int32_t ldx,
                               int32_t xoff, const float* mr, int32_t act, const void* res, int32_t ldr, int32_t roff,
                               void* y, int32_t ldy, int32_t yoff, void* xhat, irgan_stream_t s) {

@@ -241,6 +241,10 @@ class INLayer:
     """
     fused_stats = True
     fused_resample = not os.environ.get("IRGAN_NO_IN_RESAMPLE")
+    # measured: the fused reduce adds ~16 us to each resblock dgrad (its
+    # epilogue reads z at one block per CU) against ~19 us for the separate reduce pass:
+    # +0.2 % per step, within box noise -- opt-in (IRGAN_FUSED_IN_BWD=1)
+    fused_in_bwd = bool(os.environ.get("IRGAN_FUSED_IN_BWD"))
     sum_bias_grad = False
 
     def fwd(self, bufs: Buffers, name: str, x: Feat, y: Feat, act, res: Feat = None, xhat=None, nb=0, q8=None):
@@ -296,15 +300,27 @@ class INLayer:
         ops.in_apply(z, mr, a, act=act)
         plain(a, y)
 
-    def bwd(self, bufs: Buffers, name: str, dy: Feat, z: Feat, act, dx: Feat, db=None, dy2: Feat = None, q8=None):
+    def bwd(self, bufs: Buffers, name: str, dy: Feat, z: Feat, act, dx: Feat, db=None, dy2: Feat = None, q8=None,
+            nb=0):
         """z: the PRE-norm input kept from forward; act: the activation after IN.
-        q8: also write dx's fp8 copy (ops.in_backward)."""
+        q8: also write dx's fp8 copy (ops.in_backward).  nb > 0: dy's reduce partials
+        are already in the work buffer (ops.conv_dgrad_in wrote them with dy)."""
         N, C = z.N, z.C
         work = bufs.flat("in_work", ops.IN_PARTS * N * C, torch.float64)
         red = bufs.flat("in_red", 2 * N * C)
         mr = bufs.d["mr_" + name]
         ops.in_backward(dy, z, act, mr, work, red, dx, db=db if INLayer.sum_bias_grad else None, dy2=dy2,
-                        q8=q8 if not INLayer.sum_bias_grad else None)
+                        q8=q8 if not INLayer.sum_bias_grad else None, nb=nb)
+
+    @staticmethod
+    def dgrad_in(bufs: Buffers, name: str, pc, dy: Feat, dx: Feat, z: Feat, act, accumulate=False):
+        """Reflect-padded resblock backward-data that also writes the IN-backward partials of
+        dx for the IN ``name`` (pre-norm input z): returns nb for bwd(nb=...), 0 if it did
+        not run (INLayer.fused_in_bwd off, bias-grad mode, or a layer the kernel does not take)."""
+        if not INLayer.fused_in_bwd or INLayer.sum_bias_grad:
+            return 0
+        work = bufs.flat("in_work", ops.IN_PARTS * z.N * z.C, torch.float64)
+        return ops.conv_dgrad_in(pc, dy, dx, z, bufs.d["mr_" + name], act, work, accumulate=accumulate)
 
 
 # ----------------------------------------------------------------------------
@@ -551,6 +567,7 @@ class GeneratorEngine:
         dt_ = Feat(g.get("dtmp", (B, H2, W2, c2), T))
         nb2 = 2 * self.n_blocks
         dy8 = Feat(g.get("dy8", (B, H2, W2, c2), torch.float8_e4m3fn)) if self.fp8 else None
+        nb_h = 0
         for b in reversed(range(self.n_blocks)):
             p1, p2 = self.res[b]
             key = f"resblocks.{b}.conv_block."
@@ -558,23 +575,34 @@ class GeneratorEngine:
             r1, r2 = Feat(g.d[f"r1_{b}"]), Feat(g.d[f"r2_{b}"])
             A = self.f8a if self.fp8 else None
             s2, s1 = nb2 + 2 * b, nb2 + 2 * b + 1
+            # nb_h: dh's IN-backward partials for r{b}_2, written by the previous block's dgrad
             self.norms[f"r{b}_2"].bwd(g, f"r{b}_2", dh, r2, ACT_NONE, dt_, db=S.krsc(key + "5.bias", G),
-                                      q8=A.spec(s2, dy8) if self.fp8 else None)
+                                      q8=A.spec(s2, dy8) if self.fp8 else None, nb=nb_h)
             wg(p2, key + "5", t, dt_)
             dr = Feat(g.get("dtmp2", (B, H2, W2, c2), T))
+            nb_r = 0
             if self.fp8:
                 A.ensure(s2, dt_, dy8)
                 ops.conv_dgrad_fp8(p2, *self._w8(4 * b + 3), dy8, A.dqp(s2), dt_, dr)
             else:
-                ops.conv_dgrad(p2, dt_, dr, pad_buf=padbuf)
+                # the reduce of r{b}_1's IN backward rides in this dgrad's epilogue
+                nb_r = INLayer.dgrad_in(g, f"r{b}_1", p2, dt_, dr, r1, ACT_RELU)
+                if not nb_r:
+                    ops.conv_dgrad(p2, dt_, dr, pad_buf=padbuf)
             self.norms[f"r{b}_1"].bwd(g, f"r{b}_1", dr, r1, ACT_RELU, dr, db=S.krsc(key + "1.bias", G),
-                                      q8=A.spec(s1, dy8) if self.fp8 else None)
+                                      q8=A.spec(s1, dy8) if self.fp8 else None, nb=nb_r)
             wg(p1, key + "1", hb, dr)
+            nb_h = 0
             if self.fp8:
                 A.ensure(s1, dr, dy8)
                 ops.conv_dgrad_fp8(p1, *self._w8(4 * b + 1), dy8, A.dqp(s1), dr, dh, accumulate=True)
             else:
-                ops.conv_dgrad(p1, dr, dh, accumulate=True, pad_buf=padbuf)
+                # ... and the reduce of block b-1's r2 IN backward in this one (dh = d h_b)
+                if b > 0:
+                    nb_h = INLayer.dgrad_in(g, f"r{b - 1}_2", p1, dr, dh, Feat(g.d[f"r2_{b - 1}"]), ACT_NONE,
+                                            accumulate=True)
+                if not nb_h:
+                    ops.conv_dgrad(p1, dr, dh, accumulate=True, pad_buf=padbuf)
             ready(key + "1.weight")
         if self.fp8:
             self.f8a.update(nb2, nb2)   # next step's backward-data scales

@@ -427,10 +427,15 @@ def in_bwd_parts(dy: Feat, x: Feat, act: int, mr, work, red, dx: Feat, db=None, 
     return reduce, apply
 
 
-def in_backward(dy: Feat, x: Feat, act: int, mr, work, red, dx: Feat, db=None, dy2: Feat = None, q8=None):
-    """dx = backward of act(IN(x)) applied to (dy [+ dy2]); x = PRE-norm input."""
+def in_backward(dy: Feat, x: Feat, act: int, mr, work, red, dx: Feat, db=None, dy2: Feat = None, q8=None, nb=0):
+    """dx = backward of act(IN(x)) applied to (dy [+ dy2]); x = PRE-norm input.
+    nb > 0: the reduce's partials (nb rows per image) are already in ``work``
+    (conv_dgrad_in wrote them with dy): only their finalize runs before the apply."""
     reduce, apply = in_bwd_parts(dy, x, act, mr, work, red, dx, db, dy2, q8)
-    reduce()
+    if nb:
+        _lib.call("irgan_in_bwd_finalize", P(work), x.N, x.H * x.W, x.C, nb, P(red), stream())
+    else:
+        reduce()
     apply()
 
 
@@ -805,6 +810,38 @@ def conv_fwd_fp8(pc: PackedConv, w8: torch.Tensor, dqw, x8: Feat, dqx, y: Feat, 
         "irgan_conv_fwd_fp8", ctypes.byref(d), x8.ptr, P(w8), dqx, dqw, P(pc.bias if bias else None), y.ptr,
         P(part), ctypes.byref(nb), stream()))
     return int(nb.value)
+
+
+def conv_dgrad_in(pc: PackedConv, dy: Feat, dx: Feat, z: Feat, mr: torch.Tensor, act, work: torch.Tensor,
+                  accumulate=False) -> int:
+    """conv_dgrad of a reflect-padded 3x3 ResnetBlock conv (bf16) that also writes the
+    InstanceNorm-backward partials of dx for the IN with pre-norm input z, table mr and
+    activation act (irgan_conv_dgrad_in_stats) into ``work``.  Returns the partial rows
+    per image (pass as in_backward(nb=...)), or 0 when the kernel does not take the
+    layer -- then NOTHING ran."""
+    s = pc.spec
+    if not (pc.reflect and pc.dtype == BF16 and dx.dt == BF16 and s.stride == 1 and s.k == 3 and s.pad == 1):
+        return 0
+    assert dy.C == pc.cout_eff and dx.C == s.cin and (z.N, z.H, z.W, z.C) == (dx.N, dx.H, dx.W, dx.C)
+    H, W = dx.H, dx.W
+    (_, _, ay, c0y), (_, _, ax, c0x), buf = pc.dg[0]
+    d = _desc(N=dy.N, H=dy.H, W=dy.W, Cin=pc.cout_eff, ldx=dy.ld, xoff=dy.off, Cout=s.cin, KH=ay, KW=ax,
+              pad_mode=PAD_ZERO, act=0, dtype=pc.dtype, mask_act=0, ldm=0, moff=0, Ho=H, Wo=W, ldy=dx.ld,
+              yoff=dx.off, OH=H, OW=W, omy=1, ooy=0, omx=1, oox=0, sy=1, sx=1, c0y=c0y + 1, c0x=c0x + 1,
+              accumulate=int(accumulate), out_dtype=dx.dt)
+    nb = ctypes.c_int32(0)
+    fn = getattr(_lib.load(), "irgan_conv_dgrad_in_stats")
+    rc = [0]
+
+    def launch():
+        rc[0] = fn(ctypes.byref(d), dy.ptr, P(buf), 1, dx.ptr, z.ptr, z.ld, z.off, P(mr), act, P(work),
+                   ctypes.byref(nb), stream())
+    TIMER.wrap(conv_tag("dgrad", s, (H, W), dx.N), launch)
+    if rc[0] == IRGAN_EUNSUPPORTED:
+        return 0
+    if rc[0] != 0:
+        raise _lib.IrganError(f"irgan_conv_dgrad_in_stats failed with code {rc[0]}")
+    return nb.value
 
 
 def conv_dgrad_fp8(pc: PackedConv, wd8: torch.Tensor, dqw, dy8: Feat, dqx, dy: Feat, dx: Feat, accumulate=False):

@@ -1,0 +1,5 @@
+set -e
+export TMPDIR=/tmp
+mkdir -p gpurun_out/r02_fib
+timeout -k 10 200 python -u -m pytest tests/test_gpu_fused_in_bwd.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r02_fib/t1.log 2>&1
+bash tools/gpu_ab_bench.sh r02_fib "-" "IRGAN_NO_FUSED_IN_BWD=1"
