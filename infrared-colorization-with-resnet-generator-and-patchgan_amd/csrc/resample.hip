@@ -122,10 +122,12 @@ __global__ __launch_bounds__(LTPB) void sep_lds_kernel(const void* __restrict__ 
                                                        const int* __restrict__ tx, const float* __restrict__ wx,
                                                        int Tx, int accumulate, int CB,
                                                        const float* __restrict__ mr = nullptr, int C = 0,
-                                                       int act = 0) {
+                                                       int act = 0, int swz = 0) {
     extern __shared__ float4 sm4[];
     float* const sm = (float*)sm4;
-    const int row = blockIdx.x;
+    // XCD-aware row order: consecutive output rows (which share input rows through the
+    // vertical taps) run on the same XCD, so the shared rows hit that XCD's L2
+    const int row = xcd_tile(blockIdx.x, gridDim.x, swz);
     const int n = row / Hout, oy = row - n * Hout;
     const int c0 = blockIdx.y * CB;
     const int G = CB >> 3;  // 8-channel groups
@@ -135,8 +137,8 @@ __global__ __launch_bounds__(LTPB) void sep_lds_kernel(const void* __restrict__ 
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const float4 t = m4[k];
-            nm[2 * k] = t.x; nr[2 * k] = t.y; nm[2 * k + 1] = t.z; nr[2 * k + 1] = t.w;
-        }
+            nm[2 * k] = -t.x * t.y; nr[2 * k] = t.y; nm[2 * k + 1] = -t.z * t.w; nr[2 * k + 1] = t.w;
+        }  // nm = -mean * rstd: (z - mean) * rstd as one FMA per loaded element
     }
     float wyv[TM];
     long rb[TM];
@@ -158,7 +160,7 @@ __global__ __launch_bounds__(LTPB) void sep_lds_kernel(const void* __restrict__ 
             if constexpr (NORM) {
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
-                    const float h = (xv[k] - nm[k]) * nr[k];
+                    const float h = fmaf(xv[k], nr[k], nm[k]);
                     xv[k] = act == IRGAN_ACT_RELU ? fmaxf(h, 0.f) : (act == IRGAN_ACT_LRELU && h < 0.f ? 0.2f * h : h);
                 }
             }
@@ -200,6 +202,13 @@ __global__ __launch_bounds__(LTPB) void sep_lds_kernel(const void* __restrict__ 
         }
         stvec<8>(out, odt, o, acc);
     }
+}
+
+// XCD-aware row order for sep_lds_kernel (A/B knob IRGAN_SEP_SWZ=0/1)
+int sep_swz() {
+    static int v = -1;
+    if (v < 0) v = getenv("IRGAN_SEP_SWZ") ? atoi(getenv("IRGAN_SEP_SWZ")) : 0;
+    return v;
 }
 
 // Reflect-pad backward, border part.  The backward-data result g over the
@@ -499,7 +508,7 @@ extern "C" int irgan_sep_resample(const void* in, int32_t in_dtype, int32_t N, i
             hipStream_t st = (hipStream_t)s;
 #define SEPL(T)                                                                                                      \
     sep_lds_kernel<T><<<g, LTPB, sh, st>>>(in, in_dtype, Hin, Win, ldi, offi, out, out_dtype, Hout, Wout, ldo, offo, \
-                                           ty, wy, Ty, tx, wx, Tx, accumulate, CB)
+                                           ty, wy, Ty, tx, wx, Tx, accumulate, CB, nullptr, 0, 0, sep_swz())
             if (TM <= 2) SEPL(2);
             else if (TM <= 4) SEPL(4);
             else if (TM <= 6) SEPL(6);
@@ -544,7 +553,7 @@ extern "C" int irgan_sep_resample_in(const void* in, int32_t in_dtype, int32_t N
     hipStream_t st = (hipStream_t)s;
 #define SEPN(T)                                                                                                   \
     sep_lds_kernel<T, true><<<g, LTPB, sh, st>>>(in, in_dtype, Hin, Win, ldi, offi, out, out_dtype, Hout, Wout, ldo, \
-                                                 offo, ty, wy, Ty, tx, wx, Tx, 0, CB, mr, C, act)
+                                                 offo, ty, wy, Ty, tx, wx, Tx, 0, CB, mr, C, act, sep_swz())
     if (TM <= 2) SEPN(2);
     else if (TM <= 4) SEPN(4);
     else if (TM <= 6) SEPN(6);

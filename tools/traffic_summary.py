@@ -12,8 +12,8 @@ import json
 import os
 import sys
 
-FAMILIES = {"fwd": ("conv_pp_kernel<3, 3, 256, false, false, false>",),
-            "dgrad": ("conv_pp_kernel<3, 3, 256, false, false, false>", "reflect_ring_kernel"),
+FAMILIES = {"fwd": ("conv_pp_kernel<3, 3, 256, false, false, false, false>",),
+            "dgrad": ("conv_pp_kernel<3, 3, 256, false, false, false, false>", "reflect_ring_kernel"),
             "wgrad": ("wgrad_pc_kernel<8>", "wgrad_pc_reduce")}
 
 
