@@ -180,6 +180,13 @@ enum { IRGAN_IN_PARTS = 256 };
  * written by irgan_conv_fwd_stats (the reduction half of irgan_in_stats). */
 int irgan_in_finalize(const void* part, int32_t N, int32_t HW, int32_t C, int32_t nb, float* mr,
                       irgan_stream_t s);
+/* irgan_in_finalize + irgan_in_apply in one launch (bf16 x / res / y, C <= 1024, slices
+ * 8-aligned; else IRGAN_EUNSUPPORTED, nothing launched): mr (out, bit-identical to
+ * irgan_in_finalize's) and y = act(IN(x)) [+ res] (ir:392, 417-418). */
+int irgan_in_finalize_apply(const void* part, int32_t nb, const void* x, int32_t N, int32_t HW,
+                            int32_t C, int32_t ldx, int32_t xoff, float* mr, int32_t act,
+                            const void* res, int32_t ldr, int32_t roff, void* y, int32_t ldy,
+                            int32_t yoff, irgan_stream_t s);
 /* red[n][c] = {mean g, mean g*xhat} from nb per-image partial rows (the reduce half of
  * irgan_in_bwd_reduce) written by irgan_conv_dgrad_in_stats. */
 int irgan_in_bwd_finalize(const void* part, int32_t N, int32_t HW, int32_t C, int32_t nb, float* red,

@@ -241,6 +241,9 @@ class INLayer:
     """
     fused_stats = True
     fused_resample = not os.environ.get("IRGAN_NO_IN_RESAMPLE")
+    # finalize + apply in one launch (irgan_in_finalize_apply): bit-identical, but the step is
+    # unchanged (1062 vs 1062 img/s): opt-in IRGAN_FIN_APPLY=1
+    fused_fin_apply = bool(os.environ.get("IRGAN_FIN_APPLY"))
     # measured: the fused reduce adds ~16 us to each resblock dgrad (its
     # epilogue reads z at one block per CU) against ~19 us for the separate reduce pass:
     # +0.2 % per step, within box noise -- opt-in (IRGAN_FUSED_IN_BWD=1)
@@ -255,6 +258,9 @@ class INLayer:
         N, C = x.N, x.C
         work = bufs.flat("in_work", ops.IN_PARTS * N * C, torch.float64)
         mr = bufs.get("mr_" + name, (N * C * 2,), torch.float32)
+        if nb and xhat is None and q8 is None and INLayer.fused_fin_apply and \
+                ops.in_finalize_apply(x, work, nb, mr, y, act=act, res=res):
+            return
         if nb:
             ops.in_finalize(x, work, nb, mr)
         else:

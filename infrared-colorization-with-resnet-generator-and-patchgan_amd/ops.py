@@ -389,6 +389,22 @@ def in_finalize(x: Feat, part: torch.Tensor, nb: int, mr: torch.Tensor):
     _lib.call("irgan_in_finalize", P(part), x.N, x.H * x.W, x.C, nb, P(mr), stream())
 
 
+def in_finalize_apply(x: Feat, part: torch.Tensor, nb: int, mr: torch.Tensor, y: Feat, act=ACT_NONE,
+                      res: Feat = None) -> bool:
+    """in_finalize + in_apply as one launch (irgan_in_finalize_apply; bf16).  False when
+    the kernel does not take the shapes -- then NOTHING ran."""
+    if x.dt != BF16 or y.dt != BF16 or (res is not None and res.dt != BF16):
+        return False
+    rc = getattr(_lib.load(), "irgan_in_finalize_apply")(
+        P(part), nb, x.ptr, x.N, x.H * x.W, x.C, x.ld, x.off, P(mr), act, res.ptr if res else None,
+        res.ld if res else 0, res.off if res else 0, y.ptr, y.ld, y.off, stream())
+    if rc == IRGAN_EUNSUPPORTED:
+        return False
+    if rc != 0:
+        raise _lib.IrganError(f"irgan_in_finalize_apply failed with code {rc}")
+    return True
+
+
 def in_apply(x: Feat, mr, y: Feat, act=ACT_NONE, res: Feat = None, xhat: torch.Tensor = None, q8=None):
     """y = act(IN(x)) [+ res].  q8 = (y8 Feat, q ptr, amax ptr): also the fp8 copy of y
     (irgan_in_apply_fp8; bf16, no xhat)."""
