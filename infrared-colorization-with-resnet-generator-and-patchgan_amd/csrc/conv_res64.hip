@@ -50,7 +50,7 @@ __global__ __launch_bounds__(512, 1) void conv_res64_kernel(const irgan_conv_des
                                                            const bf16_t* __restrict__ w,
                                                            const float* __restrict__ bias, bf16_t* __restrict__ y,
                                                            const bf16_t* __restrict__ mask, int ntn, int tpx,
-                                                           int tpy, float2* __restrict__ part) {
+                                                           int tpy, float2* __restrict__ part, int xcdg) {
     constexpr int TAPS = 9, HWd = PW + 2, HROWS = (PH + 2) * HWd, MI = 2, NJ = 4, Kw = TAPS * 64;
     static_assert(HROWS <= R64_HP * 8 && R64_HP * 8 - HROWS < 8, "halo pieces");
     __shared__ __attribute__((aligned(1024))) char smem[R64_LDS];
@@ -60,7 +60,19 @@ __global__ __launch_bounds__(512, 1) void conv_res64_kernel(const irgan_conv_des
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int nt = blockIdx.x % ntn, q0 = blockIdx.x / ntn, qs = gridDim.x / ntn;
+    // block -> (channel tile, patch sequence).  With gridDim % (8 ntn) == 0 the ntn tiles of one
+    // patch sequence sit on the same XCD (blocks b, b+8, ...: workgroups are dealt to the 8
+    // XCDs round-robin), so the second tile's halo reads hit the L2 the first one filled
+    int nt, q0;
+    const int qs = gridDim.x / ntn;
+    if (xcdg) {
+        const int x = blockIdx.x & 7, sl = blockIdx.x >> 3;
+        nt = sl % ntn;
+        q0 = (sl / ntn) * 8 + x;
+    } else {
+        nt = blockIdx.x % ntn;
+        q0 = blockIdx.x / ntn;
+    }
     const int P = d.N * tpy * tpx;
     const int n0 = nt * 64;
     const int nh = (R64_HP - wid + 7) >> 3;  // halo pieces of this wave: 6 (wave 0) or 5
@@ -308,9 +320,11 @@ void launch(const irgan_conv_desc* d, const void* x, const void* w, const float*
             float2* part, hipStream_t st) {
     const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH), ntn = d->Cout / 64;
     const int grid = grid_for(ntn, d->N * tpx * tpy * ntn);
+    static const int xg = getenv("IRGAN_RES64_NO_XCDG") ? 0 : 1;
+    const int xcdg = xg && ntn > 1 && grid % (8 * ntn) == 0;
 #define R64(ACCV, STV)                                                                                    \
     conv_res64_kernel<ACCV, STV><<<grid, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, (bf16_t*)y, \
-                                                       (const bf16_t*)mask, ntn, tpx, tpy, part)
+                                                       (const bf16_t*)mask, ntn, tpx, tpy, part, xcdg)
     if (part) R64(false, true);
     else if (d->accumulate) R64(true, false);
     else R64(false, false);
