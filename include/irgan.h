@@ -378,6 +378,15 @@ int irgan_ssim_eval_u8(const void* pred, const void* gt, int32_t N, int32_t H, i
 /* Version / capability probe (no GPU work). */
 int irgan_version(void);
 
+/* Deterministic mode (process-wide, default off).  On: every split-K weight gradient
+ * (wgrad_halo, wgrad_pc, wgrad_glds) reduces its partials through the caller's slab
+ * workspace in a fixed order, never through fp32 atomics, so a step gives bit-identical
+ * gradients run to run and under any stream schedule (torch's
+ * use_deterministic_algorithms analogue).  Off: the atomics are kept where they are
+ * faster (high split counts: up2 / down1-class layers at 256^2).  Loss VALUES are
+ * fp64 atomic block sums in either mode (they feed no gradient).  Returns the old value. */
+int irgan_set_deterministic(int32_t on);
+
 #ifdef __cplusplus
 }
 #endif

@@ -10,6 +10,9 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 #define IRGAN_HD __device__ __forceinline__
 
+// irgan_set_deterministic (conv.hip): host-side switch read by the split-K wgrad launchers
+int irgan_deterministic_mode();
+
 IRGAN_HD float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 // fp32 -> bf16, round to nearest even (NaN stays NaN): gfx950's v_cvt_pk_bf16_f32
 IRGAN_HD bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }

@@ -31,7 +31,7 @@ extern "C" int irgan_conv_wgrad_pc(const irgan_conv_desc* d, const void* x, cons
 extern "C" int irgan_conv_wgrad_narrow(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, float* ws,
                                        long ws_cap, hipStream_t st);
 extern "C" int irgan_conv_wgrad_glds(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, int splitk,
-                                     hipStream_t st);
+                                     hipStream_t st, float* ws, long ws_cap);
 
 namespace {
 
@@ -618,7 +618,7 @@ int launch_wgrad(const irgan_conv_desc* d, const void* x, const void* dy, float*
         }
         static const bool use_glds = !getenv("IRGAN_NO_GLDS");
         if (use_glds && fb && (d->Cout % 64 == 0 || d->Cout < 64) && d->ldy % 8 == 0 && d->yoff % 8 == 0)
-            return irgan_conv_wgrad_glds(d, x, dy, dw, splitk, st);
+            return irgan_conv_wgrad_glds(d, x, dy, dw, splitk, st, ws, ws_cap);
     }
     const int BM = d->Cout > 64 ? 128 : 64;
     const int tiles = irgan_cdiv(d->Cout, BM) * irgan_cdiv(K, 64);
@@ -707,6 +707,12 @@ extern "C" int irgan_weight_pack_batch(const irgan_pack_desc* descs, int32_t n, 
 }
 
 extern "C" int irgan_version(void) { return 1; }
+
+static int g_irgan_deterministic = 0;
+int irgan_deterministic_mode() { return __atomic_load_n(&g_irgan_deterministic, __ATOMIC_RELAXED); }
+extern "C" int irgan_set_deterministic(int32_t on) {
+    return __atomic_exchange_n(&g_irgan_deterministic, on ? 1 : 0, __ATOMIC_RELAXED);
+}
 
 // Split-K partial sums (no bias / activation / mask): partial ks of the
 // fp32 output lands at y + ks*split_stride.  Used for thin output domains

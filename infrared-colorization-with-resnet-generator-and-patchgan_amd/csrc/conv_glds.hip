@@ -230,7 +230,8 @@ template <int BMC, int BNC>  // co tile, ci tile (128 or 64)
 __global__ __launch_bounds__(512, 2) void conv_wgrad_glds_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
                                                                  const bf16_t* __restrict__ dy, float* __restrict__ dw,
                                                                  int kchunk, const bf16_t* __restrict__ zero,
-                                                                 int ntx, int nty, int swz) {
+                                                                 int ntx, int nty, int swz,
+                                                                 float* __restrict__ slab = nullptr) {
     constexpr int KP = 64, STAGES = 3;
     constexpr int RA = BMC * 2, RBB = BNC * 2;          // bytes per pixel row in each image
     constexpr int ABYTES = KP * RA, STAGE = ABYTES + KP * RBB;
@@ -328,6 +329,9 @@ __global__ __launch_bounds__(512, 2) void conv_wgrad_glds_kernel(const irgan_con
                                                                         acc[i][j], 0, 0, 0);
         }
     }
+    // split-K partials: plain stores into this split's slab (glds_slab_reduce sums them in
+    // a fixed order) or, without a slab, fp32 atomics into dw (order-dependent rounding)
+    float* const dst = slab ? slab + (long)bz * d.Cout * K : nullptr;
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -337,15 +341,30 @@ __global__ __launch_bounds__(512, 2) void conv_wgrad_glds_kernel(const irgan_con
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
                 const int kc = n0 + wn * (BNC / WN) + j * 16 + (lane & 15);
-                atomicAdd(dw + (long)co * K + kc, acc[i][j][r]);
+                if (dst) dst[(long)co * K + kc] = acc[i][j][r];
+                else atomicAdd(dw + (long)co * K + kc, acc[i][j][r]);
             }
         }
+}
+
+// dw[i] += sum over splits s (in order) of slab[s][i]: the deterministic second stage
+// of the slab split-K (every element sees the same summation order on every run)
+__global__ __launch_bounds__(256) void glds_slab_reduce(const float* __restrict__ slab, int splits, long n,
+                                                        float* __restrict__ dw) {
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n / 4; i += (long)gridDim.x * 256) {
+        float4 a = ((const float4*)dw)[i];
+        for (int s = 0; s < splits; ++s) {
+            const float4 v = ((const float4*)(slab + (long)s * n))[i];
+            a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+        }
+        ((float4*)dw)[i] = a;
+    }
 }
 
 }  // namespace
 
 extern "C" int irgan_conv_wgrad_glds(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, int splitk,
-                                     hipStream_t st) {
+                                     hipStream_t st, float* ws, long ws_cap) {
     const long P = (long)d->N * d->Ho * d->Wo;
     const int K = d->KH * d->KW * d->Cin;
     if (P <= 0) return 0;
@@ -374,13 +393,19 @@ extern "C" int irgan_conv_wgrad_glds(const irgan_conv_desc* d, const void* x, co
     const int nb = ntx * nty * splitk;
     const bf16_t* xp = (const bf16_t*)x;
     const bf16_t* dp = (const bf16_t*)dy;
+    const long n = (long)d->Cout * K;
+    float* slab = (ws && splitk > 1 && n % 4 == 0 && (long)splitk * n <= ws_cap) ? ws : nullptr;
     if (BMC == 128 && BNC == 128)
-        conv_wgrad_glds_kernel<128, 128><<<nb, 512, 0, st>>>(*d, xp, dp, dw, (int)kc, zero, ntx, nty, swz);
+        conv_wgrad_glds_kernel<128, 128><<<nb, 512, 0, st>>>(*d, xp, dp, dw, (int)kc, zero, ntx, nty, swz, slab);
     else if (BMC == 128)
-        conv_wgrad_glds_kernel<128, 64><<<nb, 512, 0, st>>>(*d, xp, dp, dw, (int)kc, zero, ntx, nty, swz);
+        conv_wgrad_glds_kernel<128, 64><<<nb, 512, 0, st>>>(*d, xp, dp, dw, (int)kc, zero, ntx, nty, swz, slab);
     else if (BNC == 128)
-        conv_wgrad_glds_kernel<64, 128><<<nb, 512, 0, st>>>(*d, xp, dp, dw, (int)kc, zero, ntx, nty, swz);
-    else conv_wgrad_glds_kernel<64, 64><<<nb, 512, 0, st>>>(*d, xp, dp, dw, (int)kc, zero, ntx, nty, swz);
+        conv_wgrad_glds_kernel<64, 128><<<nb, 512, 0, st>>>(*d, xp, dp, dw, (int)kc, zero, ntx, nty, swz, slab);
+    else conv_wgrad_glds_kernel<64, 64><<<nb, 512, 0, st>>>(*d, xp, dp, dw, (int)kc, zero, ntx, nty, swz, slab);
+    if (slab) {
+        const int blocks = (int)std::min<long>((n / 4 + 255) / 256, 2048);
+        glds_slab_reduce<<<blocks, 256, 0, st>>>(slab, splitk, n, dw);
+    }
     IRGAN_LAUNCH_CHECK();
     return 0;
 }

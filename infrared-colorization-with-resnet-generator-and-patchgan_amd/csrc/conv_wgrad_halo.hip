@@ -292,7 +292,9 @@ void launch_t(const irgan_conv_desc* d, const void* x, const void* dy, float* dw
     // slabs pay splitk*n*4 bytes twice (store + reduce); measured on MI355X they beat
     // fp32 atomics only at low split counts (resblock 3x3: 21 splits, -7 %), and
     // lose at 56-170 splits (down1 / up2 at 256^2: +3..12 %)
-    float* slab = (ws && splitk > 1 && splitk <= 24 && n % 4 == 0 && (long)splitk * n <= ws_cap) ? ws : nullptr;
+    // (deterministic mode: slabs at any split count)
+    float* slab = (ws && splitk > 1 && (splitk <= 24 || irgan_deterministic_mode()) && n % 4 == 0 &&
+                   (long)splitk * n <= ws_cap) ? ws : nullptr;
     wgrad_halo_kernel<BMC, KW, SX, WM, WN><<<tiles * splitk, WM * WN * 64, 0, st>>>(
         *d, (const bf16_t*)x, (const bf16_t*)dy, dw, spb, nseg, ntco, nci, zero, swz, slab);
     if (slab) {

@@ -832,6 +832,33 @@ def grad_allreduce(t: torch.Tensor, group=None) -> torch.Tensor:
     return t
 
 
+def replica_digest(tensors) -> torch.Tensor:
+    """Exact int64 digest of fp32 tensors (their bit patterns): a plain and a
+    position-weighted sum per tensor.  Equal digests on every rank = the data-parallel
+    replicas hold bit-identical parameters (bench.py's post-run check)."""
+    out = []
+    for t in tensors:
+        b = t.detach().reshape(-1).view(torch.int32).to(torch.int64)
+        w = torch.arange(b.numel(), device=b.device, dtype=torch.int64) % 65521 + 1
+        out += [b.sum(), (b * w).sum()]
+    return torch.stack(out)
+
+
+def replicas_identical(tensors, group=None) -> bool:
+    """True when every rank of ``group`` holds bit-identical ``tensors`` (max == min of
+    the digests over ranks); True without a process group."""
+    import torch.distributed as dist
+    d = replica_digest(tensors)
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return True
+    if dist.get_backend(group) != "nccl":
+        d = d.cpu()
+    hi, lo = d.clone(), d.clone()
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=group)
+    return bool(torch.equal(hi, lo))
+
+
 class BucketedAllreduce:
     """Mean of a flat gradient buffer over the ranks, reduced tail-first in buckets
     while the producing backward is still running (SURVEY.md 8e overlap schedule).

@@ -100,6 +100,7 @@ class Config:
         self.vgg_seed = 3
         self.log_every = 50
         self.test_batch = 16             # run_test: frames per generator call (the reference runs one)
+        self.deterministic = False       # ops.set_deterministic: bitwise-reproducible weight gradients
 
 
 # =============================================================================
@@ -295,7 +296,9 @@ class _GFn(torch.autograd.Function):
 
 class ResnetUNetGenerator(_StoreModule):
     """ir:425-569.  forward(x) -> (out, None).  Input (B, input_nc, H, W) in
-    [-1,1] on the HIP device, H and W divisible by 4."""
+    [-1,1] on the HIP device, any H, W >= 2: when H or W is not divisible by 4 the
+    decoder resizes the up-sampled map to the skip's size as the reference does
+    (ir:555-556, 562-563)."""
 
     def __init__(self, input_nc, output_nc, ngf=64, norm_layer=nn.InstanceNorm2d, use_dropout=False, n_blocks=9,
                  padding_type="reflect", no_antialias=False, no_antialias_up=False, device=None,
@@ -585,6 +588,8 @@ class GANTrainer:
         self.cfg = cfg
         dev = torch.device(cfg.device)
         dt = getattr(cfg, "compute_dtype", "bf16")
+        if getattr(cfg, "deterministic", False):
+            ops.set_deterministic(True)
         self.model = model or IRColorizationModel(cfg)
         self.netD = netD or init_net(NLayerDiscriminator(cfg.input_nc + cfg.output_nc, 64, 3,
                                                          get_norm_layer(cfg.norm), device=dev, compute_dtype=dt))

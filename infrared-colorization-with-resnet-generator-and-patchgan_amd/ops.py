@@ -42,6 +42,13 @@ def Pi(t, i):
     return ctypes.c_void_p(t.data_ptr() + i * t.element_size())
 
 
+def set_deterministic(on: bool) -> bool:
+    """Process-wide deterministic mode (irgan_set_deterministic): every split-K weight
+    gradient reduces through ordered slabs, so the step is bitwise reproducible under any
+    stream schedule.  Returns the previous setting."""
+    return bool(_lib.load().irgan_set_deterministic(int(bool(on))))
+
+
 class LaunchTimer:
     """Optional HIP-event timing of tagged conv launches (bench.py's live
     roofline).  Events are recorded on the launching stream around each launch."""
@@ -71,6 +78,15 @@ class LaunchTimer:
 
 
 TIMER = LaunchTimer(())
+
+
+def hbm_tag(kind, x: "Feat"):
+    """Tag of an HBM-bound pass over the NHWC tensor x (bench.py's GB/s lines)."""
+    return f"{kind}:b{x.N}@{x.H}x{x.W}x{x.C}"
+
+
+def _timed(kind, x, fn):
+    return TIMER.wrap(hbm_tag(kind, x), fn) if TIMER.enabled else fn()
 
 
 def conv_tag(kind, spec, x_hw, n=None):
@@ -416,9 +432,9 @@ def in_apply(x: Feat, mr, y: Feat, act=ACT_NONE, res: Feat = None, xhat: torch.T
                   res.ptr if res else None, res.ld if res else 0, res.off if res else 0, y.ptr, y.ld, y.off,
                   y8.ptr, y8.ld, y8.off, qp, ap, stream())
         return
-    _lib.call("irgan_in_apply", x.ptr, x.dt, x.N, x.H * x.W, x.C, x.ld, x.off, P(mr), act,
-              res.ptr if res else None, res.ld if res else 0, res.off if res else 0, y.ptr, y.ld, y.off, P(xhat),
-              stream())
+    _timed("in_apply_res" if res is not None else "in_apply", x, lambda: _lib.call(
+        "irgan_in_apply", x.ptr, x.dt, x.N, x.H * x.W, x.C, x.ld, x.off, P(mr), act, res.ptr if res else None,
+        res.ld if res else 0, res.off if res else 0, y.ptr, y.ld, y.off, P(xhat), stream()))
 
 
 def in_bwd_parts(dy: Feat, x: Feat, act: int, mr, work, red, dx: Feat, db=None, dy2: Feat = None, q8=None):
@@ -451,8 +467,8 @@ def in_backward(dy: Feat, x: Feat, act: int, mr, work, red, dx: Feat, db=None, d
     if nb:
         _lib.call("irgan_in_bwd_finalize", P(work), x.N, x.H * x.W, x.C, nb, P(red), stream())
     else:
-        reduce()
-    apply()
+        _timed("in_bwd_reduce", x, reduce)
+    _timed("in_bwd_apply", x, apply)
 
 
 _CS_WORK = {}

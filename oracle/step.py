@@ -349,7 +349,7 @@ def _trainable(P):
 
 
 def train_step(G, D, V, ir, rgb, optG, optD, lam=None, no_antialias=False,
-               no_antialias_up=False, n_blocks=9, grad_hook=None, fp8=False):
+               no_antialias_up=False, n_blocks=9, grad_hook=None, fp8=False, as_written=False):
     """One train step, minimal form of ir:1636-1681.
 
     D step: hinge on D(cat[ir,rgb]) and D(cat[ir,G(ir)]) (G detached), D Adam.
@@ -361,17 +361,25 @@ def train_step(G, D, V, ir, rgb, optG, optD, lam=None, no_antialias=False,
     ``grad_hook(name, grads)`` (name "D" or "G") may rewrite the grad dict in
     place before the Adam update -- the data-parallel tests use it to insert
     the product's gradient all-reduce.
+    ``as_written=True`` does the work of ir:1636-1681 exactly as written (the CPU
+    baseline's second leg): a separate no-grad G forward for the D step (ir:1638-1639),
+    a second G forward for the G step (ir:1657), and loss_G.backward() also producing
+    the (unused) D weight gradients, since D's parameters still require grad (ir:1680).
+    Same values, more work.
     """
     lam = dict(LAMBDAS, **(lam or {}))
     out = {}
     gk = {k: G[k].detach().clone().requires_grad_(k in _trainable(G)) for k in G}
+    if as_written:
+        with torch.no_grad():
+            fake_d = g_forward(gk, ir, no_antialias, no_antialias_up, n_blocks, fp8=fp8)
     fake = g_forward(gk, ir, no_antialias, no_antialias_up, n_blocks, fp8=fp8)
     out["fake"] = fake.detach().clone()
 
     # ---- D step (ir:1636-1651)
     dk = {k: D[k].detach().clone().requires_grad_(True) for k in D}
     pred_real = d_forward(dk, torch.cat([ir, rgb], 1))
-    pred_fake = d_forward(dk, torch.cat([ir, fake.detach()], 1))
+    pred_fake = d_forward(dk, torch.cat([ir, (fake_d if as_written else fake).detach()], 1))
     loss_D = 0.5 * (F.relu(1.0 - pred_real).mean() + F.relu(1.0 + pred_fake).mean())
     gD = torch.autograd.grad(loss_D, [dk[k] for k in D])
     out.update(pred_real=pred_real.detach(), pred_fake=pred_fake.detach(), loss_D=loss_D.detach())
@@ -381,7 +389,8 @@ def train_step(G, D, V, ir, rgb, optG, optD, lam=None, no_antialias=False,
     adam_update(D, out["gradD"], optD)
 
     # ---- G step (ir:1656-1681), D frozen at its updated weights
-    pred_fake_G = d_forward(D, torch.cat([ir, fake], 1))
+    dg = {k: D[k].detach().clone().requires_grad_(True) for k in D} if as_written else D
+    pred_fake_G = d_forward(dg, torch.cat([ir, fake], 1))
     l_gan = -pred_fake_G.mean()
     l_l1 = (fake - rgb).abs().mean() * lam["lambda_L1"]
     l_perc = (vgg_features(V, fake) - vgg_features(V, rgb)).abs().mean() * lam["lambda_perc"]
@@ -389,7 +398,10 @@ def train_step(G, D, V, ir, rgb, optG, optD, lam=None, no_antialias=False,
     l_ssim = ssim_loss((fake + 1.0) / 2.0, (rgb + 1.0) / 2.0) * lam["lambda_ssim"]
     loss_G = lam["lambda_gan"] * l_gan + l_l1 + l_perc + l_tv + l_ssim
     keys = _trainable(G)
-    gG = torch.autograd.grad(loss_G, [gk[k] for k in keys])
+    if as_written:   # loss_G.backward() also fills D's .grad (ir:1680); discarded
+        gG = torch.autograd.grad(loss_G, [gk[k] for k in keys] + [dg[k] for k in D])[:len(keys)]
+    else:
+        gG = torch.autograd.grad(loss_G, [gk[k] for k in keys])
     out.update(pred_fake_G=pred_fake_G.detach(), loss_G=loss_G.detach(), loss_G_GAN=l_gan.detach(),
                loss_G_L1=l_l1.detach(), loss_G_perc=l_perc.detach(), loss_G_TV=l_tv.detach(),
                loss_G_ssim=l_ssim.detach())

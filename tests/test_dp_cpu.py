@@ -90,8 +90,17 @@ def _worker(rank, port, outdir):
                            grad_hook=_flat_hook(engine))
         val = irc.validate_kaist(lambda x: x.repeat(1, 3, 1, 1) * 0.5, vl, "cpu")
         nval = sum(b["ir"].shape[0] for b in vl)
+        # bench.py's post-run replica check: identical after the step, and a one-ulp
+        # difference on one rank is caught on every rank
+        params = [G[k] for k in G] + [D[k] for k in D]
+        same = engine.replicas_identical(params)
+        bumped = [t.clone() for t in params]
+        if rank == 1:
+            bumped[3].view(-1)[7] = torch.nextafter(bumped[3].view(-1)[7], torch.tensor(1e9, dtype=torch.float64))
+        caught = not engine.replicas_identical(bumped)
         torch.save({"idx": batch["idx"].tolist(), "G": G, "D": D, "loss_D": out["loss_D"],
-                    "loss_G": out["loss_G"], "val": val, "nval": nval, "ntrain": len(tl)},
+                    "loss_G": out["loss_G"], "val": val, "nval": nval, "ntrain": len(tl),
+                    "replicas_same": same, "replica_diff_caught": caught},
                    os.path.join(outdir, f"rank{rank}.pt"))
     finally:
         dist.destroy_process_group()
@@ -115,6 +124,7 @@ def test_dp_two_ranks_match_single_process(tmp_path):
     rgb = torch.stack([ds[i]["rgb"] for i in idx]).double()
     G, D, V = _params()
     ref = O.train_step(G, D, V, ir, rgb, O.AdamState(G), O.AdamState(D))
+    assert all(r["replicas_same"] and r["replica_diff_caught"] for r in res)
     for r in res:   # replicas stay identical and equal the global-batch step
         for name, P in (("G", G), ("D", D)):
             for k in P:

@@ -221,7 +221,8 @@ def _fp8_oracle(ir, rgb, lam, fp8=True):
     return O.train_step(G, D, V, ir, rgb, O.AdamState(G), O.AdamState(D), lam=lam, fp8=fp8)
 
 
-def test_fp8_step_vs_fp8_oracle():
+@pytest.mark.parametrize("size", [64, 256])
+def test_fp8_step_vs_fp8_oracle(size):
     """BASELINE config 5's step (compute_dtype "fp8") against the CPU oracle run with
     the same fp8 quantisation of the ResnetBlock conv operands (oracle.step.fp8_q /
     _Fp8ResConv, fp32 elsewhere), on the first step (the delayed scales are then
@@ -231,7 +232,7 @@ def test_fp8_step_vs_fp8_oracle():
     same fp8 oracle gets (the bf16 engine is held to that rule in test_gpu_step.py;
     e4m3 rounding turns bf16-level input differences into fp8-level output ones,
     measured: 0.047 mean |err| of the output against 0.053 between the fp8 and the
-    plain oracle)."""
+    plain oracle).  At 64x64 and at config 5's own resolution 256x256 (B=2)."""
     import numpy as np
     from conftest import load_golden
     from oracle import step as O
@@ -241,8 +242,8 @@ def test_fp8_step_vs_fp8_oracle():
     tr, cfg = make_trainer(fx, "fp8")
     assert tr.netG.engine.fp8
     g = torch.Generator().manual_seed(41)
-    ir = torch.rand(2, 1, 64, 64, generator=g) * 2 - 1
-    rgb = torch.rand(2, 3, 64, 64, generator=g) * 2 - 1
+    ir = torch.rand(2, 1, size, size, generator=g) * 2 - 1
+    rgb = torch.rand(2, 3, size, size, generator=g) * 2 - 1
     d = tr.losses(tr.step(ir.to(DEV), rgb.to(DEV)))
     o = _fp8_oracle(ir, rgb, lam)
     o_nofp8 = _fp8_oracle(ir, rgb, lam, fp8=False)

@@ -67,3 +67,81 @@ def test_bf16_step_with_fused_in_bwd_vs_oracle():
         test_gpu_step.test_bf16_step_256_vs_oracle_and_b16_finite()
     finally:
         eng.INLayer.fused_in_bwd = old
+
+
+def test_fused_in_bwd_step_divergence_is_summation_order():
+    """the bf16 step's G grads with the fused reduce differed from the
+    separate-pass step by 5.5e-3 rel-L2 (gpurun_out/r02_fib2).  Source of that difference:
+    three runs of the same bf16 step (256^2 -> 64^2 resblocks, B=2):
+      (a) separate reduce passes (the default),
+      (b) the fused reduce in the dgrad epilogue + ring (irgan_conv_dgrad_in_stats),
+      (c) the separate passes with the reduce's statistics (mean g, mean g*xhat) computed
+          EXACTLY (fp64 on the same bf16 operands) instead of by fp32 partial sums.
+    If (b) carried a wrong partial row (e.g. a ring row counted twice or missed), it would
+    sit far from (c) while (a) sits close; if the difference is fp32 summation order
+    amplified through bf16 re-rounding and 18 IN layers, (a) and (b) are equally far
+    from (c).  Asserted: |b - c| <= 3 |a - c| + 1e-4, per network tensor group."""
+    m = pkg()
+    eng, ops = m.engine, m.ops
+    B, H = 2, 256
+
+    def exact_in_backward(dy, x, act, mr, work, red, dx, db=None, dy2=None, q8=None, nb=0):
+        N, C = x.N, x.C
+        z = x.t[..., x.off:x.off + C].reshape(N, -1, C)
+        mm = mr.view(N, 1, C, 2)
+        xh32 = (z.float() - mm[..., 0]) * mm[..., 1]          # the kernels' fp32 xhat
+        g = dy.t[..., dy.off:dy.off + C].reshape(N, -1, C).double()
+        if dy2 is not None:
+            g = g + dy2.t[..., dy2.off:dy2.off + C].reshape(N, -1, C).double()
+        if act == ops.ACT_RELU:
+            g = g * (xh32 > 0)
+        elif act == ops.ACT_LRELU:
+            g = g * torch.where(xh32 > 0, 1.0, 0.2).double()
+        r = torch.stack([g.mean(1), (g * xh32.double()).mean(1)], dim=-1)   # N, C, 2
+        red[:2 * N * C].copy_(r.reshape(-1).float())
+        _, apply = ops.in_bwd_parts(dy, x, act, mr, work, red, dx, db, dy2, q8)
+        apply()
+
+    def run(fused, exact=False):
+        eng.INLayer.fused_in_bwd = fused
+        saved = eng.ops.in_backward
+        if exact:
+            eng.ops.in_backward = exact_in_backward
+        try:
+            cfg = m.Config()
+            cfg.device, cfg.batch_size, cfg.img_size = "cuda:0", B, H
+            tr = m.GANTrainer(cfg)
+            tr.netG.store.load(m.seeded_state(m.g_param_shapes(), 0), strict=True)
+            tr.netD.store.load(m.seeded_state(m.d_param_shapes(), 1), strict=True)
+            for mod in (tr.netG, tr.netD, tr.vgg):
+                mod.repack()
+            g = torch.Generator().manual_seed(3)
+            ir = (torch.rand(B, 1, H, H, generator=g) * 2 - 1).cuda()
+            rgb = (torch.rand(B, 3, H, H, generator=g) * 2 - 1).cuda()
+            tr.step(ir, rgb)
+            torch.cuda.synchronize()
+            return tr.netG.store.grad.clone(), tr.netG.store
+        finally:
+            eng.ops.in_backward = saved
+
+    old = eng.INLayer.fused_in_bwd
+    try:
+        ga, st = run(False)
+        gb, _ = run(True)
+        gc, _ = run(False, exact=True)
+    finally:
+        eng.INLayer.fused_in_bwd = old
+    rel = lambda u, v: ((u - v).norm() / v.norm().clamp_min(1e-30)).item()   # noqa: E731
+    print(f"whole G grad: separate vs exact {rel(ga, gc):.3e}, fused vs exact {rel(gb, gc):.3e}, "
+          f"fused vs separate {rel(gb, ga):.3e}")
+    groups = {"resblocks": [], "encoder": [], "decoder": []}
+    for k in st.shapes:
+        o, n = st.offsets[k], st.krsc(k).numel()
+        grp = "resblocks" if k.startswith("resblocks") else ("encoder" if k.startswith(("inc", "down")) else "decoder")
+        groups[grp].append((o, n))
+    for grp, spans in groups.items():
+        idx = torch.cat([torch.arange(o, o + n, device=ga.device) for o, n in spans])
+        a, b, c = ga[idx], gb[idx], gc[idx]
+        ea, eb = rel(a, c), rel(b, c)
+        print(f"{grp}: separate vs exact {ea:.3e}, fused vs exact {eb:.3e}")
+        assert eb <= 3 * ea + 1e-4, (grp, ea, eb)

@@ -180,12 +180,34 @@ def test_generator_module_api_and_checkpoint_layout(tmp_path):
         assert err < 5e-3, (k, err)
 
 
+def _grads_vs_oracle(tr, o, oac):
+    """G / D weight grads (rel-L2 against the fp32 oracle ``o``) no further than 1.5x + 0.02
+    what PyTorch's bf16 autocast of the same oracle step (``oac``) gets."""
+    pre_in = set(O.pre_in_bias_keys(list(o["gradG"]) + list(o["gradD"])))
+    for store, tag in ((tr.netG.store, "gradG"), (tr.netD.store, "gradD")):
+        for k, gr in o[tag].items():
+            if k in pre_in:
+                continue
+            den = gr.double().norm().clamp_min(1e-30)
+            got = store.oihw(k, store.grad).cpu().double()
+            e = float((got - gr.double()).norm() / den)
+            e_ac = float((oac[tag][k].double() - gr.double()).norm() / den)
+            print("grad rel-L2", tag, k, round(e, 4), "autocast-bf16", round(e_ac, 4))
+            assert np.isfinite(e) and e <= 1.5 * e_ac + 0.02, (tag, k, e, e_ac)
+
+
 def test_kaist_native_resolution_512x640():
-    """BASELINE config 4 shape (512x640, KAIST native): W/4 = 160 is not a
-    multiple of 64, so the wgrad row-segment kernel and several tile paths take
-    their general branches.  G forward (fp32) vs the CPU oracle, and a bf16
-    train step at batch 4 vs the fp32 step on the same inputs and weights."""
+    """BASELINE config 4 at its own resolution (512x640, KAIST native): W/4 = 160 is not
+    a multiple of 64, so the wgrad row-segment kernel and several tile paths take their
+    general branches.
+    (a) G forward (fp32 parity mode) vs the CPU oracle.
+    (b) The benchmarked bf16 step at 512x640, B=1 against the fp32 CPU oracle on the same
+        seeded inputs and weights, with the bf16 rule of test_bf16_step_256_vs_oracle_...:
+        losses <= 3e-2 rel, G output mean |err| <= 1e-2, G / D weight grads within 1.5x +
+        0.02 of PyTorch's own bf16 autocast error on the same oracle step.
+    (c) The config's per-GPU batch (B=4): one bf16 step, everything finite."""
     fx = load_golden("s32")
+    lam = dict(zip(LAMBDA_ORDER, (float(v) for v in fx["lambdas"])))
     g = torch.Generator().manual_seed(21)
     ir = torch.rand(4, 1, 512, 640, generator=g) * 2 - 1
     rgb = torch.rand(4, 3, 512, 640, generator=g) * 2 - 1
@@ -195,12 +217,29 @@ def test_kaist_native_resolution_512x640():
     with torch.no_grad():
         ref = O.g_forward(G, ir[:1])
     assert float((fake.cpu().permute(0, 3, 1, 2) - ref).abs().max()) < 1e-4
-    l32 = tr32.losses(tr32.step(ir.to(DEV), rgb.to(DEV)))
+    del tr32
+    # (b) bf16 step, B = 1, vs the oracle
     tr16, _ = make_trainer(fx, "bf16")
-    l16 = tr16.losses(tr16.step(ir.to(DEV), rgb.to(DEV)))
-    for k in ("loss_D", "loss_G", "loss_G_L1", "loss_G_perc", "loss_G_ssim"):
-        assert np.isfinite(l16[k]) and np.isfinite(l32[k]), k
-        assert abs(l16[k] - l32[k]) <= 3e-2 * max(1.0, abs(l32[k])), (k, l16[k], l32[k])
+    d = tr16.losses(tr16.step(ir[:1].to(DEV), rgb[:1].to(DEV)))
+    o = _oracle(torch.float32, ir[:1], rgb[:1], lam)
+    for k in ("loss_D", "loss_G", "loss_G_L1", "loss_G_perc", "loss_G_ssim", "loss_G_GAN"):
+        r = float(o[k])
+        assert abs(d[k] - r) <= 3e-2 * max(1.0, abs(r)), (k, d[k], r)
+    err = (tr16.netG.engine.bufs.d["fake"].permute(0, 3, 1, 2).cpu() - o["fake"]).abs()
+    print("bf16 512x640 B=1: fake mean/max err", err.mean().item(), err.max().item())
+    assert err.mean() <= 1e-2, err.mean()
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        oac = _oracle(torch.float32, ir[:1], rgb[:1], lam)
+    _grads_vs_oracle(tr16, o, oac)
+    del tr16
+    # (c) B = 4
+    t4, _ = make_trainer(fx, "bf16")
+    l4 = t4.losses(t4.step(ir.to(DEV), rgb.to(DEV)))
+    assert all(np.isfinite(v) for v in l4.values()), l4
+    f4 = t4.netG.engine.bufs.d["fake"]
+    assert torch.isfinite(f4).all() and f4.abs().max() <= 1.0
+    for st in (t4.netG.store, t4.netD.store):
+        assert torch.isfinite(st.grad).all() and torch.isfinite(st.flat).all()
 
 
 def _seeded_trainer(irc, seed_shift=0):
@@ -360,17 +399,7 @@ def test_bf16_step_256_vs_oracle_and_b16_finite():
     assert err.mean() <= 1e-2, err.mean()
     with torch.autocast("cpu", dtype=torch.bfloat16):
         oac = _oracle(torch.float32, ir, rgb, lam)
-    pre_in = set(O.pre_in_bias_keys(list(o["gradG"]) + list(o["gradD"])))
-    for store, tag in ((tr.netG.store, "gradG"), (tr.netD.store, "gradD")):
-        for k, gr in o[tag].items():
-            if k in pre_in:
-                continue
-            den = gr.double().norm().clamp_min(1e-30)
-            got = store.oihw(k, store.grad).cpu().double()
-            e = float((got - gr.double()).norm() / den)
-            e_ac = float((oac[tag][k].double() - gr.double()).norm() / den)
-            print("grad rel-L2", tag, k, round(e, 4), "autocast-bf16", round(e_ac, 4))
-            assert e <= 1.5 * e_ac + 0.02, (tag, k, e, e_ac)
+    _grads_vs_oracle(tr, o, oac)
     # (b) B = 16
     g = torch.Generator().manual_seed(32)
     ir = (torch.rand(16, 1, 256, 256, generator=g) * 2 - 1).to(DEV)
@@ -387,3 +416,51 @@ def test_bf16_step_256_vs_oracle_and_b16_finite():
         assert np.isfinite(l16[k]), k
         if k != "loss_G_TV":
             assert abs(l16[k] - l32[k]) <= 3e-2 * max(1.0, abs(l32[k])), (k, l16[k], l32[k])
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp8"])
+def test_stream_overlap_schedule_bit_identical(monkeypatch, dtype):
+    """The default step runs the VGG real half, the D step, D Adam and the GAN-term D pass
+    on a side stream, joined to the main stream by events (GANStep.step).  In deterministic
+    mode (ops.set_deterministic: every split-K weight gradient reduced through ordered
+    slabs, no fp32 atomics) every kernel is run-to-run reproducible and the shared
+    workspaces are per stream, so the overlapped schedule must give BIT-IDENTICAL grads,
+    parameters and Adam moments to the single-stream one (IRGAN_NO_D_OVERLAP=1,
+    IRGAN_NO_VGG_OVERLAP=1) over three steps: a missed wait would show up here.
+    Loss values are fp64 atomic block sums (order-dependent): compared to 1e-12 rel."""
+    fx = load_golden("s64")
+    g = torch.Generator().manual_seed(51)
+    batches = [((torch.rand(2, 1, 128, 128, generator=g) * 2 - 1).to(DEV),
+                (torch.rand(2, 3, 128, 128, generator=g) * 2 - 1).to(DEV)) for _ in range(3)]
+    ops = pkg().ops
+
+    def run(overlap):
+        for k in ("IRGAN_NO_D_OVERLAP", "IRGAN_NO_VGG_OVERLAP"):
+            if overlap:
+                monkeypatch.delenv(k, raising=False)
+            else:
+                monkeypatch.setenv(k, "1")
+        tr, _ = make_trainer(fx, dtype)
+        assert (tr.core.side is not None) == overlap
+        losses = []
+        for ir, rgb in batches:
+            losses.append(tr.losses(tr.step(ir, rgb)))
+        torch.cuda.synchronize()
+        return tr, losses
+
+    old = ops.set_deterministic(True)
+    try:
+        ta, la = run(True)
+        tb, lb = run(False)
+        tc, _ = run(True)            # the same schedule twice: reproducible at all?
+    finally:
+        ops.set_deterministic(old)
+    for x, y in zip(la, lb):
+        for k in x:
+            assert abs(x[k] - y[k]) <= 1e-12 * max(1.0, abs(y[k])), (k, x[k], y[k])
+    for name in ("netG", "netD"):
+        sa, sb, sc = getattr(ta, name).store, getattr(tb, name).store, getattr(tc, name).store
+        assert torch.equal(sa.grad, sc.grad), f"{name}: deterministic mode is not reproducible run to run"
+        assert torch.equal(sa.grad, sb.grad), f"{name} grads differ between the schedules"
+        assert torch.equal(sa.flat, sb.flat), f"{name} params differ between the schedules"
+        assert torch.equal(sa.m, sb.m) and torch.equal(sa.v, sb.v), f"{name} Adam moments differ"

@@ -126,3 +126,30 @@ def test_ssim_oracle_matches_skimage_golden():
             assert abs(got - want) < 1e-12, (k, got, want)
         k += 1
     assert k == 3 and fx["ssim0"][1] == 1.0
+
+
+def test_oracle_as_written_equals_minimal_step():
+    """oracle.step.train_step(as_written=True) (bench.py's second CPU-baseline leg: the
+    reference's own ir:1636-1681 order with two G forwards and D grads from loss_G) gives
+    the same losses, grads and post-step parameters as the minimal step (fp64)."""
+    import torch
+    from oracle import step as O
+    g = torch.Generator().manual_seed(2)
+    ir = torch.rand(2, 1, 32, 32, generator=g, dtype=torch.float64) * 2 - 1
+    rgb = torch.rand(2, 3, 32, 32, generator=g, dtype=torch.float64) * 2 - 1
+    outs = []
+    for aw in (False, True):
+        G = {k: v.double() for k, v in O.seeded_params(O.g_param_shapes(), 1, bias_std=0.02).items()}
+        D = {k: v.double() for k, v in O.seeded_params(O.d_param_shapes(), 2, bias_std=0.02).items()}
+        V = {k: v.double() for k, v in O.seeded_params(O.vgg_param_shapes(), 3, kaiming=True).items()}
+        o = O.train_step(G, D, V, ir, rgb, O.AdamState(G), O.AdamState(D), as_written=aw)
+        outs.append((o, G, D))
+    (a, Ga, Da), (b, Gb, Db) = outs
+    for k in ("loss_D", "loss_G", "loss_G_GAN", "loss_G_L1", "loss_G_perc", "loss_G_TV", "loss_G_ssim"):
+        assert abs(float(a[k]) - float(b[k])) <= 1e-12 * max(1.0, abs(float(a[k]))), k
+    for tag in ("gradG", "gradD"):
+        for k in a[tag]:
+            assert torch.allclose(a[tag][k], b[tag][k], rtol=1e-10, atol=1e-14), (tag, k)
+    for P, Q in ((Ga, Gb), (Da, Db)):
+        for k in P:
+            assert torch.equal(P[k], Q[k]) or torch.allclose(P[k], Q[k], rtol=1e-12, atol=1e-15), k
