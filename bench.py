@@ -145,6 +145,8 @@ def main():
     ap.add_argument("--batch", type=int, default=16, help="per-GPU batch")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp8"],
                     help="fp8: BASELINE configs[4] -- the ResnetBlock convs on e4m3 operands (use --batch 32)")
+    ap.add_argument("--kernel-steps", type=int, default=5,
+                    help="steps after the timed region with per-kernel HIP events (roofline lines)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds per CPU thread-count run")
     args = ap.parse_args()
@@ -192,8 +194,10 @@ def main():
     hbm_bytes = {ops.hbm_tag("in_bwd_reduce", rb): 4, ops.hbm_tag("in_bwd_apply", rb): 6,
                  ops.hbm_tag("in_apply", rb): 4, ops.hbm_tag("in_apply_res", rb): 6}   # bytes per element
     ops.TIMER.tags = set(res_tags) | set(hbm_bytes)
-    ops.TIMER.enabled = True
-    # per-step HIP events (no host sync inside the timed region) for the median
+    # per-step HIP events (no host sync inside the timed region) for the median; the
+    # per-kernel events of the roofline are recorded in the --kernel-steps steps right
+    # after it (an event record between two launches is a ~5-10 us bubble on the stream:
+    # around every tagged launch it would inflate the timed step by ~0.5 ms)
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
     evs[0].record()
@@ -205,6 +209,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    # per-kernel HIP events on the launching streams, same inputs, right after the timed region
+    ops.TIMER.enabled = True
+    for _ in range(args.kernel_steps):
+        tr.step(ir, rgb)
+    torch.cuda.synchronize()
     ops.TIMER.enabled = False
     el_min = el
     replicas_ok = True
@@ -269,6 +278,9 @@ def main():
                          "traffic_unit": "HBM bytes per launch (rocprofv3 PMC: 2*FETCH_SIZE + WRITE_SIZE, "
                                          "profiles/r02_pmc_traffic.json)",
                          "flop_per_launch": res_flop, "per_kernel": kern,
+                         "kernel_timing": f"HIP events around each tagged launch on its stream, {args.kernel_steps} "
+                                          "steps right after the timed region (same process, inputs and "
+                                          "buffers); the timed region itself carries no per-kernel events",
                          "hbm_kernels": hbm,
                          "hbm_note": "InstanceNorm passes at the resblock shape, HIP events on the launching "
                                      "stream; alg_bytes = bf16 bytes read + written once (in_bwd_reduce: dy, z; "

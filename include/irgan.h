@@ -261,6 +261,14 @@ int irgan_reflect_ring_fold(const float* rows, const float* cols, int32_t nsplit
  * border pixel of dx (one owner per pixel, no atomics). */
 int irgan_reflect_dgrad_ring(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p, void* dx,
                              irgan_stream_t s);
+/* The whole backward-data of a reflect-padded stride-1 conv (ir:381-392, 401-411): the
+ * interior correlation and the fold of its pad ring (d, w, p as irgan_reflect_dgrad_ring).
+ * ResnetBlock shapes (bf16, 3x3, p = 1, dY channels % 64, dx channels % 256, H and W
+ * multiples of 16 and >= 32, no mask / activation) run as ONE conv_pp launch with the
+ * ring folded into its border patches (every dx pixel rounded once); other shapes run
+ * irgan_conv_fwd + irgan_reflect_dgrad_ring (IRGAN_NO_RING_FOLD=1 forces that pair). */
+int irgan_conv_dgrad_reflect(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p, void* dx,
+                             irgan_stream_t s);
 /* out = (Wy (x) Wx) in on NHWC slices, tables from irgan_resample_table (device
  * copies, rows [Hout][Ty] and [Wout][Tx]: the host may drop trailing all-zero
  * tap columns); accumulate: out += result.  Downsample / UpsampleAA forward
@@ -326,6 +334,10 @@ int irgan_tv(const float* x, int32_t N, int32_t H, int32_t W, int32_t C, float w
  * grad wrt a accumulated into g.  work: 10*N*H*W*C floats of scratch. */
 int irgan_ssim(const float* a, const float* b, int32_t N, int32_t H, int32_t W, int32_t C, float w,
                float* g, double* loss, float* work, irgan_stream_t s);
+/* irgan_ssim with ssim_loss_torch's window_size (ir:714-736): any odd size 1..15
+ * (Gaussian sigma 1.5, zero padding window / 2); IRGAN_EUNSUPPORTED otherwise. */
+int irgan_ssim_ws(const float* a, const float* b, int32_t N, int32_t H, int32_t W, int32_t C, float w,
+                  float* g, double* loss, float* work, int32_t window, irgan_stream_t s);
 
 /* ---- optimizer (torch.optim.Adam, ir:1601-1604) over a flat fp32 buffer ---- */
 /* step_size = lr/(1-beta1^t), bc2_sqrt = sqrt(1-beta2^t) (host, fp64 -> fp32). */
@@ -361,6 +373,15 @@ int irgan_area_resize_u8(const void* src, int32_t N, int32_t Hin, int32_t Win, i
                          const int32_t* yptr, const int32_t* ysrc, const float* yw, int32_t Hout,
                          const int32_t* xptr, const int32_t* xsrc, const float* xw, int32_t Wout,
                          const void* flip, void* out_u8, int32_t* img_max, irgan_stream_t s);
+/* cv2.resize(INTER_AREA) when an axis UPscales (img_size above the source, ir:818,
+ * 1139, 1156): OpenCV's linear resampler with area-mode coefficients in 8-bit fixed
+ * point.  Tables (data.linear_area_table): yofs [Hout], ycoef [Hout][2], xofs [Wout],
+ * xcoef [Wout][2] (int, x 2048), xlim = first destination column with a single tap.
+ * Layouts, flip and img_max as irgan_area_resize_u8. */
+int irgan_linear_area_resize_u8(const void* src, int32_t N, int32_t Hin, int32_t Win, int32_t C,
+                                int64_t img_stride, const int32_t* yofs, const int32_t* ycoef, int32_t Hout,
+                                const int32_t* xofs, const int32_t* xcoef, int32_t xlim, int32_t Wout,
+                                const void* flip, void* out_u8, int32_t* img_max, irgan_stream_t s);
 /* out[n][i] = float32(in[n][i]) / 255 * 2 - 1 for per_image bytes per image (the
  * [-1, 1] tensors of ir:1157, 1175-1176); max_rule = 1: the IR rule of ir:1142 --
  * images whose img_max[n] <= 1 are not divided by 255. */
@@ -376,6 +397,13 @@ int irgan_ssim_eval_u8(const void* pred, const void* gt, int32_t N, int32_t H, i
                        double* work, int64_t work_cap, double* ssim, irgan_stream_t s);
 
 /* Version / capability probe (no GPU work). */
+/* nn.Dropout(p) in training mode (ResnetBlock use_dropout, ir:394-395) on NHWC slices:
+ * y = keep ? x / (1 - p) : 0, keep decided per element (pixel * C + channel) by a
+ * counter-based hash of seed; the backward is the same call on the gradient (same seed).
+ * x and y may alias. */
+int irgan_dropout(const void* x, int32_t xdt, int32_t P, int32_t C, int32_t ldx, int32_t xoff, void* y,
+                  int32_t ydt, int32_t ldy, int32_t yoff, uint64_t seed, float p, irgan_stream_t s);
+
 int irgan_version(void);
 
 /* Deterministic mode (process-wide, default off).  On: every split-K weight gradient

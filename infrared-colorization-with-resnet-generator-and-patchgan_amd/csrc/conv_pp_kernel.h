@@ -1,0 +1,721 @@
+// bf16 / fp8 stride-1 convolution kernel template (conv_pp_kernel), shared by conv_pp.hip
+// (forward, backward-data, fused statistics) and conv_pp_ring.hip (the reflect-pad
+// backward-data with its ring folded in).  Design notes:
+//
+// bf16 stride-1 convolution, resident input halo, ping-pong wave groups.
+//
+// Same operand staging as conv_halo.hip (a block owns a 16x16 output patch of
+// one image; per 64-channel chunk the (16+KH-1)x(16+KW-1) input halo is DMA'd
+// into LDS once and every tap is an LDS row shift of it; the weight tile of a
+// K-step = one tap x 64 channels streams through a 2-stage ring), but the
+// schedule is built for MFMA occupancy at one block per CU:
+//
+//  * block tile 256 pixels x 256 output channels, 8 waves = 2 groups x 4 waves;
+//    group g owns patch rows [8g, 8g+8), wave wn owns channels [64wn, 64wn+64):
+//    a 128 x 64 wave tile (8 x 4 fragments of mfma_f32_16x16x32_bf16), so a
+//    32-deep sub-step is 12 ds_read_b128 per 32 MFMAs (narrower channel tiles
+//    split the group's rows instead, see PP<BN>);
+//  * each sub-step (one tap, 32 channels) is two phases per wave: READ (issue
+//    the 12 fragment reads and this wave's share of the next K-step's DMA) and
+//    MFMA (32 MFMAs), each closed by a block barrier.  Group 1 starts one
+//    barrier late, so in every barrier window one group multiplies while the
+//    other reads: each SIMD holds one wave of each group;
+//  * taps are compile-time (KH, KW template); the K-step loop keeps its
+//    chunk / tap counters in scalars, so a phase costs a few SALU ops plus
+//    4 VALU per swizzled fragment address;
+//  * the MFMA computes C^T (weights are the A operand): a lane's 4 accumulator
+//    rows are 4 consecutive output channels of one pixel, so the epilogue
+//    stages bf16 [pixel][channel] rows with 8-byte LDS writes in one pass and
+//    stores 16-byte runs.
+//
+// DMA ordering: K-step k's weights sit in stage k&1 and are read in windows
+// 4k..4k+3 (group 0: 4k, 4k+2; group 1: 4k+1, 4k+3).  W(k+1) is issued in each
+// wave's first READ of step k (that stage was last read in window 4k-1) and is
+// retired by every wave with a counted vmcnt before the barrier closing window
+// 4k+3.  The halo of chunk c+1 is issued after W(k+1) at the first tap of chunk
+// c (its buffer last served chunk c-1).  Reads need no lgkmcnt wait before
+// their barrier except group 1's last READ of a K-step (window 4k+3): the next
+// window may overwrite that stage; every other READ is consumed by the same
+// wave's MFMA phase before any DMA can target its buffer.
+//
+// fp8 (F8, irgan_conv_fwd_fp8): the same kernel on OCP e4m3 operands.  A K-step
+// is one tap x 128 channels (a 128-byte halo / weight row, so every DMA, LDS
+// image and barrier window is byte-for-byte the bf16 schedule); its MFMA is
+// mfma_scale_f32_16x16x128_f8f6f4 (unit block scales: 2x the bf16 rate), a
+// fragment is 32 bytes (chunks g and g+4 of the row for lane group g, the same
+// channels for both operands), and the sub-steps of a K-step split the wave's
+// pixel fragments instead of the channels (sub-step 0 also reads the weight
+// fragments, which stay in registers for the others); at 8 pixel fragments a
+// K-step has 4 sub-steps (8 barrier windows), so the operand registers stay at
+// the bf16 kernel's 48.  The per-tensor
+// scales are undone in the epilogue: y = acc * (dqx[0] * dqw[0]) + bias.
+//
+// Preconditions (checked by irgan_conv_fwd_pp): bf16, sy = sx = 1, Cin % 64 == 0,
+// (KH, KW) in {(3,3), (4,4)}, ldx, xoff % 8 == 0, Cout % 256 == 0 (channel
+// tiles of 256), no tanh epilogue, input slice and weights < 2^30 elements (byte offsets
+// below the buffer-resource out-of-range marker 2^31).
+
+#pragma once
+#include <type_traits>
+
+#include "conv_epilogue.h"
+
+#ifndef PP_EXP
+#define PP_EXP 0  // A/B timing experiments only (tools/build_variant.sh); 0 = the real kernel
+#endif
+// bits: 1 no MFMA, 2 no weight DMA in the loop, 4 no fragment reads, 8 no barriers in the loop, 16 no epilogue
+#define PPX(b) ((PP_EXP & (b)) != 0)
+
+namespace {
+
+IRGAN_HD int lds_off(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+
+IRGAN_HD void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
+// block barrier that the scheduler cannot move instructions across
+IRGAN_HD void phase_barrier() {
+    sched_fence();
+#if !PPX(8)
+    lds_barrier();
+#endif
+    sched_fence();
+}
+IRGAN_HD void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+constexpr int PH = 16, PW = 16;   // output patch
+constexpr int HPMAX = 46;         // halo pieces (8 rows of 128 B) for taps up to 4x4: 19*19 = 361 rows
+constexpr int HBYTES = HPMAX * 1024;
+// per output-channel tile BN (256: resblock / D / VGG conv3; 192: up2 dgrad; 128: down1,
+// up1, VGG conv2; 64: up2, down1 dgrad, VGG conv1_2).  A group's 128 pixels (8 patch rows)
+// x BN channels are split over its 4 waves as RW row bands x CW channel bands; the wave
+// tile is MIW pixel fragments x NJ channel fragments.  Narrow BN splits rows rather than
+// channels, so every wave keeps 4 channel fragments: LDS fragment reads per MFMA are
+// (MIW + NJ) / (MIW * NJ) = 0.375 (BN 256), 0.5 (128), 0.75 (64) instead of
+// 0.625 / 1.125 with 128-pixel wave tiles.
+template <int BN>
+struct PP {
+    static constexpr int BBYTES = BN * 128;
+    static constexpr int LDS = 2 * HBYTES + 2 * BBYTES;
+    static constexpr int MIW = BN >= 192 ? 8 : (BN == 128 ? 4 : 2);  // pixel fragments (patch rows) per wave
+    static constexpr int RW = 8 / MIW, CW = 4 / RW;
+    static constexpr int NJ = BN / 16 / CW;            // 16-channel fragments per wave
+    static constexpr int WU = BBYTES / 1024 / 8;       // weight pieces per wave per K-step
+    static constexpr int RSB = BN * 2 + 16;            // bf16 staging row (pixel) stride, bytes
+    static constexpr int LPP = BN / 8;                 // epilogue lanes per pixel row (8 channels each)
+    static constexpr int PPASS = 512 / LPP;            // pixel rows stored per pass (BN = 192: 21, lanes 504+ idle)
+    static_assert(256 * RSB <= LDS && BN % 64 == 0 && WU * 8 * 1024 == BBYTES && NJ * 16 * CW == BN, "tile");
+};
+
+typedef int v8i_t __attribute__((ext_vector_type(8)));
+IRGAN_HD v8i_t cat8(i32x4 a, i32x4 b) { return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7); }
+
+// InstanceNorm-backward statistics in the STATS epilogue (irgan_conv_dgrad_in_stats):
+// with z set, the partials of the stored output v are (sum g, sum g*xhat) with
+// xhat = (z - mean) * rstd and g = v * act'(xhat) -- the reduce half of the IN backward
+// of the layer whose gradient this dgrad produces -- instead of (sum v, sum v^2).
+// pstride: partial rows per image (0: the patch count; > it leaves slots for the ring).
+struct InBwdStats {
+    const bf16_t* z;
+    int ldz, zoff, act, pstride;
+    const float* mr;
+};
+IRGAN_HD float in_act_grad(float xh, int act) {  // as norm.hip's act_grad
+    if (act == IRGAN_ACT_RELU) return xh > 0.f ? 1.f : 0.f;
+    if (act == IRGAN_ACT_LRELU) return xh > 0.f ? 1.f : 0.2f;
+    return 1.f;
+}
+
+// ONE: a single halo buffer, so at BN = 64 the block fits twice per CU (LDS 62 KiB,
+// <= 128 VGPRs) and one block's halo loads / epilogue overlap the other's MFMA loop
+// (BN = 128 would need 159 VGPRs: at 128 it spills 30 and runs slower than two BN-64
+// tiles, profiles/r02_s5_pp_one_ab.txt).  With more than one channel chunk the next chunk's halo cannot be
+// prefetched: after the last window that reads chunk c (4k+3 of its last tap) every
+// wave issues its pieces of chunk c+1, retires them and meets at one extra barrier.
+// RING epilogue: the padded-domain ring COLUMN of a left / right border patch (ir:386-411:
+// backward-data of conv(ReflectionPad2d(1)(x)) is the fold of the zero-padded correlation g
+// over the (H+2) x (W+2) domain; the interior of g is the K loop's result).  Column -1
+// (left) reads only tap column tx = 2, column W (right) only tx = 0, so its 16 values
+// (rows py0..py0+15) plus the corner (row -1 of a top patch / H of a bottom one) are a
+// 17 x BN x (3 * Cin) GEMM.  The operand halos are gone by now, so it streams straight
+// from L2 / HBM: 8 waves x 32 output channels, two pixel fragments (the 16 rows; the
+// corner in lane 0 of the second), 3 * Cin / 32 K-steps with the next step's loads in
+// flight.  Result: fp32 table[17][BN] (row 16 = the corner), which emit() adds onto the
+// mirrored pixels before the single bf16 rounding of the output.
+IRGAN_HD void ring_col_epilogue(const irgan_conv_desc& d, const bf16_t* __restrict__ dy, const bf16_t* __restrict__ w,
+                                int img, int py0, bool left, bool top, bool bot, int n0, float* table) {
+    constexpr int BN = 256;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int Kw = 9 * d.Cin;
+    const int txr = left ? 2 : 0;
+    const int oc = left ? -1 : d.W;                      // padded-domain column (output coordinates)
+    const int dcol = oc + d.c0x + txr;                   // the dy column it reads
+    const int kc = (lane >> 4) * 8;
+    const bool corner = top || bot;                      // block-uniform
+    const int orow0 = py0 + (lane & 15);                 // pixel fragment 0: rows py0 .. py0+15
+    const int orow1 = top ? -1 : d.H;                    // fragment 1, lane 0: the corner row
+    const bool c_lane = corner && (lane & 15) == 0;
+    const bf16_t* wr[2];
+#pragma unroll
+    for (int nf = 0; nf < 2; ++nf) wr[nf] = w + (long)(n0 + wv * 32 + nf * 16 + (lane & 15)) * Kw + kc;
+    const long pixb = ((long)img * d.H) * d.W;
+    auto dy_at = [&](int orow, int ty, int cs, bool ok) -> uint4 {
+        const int r = orow + d.c0y + ty;
+        if (!ok || (unsigned)r >= (unsigned)d.H || (unsigned)dcol >= (unsigned)d.W) return uint4{0, 0, 0, 0};
+        return *(const uint4*)(dy + (pixb + (long)r * d.W + dcol) * d.ldx + d.xoff + cs * 32 + kc);
+    };
+    const int ncs = d.Cin / 32, nk = 3 * ncs;
+    auto load = [&](int k, uint4 (&a)[2], uint4 (&b)[2]) {
+        const int ty = k / ncs, cs = k - ty * ncs;
+        const int kcol = (ty * 3 + txr) * d.Cin + cs * 32;
+#pragma unroll
+        for (int nf = 0; nf < 2; ++nf) a[nf] = *(const uint4*)(wr[nf] + kcol);
+        b[0] = dy_at(orow0, ty, cs, true);
+        b[1] = dy_at(orow1, ty, cs, c_lane);
+    };
+    f32x4 ra[2][2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int nf = 0; nf < 2; ++nf) ra[m][nf] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto mma = [&](const uint4 (&a)[2], const uint4 (&b)[2]) {
+#pragma unroll
+        for (int nf = 0; nf < 2; ++nf) {
+            ra[0][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a[nf]),
+                                                                __builtin_bit_cast(bf16x8_t, b[0]), ra[0][nf], 0, 0, 0);
+            if (corner)
+                ra[1][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a[nf]),
+                                                                    __builtin_bit_cast(bf16x8_t, b[1]), ra[1][nf], 0, 0,
+                                                                    0);
+        }
+    };
+    uint4 a0[2], b0[2], a1[2], b1[2];
+    load(0, a0, b0);
+#pragma unroll 1
+    for (int k = 0; k < nk; k += 2) {
+        if (k + 1 < nk) load(k + 1, a1, b1);
+        mma(a0, b0);
+        if (k + 1 >= nk) break;
+        if (k + 2 < nk) load(k + 2, a0, b0);
+        mma(a1, b1);
+    }
+    // C^T fragments: lane = pixel (lane & 15), channels 4 * (lane >> 4) + r of the 16
+#pragma unroll
+    for (int nf = 0; nf < 2; ++nf) {
+        const int cl = wv * 32 + nf * 16 + 4 * (lane >> 4);
+        *(float4*)(table + (lane & 15) * BN + cl) = make_float4(ra[0][nf][0], ra[0][nf][1], ra[0][nf][2], ra[0][nf][3]);
+        if (c_lane)
+            *(float4*)(table + 16 * BN + cl) = make_float4(ra[1][nf][0], ra[1][nf][1], ra[1][nf][2], ra[1][nf][3]);
+    }
+}
+
+// RING (conv_pp_ring.hip: the reflect-padded ResnetBlock backward-data, ir:386-411, with
+// its pad ring folded in -- see ring_col_epilogue below): bf16, 3x3, BN 256, Ho == H and
+// Wo == W multiples of 16 with >= 2 patches per axis (host-checked).
+template <int KH, int KW, int BN, bool ACC, bool STATS = false, bool F8 = false, bool ONE = false,
+          bool RING = false>
+__global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
+                                                         const bf16_t* __restrict__ w, const float* __restrict__ bias,
+                                                         void* __restrict__ y, const void* __restrict__ mask,
+                                                         int ntn, int tpx, int tpy, int swz,
+                                                         float2* __restrict__ part = nullptr,
+                                                         const float* __restrict__ dqx = nullptr,
+                                                         const float* __restrict__ dqw = nullptr,
+                                                         const InBwdStats ib = InBwdStats{}) {
+    constexpr int ESZ = F8 ? 1 : 2, CHN = 128 / ESZ;  // operand bytes, channels per 128-byte chunk
+    const char* const xb = (const char*)x;
+    const char* const wb = (const char*)w;
+    constexpr int TAPS = KH * KW, HWd = PW + KW - 1, HROWS = (PH + KH - 1) * HWd, HP = (HROWS + 7) / 8;
+    constexpr int BBYTES = PP<BN>::BBYTES, NJ = PP<BN>::NJ, WU = PP<BN>::WU, RSB = PP<BN>::RSB;
+    constexpr int LDS = ONE ? HBYTES + 2 * BBYTES : PP<BN>::LDS;
+    static_assert(!ONE || (BN == 64 && 256 * RSB <= LDS && !F8), "single-halo variant: staging must fit");
+    constexpr int MI = PP<BN>::MIW, RW = PP<BN>::RW;
+    // sub-steps per K-step: bf16 2 (32 channels each); fp8 splits the pixel fragments,
+    // MS per sub-step (4 sub-steps at MI = 8 keep the operand registers at the bf16 48)
+    constexpr int HS = F8 && MI >= 8 ? 4 : 2, MS = F8 ? MI / HS : MI;
+    static_assert(HP <= HPMAX && HP > 40 && TAPS >= 2, "halo pieces per wave are 5 or 6");
+    __shared__ __attribute__((aligned(1024))) char smem[LDS];
+    char* const sH = smem;
+    char* const sB = smem + (ONE ? 1 : 2) * HBYTES;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wid >> 2, wn = wid & 3;
+    const int prow = grp * 8 + (wn % RW) * MI;  // first patch row of this wave's pixel fragments
+    const int cb = (wn / RW) * NJ * 16;         // first block-local channel of this wave
+    int t = xcd_tile(blockIdx.x, gridDim.x, swz);
+    const int nt = t % ntn;
+    t /= ntn;
+    const int pxi = t % tpx;
+    t /= tpx;
+    const int pyi = t % tpy;
+    const int img = t / tpy;
+    const int py0 = pyi * PH, px0 = pxi * PW, n0 = nt * BN;
+    const int nh = (HP - wid + 7) >> 3;  // halo pieces this wave loads: wid, wid+8, ... (5 or 6)
+    const int Kw = TAPS * d.Cin;
+    const int nchunk = d.Cin / CHN;
+    const int sub = lane >> 3;
+    const int chunk = (lane & 7) ^ sub;  // source chunk for this lane's LDS slot (row & 7 == sub)
+    const bool reflect = d.pad_mode == IRGAN_PAD_REFLECT;
+    static_assert(!RING || (KH == 3 && KW == 3 && BN == 256 && !F8 && !ONE), "ring fold: resblock dgrad tiles");
+    // RING: which sides of the padded domain this patch borders (block-uniform)
+    const bool rtop = RING && pyi == 0, rbot = RING && pyi == tpy - 1;
+    const bool rleft = RING && pxi == 0, rright = RING && pxi == tpx - 1;
+
+    // DMA sources as byte offsets into buffer resources (out-of-range offsets
+    // arrive as zeros: padding and Cout tails cost no address math in the loop)
+    const uint32_t xbytes = (uint32_t)((long)d.N * d.H * d.W * d.ldx * ESZ);
+    // byte offset of this lane's row of halo piece (u*8 + wid) (computed at issue
+    // time, once per chunk: keeping six offsets live costs registers the MFMA
+    // tile needs)
+    auto halo_off = [&](int u, int lsub) -> uint32_t {
+        const int h = (u * 8 + wid) * 8 + lsub;
+        const int hy = h / HWd, hx = h - hy * HWd;
+        int iy = py0 + hy + d.c0y, ix = px0 + hx + d.c0x;
+        if (reflect) {
+            iy = reflect_idx(iy, d.H);
+            ix = reflect_idx(ix, d.W);
+        }
+        const bool ok = (h < HROWS) & ((unsigned)iy < (unsigned)d.H) & ((unsigned)ix < (unsigned)d.W);
+        return ok ? (uint32_t)((((img * d.H + iy) * d.W + ix) * d.ldx + d.xoff) * ESZ + ((lane & 7) ^ lsub) * 16)
+                  : IRGAN_OOB;
+    };
+    // weight rows co >= Cout lie beyond num_records: they arrive as zeros
+    const uint32_t wbytes = (uint32_t)((long)d.Cout * Kw * ESZ);
+    const uint32_t b_off = (uint32_t)((n0 + wid * WU * 8 + sub) * Kw * ESZ + chunk * 16);  // piece u (8 rows): + u*8*Kw*ESZ
+    auto issue_halo = [&](int c) {
+        char* dst = sH + (ONE ? 0 : (c & 1) * HBYTES);
+        const i32x4 rs = make_rsrc(xb + c * 128, xbytes - c * 128);
+        int lsub = sub;
+        asm volatile("" : "+v"(lsub));  // recompute the offsets here instead of hoisting them out of the loop
+#pragma unroll
+        for (int u = 0; u < 6; ++u)
+            if (u < nh) blds16(rs, halo_off(u, lsub), dst + (u * 8 + wid) * 1024);
+    };
+    auto issue_w = [&](int c, int tp, int stage) {
+        const int kcol = tp * d.Cin + c * CHN;
+        const i32x4 rs = make_rsrc(wb + kcol * ESZ, wbytes - kcol * ESZ);
+        char* dst = sB + stage * BBYTES + wid * WU * 1024;
+#pragma unroll
+        for (int u = 0; u < WU; ++u) blds16(rs, b_off, (uint32_t)(u * 8 * Kw * ESZ), dst + u * 1024);
+    };
+    // ONE: chunk c's halo after the barrier closing its last reading window (the same
+    // barrier instance for both groups), landed before anyone reads it
+    auto reload_halo = [&](int c) {
+        issue_halo(c);
+        wait_vmcnt<0>();
+        phase_barrier();
+    };
+    // W(k+1) landed; the halo issued at step k (after W(k+1)) may stay in flight
+    auto retire = [&](bool halo_now) {
+        if (!halo_now) wait_vmcnt<0>();
+        else if (nh == 6) wait_vmcnt<6>();
+        else wait_vmcnt<5>();
+    };
+
+    f32x4 acc[MI][NJ];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    uint4 af[MI], bfr[NJ];
+    uint4 afr;  // RING: the ring-row fragment (padded-domain row -1 or H) of this K-step
+    v8i_t af8[MS], bf8[NJ];  // fp8: 32-byte fragments (chunks g, g + 4)
+    // prologue: W(0), halo(0), W(1); retire the first two
+    issue_w(0, 0, 0);
+    issue_halo(0);
+    issue_w(0, 1, 1);
+    wait_vmcnt<WU>();
+    phase_barrier();
+    if (grp == 1) phase_barrier();  // group 1 runs one window behind
+
+    // LDS addressing.  Fragment rows of a tap are constant shifts K of the
+    // lane's row arow0 and lds_off's XOR term depends only on (arow0 + K) & 7,
+    // so with the tap loop unrolled an A address is tsw[K & 7] + hb plus the
+    // ds_read immediate K * 128: one VALU add per fragment read.
+    const int arow0 = prow * HWd + (lane & 15);  // halo row of fragment 0 at tap (0,0)
+    const int brow0 = cb + (lane & 15);          // weight row of fragment 0 (rows +16j share the XOR)
+    // bf16: sub-step h reads chunk (lane >> 4) + 4h; fp8: a fragment is chunks (lane >> 4) and
+    // (lane >> 4) + 4 (the same byte <-> channel map for both operands)
+    const int g0 = lane >> 4;
+    const int bb0 = lds_off(brow0, g0), bb1 = lds_off(brow0, 4 + g0);
+    int tsw[F8 ? 1 : 8];  // h = 1 / the second fp8 chunk flips chunk bit 2: tsw ^ 64 (v_xad_u32)
+    if constexpr (!F8) {
+#pragma unroll
+        for (int k8 = 0; k8 < 8; ++k8) tsw[k8] = (g0 ^ ((arow0 + k8) & 7)) << 4;
+    }
+#pragma unroll 1
+    for (int c = 0; c < nchunk; ++c) {
+        const int hb = arow0 * 128 + (ONE ? 0 : (c & 1) * HBYTES);
+        const bool more = c + 1 < nchunk;
+#pragma unroll
+        for (int tp = 0; tp < TAPS; ++tp) {
+            const int ty = tp / KW, tx = tp % KW;
+            const int k = c * TAPS + tp;  // K-step
+            const char* B = sB + (k & 1) * BBYTES;
+            const bool last_k = !more && tp == TAPS - 1;
+            const bool halo_now = tp == 0 && more && !ONE;
+            const bool reload = ONE && more && tp == TAPS - 1;  // single buffer: chunk c+1 after window 4k+3
+#pragma unroll
+            for (int h = 0; h < HS; ++h) {
+                // ---- READ phase (group 0: even windows, group 1: odd)
+                const int bb = h ? bb1 : bb0;
+                int hbp = hb;
+                asm volatile("" : "+v"(hbp));  // per-phase base: the address adds stay here, not hoisted
+                if constexpr (F8) {
+                    if (h == 0) {
+#pragma unroll
+                        for (int j = 0; j < NJ; ++j)
+                            bf8[j] = cat8(*(const i32x4*)(B + bb0 + j * 2048), *(const i32x4*)(B + bb1 + j * 2048));
+                    }
+#pragma unroll
+                    for (int ii = 0; ii < MS; ++ii) {
+                        const int K = (h * MS + ii + ty) * HWd + tx;
+                        // the swizzle term from arow0 on the fly (fp8 has no registers to spare)
+                        const int sw = (g0 ^ ((arow0 + K) & 7)) << 4;
+                        af8[ii] = cat8(*(const i32x4*)(sH + (hbp + sw) + K * 128),
+                                       *(const i32x4*)(sH + (hbp + (sw ^ 64)) + K * 128));
+                    }
+                } else {
+#if !PPX(4)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) bfr[j] = *(const uint4*)(B + bb + j * 2048);
+#pragma unroll
+                for (int i = 0; i < MI; ++i) {
+                    const int K = (i + ty) * HWd + tx;
+                    af[i] = *(const uint4*)(sH + (hbp + (tsw[K & 7] ^ (h * 64))) + K * 128);
+                }
+                if constexpr (RING) {
+                    // padded-domain ring rows: row -1 (top patches, group 0) reads only tap
+                    // row ty = 2 (dy row 0 = halo row 1), row H (bottom, group 1: fragment row
+                    // i = 8 of its 8) only ty = 0 (dy row H-1 = halo row 16)
+                    if (ty == 2 && grp == 0 && rtop) {
+                        const int K = HWd + tx;
+                        afr = *(const uint4*)(sH + (hbp + (tsw[K & 7] ^ (h * 64))) + K * 128);
+                    }
+                    if (ty == 0 && grp == 1 && rbot) {
+                        const int K = 8 * HWd + tx;
+                        afr = *(const uint4*)(sH + (hbp + (tsw[K & 7] ^ (h * 64))) + K * 128);
+                    }
+                }
+#else
+                if (k == 0 && h == 0) {
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j) bfr[j] = *(const uint4*)(B + bb + j * 2048);
+#pragma unroll
+                    for (int i = 0; i < MI; ++i) af[i] = *(const uint4*)(sH + hbp + i * 128);
+                }
+#endif
+                }
+                if (h == 0 && !PPX(2)) {
+                    // W(k+1) (W(1) came with the prologue), then the next chunk's halo
+                    if (k >= 1 && !last_k) {
+                        if (tp + 1 < TAPS) issue_w(c, tp + 1, (k + 1) & 1);
+                        else issue_w(c + 1, 0, (k + 1) & 1);
+                    }
+                    if (halo_now) issue_halo(c + 1);
+                }
+                if (h == HS - 1 && grp == 1) {  // last window of step k (4k+3 in bf16): last reads, then retire
+                    wait_lgkm0();
+                    if (!last_k) retire(halo_now);
+                }
+                phase_barrier();
+                if (reload && h == HS - 1 && grp == 1) reload_halo(c + 1);
+                // ---- MFMA phase: C^T fragment (weights as A, pixels as B)
+                if constexpr (F8) {
+#pragma unroll
+                    for (int ii = 0; ii < MS; ++ii)
+#pragma unroll
+                        for (int j = 0; j < NJ; ++j)
+                            acc[h * MS + ii][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                                bf8[j], af8[ii], acc[h * MS + ii][j], 0, 0, 0, 127, 0, 127);
+                    // pin the scaled MFMAs inside this phase: hipcc otherwise sinks them past the
+                    // barriers to the end of the chunk, keeping every tap's fragments live (spills)
+#pragma unroll
+                    for (int ii = 0; ii < MS; ++ii)
+#pragma unroll
+                        for (int j = 0; j < NJ; ++j) asm volatile("" : "+v"(acc[h * MS + ii][j]));
+                } else {
+#pragma unroll
+                    for (int i = 0; i < MI * !PPX(1); ++i)
+#pragma unroll
+                        for (int j = 0; j < NJ; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                                __builtin_bit_cast(bf16x8_t, bfr[j]), __builtin_bit_cast(bf16x8_t, af[i]), acc[i][j],
+                                0, 0, 0);
+                    if constexpr (RING) {
+                        // the reflect fold of the ring rows: padded row -1 lands on dx row 1,
+                        // row H on row H-2 -- the same columns, so straight into those
+                        // fragments' accumulators (acc[1] of group 0, acc[6] of group 1)
+                        if (ty == 2 && grp == 0 && rtop) {
+#pragma unroll
+                            for (int j = 0; j < NJ; ++j)
+                                acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                                    __builtin_bit_cast(bf16x8_t, bfr[j]), __builtin_bit_cast(bf16x8_t, afr),
+                                    acc[1][j], 0, 0, 0);
+                        }
+                        if (ty == 0 && grp == 1 && rbot) {
+#pragma unroll
+                            for (int j = 0; j < NJ; ++j)
+                                acc[6][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                                    __builtin_bit_cast(bf16x8_t, bfr[j]), __builtin_bit_cast(bf16x8_t, afr),
+                                    acc[6][j], 0, 0, 0);
+                        }
+                    }
+                }
+                if (h == HS - 1 && grp == 0 && !last_k) retire(halo_now);  // last window of step k
+                phase_barrier();
+                if (reload && h == HS - 1 && grp == 0) reload_halo(c + 1);
+            }
+        }
+    }
+    if (grp == 0) phase_barrier();  // match group 1's extra barrier
+    __syncthreads();                // all operand reads done: LDS becomes the staging buffer
+    // RING: the ring columns (padded col -1 / W, incl. the corner of a top / bottom patch)
+    // as a small GEMM from L2 into an fp32 LDS table past the staging rows; emit() adds
+    // them onto their mirrored pixels (dx col 1 / W-2)
+    constexpr int RING_OFF = 256 * PP<BN>::RSB;  // bytes: [17 rows][BN] fp32
+    if constexpr (RING) {
+        static_assert(!RING || RING_OFF + 17 * BN * 4 <= LDS, "ring table fits past the staging rows");
+        if (rleft || rright) {
+            ring_col_epilogue(d, x, w, img, py0, rleft, rtop, rbot, n0, (float*)(smem + RING_OFF));
+            __syncthreads();
+        }
+    }
+#if PPX(16)
+    {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) s += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+        if (s == 123.f) *(float*)y = s;
+        return;
+    }
+#endif
+
+    // ---- epilogue.  Fragment (i, j): pixel m = (prow + i)*16 + (lane & 15),
+    // channels co = n0 + cb + j*16 + 4*(lane >> 4) + r, r = 0..3.
+    const int cl0 = cb + 4 * (lane >> 4);  // block-local channel of r = 0, j = 0
+    const float osc = F8 ? *dqx * *dqw : 1.f;  // fp8: 1 / (x scale * w scale), powers of two
+    float4 b4[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int co = n0 + cl0 + j * 16;
+        b4[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (bias) {
+            if (co + 3 < d.Cout) {
+                b4[j] = *(const float4*)(bias + co);
+            } else {
+                if (co < d.Cout) b4[j].x = bias[co];
+                if (co + 1 < d.Cout) b4[j].y = bias[co + 1];
+                if (co + 2 < d.Cout) b4[j].z = bias[co + 2];
+            }
+        }
+    }
+    auto pix_of = [&](int m) -> long {
+        const int oy = py0 + (m >> 4), ox = px0 + (m & 15);
+        if (oy >= d.Ho || ox >= d.Wo) return -1;
+        return ((long)img * d.OH + oy * d.omy + d.ooy) * d.OW + ox * d.omx + d.oox;
+    };
+    // Each lane owns (pixel, 4 consecutive channels) per fragment: mask and
+    // accumulate are applied right here on those 4 channels (8-byte loads).
+    // bf16 output: stage bf16 [256 px][256 ch] in LDS, then 16-byte row stores;
+    // fp32 output: 16-byte stores straight from the registers.
+    const bool out_f32 = d.out_dtype == IRGAN_F32;
+    // bf16 accumulate (dgrad into a tensor that already holds another branch's
+    // gradient): the 4 old channels of a fragment are one 8-byte load, and a
+    // fragment row's NJ loads are all issued before the row is combined, so the
+    // read latency is paid once per row instead of once per 2-byte element.
+    // (a template flag, so the plain-store kernels keep their register allocation)
+    const bool acc_vec = ACC && !out_f32 && d.ldy % 4 == 0 && d.yoff % 4 == 0;
+    auto emit = [&](auto actc) {
+        constexpr int A = decltype(actc)::value;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+            const int m = (prow + i) * 16 + (lane & 15);
+            const long pix = pix_of(m);
+            uint2 old[NJ];
+            if (acc_vec && pix >= 0) {
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                    const int co = n0 + cl0 + j * 16;
+                    old[j] = co + 4 <= d.Cout ? *(const uint2*)((const bf16_t*)y + pix * d.ldy + d.yoff + co)
+                                              : make_uint2(0u, 0u);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int cl = cl0 + j * 16, co = n0 + cl;
+                const float4 b = b4[j];
+                float v[4] = {acc[i][j][0] + b.x, acc[i][j][1] + b.y, acc[i][j][2] + b.z, acc[i][j][3] + b.w};
+                if constexpr (F8) {
+                    v[0] = acc[i][j][0] * osc + b.x;
+                    v[1] = acc[i][j][1] * osc + b.y;
+                    v[2] = acc[i][j][2] * osc + b.z;
+                    v[3] = acc[i][j][3] * osc + b.w;
+                }
+                if constexpr (RING) {
+                    // ring column -> dx col 1 (left) / W-2 = patch col 14 (right, W % 16 == 0);
+                    // the corner ring value -> dx row 1 (top) / H-2 = patch row 14 (bottom)
+                    const int col = lane & 15, row = prow + i;
+                    if ((rleft && col == 1) || (rright && col == 14)) {
+                        const float* rt = (const float*)(smem + RING_OFF);
+                        const float4 cv = *(const float4*)(rt + row * BN + cl);
+                        v[0] += cv.x; v[1] += cv.y; v[2] += cv.z; v[3] += cv.w;
+                        if ((rtop && row == 1) || (rbot && row == 14)) {
+                            const float4 kv = *(const float4*)(rt + 16 * BN + cl);
+                            v[0] += kv.x; v[1] += kv.y; v[2] += kv.z; v[3] += kv.w;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = conv_act(v[r], A);
+                const bool full = co + 4 <= d.Cout;
+                if (pix >= 0 && mask) {
+                    const bf16_t* mp = (const bf16_t*)mask + pix * d.ldm + d.moff + co;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (full || co + r < d.Cout) v[r] *= mask_mul(bf2f(mp[r]), d.mask_act);
+                }
+                if (out_f32) {
+                    if (pix < 0) continue;
+                    float* yp = (float*)y + pix * d.ldy + d.yoff + co;
+                    if (full && ((pix * d.ldy + d.yoff + co) & 3) == 0) {
+                        float4 o = make_float4(v[0], v[1], v[2], v[3]);
+                        if (ACC) {
+                            const float4 p = *(const float4*)yp;
+                            o.x += p.x; o.y += p.y; o.z += p.z; o.w += p.w;
+                        }
+                        *(float4*)yp = o;
+                    } else {
+                        for (int r = 0; r < 4 && co + r < d.Cout; ++r) yp[r] = ACC ? yp[r] + v[r] : v[r];
+                    }
+                } else {
+                    if (acc_vec && pix >= 0 && full) {
+                        v[0] += bf2f((bf16_t)(old[j].x & 0xffffu));
+                        v[1] += bf2f((bf16_t)(old[j].x >> 16));
+                        v[2] += bf2f((bf16_t)(old[j].y & 0xffffu));
+                        v[3] += bf2f((bf16_t)(old[j].y >> 16));
+                    } else if (ACC && pix >= 0) {
+                        const bf16_t* yp = (const bf16_t*)y + pix * d.ldy + d.yoff + co;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            if (full || co + r < d.Cout) v[r] += bf2f(yp[r]);
+                    }
+                    uint2 pk;
+                    pk.x = pk_bf16(v[0], v[1]);
+                    pk.y = pk_bf16(v[2], v[3]);
+                    *(uint2*)(smem + m * RSB + cl * 2) = pk;
+                }
+            }
+        }
+    };
+    switch (d.act) {
+        case IRGAN_ACT_RELU: emit(std::integral_constant<int, IRGAN_ACT_RELU>()); break;
+        case IRGAN_ACT_LRELU: emit(std::integral_constant<int, IRGAN_ACT_LRELU>()); break;
+        default: emit(std::integral_constant<int, IRGAN_ACT_NONE>()); break;
+    }
+    if (out_f32) return;
+    __syncthreads();
+    constexpr int LPP = PP<BN>::LPP;
+    constexpr int PPASS = PP<BN>::PPASS;
+    if constexpr (STATS) {
+        // InstanceNorm statistics of the stored (bf16) outputs fused into the store
+        // pass: per-channel (sum, sum of squares) over this block's valid pixels, one
+        // float2 partial per (image, patch, channel) in the layout finalize_kernel
+        // (norm.hip) reduces.  Host guarantees Cout % BN == 0, LPP * PPASS == 512.
+        static_assert(!STATS || PP<BN>::LPP * PP<BN>::PPASS == 512, "all threads store");
+        const int c8 = (tid % LPP) * 8, co8 = n0 + c8;
+        float s1[8], s2[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.f;
+        const bool bw = ib.z != nullptr;  // IN-backward statistics (block-uniform)
+        float mn[8], rs[8];
+        if (bw) {
+            const float4* m4 = (const float4*)(ib.mr + 2 * ((long)img * d.Cout + co8));
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float4 t4 = m4[k];
+                mn[2 * k] = t4.x; rs[2 * k] = t4.y; mn[2 * k + 1] = t4.z; rs[2 * k + 1] = t4.w;
+            }
+        }
+        for (int m = tid / LPP; m < 256; m += PPASS) {
+            const long pix = pix_of(m);
+            if (pix < 0) continue;
+            const uint4 v = *(const uint4*)(smem + m * RSB + c8 * 2);
+            *(uint4*)((bf16_t*)y + pix * d.ldy + d.yoff + co8) = v;
+            const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+            if (bw) {
+                const uint4 zz = *(const uint4*)(ib.z + pix * ib.ldz + ib.zoff + co8);
+                const uint32_t zw[4] = {zz.x, zz.y, zz.z, zz.w};
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const float f = __uint_as_float((k & 1) ? (wv[k / 2] & 0xffff0000u) : (wv[k / 2] << 16));
+                    const float zf = __uint_as_float((k & 1) ? (zw[k / 2] & 0xffff0000u) : (zw[k / 2] << 16));
+                    const float xh = (zf - mn[k]) * rs[k];
+                    const float g = f * in_act_grad(xh, ib.act);
+                    s1[k] += g;
+                    s2[k] += g * xh;
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float lo = __uint_as_float(wv[k] << 16), hi = __uint_as_float(wv[k] & 0xffff0000u);
+                    s1[2 * k] += lo; s2[2 * k] += lo * lo;
+                    s1[2 * k + 1] += hi; s2[2 * k + 1] += hi * hi;
+                }
+            }
+        }
+        __syncthreads();  // staging reads done: reuse LDS for the cross-row reduction
+        float2* red = (float2*)smem;  // [PPASS][BN]
+#pragma unroll
+        for (int k = 0; k < 8; ++k) red[(tid / LPP) * BN + c8 + k] = make_float2(s1[k], s2[k]);
+        __syncthreads();
+        // two-level fixed-order sum over the PPASS row groups: NR = 512 / BN threads per
+        // channel each add PPASS / NR rows, then one thread per channel adds the NR
+        constexpr int NR = 512 / BN, RPT = PPASS / NR;
+        static_assert(RPT * NR == PPASS, "row split");
+        float a = 0.f, b = 0.f;
+        {
+            const int c = tid % BN, r0 = tid / BN;
+#pragma unroll
+            for (int r = 0; r < RPT; ++r) {
+                const float2 e = red[(r0 * RPT + r) * BN + c];
+                a += e.x;
+                b += e.y;
+            }
+        }
+        __syncthreads();
+        red[tid] = make_float2(a, b);  // [NR][BN]
+        __syncthreads();
+        if (tid < BN) {
+            a = 0.f;
+            b = 0.f;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const float2 e = red[r * BN + tid];
+                a += e.x;
+                b += e.y;
+            }
+            const long patch = (long)img * (ib.pstride > 0 ? ib.pstride : tpx * tpy) + pyi * tpx + pxi;
+            part[patch * d.Cout + n0 + tid] = make_float2(a, b);
+        }
+        return;
+    }
+    if (tid >= PPASS * LPP) return;
+    const int c8 = (tid % LPP) * 8, co8 = n0 + c8;
+    if (co8 >= d.Cout) return;
+    const bool vec = co8 + 8 <= d.Cout && d.ldy % 8 == 0 && d.yoff % 8 == 0;
+    for (int m = tid / LPP; m < 256; m += PPASS) {
+        const long pix = pix_of(m);
+        if (pix < 0) continue;
+        bf16_t* yp = (bf16_t*)y + pix * d.ldy + d.yoff + co8;
+        const char* sp = smem + m * RSB + c8 * 2;
+        if (vec) {
+            *(uint4*)yp = *(const uint4*)sp;
+        } else {
+            for (int q = 0; q < 8 && co8 + q < d.Cout; ++q) yp[q] = ((const bf16_t*)sp)[q];
+        }
+    }
+}
+
+}  // namespace

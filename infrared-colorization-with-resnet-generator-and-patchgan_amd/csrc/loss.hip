@@ -155,14 +155,18 @@ __global__ __launch_bounds__(TPB) void tv_kernel(const float* __restrict__ x, in
     block_add(loss, w * acc);
 }
 
-struct Win11 {
-    float g[11];
+// the separable Gaussian window of ssim_loss_torch (ir:699-712): K taps, K odd
+template <int K>
+struct WinK {
+    float g[K];
 };
 
 // SSIM (ir:714-750) on a' = (a+1)/2, b' = (b+1)/2 with the separable 11-tap
 // Gaussian (sigma 1.5) and zero padding 5.  Planar fp32 work maps of size S.
+template <int K>
 __global__ __launch_bounds__(TPB) void ssim_h5_kernel(const float* __restrict__ a, const float* __restrict__ b, int W,
-                                                      int C, Win11 win, float* __restrict__ out, long S) {
+                                                      int C, WinK<K> win, float* __restrict__ out, long S) {
+    constexpr int HK = K / 2;
     const int xw = blockIdx.x * TPB + threadIdx.x;
     if (xw >= W) return;
     const long rowb = (long)blockIdx.y * W * C;
@@ -170,10 +174,10 @@ __global__ __launch_bounds__(TPB) void ssim_h5_kernel(const float* __restrict__ 
         const long idx = rowb + (long)xw * C + c;
         float m1 = 0.f, m2 = 0.f, e11 = 0.f, e22 = 0.f, e12 = 0.f;
 #pragma unroll
-        for (int k = 0; k < 11; ++k) {
-            const int xx = xw + k - 5;
+        for (int k = 0; k < K; ++k) {
+            const int xx = xw + k - HK;
             if (xx < 0 || xx >= W) continue;
-            const long j = idx + (long)(k - 5) * C;
+            const long j = idx + (long)(k - HK) * C;
             const float p = (a[j] + 1.f) * 0.5f, q = (b[j] + 1.f) * 0.5f, gk = win.g[k];
             m1 += gk * p;
             m2 += gk * q;
@@ -194,10 +198,11 @@ __global__ __launch_bounds__(TPB) void ssim_h5_kernel(const float* __restrict__ 
 // outputs mu1, mu2, E[a'^2], E[b'^2], E[a'b']; else NI = NO planar maps), then every
 // output element reads its 11 taps from LDS.  Same tap order as ssim_h5_kernel /
 // ssim_h_kernel (bit-identical results) without their stride-C global re-reads.
-template <int NI, int NO, bool FIRST>
+template <int K, int NI, int NO, bool FIRST>
 __global__ __launch_bounds__(TPB) void ssim_hrow_kernel(const float* __restrict__ a, const float* __restrict__ b,
-                                                        const float* __restrict__ in, int W, int C, Win11 win,
+                                                        const float* __restrict__ in, int W, int C, WinK<K> win,
                                                         float* __restrict__ out, long S) {
+    constexpr int HK = K / 2;
     extern __shared__ float rowm[];  // NI x W*C
     const int WC = W * C;
     const long rb = (long)blockIdx.x * WC;
@@ -217,10 +222,10 @@ __global__ __launch_bounds__(TPB) void ssim_hrow_kernel(const float* __restrict_
 #pragma unroll
         for (int m = 0; m < NO; ++m) acc[m] = 0.f;
 #pragma unroll
-        for (int k = 0; k < 11; ++k) {
-            const int xx = xw + k - 5;
+        for (int k = 0; k < K; ++k) {
+            const int xx = xw + k - HK;
             if (xx < 0 || xx >= W) continue;
-            const int j = e + (k - 5) * C;
+            const int j = e + (k - HK) * C;
             const float gk = win.g[k];
             if (FIRST) {
                 const float p = rowm[j], q = rowm[WC + j];
@@ -243,19 +248,20 @@ __global__ __launch_bounds__(TPB) void ssim_hrow_kernel(const float* __restrict_
 // of R consecutive rows: it loads the R + 10 input rows once into registers and
 // slides the window, so each input is read (R+10)/R times instead of 11 (the
 // pass was bound by those L2 re-reads).  blockIdx.y = n * ceil(H/R) + row block.
-template <int NM, int R>
-__global__ __launch_bounds__(TPB) void ssim_v_kernel(const float* __restrict__ in, int H, int W, int C, Win11 win,
+template <int K, int NM, int R>
+__global__ __launch_bounds__(TPB) void ssim_v_kernel(const float* __restrict__ in, int H, int W, int C, WinK<K> win,
                                                      float* __restrict__ out, long S) {
+    constexpr int HK = K / 2;
     const int e = blockIdx.x * TPB + threadIdx.x;  // element within the row (x*C + c)
     if (e >= W * C) return;
     const int hb = (H + R - 1) / R;
     const int n = blockIdx.y / hb, y0 = (blockIdx.y - n * hb) * R;
     const long WC = (long)W * C;
     const long base = (long)n * H * WC + e;
-    float v[NM][R + 10];
+    float v[NM][R + K - 1];
 #pragma unroll
-    for (int r = 0; r < R + 10; ++r) {
-        const int yy = y0 + r - 5;
+    for (int r = 0; r < R + K - 1; ++r) {
+        const int yy = y0 + r - HK;
         const bool ok = yy >= 0 && yy < H;
 #pragma unroll
         for (int m = 0; m < NM; ++m) v[m][r] = ok ? in[m * S + base + yy * WC] : 0.f;
@@ -267,16 +273,17 @@ __global__ __launch_bounds__(TPB) void ssim_v_kernel(const float* __restrict__ i
         for (int m = 0; m < NM; ++m) {
             float acc = 0.f;
 #pragma unroll
-            for (int k = 0; k < 11; ++k) acc += win.g[k] * v[m][r + k];
+            for (int k = 0; k < K; ++k) acc += win.g[k] * v[m][r + k];
             out[m * S + base + (y0 + r) * WC] = acc;
         }
     }
 }
 
 // horizontal 11-tap pass over NM planar maps
-template <int NM>
-__global__ __launch_bounds__(TPB) void ssim_h_kernel(const float* __restrict__ in, int W, int C, Win11 win,
+template <int K, int NM>
+__global__ __launch_bounds__(TPB) void ssim_h_kernel(const float* __restrict__ in, int W, int C, WinK<K> win,
                                                      float* __restrict__ out, long S) {
+    constexpr int HK = K / 2;
     const int xw = blockIdx.x * TPB + threadIdx.x;
     if (xw >= W) return;
     const long rowb = (long)blockIdx.y * W * C;
@@ -286,10 +293,10 @@ __global__ __launch_bounds__(TPB) void ssim_h_kernel(const float* __restrict__ i
 #pragma unroll
         for (int m = 0; m < NM; ++m) acc[m] = 0.f;
 #pragma unroll
-        for (int k = 0; k < 11; ++k) {
-            const int xx = xw + k - 5;
+        for (int k = 0; k < K; ++k) {
+            const int xx = xw + k - HK;
             if (xx < 0 || xx >= W) continue;
-            const long j = idx + (long)(k - 5) * C;
+            const long j = idx + (long)(k - HK) * C;
 #pragma unroll
             for (int m = 0; m < NM; ++m) acc[m] += win.g[k] * in[m * S + j];
         }
@@ -351,17 +358,48 @@ __global__ __launch_bounds__(TPB) void adam_kernel(float* __restrict__ p, const 
     }
 }
 
-Win11 gauss11() {
-    // ir:699-703 in fp32: coords = arange(11) - 5, exp(-c^2 / (2*1.5^2)), normalised
-    Win11 w;
+template <int K>
+WinK<K> gauss_win() {
+    // ir:699-703 in fp32: coords = arange(K) - (K-1)/2, exp(-c^2 / (2*1.5^2)), normalised
+    WinK<K> w;
     float s = 0.f;
-    for (int k = 0; k < 11; ++k) {
-        float c = (float)k - 5.0f;
+    for (int k = 0; k < K; ++k) {
+        float c = (float)k - (float)(K - 1) / 2.0f;
         w.g[k] = expf(-(c * c) / (2.f * 1.5f * 1.5f));
         s += w.g[k];
     }
-    for (int k = 0; k < 11; ++k) w.g[k] /= s;
+    for (int k = 0; k < K; ++k) w.g[k] /= s;
     return w;
+}
+
+// the forward + gradient launches for one window size (S = N*H*W*C, maps in work)
+template <int K>
+int ssim_launch(const float* a, const float* b, int N, int H, int W, int C, float w, float* g, double* loss,
+                float* work, hipStream_t st) {
+    const long S = (long)N * H * W * C;
+    const WinK<K> win = gauss_win<K>();
+    float* w0 = work;          // 5 maps
+    float* w1 = work + 5 * S;  // 5 maps
+    const int nb = nblocks(S);
+    constexpr int VR = 8;  // rows per thread in the vertical passes
+    const dim3 gx(irgan_cdiv(W, TPB), N * H), ge(irgan_cdiv((long)W * C, TPB), N * irgan_cdiv(H, VR));
+    const size_t row5 = (size_t)W * C * 2 * sizeof(float), row3 = (size_t)W * C * 3 * sizeof(float);
+    if (row3 <= 64 * 1024) {  // row-staged horizontal passes (W*C <= 5461)
+        ssim_hrow_kernel<K, 2, 5, true><<<N * H, TPB, row5, st>>>(a, b, nullptr, W, C, win, w0, S);
+    } else {
+        ssim_h5_kernel<K><<<gx, TPB, 0, st>>>(a, b, W, C, win, w0, S);
+    }
+    ssim_v_kernel<K, 5, VR><<<ge, TPB, 0, st>>>(w0, H, W, C, win, w1, S);
+    ssim_map_kernel<<<nblocks_red(S), TPB, 0, st>>>(w1, w, w0, loss, S);
+    if (row3 <= 64 * 1024) {
+        ssim_hrow_kernel<K, 3, 3, false><<<N * H, TPB, row3, st>>>(nullptr, nullptr, w0, W, C, win, w1, S);
+    } else {
+        ssim_h_kernel<K, 3><<<gx, TPB, 0, st>>>(w0, W, C, win, w1, S);
+    }
+    ssim_v_kernel<K, 3, VR><<<ge, TPB, 0, st>>>(w1, H, W, C, win, w0, S);
+    ssim_grad_kernel<<<nb, TPB, 0, st>>>(w0, a, b, g, S);
+    IRGAN_LAUNCH_CHECK();
+    return 0;
 }
 
 }  // namespace
@@ -412,35 +450,27 @@ extern "C" int irgan_tv(const float* x, int32_t N, int32_t H, int32_t W, int32_t
     return 0;
 }
 
+extern "C" int irgan_ssim_ws(const float* a, const float* b, int32_t N, int32_t H, int32_t W, int32_t C, float w,
+                             float* g, double* loss, float* work, int32_t window, irgan_stream_t s) {
+    hipStream_t st = (hipStream_t)s;
+    if ((long)N * H * W * C <= 0) return 0;
+    if ((long)N * H > 65535) return IRGAN_EUNSUPPORTED;
+    switch (window) {
+        case 1: return ssim_launch<1>(a, b, N, H, W, C, w, g, loss, work, st);
+        case 3: return ssim_launch<3>(a, b, N, H, W, C, w, g, loss, work, st);
+        case 5: return ssim_launch<5>(a, b, N, H, W, C, w, g, loss, work, st);
+        case 7: return ssim_launch<7>(a, b, N, H, W, C, w, g, loss, work, st);
+        case 9: return ssim_launch<9>(a, b, N, H, W, C, w, g, loss, work, st);
+        case 11: return ssim_launch<11>(a, b, N, H, W, C, w, g, loss, work, st);
+        case 13: return ssim_launch<13>(a, b, N, H, W, C, w, g, loss, work, st);
+        case 15: return ssim_launch<15>(a, b, N, H, W, C, w, g, loss, work, st);
+        default: return IRGAN_EUNSUPPORTED;
+    }
+}
+
 extern "C" int irgan_ssim(const float* a, const float* b, int32_t N, int32_t H, int32_t W, int32_t C, float w,
                           float* g, double* loss, float* work, irgan_stream_t s) {
-    hipStream_t st = (hipStream_t)s;
-    const long S = (long)N * H * W * C;
-    const Win11 win = gauss11();
-    float* w0 = work;          // 5 maps
-    float* w1 = work + 5 * S;  // 5 maps
-    if (S <= 0) return 0;
-    if ((long)N * H > 65535) return IRGAN_EUNSUPPORTED;
-    const int nb = nblocks(S);
-    constexpr int VR = 8;  // rows per thread in the vertical passes
-    const dim3 gx(irgan_cdiv(W, TPB), N * H), ge(irgan_cdiv((long)W * C, TPB), N * irgan_cdiv(H, VR));
-    const size_t row5 = (size_t)W * C * 2 * sizeof(float), row3 = (size_t)W * C * 3 * sizeof(float);
-    if (row3 <= 64 * 1024) {  // row-staged horizontal passes (W*C <= 5461)
-        ssim_hrow_kernel<2, 5, true><<<N * H, TPB, row5, st>>>(a, b, nullptr, W, C, win, w0, S);
-    } else {
-        ssim_h5_kernel<<<gx, TPB, 0, st>>>(a, b, W, C, win, w0, S);
-    }
-    ssim_v_kernel<5, VR><<<ge, TPB, 0, st>>>(w0, H, W, C, win, w1, S);
-    ssim_map_kernel<<<nblocks_red(S), TPB, 0, st>>>(w1, w, w0, loss, S);
-    if (row3 <= 64 * 1024) {
-        ssim_hrow_kernel<3, 3, false><<<N * H, TPB, row3, st>>>(nullptr, nullptr, w0, W, C, win, w1, S);
-    } else {
-        ssim_h_kernel<3><<<gx, TPB, 0, st>>>(w0, W, C, win, w1, S);
-    }
-    ssim_v_kernel<3, VR><<<ge, TPB, 0, st>>>(w1, H, W, C, win, w0, S);
-    ssim_grad_kernel<<<nb, TPB, 0, st>>>(w0, a, b, g, S);
-    IRGAN_LAUNCH_CHECK();
-    return 0;
+    return irgan_ssim_ws(a, b, N, H, W, C, w, g, loss, work, 11, s);
 }
 
 extern "C" int irgan_adam(float* p, const float* g, float* m, float* v, int64_t n, float step_size, float beta1,

@@ -409,6 +409,27 @@ __global__ __launch_bounds__(TPB) void act_bwd_kernel(const void* __restrict__ d
     }
 }
 
+// nn.Dropout(p), training mode (ResnetBlock use_dropout, ir:394-395): keep element e with
+// probability 1 - p from a counter-based hash of (seed, e), e = pixel * C + channel, and
+// scale kept values by 1 / (1 - p).  The backward is the same launch on the gradient
+// (same seed: same mask, same scale), so no mask is stored.
+IRGAN_HD uint64_t mix64(uint64_t z) {  // splitmix64 finaliser
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+__global__ __launch_bounds__(TPB) void dropout_kernel(const void* x, int xdt, int ldx, int xoff,
+                                                      void* y, int ydt, int ldy, int yoff, int C,
+                                                      long total, uint64_t seed, uint32_t thresh, float scale) {
+    for (long idx = blockIdx.x * (long)TPB + threadIdx.x; idx < total; idx += (long)gridDim.x * TPB) {
+        const long p = idx / C;
+        const int c = (int)(idx - p * C);
+        const uint32_t u = (uint32_t)(mix64(seed + 0x9e3779b97f4a7c15ull * (uint64_t)(idx + 1)) >> 40);  // 24 bits
+        const float v = ldv(x, xdt, p * ldx + xoff + c);
+        stv(y, ydt, p * ldy + yoff + c, u >= thresh ? v * scale : 0.f);
+    }
+}
+
 int nblocks(long total) { return (int)std::max<long>(1, std::min<long>((total + TPB - 1) / TPB, 16384)); }
 
 }  // namespace
@@ -661,6 +682,18 @@ extern "C" int irgan_affine(const void* x, int32_t xdt, int32_t ldx, int32_t xof
     RS_CHECK(total);
     affine_kernel<<<nblocks(total), TPB, 0, (hipStream_t)s>>>(x, xdt, ldx, xoff, scale, shift, y, ydt, ldy, yoff,
                                                               accumulate, C, total);
+    IRGAN_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int irgan_dropout(const void* x, int32_t xdt, int32_t P, int32_t C, int32_t ldx, int32_t xoff, void* y,
+                             int32_t ydt, int32_t ldy, int32_t yoff, uint64_t seed, float p, irgan_stream_t s) {
+    const long total = (long)P * C;
+    RS_CHECK(total);
+    if (!x || !y || !(p >= 0.f && p < 1.f)) return IRGAN_EINVAL;
+    const uint32_t thresh = (uint32_t)(p * 16777216.f);  // keep iff u24 >= p * 2^24
+    dropout_kernel<<<nblocks(total), TPB, 0, (hipStream_t)s>>>(x, xdt, ldx, xoff, y, ydt, ldy, yoff, C, total, seed,
+                                                                thresh, 1.f / (1.f - p));
     IRGAN_LAUNCH_CHECK();
     return 0;
 }

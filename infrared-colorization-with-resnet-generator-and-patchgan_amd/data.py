@@ -38,7 +38,7 @@ import torch
 from . import _lib
 from .ops import P, stream
 
-__all__ = ["EXTS", "area_table", "resize_area_u8", "imread_gray", "imread_rgb", "load_ir_image", "load_rgb_image",
+__all__ = ["EXTS", "area_table", "linear_area_table", "resize_area_u8", "resize_linear_area_u8", "imread_gray", "imread_rgb", "load_ir_image", "load_rgb_image",
            "collect_kaist_ir_files_from_sets", "scan_kaist_pairs", "KAISTPairDataset", "DeviceResizer",
            "collate_raw", "kaist_loader"]
 
@@ -60,8 +60,7 @@ def area_table(ssize: int, dsize: int):
     source index."""
     scale = 1.0 / (dsize / ssize)
     if scale < 1.0:
-        raise NotImplementedError("INTER_AREA upscaling (cv2 switches to a bilinear variant) is not implemented; "
-                                  "KAIST frames are 640x512 and are only downscaled")
+        raise ValueError("area_table is the downscaling table; upscaling uses linear_area_table")
     ptr, src, w = [0], [], []
     for dx in range(dsize):
         fsx1 = dx * scale
@@ -83,6 +82,72 @@ def area_table(ssize: int, dsize: int):
     return np.array(ptr, np.int32), np.array(src, np.int32), np.array(w, np.float32)
 
 
+INTER_RESIZE_COEF_BITS = 11
+INTER_RESIZE_COEF_SCALE = 1 << INTER_RESIZE_COEF_BITS
+
+
+def _cv_round(v):
+    return int(np.rint(v))   # cvRound: nearest, ties to even
+
+
+def linear_area_table(ssize: int, dsize: int, columns: bool = True):
+    """Per-axis table of cv2.resize(INTER_AREA) when either axis UPscales: OpenCV then
+    runs its linear resampler with "area mode" coefficients (resizeGeneric_ with
+    area_mode): source index s = floor(d * scale), fraction
+    f = (d + 1) - (s + 1) / scale (as float32), f <= 0 -> 0 else f - floor(f); left /
+    right border clamps (s < 0 -> s = 0, f = 0; s >= ssize - 1 -> s = ssize - 1, f = 0);
+    8-bit fixed-point weights round((1 - f) * 2048), round(f * 2048).  The border
+    clamps are the column table's (columns=True); the row table keeps s and f as
+    computed (OpenCV clamps the second source ROW index instead).
+    Returns (ofs int32 [dsize], coef int16-valued int32 [dsize][2], lim): destinations
+    d >= lim take the single tap S[ofs] * 2048 (OpenCV's xmax; rows never do)."""
+    inv = dsize / ssize
+    scale = 1.0 / inv
+    ofs = np.zeros(dsize, np.int32)
+    coef = np.zeros((dsize, 2), np.int32)
+    lim = dsize
+    for d in range(dsize):
+        sx = int(np.floor(d * scale))
+        f = float(np.float32((d + 1) - (sx + 1) * inv))
+        f = 0.0 if f <= 0 else float(np.float32(f - np.floor(f)))
+        if columns and sx < 0:
+            f, sx = 0.0, 0
+        if columns and sx + 1 >= ssize:
+            lim = min(lim, d)
+            if sx >= ssize - 1:
+                f, sx = 0.0, ssize - 1
+        ofs[d] = sx
+        c0, c1 = np.float32(1.0) - np.float32(f), np.float32(f)
+        coef[d] = (_cv_round(np.float32(c0 * np.float32(INTER_RESIZE_COEF_SCALE))),
+                   _cv_round(np.float32(c1 * np.float32(INTER_RESIZE_COEF_SCALE))))
+    return ofs, coef, lim
+
+
+def resize_linear_area_u8(img: np.ndarray, width: int, height: int) -> np.ndarray:
+    """cv2.resize(img, (width, height), interpolation=INTER_AREA) for uint8 when either axis
+    upscales (OpenCV's generic linear path in 8-bit fixed point): horizontal
+    D = S[x0] * a0 + S[x0 + C] * a1 (int32; single tap S[x0] * 2048 from the xmax border
+    on), vertical dst = (((b0 * (D0 >> 4)) >> 16) + ((b1 * (D1 >> 4)) >> 16) + 2) >> 2 with
+    the second row clamped to the image (VResizeLinear<uchar, int, short>)."""
+    a = np.asarray(img)
+    squeeze = a.ndim == 2
+    if squeeze:
+        a = a[:, :, None]
+    H, W, C = a.shape
+    xo, xc, xlim = linear_area_table(W, width)
+    yo, yc, _ = linear_area_table(H, height, columns=False)
+    S = a.astype(np.int64)
+    x1 = np.minimum(xo + 1, W - 1)
+    D = S[:, xo, :] * xc[None, :, 0, None] + S[:, x1, :] * xc[None, :, 1, None]
+    D[:, xlim:, :] = S[:, xo[xlim:], :] * INTER_RESIZE_COEF_SCALE
+    y1 = np.minimum(yo + 1, H - 1)
+    D0, D1 = D[yo], D[y1]
+    b0, b1 = yc[:, 0, None, None], yc[:, 1, None, None]
+    r = (((b0 * (D0 >> 4)) >> 16) + ((b1 * (D1 >> 4)) >> 16) + 2) >> 2
+    r = (r & 0xFF).astype(np.uint8)   # uchar(...) cast, no saturation (as OpenCV)
+    return r[:, :, 0] if squeeze else r
+
+
 def _slots(ptr, src, w):
     """Regroup a CSR table by position-within-run: slot t = the t-th entry of every
     destination that has one (so a vectorised pass adds in the table's order)."""
@@ -98,11 +163,14 @@ def _slots(ptr, src, w):
 
 def resize_area_u8(img: np.ndarray, size: int) -> np.ndarray:
     """cv2.resize(img, (size, size), interpolation=INTER_AREA) for uint8 HxW or
-    HxWxC input (scale >= 1), host side, float32 in OpenCV's operation order:
-    per destination row, each source row of its cell reduced horizontally
-    (buf = 0 + a0*S0 + a1*S1 ...), then sum = b0*buf0 + b1*buf1 ..., rounded
-    half to even and clamped to uint8."""
+    HxWxC input, host side.  Both axes downscaling (OpenCV's area path): float32 in
+    OpenCV's operation order -- per destination row, each source row of its cell
+    reduced horizontally (buf = 0 + a0*S0 + a1*S1 ...), then sum = b0*buf0 + b1*buf1
+    ..., rounded half to even and clamped to uint8.  Otherwise (an img_size above the
+    source size): resize_linear_area_u8."""
     a = np.asarray(img)
+    if a.shape[0] < size or a.shape[1] < size:
+        return resize_linear_area_u8(a, size, size)
     squeeze = a.ndim == 2
     if squeeze:
         a = a[:, :, None]
@@ -129,12 +197,16 @@ def resize_area_u8(img: np.ndarray, size: int) -> np.ndarray:
 def imread_gray(path) -> np.ndarray:
     """cv2.imread(path, IMREAD_GRAYSCALE) -> HxW uint8 (ir:812, 1134).  16-bit
     sources keep their high byte (libpng strip-16, as OpenCV's PNG decoder
-    without IMREAD_ANYDEPTH); colour sources use cvtColor's BGR2GRAY fixed-point
-    weights (4899, 9617, 1868) / 2^14 with rounding."""
+    without IMREAD_ANYDEPTH).  JPEG: OpenCV asks libjpeg for JCS_GRAYSCALE, i.e. the
+    decoded Y plane itself -- PIL's draft('L') mode does the same (no YCbCr -> RGB ->
+    gray round trip).  Other colour sources (PNG / BMP / TIFF): cvtColor's BGR2GRAY
+    fixed-point weights (4899, 9617, 1868) / 2^14 with rounding."""
     from PIL import Image
     with Image.open(path) as im:
         if im.mode in ("I;16", "I;16B", "I;16L", "I"):   # 16-bit source
             return (np.asarray(im).astype(np.uint32) >> 8).astype(np.uint8)
+        if im.format == "JPEG" and im.mode != "L":
+            im.draft("L", im.size)                        # libjpeg's grayscale output (Y)
         if im.mode == "L":
             return np.asarray(im).copy()
         rgb = np.asarray(im.convert("RGB")).astype(np.uint32)
@@ -282,10 +354,13 @@ class _RawView(torch.utils.data.Dataset):
 
 
 def collate_raw(items):
-    """Stack decoded items into uint8 batches (pinned by the DataLoader)."""
-    shapes = {tuple(it["ir_u8"].shape) for it in items} | {tuple(it["rgb_u8"].shape[:2]) for it in items}
-    if len(shapes) != 1:
-        raise RuntimeError(f"a device batch needs one source image size, got {sorted(shapes)}")
+    """Stack decoded items into uint8 batches (pinned by the DataLoader).  Each modality
+    needs one source size within the batch (one resize launch per modality); the IR and
+    RGB sources may differ (the reference resizes each image on its own, ir:1139, 1156)."""
+    for key in ("ir_u8", "rgb_u8"):
+        shapes = {tuple(it[key].shape[:2]) for it in items}
+        if len(shapes) != 1:
+            raise RuntimeError(f"a device batch needs one {key[:-3]} source size, got {sorted(shapes)}")
     return {"ir_u8": torch.stack([it["ir_u8"] for it in items]),
             "rgb_u8": torch.stack([it["rgb_u8"] for it in items]),
             "flip": torch.tensor([it["flip"] for it in items], dtype=torch.uint8)}
@@ -306,6 +381,14 @@ class DeviceResizer:
             t = self._tabs[n] = tuple(torch.from_numpy(a).to(self.device) for a in area_table(n, self.size))
         return t
 
+    def _ltab(self, n, columns):
+        key = ("lin", n, columns)
+        t = self._tabs.get(key)
+        if t is None:
+            ofs, coef, lim = linear_area_table(n, self.size, columns)
+            t = self._tabs[key] = (torch.from_numpy(ofs).to(self.device), torch.from_numpy(coef).to(self.device), lim)
+        return t
+
     def resize_u8(self, u8, C, flip=None, img_max=None):
         """(B,H,W[,C]) uint8 device batch -> (B,C,S,S) uint8 (cv2.resize INTER_AREA,
         optional per-image horizontal flip)."""
@@ -314,21 +397,30 @@ class DeviceResizer:
         u8 = u8.contiguous()
         B, H, W = u8.shape[:3]
         S = self.size
+        out8 = torch.empty(B, C, S, S, dtype=torch.uint8, device=self.device)
+        if H < S or W < S:   # an upscaling axis: OpenCV's linear path with area coefficients
+            yo, yc, _ = self._ltab(H, False)
+            xo, xc, xlim = self._ltab(W, True)
+            _lib.call("irgan_linear_area_resize_u8", P(u8), B, H, W, C, ctypes.c_int64(H * W * C), P(yo), P(yc), S,
+                      P(xo), P(xc), xlim, S, P(flip) if flip is not None else None, P(out8),
+                      P(img_max) if img_max is not None else None, stream())
+            return out8
         yp, ys, yw = self._tab(H)
         xp, xs, xw = self._tab(W)
-        out8 = torch.empty(B, C, S, S, dtype=torch.uint8, device=self.device)
         _lib.call("irgan_area_resize_u8", P(u8), B, H, W, C, ctypes.c_int64(H * W * C), P(yp), P(ys), P(yw), S,
                   P(xp), P(xs), P(xw), S, P(flip) if flip is not None else None, P(out8),
                   P(img_max) if img_max is not None else None, stream())
         return out8
 
-    def _one(self, u8, C, flip, max_rule):
+    def _one(self, u8, C, flip, max_rule, keep_u8=False):
+        """(B,C,S,S) float32 [-1, 1]; keep_u8: also the resized uint8 batch (what the
+        reference's loaders hold before their float conversion)."""
         B, S = u8.shape[0], self.size
         mx = torch.zeros(B, dtype=torch.int32, device=self.device)
         out8 = self.resize_u8(u8, C, flip, mx)
         out = torch.empty(B, C, S, S, dtype=torch.float32, device=self.device)
         _lib.call("irgan_u8_to_unit", P(out8), B, ctypes.c_int64(C * S * S), P(mx), int(max_rule), P(out), stream())
-        return out
+        return (out, out8) if keep_u8 else out
 
     def __call__(self, batch):
         ir8 = batch["ir_u8"].to(self.device, non_blocking=True).contiguous()

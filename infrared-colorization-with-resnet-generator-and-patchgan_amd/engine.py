@@ -36,37 +36,65 @@ IMAGENET_STD = (0.229, 0.224, 0.225)    # ir:673
 # parameter layout (reference state_dict keys / OIHW shapes / order)
 # ----------------------------------------------------------------------------
 
-def g_param_shapes(input_nc=1, output_nc=3, ngf=64, n_blocks=9, no_antialias=False, no_antialias_up=False):
-    """ResnetUNetGenerator state_dict layout (ir:443-531), buffers included."""
+def g_param_shapes(input_nc=1, output_nc=3, ngf=64, n_blocks=9, no_antialias=False, no_antialias_up=False,
+                   use_bias=True, padding_type="reflect", use_dropout=False):
+    """ResnetUNetGenerator state_dict layout (ir:443-531), buffers included.  use_bias:
+    the reference's ``norm_layer == nn.InstanceNorm2d`` (ir:450-455); without it (norm
+    'none') every conv but outc, and the ConvTranspose2d, has no bias."""
     s = OrderedDict()
-    s["inc.1.weight"] = (ngf, input_nc, 7, 7); s["inc.1.bias"] = (ngf,)
-    s["down1.0.weight"] = (2 * ngf, ngf, 3, 3); s["down1.0.bias"] = (2 * ngf,)
+
+    def conv(key, shape):
+        s[key + ".weight"] = shape
+        if use_bias:
+            s[key + ".bias"] = (shape[0],)
+    conv("inc.1", (ngf, input_nc, 7, 7))
+    conv("down1.0", (2 * ngf, ngf, 3, 3))
     if not no_antialias:
         s["down1_down.filt"] = (2 * ngf, 1, 3, 3)
-    s["down2.0.weight"] = (4 * ngf, 2 * ngf, 3, 3); s["down2.0.bias"] = (4 * ngf,)
+    conv("down2.0", (4 * ngf, 2 * ngf, 3, 3))
     if not no_antialias:
         s["down2_down.filt"] = (4 * ngf, 1, 3, 3)
     for b in range(n_blocks):
-        for c in (1, 5):
-            s[f"resblocks.{b}.conv_block.{c}.weight"] = (4 * ngf, 4 * ngf, 3, 3)
-            s[f"resblocks.{b}.conv_block.{c}.bias"] = (4 * ngf,)
+        for c in res_conv_keys(padding_type, use_dropout):
+            conv(f"resblocks.{b}.conv_block.{c}", (4 * ngf, 4 * ngf, 3, 3))
     for name, ch, cat in (("up1", 4 * ngf, 6 * ngf), ("up2", 2 * ngf, 3 * ngf)):
         if no_antialias_up:
-            s[f"{name}_up.weight"] = (ch, ch, 3, 3); s[f"{name}_up.bias"] = (ch,)
+            conv(f"{name}_up", (ch, ch, 3, 3))
         else:
             s[f"{name}_up.filt"] = (ch, 1, 3, 3)
-        s[f"{name}_conv.0.weight"] = (ch // 2, cat, 3, 3); s[f"{name}_conv.0.bias"] = (ch // 2,)
+        conv(f"{name}_conv.0", (ch // 2, cat, 3, 3))
     s["outc.1.weight"] = (output_nc, ngf, 7, 7); s["outc.1.bias"] = (output_nc,)
     return s
 
 
-def d_param_shapes(input_nc=4, ndf=64):
-    """NLayerDiscriminator(n_layers=3) layout (ir:585-632)."""
+def d_layers(n_layers=3):
+    """PatchGAN layer table (ir:585-632): (state key, stride, normalised) per conv.
+    model.0 (s2, LeakyReLU), n_layers - 1 s2 conv/norm/LeakyReLU blocks, one s1
+    conv/norm/LeakyReLU, the s1 1-channel output conv."""
+    out = [("model.0", 2, False)]
+    idx = 2
+    for _ in range(1, n_layers):
+        out.append((f"model.{idx}", 2, True))
+        idx += 3
+    out.append((f"model.{idx}", 1, True))
+    out.append((f"model.{idx + 3}", 1, False))
+    return out
+
+
+def d_channels(input_nc=4, ndf=64, n_layers=3):
+    """Channel counts along the PatchGAN (ir:598-632): ndf * min(2^n, 8)."""
+    return [input_nc] + [ndf * min(2 ** n, 8) for n in range(n_layers + 1)] + [1]
+
+
+def d_param_shapes(input_nc=4, ndf=64, n_layers=3, use_bias=True):
+    """NLayerDiscriminator layout (ir:585-632); the first and last convs always carry a
+    bias, the normalised ones only with InstanceNorm (use_bias, ir:588-593)."""
     s = OrderedDict()
-    chans = [input_nc, ndf, 2 * ndf, 4 * ndf, 8 * ndf, 1]
-    for i, idx in enumerate((0, 2, 5, 8, 11)):
-        s[f"model.{idx}.weight"] = (chans[i + 1], chans[i], 4, 4)
-        s[f"model.{idx}.bias"] = (chans[i + 1],)
+    ch = d_channels(input_nc, ndf, n_layers)
+    for i, (key, _, normed) in enumerate(d_layers(n_layers)):
+        s[key + ".weight"] = (ch[i + 1], ch[i], 4, 4)
+        if use_bias or not normed:
+            s[key + ".bias"] = (ch[i + 1],)
     return s
 
 
@@ -187,9 +215,10 @@ class ParamStore:
         return apply
 
 
-def _pc(store: ParamStore, key: str, spec: ConvSpec, dtype, need_dgrad=True, bias=True):
-    return PackedConv(spec, store.krsc(key + ".weight"), store.krsc(key + ".bias") if bias else None, dtype,
-                      need_dgrad=need_dgrad)
+def _pc(store: ParamStore, key: str, spec: ConvSpec, dtype, need_dgrad=True):
+    """Packed conv of state key ``key``; its bias only if the layout has one (use_bias)."""
+    bias = store.krsc(key + ".bias") if key + ".bias" in store.shapes else None
+    return PackedConv(spec, store.krsc(key + ".weight"), bias, dtype, need_dgrad=need_dgrad)
 
 
 class Buffers:
@@ -329,6 +358,72 @@ class INLayer:
         return ops.conv_dgrad_in(pc, dy, dx, z, bufs.d["mr_" + name], act, work, accumulate=accumulate)
 
 
+class NoNorm(INLayer):
+    """norm='none' (ir:162-163: ``lambda num_features: Identity()``): the layer is just its
+    activation, y = act(z) [+ res], and the conv in front has no bias (use_bias is False,
+    ir:450-455, 588-593).  Same interface as INLayer: the forward applies an identity
+    {mean 0, rstd 1} table through the same apply / fused-resample kernels ((z - 0) * 1 = z
+    exactly), the backward is the activation's derivative."""
+
+    def _ident(self, bufs: Buffers, name: str, N: int, C: int) -> torch.Tensor:
+        mr = bufs.get("mr_" + name, (N * C * 2,), torch.float32)
+        if bufs.state.get("ident_" + name) is not mr:
+            mr.view(-1, 2)[:, 0] = 0.0
+            mr.view(-1, 2)[:, 1] = 1.0
+            bufs.state["ident_" + name] = mr
+        return mr
+
+    def fwd(self, bufs, name, x, y, act, res=None, xhat=None, nb=0, q8=None):
+        if q8 is not None:
+            raise NotImplementedError("the fp8 path runs with InstanceNorm (norm='instance')")
+        ops.in_apply(x, self._ident(bufs, name, x.N, x.C), y, act=act, res=res)
+
+    def conv_fwd8(self, *a, **kw):
+        raise NotImplementedError("the fp8 path runs with InstanceNorm (norm='instance')")
+
+    def conv_fwd(self, bufs, name, pc, x, z, y, act, res=None):
+        ops.conv_fwd(pc, x, z, bias=pc.bias is not None)
+        self.fwd(bufs, name, z, y, act, res=res)
+
+    def conv_stats(self, bufs, name, pc, x, z):
+        ops.conv_fwd(pc, x, z, bias=pc.bias is not None)
+        return self._ident(bufs, name, z.N, z.C)
+
+    def bwd(self, bufs, name, dy, z, act, dx, db=None, dy2=None, q8=None, nb=0):
+        if dy2 is not None or q8 is not None or nb:
+            raise NotImplementedError("NoNorm.bwd: dy2 / q8 / nb are InstanceNorm-path features")
+        if act == ACT_NONE and dx.t.data_ptr() == dy.t.data_ptr() and dx.off == dy.off:
+            pass                                   # identity, in place
+        else:
+            ops.act_bwd(dy, z, act, dx)            # z > 0 <=> act(z) > 0 for ReLU / LeakyReLU
+        if db is not None:
+            ops.channel_sum(dx, db)
+
+    @staticmethod
+    def dgrad_in(*a, **kw):
+        return 0
+
+
+def make_norm(norm: str) -> INLayer:
+    """The engine's per-layer norm for Config.norm (ir:154-165): 'instance' or 'none'
+    ('batch' needs cross-sample statistics (SyncBN under DP): out of scope)."""
+    if norm == "instance":
+        return INLayer()
+    if norm in ("none", None):
+        return NoNorm()
+    raise NotImplementedError(f"norm '{norm}': the HIP engines implement 'instance' and 'none'")
+
+
+def res_conv_keys(padding_type="reflect", use_dropout=False):
+    """Indices of the two convs inside ResnetBlock.conv_block (ir:375-411): the pad
+    modules exist only for reflect / replicate, the Dropout only with use_dropout."""
+    if padding_type not in ("reflect", "replicate", "zero"):
+        raise NotImplementedError(f"Padding [{padding_type}] is not implemented")
+    first = 0 if padding_type == "zero" else 1
+    second = first + 3 + (1 if use_dropout else 0) + (0 if padding_type == "zero" else 1)
+    return first, second
+
+
 # ----------------------------------------------------------------------------
 # generator  (ir:425-569)
 # ----------------------------------------------------------------------------
@@ -337,15 +432,24 @@ class GeneratorEngine:
     _pack_batch = None  # ops.PackBatch of self.packs, built on the first pack()
 
     def __init__(self, store: ParamStore, dtype=BF16, ngf=64, input_nc=1, output_nc=3, n_blocks=9,
-                 no_antialias=False, no_antialias_up=False, fp8=False):
+                 no_antialias=False, no_antialias_up=False, fp8=False, norm="instance", padding_type="reflect",
+                 use_dropout=False, dropout_seed=0):
         """fp8: the ResnetBlock convs (forward and the backward-data interior) run on
         OCP e4m3 operands (BASELINE config 5): per-tensor power-of-two scales, current
         scaling for the re-packed weights, delayed scaling for the activations and
-        gradients they read; everything else (and every weight gradient) stays bf16."""
+        gradients they read; everything else (and every weight gradient) stays bf16.
+        norm / padding_type / use_dropout: the reference's constructor options (ir:154-165,
+        375-411, 443-447); the ResnetBlock convs of padding 'replicate' read an explicitly
+        padded copy of their input (ops.pad) and fold their input gradient back (ops.pad_fold)."""
         self.store, self.dtype, self.ngf = store, dtype, ngf
         self.fp8 = bool(fp8)
         if self.fp8 and (dtype != BF16 or 4 * ngf % 128):
             raise ValueError("the fp8 path runs on the bf16 engine with 4*ngf % 128 == 0")
+        if self.fp8 and (norm != "instance" or padding_type != "reflect" or use_dropout):
+            raise ValueError("the fp8 path runs the default ResnetBlock (InstanceNorm, reflect, no dropout)")
+        self.norm_type, self.padding_type, self.use_dropout = norm, padding_type, bool(use_dropout)
+        self.dropout_seed, self.dropout_calls = int(dropout_seed), 0
+        self.training = True
         self.input_nc, self.output_nc, self.n_blocks = input_nc, output_nc, n_blocks
         self.no_aa, self.no_aa_up = no_antialias, no_antialias_up
         self.tdt = ops.TORCH_DT[dtype]
@@ -355,9 +459,12 @@ class GeneratorEngine:
         self.inc = _pc(S, "inc.1", ConvSpec(input_nc, c0, 7, 1, 3, PAD_REFLECT), dtype, need_dgrad=False)
         self.down1 = _pc(S, "down1.0", ConvSpec(c0, c1, 3, sd, 1, PAD_ZERO), dtype)
         self.down2 = _pc(S, "down2.0", ConvSpec(c1, c2, 3, sd, 1, PAD_ZERO), dtype)
-        self.res = [(_pc(S, f"resblocks.{b}.conv_block.1", ConvSpec(c2, c2, 3, 1, 1, PAD_REFLECT), dtype),
-                     _pc(S, f"resblocks.{b}.conv_block.5", ConvSpec(c2, c2, 3, 1, 1, PAD_REFLECT), dtype))
-                    for b in range(n_blocks)]
+        k1, k2 = res_conv_keys(padding_type, use_dropout)
+        self.res_keys = (k1, k2)
+        rspec = {"reflect": ConvSpec(c2, c2, 3, 1, 1, PAD_REFLECT), "zero": ConvSpec(c2, c2, 3, 1, 1, PAD_ZERO),
+                 "replicate": ConvSpec(c2, c2, 3, 1, 0, PAD_ZERO)}[padding_type]   # replicate: on the padded copy
+        self.res = [(_pc(S, f"resblocks.{b}.conv_block.{k1}", rspec, dtype),
+                     _pc(S, f"resblocks.{b}.conv_block.{k2}", rspec, dtype)) for b in range(n_blocks)]
         if no_antialias_up:
             # ConvTranspose2d(C, C, 3, s2, p1, op1) == backward-data of conv(3, s2, p1)
             self.up1_up = _pc(S, "up1_up", ConvSpec(c2, c2, 3, 2, 1, PAD_ZERO), dtype)
@@ -375,7 +482,7 @@ class GeneratorEngine:
                                                                              p2.dg[0][2])], store.device)
             self.f8a = ops.Fp8Acts(4 * n_blocks, store.device)
         n_in = 5 + 2 * n_blocks
-        self.norms = {k: INLayer() for k in ["inc", "down1", "down2", "up1", "up2"] +
+        self.norms = {k: make_norm(norm) for k in ["inc", "down1", "down2", "up1", "up2"] +
                       [f"r{b}_{i}" for b in range(n_blocks) for i in (1, 2)]}
         assert len(self.norms) == n_in
         self.bufs = Buffers(store.device)
@@ -389,6 +496,30 @@ class GeneratorEngine:
 
     def _w8(self, k):
         return self.f8w.dst[k], ops.Pi(self.f8w.dq, k)
+
+    def _res_in(self, g: Buffers, name: str, x: Feat) -> Feat:
+        """A ResnetBlock conv's input as its conv reads it: x itself (reflect: folded into the
+        conv's loads; zero: the conv's own padding), or the ReplicationPad2d(1) copy (kept for
+        the weight gradient)."""
+        if self.padding_type != "replicate":
+            return x
+        xp = Feat(g.get(name, (x.N, x.H + 2, x.W + 2, x.C), self.tdt))
+        ops.pad(x, xp, 1, "replicate")
+        return xp
+
+    def _res_dgrad(self, g: Buffers, pc, dy: Feat, dx: Feat, accumulate, padbuf):
+        """dx (+)= backward-data of a ResnetBlock conv for the padding type."""
+        if self.padding_type != "replicate":
+            ops.conv_dgrad(pc, dy, dx, accumulate=accumulate, pad_buf=padbuf)
+            return
+        dxp = Feat(g.get("res_dxp", (dx.N, dx.H + 2, dx.W + 2, dx.C), self.tdt))
+        ops.conv_dgrad(pc, dy, dxp)
+        ops.pad_fold(dxp, dx, 1, "replicate", accumulate=accumulate)
+
+    def _bgrad(self, key):
+        """Flat-buffer slice of parameter ``key``'s gradient, None when the layout has no
+        such parameter (use_bias False: no conv biases)."""
+        return self.store.krsc(key, self.store.grad) if key in self.store.shapes else None
 
     # -- shapes
     def _dims(self, H, W):
@@ -404,6 +535,9 @@ class GeneratorEngine:
         c0, c1, c2 = self.ngf, 2 * self.ngf, 4 * self.ngf
         H1, W1, H2, W2 = self._dims(H, W)
         g.state["shape"] = (B, H, W)
+        if self.use_dropout and self.training:   # a fresh mask per forward call; the backward reuses it
+            self.dropout_calls += 1
+            g.state["dropout_seed"] = (self.dropout_seed << 32) ^ (self.dropout_calls << 8)
         ir_buf = g.zeros("ir", (B, H, W, max(8, self.input_nc)), T)   # narrow input zero-padded to 8 ch
         ops.nchw_to_nhwc(ir_nchw.contiguous(), Feat(ir_buf, 0, self.input_nc))
         ir_t = Feat(ir_buf, 0, self.inc.cin_eff)
@@ -450,7 +584,7 @@ class GeneratorEngine:
                                                 ACT_RELU, q8=A.spec(2 * b + 1, x8))
                 A.ensure(2 * b + 1, t, x8)
             else:
-                self.norms[f"r{b}_1"].conv_fwd(g, f"r{b}_1", p1, h, r1, t, ACT_RELU)
+                self.norms[f"r{b}_1"].conv_fwd(g, f"r{b}_1", p1, self._res_in(g, f"xp1_{b}", h), r1, t, ACT_RELU)
             r2 = Feat(g.get(f"r2_{b}", (B, H2, W2, c2), T))
             hn = Feat(g.get(f"h{b + 1}", (B, H2, W2, c2), T))
             if self.fp8:
@@ -460,7 +594,12 @@ class GeneratorEngine:
                 if nxt:
                     A.ensure(nxt, hn, x8)
             else:
-                self.norms[f"r{b}_2"].conv_fwd(g, f"r{b}_2", p2, t, r2, hn, ACT_NONE, res=h)
+                t2 = t
+                if self.use_dropout and self.training:   # nn.Dropout(0.5) after the ReLU (ir:394-395)
+                    t2 = Feat(g.get(f"td{b}", (B, H2, W2, c2), T))
+                    ops.dropout(t, t2, g.state["dropout_seed"] + 2 * b)
+                self.norms[f"r{b}_2"].conv_fwd(g, f"r{b}_2", p2, self._res_in(g, f"xp2_{b}", t2), r2, hn, ACT_NONE,
+                                               res=h)
             h = hn
         if self.fp8:
             self.f8a.update(0, 2 * self.n_blocks)   # next step's forward scales
@@ -544,7 +683,7 @@ class GeneratorEngine:
         da4 = Feat(g.get("da4", (B, H, W, c0), T))
         ops.conv_dgrad(self.outc, Feat(dzo_buf, 0, self.outc.cout_eff), da4, pad_buf=padbuf)
         # up2_conv
-        self.norms["up2"].bwd(g, "up2", da4, Feat(g.d["z4"]), ACT_RELU, da4, db=S.krsc("up2_conv.0.bias", G))
+        self.norms["up2"].bwd(g, "up2", da4, Feat(g.d["z4"]), ACT_RELU, da4, db=self._bgrad("up2_conv.0.bias"))
         wg(self.up2, "up2_conv.0", cat2, da4)
         dcat2 = Feat(g.get("dcat2", (B, H, W, c1 + c0), T))
         ops.conv_dgrad(self.up2, da4, dcat2)
@@ -556,7 +695,7 @@ class GeneratorEngine:
         else:
             ops.upsample_bwd(dy2, da3)
         # up1_conv
-        self.norms["up1"].bwd(g, "up1", da3, Feat(g.d["z3"]), ACT_RELU, da3, db=S.krsc("up1_conv.0.bias", G))
+        self.norms["up1"].bwd(g, "up1", da3, Feat(g.d["z3"]), ACT_RELU, da3, db=self._bgrad("up1_conv.0.bias"))
         wg(self.up1, "up1_conv.0", cat1, da3)
         dcat1 = Feat(g.get("dcat1", (B, H1, W1, c2 + c1), T))
         ops.conv_dgrad(self.up1, da3, dcat1)
@@ -574,30 +713,39 @@ class GeneratorEngine:
         nb2 = 2 * self.n_blocks
         dy8 = Feat(g.get("dy8", (B, H2, W2, c2), torch.float8_e4m3fn)) if self.fp8 else None
         nb_h = 0
+        k1, k2 = self.res_keys
         for b in reversed(range(self.n_blocks)):
             p1, p2 = self.res[b]
             key = f"resblocks.{b}.conv_block."
             t, hb = Feat(g.d[f"t{b}"]), Feat(g.d[f"h{b}"])
             r1, r2 = Feat(g.d[f"r1_{b}"]), Feat(g.d[f"r2_{b}"])
+            drop = self.use_dropout and "dropout_seed" in g.state
+            # the convs' inputs as they read them: the replicate-padded copies, the dropped-out t
+            t2 = Feat(g.d[f"td{b}"]) if drop else t
+            xin1 = Feat(g.d[f"xp1_{b}"]) if self.padding_type == "replicate" else hb
+            xin2 = Feat(g.d[f"xp2_{b}"]) if self.padding_type == "replicate" else t2
             A = self.f8a if self.fp8 else None
             s2, s1 = nb2 + 2 * b, nb2 + 2 * b + 1
             # nb_h: dh's IN-backward partials for r{b}_2, written by the previous block's dgrad
-            self.norms[f"r{b}_2"].bwd(g, f"r{b}_2", dh, r2, ACT_NONE, dt_, db=S.krsc(key + "5.bias", G),
+            self.norms[f"r{b}_2"].bwd(g, f"r{b}_2", dh, r2, ACT_NONE, dt_, db=self._bgrad(f"{key}{k2}.bias"),
                                       q8=A.spec(s2, dy8) if self.fp8 else None, nb=nb_h)
-            wg(p2, key + "5", t, dt_)
+            wg(p2, f"{key}{k2}", xin2, dt_)
             dr = Feat(g.get("dtmp2", (B, H2, W2, c2), T))
             nb_r = 0
             if self.fp8:
                 A.ensure(s2, dt_, dy8)
                 ops.conv_dgrad_fp8(p2, *self._w8(4 * b + 3), dy8, A.dqp(s2), dt_, dr)
             else:
-                # the reduce of r{b}_1's IN backward rides in this dgrad's epilogue
-                nb_r = INLayer.dgrad_in(g, f"r{b}_1", p2, dt_, dr, r1, ACT_RELU)
+                # the reduce of r{b}_1's IN backward rides in this dgrad's epilogue (not through a dropout)
+                if not drop:
+                    nb_r = self.norms[f"r{b}_1"].dgrad_in(g, f"r{b}_1", p2, dt_, dr, r1, ACT_RELU)
                 if not nb_r:
-                    ops.conv_dgrad(p2, dt_, dr, pad_buf=padbuf)
-            self.norms[f"r{b}_1"].bwd(g, f"r{b}_1", dr, r1, ACT_RELU, dr, db=S.krsc(key + "1.bias", G),
+                    self._res_dgrad(g, p2, dt_, dr, False, padbuf)
+                if drop:   # backward of the dropout: the same mask and scale on the gradient
+                    ops.dropout(dr, dr, g.state["dropout_seed"] + 2 * b)
+            self.norms[f"r{b}_1"].bwd(g, f"r{b}_1", dr, r1, ACT_RELU, dr, db=self._bgrad(f"{key}{k1}.bias"),
                                       q8=A.spec(s1, dy8) if self.fp8 else None, nb=nb_r)
-            wg(p1, key + "1", hb, dr)
+            wg(p1, f"{key}{k1}", xin1, dr)
             nb_h = 0
             if self.fp8:
                 A.ensure(s1, dr, dy8)
@@ -605,22 +753,22 @@ class GeneratorEngine:
             else:
                 # ... and the reduce of block b-1's r2 IN backward in this one (dh = d h_b)
                 if b > 0:
-                    nb_h = INLayer.dgrad_in(g, f"r{b - 1}_2", p1, dr, dh, Feat(g.d[f"r2_{b - 1}"]), ACT_NONE,
-                                            accumulate=True)
+                    nb_h = self.norms[f"r{b - 1}_2"].dgrad_in(g, f"r{b - 1}_2", p1, dr, dh, Feat(g.d[f"r2_{b - 1}"]),
+                                                              ACT_NONE, accumulate=True)
                 if not nb_h:
-                    ops.conv_dgrad(p1, dr, dh, accumulate=True, pad_buf=padbuf)
-            ready(key + "1.weight")
+                    self._res_dgrad(g, p1, dr, dh, True, padbuf)
+            ready(f"{key}{k1}.weight")
         if self.fp8:
             self.f8a.update(nb2, nb2)   # next step's backward-data scales
         # down2 (+ blur-down)
         z2 = Feat(g.d["z2"])
         if self.no_aa:
-            self.norms["down2"].bwd(g, "down2", dh, z2, ACT_RELU, dh, db=S.krsc("down2.0.bias", G))
+            self.norms["down2"].bwd(g, "down2", dh, z2, ACT_RELU, dh, db=self._bgrad("down2.0.bias"))
             dz2 = dh
         else:
             dz2 = Feat(g.get("da2", (B, H1, W1, c2), T))
             ops.blur_down_bwd(dh, dz2)
-            self.norms["down2"].bwd(g, "down2", dz2, z2, ACT_RELU, dz2, db=S.krsc("down2.0.bias", G))
+            self.norms["down2"].bwd(g, "down2", dz2, z2, ACT_RELU, dz2, db=self._bgrad("down2.0.bias"))
         wg(self.down2, "down2.0", x1, dz2)
         dx1 = dcat1.sl(c2, c1)
         ops.conv_dgrad(self.down2, dz2, dx1, accumulate=True)  # x1 feeds down2 and the up1 concat
@@ -628,16 +776,16 @@ class GeneratorEngine:
         z1 = Feat(g.d["z1"])
         if self.no_aa:
             dz1 = Feat(g.get("da1", (B, H1, W1, c1), T))
-            self.norms["down1"].bwd(g, "down1", dx1, z1, ACT_RELU, dz1, db=S.krsc("down1.0.bias", G))
+            self.norms["down1"].bwd(g, "down1", dx1, z1, ACT_RELU, dz1, db=self._bgrad("down1.0.bias"))
         else:
             dz1 = Feat(g.get("da1", (B, H, W, c1), T))
             ops.blur_down_bwd(dx1, dz1)
-            self.norms["down1"].bwd(g, "down1", dz1, z1, ACT_RELU, dz1, db=S.krsc("down1.0.bias", G))
+            self.norms["down1"].bwd(g, "down1", dz1, z1, ACT_RELU, dz1, db=self._bgrad("down1.0.bias"))
         wg(self.down1, "down1.0", x0, dz1)
         dx0 = dcat2.sl(c1, c0)
         ops.conv_dgrad(self.down1, dz1, dx0, accumulate=True)
         # inc
-        self.norms["inc"].bwd(g, "inc", dx0, Feat(g.d["z0"]), ACT_RELU, dx0, db=S.krsc("inc.1.bias", G))
+        self.norms["inc"].bwd(g, "inc", dx0, Feat(g.d["z0"]), ACT_RELU, dx0, db=self._bgrad("inc.1.bias"))
         wg(self.inc, "inc.1", Feat(g.d["ir"]), dx0)
         ready("inc.1.weight")
 
@@ -649,16 +797,16 @@ class GeneratorEngine:
 class DiscriminatorEngine:
     _pack_batch = None  # ops.PackBatch of self.packs, built on the first pack()
 
-    LAYERS = (("model.0", 2, False), ("model.2", 2, True), ("model.5", 2, True), ("model.8", 1, True),
-              ("model.11", 1, False))
-
-    def __init__(self, store: ParamStore, dtype=BF16, input_nc=4, ndf=64):
+    def __init__(self, store: ParamStore, dtype=BF16, input_nc=4, ndf=64, n_layers=3, norm="instance"):
+        """PatchGAN with ``n_layers`` stride-2 stages (ir:585-632; train_kaist builds 3) and
+        norm 'instance' or 'none' (the normalised convs then have no bias)."""
         self.store, self.dtype, self.tdt = store, dtype, ops.TORCH_DT[dtype]
-        chans = [input_nc, ndf, 2 * ndf, 4 * ndf, 8 * ndf, 1]
+        self.LAYERS = d_layers(n_layers)
+        chans = d_channels(input_nc, ndf, n_layers)
         self.chans = chans
         self.packs = [_pc(store, k, ConvSpec(chans[i], chans[i + 1], 4, s, 1, PAD_ZERO), dtype)
                       for i, (k, s, _) in enumerate(self.LAYERS)]
-        self.norms = [INLayer() if n else None for (_, _, n) in self.LAYERS]
+        self.norms = [make_norm(norm) if n else None for (_, _, n) in self.LAYERS]
         self.bufs = Buffers(store.device)
 
     def pack(self):
@@ -707,7 +855,7 @@ class DiscriminatorEngine:
                     ops.channel_sum(Feat(dout), S.krsc(key + ".bias", G))
             elif self.norms[i] is not None:
                 self.norms[i].bwd(g, f"{tag}n{i}", dy, pre[i], ACT_LRELU, dy,
-                                  db=S.krsc(key + ".bias", G) if want_wgrad else None)
+                                  db=S.krsc(key + ".bias", G) if want_wgrad and key + ".bias" in S.shapes else None)
             elif want_wgrad:  # layer 0: LReLU mask already folded into dy by the layer-1 dgrad
                 ops.channel_sum(dy, S.krsc(key + ".bias", G))
             if want_wgrad:
@@ -939,8 +1087,9 @@ class GANStep:
         self.tdt = ops.TORCH_DT[dtype]
         self.gen = gen or GeneratorEngine(G, dtype, ngf=cfg.ngf, input_nc=cfg.input_nc, output_nc=cfg.output_nc,
                                           no_antialias=cfg.no_antialias, no_antialias_up=cfg.no_antialias_up,
-                                          fp8=getattr(cfg, "compute_dtype", "bf16") == "fp8")
-        self.dis = dis or DiscriminatorEngine(D, dtype, input_nc=cfg.input_nc + cfg.output_nc)
+                                          fp8=getattr(cfg, "compute_dtype", "bf16") == "fp8", norm=cfg.norm)
+        self.dis = dis or DiscriminatorEngine(D, dtype, input_nc=cfg.input_nc + cfg.output_nc, norm=cfg.norm)
+        self.dbufs = Buffers(G.device)   # the D step's own G forward when G has dropout
         self.vgg = vgg or VGGEngine(V, dtype)
         self.bufs = Buffers(G.device)
         self.losses = torch.zeros(8, dtype=torch.float64, device=G.device)
@@ -988,7 +1137,11 @@ class GANStep:
         if vgg_side:
             ev_vgg = torch.cuda.Event()
             ev_vgg.record(self.side)
-        # ---- G forward once (ir:1638 / 1657 compute the same image)
+        # ---- G forward once: ir:1638 and ir:1657 compute the same image -- unless G has
+        # dropout, whose two calls draw two masks: then the D step gets its own forward
+        # (ir:1638-1639, under no_grad: its activations are never read back)
+        self.gen.training = True
+        fake_d = self.gen.forward(ir, bufs=self.dbufs) if self.gen.use_dropout else None
         fake = self.gen.forward(ir)
         ir_t = Feat(self.gen.bufs.d["ir"])
         # ---- D step on [real; fake] as one 2B batch (ir:1636-1651), on the side stream
@@ -999,7 +1152,7 @@ class GANStep:
         with side_ctx():
             self.D.zero_grad()
             self._din(ir_t, rgb_h, din.batch(0, B))
-            self._din(ir_t, fake, din.batch(B, B))
+            self._din(ir_t, fake if fake_d is None else fake_d, din.batch(B, B))
             pred = self.dis.forward(din, tag="d")
             dpred = b.get("dpred", tuple(pred.shape), torch.float32)
             ops.hinge(pred, pred[:B].numel(), 0, 1.0, dpred, L[0:1])

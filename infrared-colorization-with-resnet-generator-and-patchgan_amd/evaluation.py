@@ -191,7 +191,7 @@ def run_test(cfg, model=None, log=print):
         ir8 = torch.from_numpy(np.stack([u8 for _, u8 in chunk])).to(device)
         B = ir8.shape[0]
         zero = torch.zeros(B, dtype=torch.uint8, device=device)
-        ir_t = resizer._one(ir8, 1, zero, True)                       # load_ir_image + ir_to_tensor
+        ir_t, ir8r = resizer._one(ir8, 1, zero, True, keep_u8=True)   # load_ir_image + ir_to_tensor
         fake = netG.engine.forward(ir_t)                              # (B, S, S, 3) NHWC fp32
         pred8 = rgb_u8(Feat(fake))                                    # tensor_to_rgb_image, per frame
         # ground truth: <seq>/visible/<file> (ir:1401-1404), resized on the device
@@ -211,7 +211,9 @@ def run_test(cfg, model=None, log=print):
             for i, g in zip(have, g_res.cpu().numpy()):
                 gt_u8[i] = g
         pred_np = pred8.cpu().numpy()
-        ir_np = (ir_t[:, 0].cpu().numpy() + 1.0) / 2.0
+        # the collage's IR panel from load_ir_image's own float32 v / 255 (ir:823-827, 1374),
+        # not from the [-1, 1] tensor (x + 1) / 2, which truncates some gray levels one lower
+        ir_np = [D._unit_ir(u8) for u8 in ir8r[:, 0].cpu().numpy()]
         for i, ((ir_path, set_name, seq_name), _) in enumerate(chunk):
             done += 1
             base = os.path.basename(ir_path)

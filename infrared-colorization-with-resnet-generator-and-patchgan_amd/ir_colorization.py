@@ -32,8 +32,8 @@ import torch
 import torch.nn as nn
 
 from . import ops
-from .engine import (Buffers, DiscriminatorEngine, GANStep, GeneratorEngine, ParamStore, VGGEngine,
-                     d_param_shapes, g_param_shapes, vgg_param_shapes)
+from .engine import (Buffers, DiscriminatorEngine, GANStep, GeneratorEngine, ParamStore, VGGEngine, d_layers,
+                     d_param_shapes, g_param_shapes, res_conv_keys, vgg_param_shapes)
 from .ops import BF16, F32, Feat
 
 __all__ = ["Config", "Identity", "get_norm_layer", "init_weights", "init_net", "get_lr_lambda", "get_filter",
@@ -123,9 +123,23 @@ def get_norm_layer(norm_type="instance"):
     raise NotImplementedError(f"Normalization type [{norm_type}] not supported")
 
 
-def _is_instance(norm_layer):
+def _norm_name(norm_layer):
+    """The engine norm for a reference norm_layer (ir:154-165): nn.InstanceNorm2d ->
+    'instance', get_norm_layer('none')'s Identity factory -> 'none'.  nn.BatchNorm2d
+    needs cross-sample statistics (SyncBN under data parallelism): out of scope."""
     f = norm_layer.func if isinstance(norm_layer, functools.partial) else norm_layer
-    return f is nn.InstanceNorm2d
+    if f is nn.InstanceNorm2d:
+        return "instance"
+    if f is nn.BatchNorm2d:
+        raise NotImplementedError("norm='batch' is out of scope for the HIP engines (SURVEY.md 8e); "
+                                  "use 'instance' (the reference default) or 'none'")
+    try:
+        probe = norm_layer(4)
+    except Exception:
+        probe = None
+    if isinstance(probe, (Identity, nn.Identity)):
+        return "none"
+    raise NotImplementedError(f"unsupported norm_layer {norm_layer!r}")
 
 
 def init_weights(net, init_type="normal", init_gain=0.02, generator=None):
@@ -217,10 +231,10 @@ def _dtype_code(name):
 class _Slot(nn.Module):
     """Holds the weight/bias Parameters (OIHW views into a ParamStore)."""
 
-    def __init__(self, store: ParamStore, key: str, bias=True):
+    def __init__(self, store: ParamStore, key: str):
         super().__init__()
         self.weight = nn.Parameter(store.oihw(key + ".weight"))
-        if bias:
+        if key + ".bias" in store.shapes:   # use_bias (ir:450-455, 588-593)
             self.bias = nn.Parameter(store.oihw(key + ".bias"))
 
 
@@ -305,14 +319,12 @@ class ResnetUNetGenerator(_StoreModule):
                  compute_dtype="bf16"):
         super().__init__()
         assert n_blocks >= 0
-        if not _is_instance(norm_layer):
-            raise NotImplementedError("HIP generator implements norm='instance' (the reference default)")
-        if use_dropout or padding_type != "reflect":
-            raise NotImplementedError("HIP generator implements use_dropout=False, padding_type='reflect' "
-                                      "(the configuration IRColorizationModel builds, ir:767-775)")
+        norm = _norm_name(norm_layer)
+        k1, k2 = res_conv_keys(padding_type, use_dropout)   # raises on an unknown padding (ir:380-386)
         device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
-        self.store = ParamStore(g_param_shapes(input_nc, output_nc, ngf, n_blocks, no_antialias, no_antialias_up),
-                                device)
+        self.store = ParamStore(g_param_shapes(input_nc, output_nc, ngf, n_blocks, no_antialias, no_antialias_up,
+                                               use_bias=norm == "instance", padding_type=padding_type,
+                                               use_dropout=use_dropout), device)
         S = self.store
         self.inc = _seq(None, _Slot(S, "inc.1"), None, None)
         self.down1 = _seq(_Slot(S, "down1.0"), None, None)
@@ -320,10 +332,11 @@ class ResnetUNetGenerator(_StoreModule):
         self.down2 = _seq(_Slot(S, "down2.0"), None, None)
         self.down2_down = None if no_antialias else _Filt(4 * ngf, device)
         blocks = []
+        nmods = k2 + 2   # [pad] conv norm relu [dropout] [pad] conv norm (ir:375-411)
         for b in range(n_blocks):
             blk = nn.Module()
-            blk.conv_block = _seq(None, _Slot(S, f"resblocks.{b}.conv_block.1"), None, None, None,
-                                  _Slot(S, f"resblocks.{b}.conv_block.5"), None)
+            blk.conv_block = _seq(*[_Slot(S, f"resblocks.{b}.conv_block.{i}") if i in (k1, k2) else None
+                                    for i in range(nmods)])
             blocks.append(blk)
         self.resblocks = nn.Sequential(*blocks)
         self.up1_up = _Slot(S, "up1_up") if no_antialias_up else _Filt(4 * ngf, device)
@@ -333,12 +346,14 @@ class ResnetUNetGenerator(_StoreModule):
         self.outc = _seq(None, _Slot(S, "outc.1"), None)
         self.engine = GeneratorEngine(S, _dtype_code(compute_dtype), ngf=ngf, input_nc=input_nc,
                                       output_nc=output_nc, n_blocks=n_blocks, no_antialias=no_antialias,
-                                      no_antialias_up=no_antialias_up, fp8=compute_dtype == "fp8")
+                                      no_antialias_up=no_antialias_up, fp8=compute_dtype == "fp8", norm=norm,
+                                      padding_type=padding_type, use_dropout=use_dropout)
         self._dirty = True
 
     def forward(self, x, layers=None, encode_only=False):
         _require_cuda(x, "ResnetUNetGenerator")
         self.repack()  # parameters may have been changed in place by any optimizer
+        self.engine.training = self.training   # nn.Dropout follows train() / eval() (ir:394-395)
         params = [p for _, p in self.named_parameters()]
         if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params)):
             return _GFn.apply(x, self, *params), None
@@ -383,19 +398,21 @@ class _DFn(torch.autograd.Function):
 
 
 class NLayerDiscriminator(_StoreModule):
-    """ir:576-635 (n_layers=3, the configuration train_kaist builds)."""
+    """ir:576-635: any n_layers >= 1 (train_kaist builds 3), norm 'instance' or 'none'."""
 
     def __init__(self, input_nc, ndf=64, n_layers=3, norm_layer=nn.InstanceNorm2d, device=None,
                  compute_dtype="bf16"):
         super().__init__()
-        if n_layers != 3 or not _is_instance(norm_layer):
-            raise NotImplementedError("HIP PatchGAN implements n_layers=3 with InstanceNorm (ir:1591-1596)")
+        assert n_layers >= 1
+        norm = _norm_name(norm_layer)
         device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
-        self.store = ParamStore(d_param_shapes(input_nc, ndf), device)
+        self.store = ParamStore(d_param_shapes(input_nc, ndf, n_layers, use_bias=norm == "instance"), device)
         S = self.store
-        self.model = _seq(_Slot(S, "model.0"), None, _Slot(S, "model.2"), None, None, _Slot(S, "model.5"), None,
-                          None, _Slot(S, "model.8"), None, None, _Slot(S, "model.11"))
-        self.engine = DiscriminatorEngine(S, _dtype_code(compute_dtype), input_nc=input_nc, ndf=ndf)
+        keys = [k for k, _, _ in d_layers(n_layers)]
+        last = int(keys[-1].split(".")[1])
+        self.model = _seq(*[_Slot(S, f"model.{i}") if f"model.{i}" in keys else None for i in range(last + 1)])
+        self.engine = DiscriminatorEngine(S, _dtype_code(compute_dtype), input_nc=input_nc, ndf=ndf,
+                                          n_layers=n_layers, norm=norm)
         self._dirty = True
 
     def forward(self, x):
@@ -508,20 +525,20 @@ def tv_loss(x):
 
 class _SSIMFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, a, b, size_average):
+    def forward(ctx, a, b, size_average, window):
         # kernel takes [-1,1] images and maps (x+1)/2 itself; feed 2x-1 of the [0,1] inputs
         an, bn = _nhwc32(a * 2 - 1), _nhwc32(b * 2 - 1)
         g = torch.zeros_like(an)
         if size_average:   # 1 - mean over B*C*H*W (ir:744-745): one launch over the batch
             loss = torch.zeros(1, dtype=torch.float64, device=a.device)
             work = torch.empty(10 * an.numel(), device=a.device)
-            ops.ssim(Feat(an), Feat(bn), 1.0, g, loss, work)
+            ops.ssim(Feat(an), Feat(bn), 1.0, g, loss, work, window)
         else:              # 1 - per-image mean over C*H*W (ir:746-747): one launch per image
             B = an.shape[0]
             loss = torch.zeros(B, dtype=torch.float64, device=a.device)
             work = torch.empty(10 * an[0].numel(), device=a.device)
             for i in range(B):
-                ops.ssim(Feat(an[i:i + 1]), Feat(bn[i:i + 1]), 1.0, g[i:i + 1], loss[i:i + 1], work)
+                ops.ssim(Feat(an[i:i + 1]), Feat(bn[i:i + 1]), 1.0, g[i:i + 1], loss[i:i + 1], work, window)
         ctx.save_for_backward(g)
         ctx.size_average = size_average
         out = loss.float()
@@ -534,17 +551,19 @@ class _SSIMFn(torch.autograd.Function):
         ops.nhwc_to_nchw(Feat(g), out, scale=2.0)  # d/d(img01) = 2 * d/d(img[-1,1])
         if not ctx.size_average:
             gl = gl.view(-1, 1, 1, 1)
-        return out * gl, None, None
+        return out * gl, None, None, None
 
 
 def ssim_loss_torch(img1, img2, window_size=11, size_average=True):
-    """ir:714-750: 1 - SSIM of [0,1] images (11x11 Gaussian, sigma 1.5); a scalar,
-    or with size_average=False the per-image vector (B,) of ir:746-747."""
+    """ir:714-750: 1 - SSIM of [0,1] images (window_size^2 Gaussian, sigma 1.5, zero
+    padding window_size // 2); a scalar, or with size_average=False the per-image
+    vector (B,) of ir:746-747.  Odd window sizes 1..15 (default 11)."""
     assert img1.shape == img2.shape, "SSIM images must have the same shape"
-    if window_size != 11:
-        raise NotImplementedError("HIP SSIM implements window_size=11 (the reference's default, ir:714)")
+    if window_size % 2 == 0 or not 1 <= window_size <= 15:
+        raise NotImplementedError("HIP SSIM implements odd window sizes 1..15 (an even window's padding changes "
+                                  "the map size)")
     _require_cuda(img1, "ssim_loss_torch")
-    return _SSIMFn.apply(img1, img2, bool(size_average))
+    return _SSIMFn.apply(img1, img2, bool(size_average), int(window_size))
 
 
 # =============================================================================

@@ -293,10 +293,11 @@ RING_MFMA = not os.environ.get("IRGAN_NO_RING_MFMA")
 
 def conv_dgrad(pc: PackedConv, dy: Feat, dx: Feat, accumulate=False, mask: Feat = None, mask_act=0,
                pad_buf: torch.Tensor = None, bias=False):
-    """dx = d(conv)/dx^T dy.  Reflect-padded layers: interior straight into dx,
-    then the padded ring folded onto dx's border band -- by irgan_reflect_dgrad_ring
-    (bf16, one MFMA launch) or as split-K partials in pad_buf (fp32 scratch)
-    folded by irgan_reflect_ring_fold; stride-2 layers launch per phase."""
+    """dx = d(conv)/dx^T dy.  Reflect-padded layers: interior straight into dx and the
+    padded ring folded onto dx's border band -- bf16: irgan_conv_dgrad_reflect (one
+    launch with the ring folded in on the ResnetBlock shapes, else interior + the MFMA
+    ring launch); fp32: split-K ring partials in pad_buf (fp32 scratch) folded by
+    irgan_reflect_ring_fold; stride-2 layers launch per phase."""
     s = pc.spec
     assert dy.C == pc.cout_eff and dx.C == s.cin and dy.dt == pc.dtype
     if pc.reflect:
@@ -318,10 +319,12 @@ def conv_dgrad(pc: PackedConv, dy: Feat, dx: Feat, accumulate=False, mask: Feat 
                      and W >= 2 * p + 2 and dy.ld % 8 == 0 and dy.off % 8 == 0)
 
         def launch():
-            _lib.call("irgan_conv_fwd", ctypes.byref(d), dy.ptr, P(buf), None, dx.ptr, None, stream())
             if ring_mfma:
-                # one launch: ring values of g by MFMA, added onto their mirrored border pixels
-                _lib.call("irgan_reflect_dgrad_ring", ctypes.byref(d), dy.ptr, P(buf), p, dx.ptr, stream())
+                # interior + ring fold: one conv_pp launch on the ResnetBlock shapes, else the
+                # interior launch + the MFMA ring launch (irgan_conv_dgrad_reflect decides)
+                _lib.call("irgan_conv_dgrad_reflect", ctypes.byref(d), dy.ptr, P(buf), p, dx.ptr, stream())
+            else:
+                _lib.call("irgan_conv_fwd", ctypes.byref(d), dy.ptr, P(buf), None, dx.ptr, None, stream())
 
         # the timed dgrad op is the whole backward-data: interior + ring
         TIMER.wrap(conv_tag("dgrad", s, (H, W), dx.N), launch)
@@ -659,6 +662,44 @@ def resize_bwd(dy: Feat, dx: Feat, accumulate=False):
                  accumulate)
 
 
+def pad_table(n_in, p, mode, transpose=False, device=None):
+    """Per-axis (idx, w, rows, T) table of nn.ReflectionPad2d(p) (mode "reflect") or
+    nn.ReplicationPad2d(p) ("replicate", ir:383, 404): padded coordinate u reads
+    reflect(u - p) / clamp(u - p, 0, n_in - 1); transpose: the fold (its adjoint)."""
+    if mode == "reflect":
+        return resample_table(RS_PAD, n_in, p, transpose, device)
+    import numpy as np
+    dev = _dev(device)
+    key = ("replicate", n_in, p, bool(transpose), dev)
+    t = _TABLES.get(key)
+    if t is None:
+        M = np.zeros((n_in + 2 * p, n_in), np.float64)
+        for u in range(n_in + 2 * p):
+            M[u, min(max(u - p, 0), n_in - 1)] = 1.0
+        t = _TABLES[key] = _device_table(*_table_from_dense(M.T.copy() if transpose else M), dev)
+    return t
+
+
+def pad(x: Feat, y: Feat, p: int, mode):
+    """y = ReflectionPad2d(p) / ReplicationPad2d(p) of x (y is (H + 2p) x (W + 2p))."""
+    sep_resample(x, y, pad_table(x.H, p, mode, device=x.t.device), pad_table(x.W, p, mode, device=x.t.device))
+
+
+def pad_fold(dxp: Feat, dx: Feat, p: int, mode, accumulate=False):
+    """Backward of pad(): every padded position's gradient added onto the pixel it copied."""
+    sep_resample(dxp, dx, pad_table(dx.H, p, mode, True, dx.t.device), pad_table(dx.W, p, mode, True, dx.t.device),
+                 accumulate)
+
+
+def dropout(x: Feat, y: Feat, seed: int, p: float = 0.5):
+    """nn.Dropout(p) in training mode (ir:394-395): y = x * keep / (1 - p), keep ~ Bernoulli(1 - p)
+    from a counter-based hash of (seed, element index) -- the backward applies the same
+    call to the gradient (same seed -> same mask, same scale)."""
+    assert (x.N, x.H, x.W, x.C) == (y.N, y.H, y.W, y.C)
+    _lib.call("irgan_dropout", x.ptr, x.dt, x.P, x.C, x.ld, x.off, y.ptr, y.dt, y.ld, y.off,
+              ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), ctypes.c_float(p), stream())
+
+
 def reflect_fold(dxpad: Feat, dx: Feat, p: int, accumulate=False):
     """Backward of nn.ReflectionPad2d(p): dx[q] = sum over padded u with reflect(u-p) = q."""
     sep_resample(dxpad, dx, resample_table(RS_PAD, dx.H, p, transpose=True),
@@ -716,8 +757,9 @@ def tv(x: Feat, w: float, g: torch.Tensor, loss: torch.Tensor):
     _lib.call("irgan_tv", x.ptr, x.N, x.H, x.W, x.C, ctypes.c_float(w), P(g), P(loss), stream())
 
 
-def ssim(a: Feat, b: Feat, w: float, g: torch.Tensor, loss: torch.Tensor, work: torch.Tensor):
-    _lib.call("irgan_ssim", a.ptr, b.ptr, a.N, a.H, a.W, a.C, ctypes.c_float(w), P(g), P(loss), P(work), stream())
+def ssim(a: Feat, b: Feat, w: float, g: torch.Tensor, loss: torch.Tensor, work: torch.Tensor, window: int = 11):
+    _lib.call("irgan_ssim_ws", a.ptr, b.ptr, a.N, a.H, a.W, a.C, ctypes.c_float(w), P(g), P(loss), P(work), window,
+              stream())
 
 
 def adam(p, g, m, v, step: int, lr: float, b1: float, b2: float, eps: float):

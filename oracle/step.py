@@ -46,36 +46,47 @@ def binomial_filter(n: int = 3) -> torch.Tensor:
     return f / f.sum()
 
 
+def res_conv_keys(padding_type="reflect", use_dropout=False):
+    """Indices of the two convs in ResnetBlock.conv_block (ir:375-411): pad modules only
+    for reflect / replicate, the Dropout only with use_dropout."""
+    first = 0 if padding_type == "zero" else 1
+    return first, first + 3 + int(bool(use_dropout)) + (0 if padding_type == "zero" else 1)
+
+
 def g_param_shapes(input_nc=1, output_nc=3, ngf=64, n_blocks=9,
-                   no_antialias=False, no_antialias_up=False):
-    """Generator state_dict layout (ir:443-531); buffers 'filt' included."""
+                   no_antialias=False, no_antialias_up=False, use_bias=True, padding_type="reflect",
+                   use_dropout=False):
+    """Generator state_dict layout (ir:443-531); buffers 'filt' included.
+    use_bias = (norm_layer == nn.InstanceNorm2d) (ir:450-455): norm 'none' drops every
+    conv bias but outc's."""
     s = OrderedDict()
-    s["inc.1.weight"] = (ngf, input_nc, 7, 7); s["inc.1.bias"] = (ngf,)
-    s["down1.0.weight"] = (2 * ngf, ngf, 3, 3); s["down1.0.bias"] = (2 * ngf,)
+    b = lambda key, c: s.__setitem__(key, (c,)) if use_bias else None   # noqa: E731
+    s["inc.1.weight"] = (ngf, input_nc, 7, 7); b("inc.1.bias", ngf)
+    s["down1.0.weight"] = (2 * ngf, ngf, 3, 3); b("down1.0.bias", 2 * ngf)
     if not no_antialias:
         s["down1_down.filt"] = (2 * ngf, 1, 3, 3)
-    s["down2.0.weight"] = (4 * ngf, 2 * ngf, 3, 3); s["down2.0.bias"] = (4 * ngf,)
+    s["down2.0.weight"] = (4 * ngf, 2 * ngf, 3, 3); b("down2.0.bias", 4 * ngf)
     if not no_antialias:
         s["down2_down.filt"] = (4 * ngf, 1, 3, 3)
-    for b in range(n_blocks):
-        for c in (1, 5):
-            s[f"resblocks.{b}.conv_block.{c}.weight"] = (4 * ngf, 4 * ngf, 3, 3)
-            s[f"resblocks.{b}.conv_block.{c}.bias"] = (4 * ngf,)
+    for blk in range(n_blocks):
+        for c in res_conv_keys(padding_type, use_dropout):
+            s[f"resblocks.{blk}.conv_block.{c}.weight"] = (4 * ngf, 4 * ngf, 3, 3)
+            b(f"resblocks.{blk}.conv_block.{c}.bias", 4 * ngf)
     if no_antialias_up:
-        s["up1_up.weight"] = (4 * ngf, 4 * ngf, 3, 3); s["up1_up.bias"] = (4 * ngf,)
+        s["up1_up.weight"] = (4 * ngf, 4 * ngf, 3, 3); b("up1_up.bias", 4 * ngf)
     else:
         s["up1_up.filt"] = (4 * ngf, 1, 3, 3)
-    s["up1_conv.0.weight"] = (2 * ngf, 6 * ngf, 3, 3); s["up1_conv.0.bias"] = (2 * ngf,)
+    s["up1_conv.0.weight"] = (2 * ngf, 6 * ngf, 3, 3); b("up1_conv.0.bias", 2 * ngf)
     if no_antialias_up:
-        s["up2_up.weight"] = (2 * ngf, 2 * ngf, 3, 3); s["up2_up.bias"] = (2 * ngf,)
+        s["up2_up.weight"] = (2 * ngf, 2 * ngf, 3, 3); b("up2_up.bias", 2 * ngf)
     else:
         s["up2_up.filt"] = (2 * ngf, 1, 3, 3)
-    s["up2_conv.0.weight"] = (ngf, 3 * ngf, 3, 3); s["up2_conv.0.bias"] = (ngf,)
+    s["up2_conv.0.weight"] = (ngf, 3 * ngf, 3, 3); b("up2_conv.0.bias", ngf)
     s["outc.1.weight"] = (output_nc, ngf, 7, 7); s["outc.1.bias"] = (output_nc,)
     return s
 
 
-def d_param_shapes(input_nc=4, ndf=64, n_layers=3):
+def d_param_shapes(input_nc=4, ndf=64, n_layers=3, use_bias=True):
     """PatchGAN state_dict layout (ir:585-632)."""
     s = OrderedDict()
     s["model.0.weight"] = (ndf, input_nc, 4, 4); s["model.0.bias"] = (ndf,)
@@ -83,11 +94,13 @@ def d_param_shapes(input_nc=4, ndf=64, n_layers=3):
     for n in range(1, n_layers):
         prev, mult = mult, min(2 ** n, 8)
         s[f"model.{idx}.weight"] = (ndf * mult, ndf * prev, 4, 4)
-        s[f"model.{idx}.bias"] = (ndf * mult,)
+        if use_bias:
+            s[f"model.{idx}.bias"] = (ndf * mult,)
         idx += 3
     prev, mult = mult, min(2 ** n_layers, 8)
     s[f"model.{idx}.weight"] = (ndf * mult, ndf * prev, 4, 4)
-    s[f"model.{idx}.bias"] = (ndf * mult,)
+    if use_bias:
+        s[f"model.{idx}.bias"] = (ndf * mult,)
     idx += 3
     s[f"model.{idx}.weight"] = (1, ndf * mult, 4, 4); s[f"model.{idx}.bias"] = (1,)
     return s
@@ -127,8 +140,14 @@ def seeded_params(shapes, seed, weight_std=0.02, bias_std=0.0, kaiming=False):
 
 def pre_in_bias_keys(keys):
     """Biases of convs followed by InstanceNorm: their gradient is exactly 0 in
-    exact arithmetic (IN subtracts the channel mean), so fp32 values are noise."""
-    return [k for k in keys if k.endswith(".bias") and not k.startswith(("outc.", "model.0.", "model.11.", "up1_up.", "up2_up."))]
+    exact arithmetic (IN subtracts the channel mean), so fp32 values are noise.
+    Not normalised: outc, the ConvTranspose2d ups, the PatchGAN's first and last conv
+    (the last is the highest model.N, whatever n_layers is)."""
+    keys = list(keys)
+    dix = [int(k.split(".")[1]) for k in keys if k.startswith("model.")]
+    last = f"model.{max(dix)}." if dix else None
+    free = ("outc.", "model.0.", "up1_up.", "up2_up.") + ((last,) if last else ())
+    return [k for k in keys if k.endswith(".bias") and not k.startswith(free)]
 
 
 PRE_IN_BIAS_G = pre_in_bias_keys(g_param_shapes().keys())
@@ -199,63 +218,91 @@ class _Fp8ResConv(torch.autograd.Function):
         return g8[..., 1:-1, 1:-1] + ring, dw, gy.sum(dim=(0, 2, 3))
 
 
-def g_forward(P, x, no_antialias=False, no_antialias_up=False, n_blocks=9, acts=None, fp8=False):
+def _res_conv(h, w, b, padding_type):
+    """[ReflectionPad2d(1) | ReplicationPad2d(1) | -] + Conv2d(3, padding 0 | 0 | 1) (ir:380-411)."""
+    if padding_type == "reflect":
+        return F.conv2d(_rpad(h, 1), w, b)
+    if padding_type == "replicate":
+        return F.conv2d(F.pad(h, (1, 1, 1, 1), mode="replicate"), w, b)
+    if padding_type == "zero":
+        return F.conv2d(h, w, b, padding=1)
+    raise NotImplementedError(f"Padding [{padding_type}] is not implemented")
+
+
+def g_forward(P, x, no_antialias=False, no_antialias_up=False, n_blocks=9, acts=None, fp8=False, norm="instance",
+              padding_type="reflect", dropout_masks=None):
     """ResnetUNetGenerator.forward (ir:533-569); returns the tanh image.
-    fp8=True: the ResnetBlock convs as the fp8 path computes them (_Fp8ResConv)."""
+    fp8=True: the ResnetBlock convs as the fp8 path computes them (_Fp8ResConv).
+    norm 'none': Identity norm layers and no conv biases (ir:162-163, 450-455: absent
+    keys read as None).  padding_type: the ResnetBlock padding (ir:380-411).
+    dropout_masks: per block a tensor of keep / (1 - p) factors multiplied after the
+    ResnetBlock's ReLU -- nn.Dropout(0.5) in training mode with given masks (ir:394-395);
+    None = no dropout layer or eval mode."""
+    nrm = _inorm if norm == "instance" else (lambda t: t)   # noqa: E731
+    bias = lambda k: P.get(k)                                # noqa: E731
+    k1, k2 = res_conv_keys(padding_type, dropout_masks is not None)
+
     def rec(name, t):
         if acts is not None:
             acts[name] = t
         return t
-    x0 = rec("x0", F.relu(_inorm(F.conv2d(_rpad(x, 3), P["inc.1.weight"], P["inc.1.bias"]))))
+    x0 = rec("x0", F.relu(nrm(F.conv2d(_rpad(x, 3), P["inc.1.weight"], bias("inc.1.bias")))))
     s = 2 if no_antialias else 1
-    x1 = F.relu(_inorm(F.conv2d(x0, P["down1.0.weight"], P["down1.0.bias"], stride=s, padding=1)))
+    x1 = F.relu(nrm(F.conv2d(x0, P["down1.0.weight"], bias("down1.0.bias"), stride=s, padding=1)))
     if not no_antialias:
         x1 = blur_down(x1, P["down1_down.filt"])
     rec("x1", x1)
-    x2 = F.relu(_inorm(F.conv2d(x1, P["down2.0.weight"], P["down2.0.bias"], stride=s, padding=1)))
+    x2 = F.relu(nrm(F.conv2d(x1, P["down2.0.weight"], bias("down2.0.bias"), stride=s, padding=1)))
     if not no_antialias:
         x2 = blur_down(x2, P["down2_down.filt"])
     h = rec("x2", x2)
     for b in range(n_blocks):
         pre = f"resblocks.{b}.conv_block."
+        w1, b1, w2, b2 = P[f"{pre}{k1}.weight"], bias(f"{pre}{k1}.bias"), P[f"{pre}{k2}.weight"], bias(f"{pre}{k2}.bias")
         if fp8:
-            t = F.relu(_inorm(_Fp8ResConv.apply(h, P[pre + "1.weight"], P[pre + "1.bias"])))
-            t = _inorm(_Fp8ResConv.apply(t, P[pre + "5.weight"], P[pre + "5.bias"]))
+            t = F.relu(nrm(_Fp8ResConv.apply(h, w1, b1)))
+            t = nrm(_Fp8ResConv.apply(t, w2, b2))
         else:
-            t = F.relu(_inorm(F.conv2d(_rpad(h, 1), P[pre + "1.weight"], P[pre + "1.bias"])))
-            t = _inorm(F.conv2d(_rpad(t, 1), P[pre + "5.weight"], P[pre + "5.bias"]))
+            t = F.relu(nrm(_res_conv(h, w1, b1, padding_type)))
+            if dropout_masks is not None:
+                t = t * dropout_masks[b]
+            t = nrm(_res_conv(t, w2, b2, padding_type))
         h = h + t                                              # ir:417-418
     rec("x3", h)
     if no_antialias_up:
-        y = F.conv_transpose2d(h, P["up1_up.weight"], P["up1_up.bias"], stride=2,
+        y = F.conv_transpose2d(h, P["up1_up.weight"], bias("up1_up.bias"), stride=2,
                                padding=1, output_padding=1)    # ir:495-500
     else:
         y = up_aa(h, P["up1_up.filt"])
     if y.shape[-2:] != x1.shape[-2:]:                          # ir:555-556
         y = F.interpolate(y, size=x1.shape[-2:], mode="bilinear", align_corners=True)
-    y = F.relu(_inorm(F.conv2d(torch.cat([y, x1], 1), P["up1_conv.0.weight"],
-                                P["up1_conv.0.bias"], padding=1)))
+    y = F.relu(nrm(F.conv2d(torch.cat([y, x1], 1), P["up1_conv.0.weight"],
+                            bias("up1_conv.0.bias"), padding=1)))
     rec("u1", y)
     if no_antialias_up:
-        y = F.conv_transpose2d(y, P["up2_up.weight"], P["up2_up.bias"], stride=2,
+        y = F.conv_transpose2d(y, P["up2_up.weight"], bias("up2_up.bias"), stride=2,
                                padding=1, output_padding=1)
     else:
         y = up_aa(y, P["up2_up.filt"])
     if y.shape[-2:] != x0.shape[-2:]:
         y = F.interpolate(y, size=x0.shape[-2:], mode="bilinear", align_corners=True)
-    y = F.relu(_inorm(F.conv2d(torch.cat([y, x0], 1), P["up2_conv.0.weight"],
-                                P["up2_conv.0.bias"], padding=1)))
+    y = F.relu(nrm(F.conv2d(torch.cat([y, x0], 1), P["up2_conv.0.weight"],
+                            bias("up2_conv.0.bias"), padding=1)))
     rec("u2", y)
     return torch.tanh(F.conv2d(_rpad(y, 3), P["outc.1.weight"], P["outc.1.bias"]))
 
 
-def d_forward(P, x):
-    """NLayerDiscriminator.forward (ir:585-635), default n_layers=3."""
+def d_forward(P, x, n_layers=3, norm="instance"):
+    """NLayerDiscriminator.forward (ir:585-635): conv s2 + LReLU, n_layers - 1 conv s2 +
+    norm + LReLU, conv s1 + norm + LReLU, conv s1 to one channel."""
+    nrm = _inorm if norm == "instance" else (lambda t: t)   # noqa: E731
     h = F.leaky_relu(F.conv2d(x, P["model.0.weight"], P["model.0.bias"], stride=2, padding=1), LRELU)
-    for idx, s in ((2, 2), (5, 2), (8, 1)):
-        h = F.leaky_relu(_inorm(F.conv2d(h, P[f"model.{idx}.weight"], P[f"model.{idx}.bias"],
-                                         stride=s, padding=1)), LRELU)
-    return F.conv2d(h, P["model.11.weight"], P["model.11.bias"], stride=1, padding=1)
+    stages = [(2 + 3 * i, 2) for i in range(n_layers - 1)] + [(2 + 3 * (n_layers - 1), 1)]
+    for idx, s in stages:
+        h = F.leaky_relu(nrm(F.conv2d(h, P[f"model.{idx}.weight"], P.get(f"model.{idx}.bias"),
+                                      stride=s, padding=1)), LRELU)
+    last = 2 + 3 * n_layers
+    return F.conv2d(h, P[f"model.{last}.weight"], P[f"model.{last}.bias"], stride=1, padding=1)
 
 
 def vgg_features(V, x):
@@ -282,8 +329,9 @@ def gaussian_window(n=11, sigma=1.5, dtype=torch.float32):
     return g / g.sum()
 
 
-def ssim_loss(a, b, window_size=11):
-    """1 - mean SSIM with 11x11 Gaussian, zero pad, C1=1e-4, C2=9e-4 (ir:714-750)."""
+def ssim_loss(a, b, window_size=11, size_average=True):
+    """1 - mean SSIM with a window_size^2 Gaussian (sigma 1.5), zero pad window_size // 2,
+    C1=1e-4, C2=9e-4 (ir:714-750); size_average=False: the per-image vector (ir:746-747)."""
     c = a.shape[1]
     g = gaussian_window(window_size, 1.5, a.dtype)[:, None]
     w = (g @ g.t()).expand(c, 1, window_size, window_size).contiguous()
@@ -295,7 +343,7 @@ def ssim_loss(a, b, window_size=11):
     s12 = blur(a * b) - mu1 * mu2
     C1, C2 = 0.01 ** 2, 0.03 ** 2
     m = ((2 * mu1 * mu2 + C1) * (2 * s12 + C2)) / ((mu1 * mu1 + mu2 * mu2 + C1) * (s11 + s22 + C2))
-    return 1.0 - m.mean()
+    return 1.0 - (m.mean() if size_average else m.mean(dim=[1, 2, 3]))
 
 
 def lr_lambda(epoch, lr_decay_start_epoch=40, epochs=50):

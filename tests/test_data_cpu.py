@@ -143,3 +143,72 @@ def test_imread_conversions(D, tmp_path):
     ir = D.load_ir_image(prgb, 4)
     assert ir.shape == (4, 4) and ir.dtype == np.float32 and ir.max() <= 1
     assert D.load_rgb_image(prgb).shape == (5, 7, 3)
+
+
+@pytest.mark.parametrize("shape,size", [((64, 80), 256), ((200, 300, 3), 256), ((512, 640), 600), ((31, 17, 3), 64)])
+def test_host_inter_area_upscale_linear_area_path(D, shape, size):
+    """cv2.resize(INTER_AREA) with an UPscaling axis (img_size above the source, ir:818,
+    1139, 1156) is OpenCV's linear resampler with area-mode coefficients in 8-bit fixed
+    point (resize_linear_area_u8, parity with cv2 itself unpinned: cv2 absent).  Pinned
+    here: constant images stay constant, the fixed-point weights are the rounded float
+    area-mode fractions (per destination (1 - f, f), f in [0, 1)), and the result is
+    within 1 LSB of the same interpolation evaluated in float64."""
+    rng = np.random.default_rng(3)
+    img = rng.integers(0, 256, size=shape, dtype=np.uint8)
+    got = D.resize_area_u8(img, size)
+    assert got.shape == (size, size) + shape[2:] and got.dtype == np.uint8
+    for c in (0, 7, 128, 255):
+        assert np.all(D.resize_area_u8(np.full(shape, c, np.uint8), size) == c)
+    for n, cols in zip(shape[:2], (False, True)):
+        ofs, coef, lim = D.linear_area_table(n, size, cols)
+        assert np.all(np.diff(ofs) >= 0) and ofs.min() >= 0 and ofs.max() <= n - 1
+        assert np.all(np.abs(coef.sum(1) - 2048) <= 1) and np.all(coef >= 0)
+    # float64 evaluation of the same separable interpolation (weights / 2048)
+    a = img.astype(np.float64) if img.ndim == 3 else img.astype(np.float64)[:, :, None]
+
+    def axis(n, columns):
+        ofs, coef, lim = D.linear_area_table(n, size, columns)
+        M = np.zeros((size, n))
+        for d in range(size):
+            if columns and d >= lim:
+                M[d, ofs[d]] = 1.0
+            else:
+                M[d, ofs[d]] += coef[d, 0] / 2048
+                M[d, min(ofs[d] + 1, n - 1)] += coef[d, 1] / 2048
+        return M
+    My, Mx = axis(shape[0], False), axis(shape[1], True)
+    ref = np.einsum("yh,hwc,xw->yxc", My, a, Mx, optimize=True)
+    ref = ref[:, :, 0] if img.ndim == 2 else ref
+    d = np.abs(got.astype(np.float64) - ref)
+    assert d.max() <= 1.0, d.max()
+
+
+def test_imread_gray_jpeg_is_the_y_plane(D, tmp_path):
+    """cv2.imread(IMREAD_GRAYSCALE) of a colour JPEG asks libjpeg for its
+    grayscale output (the decoded Y plane), not YCbCr -> RGB -> BGR2GRAY; PIL's
+    draft('L') makes the same libjpeg request."""
+    rng = np.random.default_rng(4)
+    rgb = rng.integers(0, 256, size=(24, 32, 3), dtype=np.uint8)
+    p = str(tmp_path / "c.jpg")
+    Image.fromarray(rgb).save(p, quality=90)
+    with Image.open(p) as im:
+        im.draft("L", im.size)
+        y = np.asarray(im.convert("L"))
+    with Image.open(p) as im:
+        via_rgb = np.asarray(im.convert("RGB")).astype(np.int64)
+    g = D.imread_gray(p)
+    assert np.array_equal(g, y)
+    r, gg, b = (via_rgb[..., i] for i in range(3))
+    assert not np.array_equal(g, ((r * 4899 + gg * 9617 + b * 1868 + 8192) >> 14).astype(np.uint8))
+
+
+def test_collate_raw_modalities_may_differ(D):
+    """the IR and RGB sources of one batch may have different sizes (each is
+    resized on its own, ir:1139, 1156); within one modality the size must be uniform."""
+    items = [{"ir_u8": torch.zeros(64, 80, dtype=torch.uint8), "rgb_u8": torch.zeros(96, 120, 3, dtype=torch.uint8),
+              "flip": i % 2} for i in range(3)]
+    b = D.collate_raw(items)
+    assert b["ir_u8"].shape == (3, 64, 80) and b["rgb_u8"].shape == (3, 96, 120, 3)
+    items[1]["ir_u8"] = torch.zeros(65, 80, dtype=torch.uint8)
+    with pytest.raises(RuntimeError):
+        D.collate_raw(items)

@@ -231,3 +231,36 @@ def test_bf16_res64_act_mask_tight(ops, cout, H, mode):
         ops.conv_fwd(pc, ops.Feat(nhwc(x)), ops.Feat(y), mask=ops.Feat(nhwc(m)), mask_act=mact)
         mm = torch.where(m > 0, 1.0, slope).double()
         check(nchw64(y), y64 * mm, ya, R_BF16, f"mask {mact}")
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 32, 48), (1, 64, 64), (3, 48, 32), (2, 16, 64), (1, 37, 64)])
+def test_reflect_dgrad_ring_fold_tight(ops, N, H, W):
+    """irgan_conv_dgrad_reflect (ResnetBlock backward-data, ir:386-411): on 16-multiple
+    sides >= 32 the reflect-pad ring is folded into the conv_pp launch itself (ring rows in
+    the border patches' K loop, ring columns + corners as an epilogue GEMM), so every dx
+    pixel is rounded to bf16 ONCE: held to the plain bound (no twice-rounded band), for
+    plain / accumulating bf16 and fp32 outputs, non-square and multi-image shapes (every
+    corner / edge patch kind).  Sides that are not (16, 37) take interior + ring launch."""
+    C = 256
+    torch.manual_seed(12)
+    x = q(torch.randn(N, C, H, W))
+    w = q(torch.randn(C, C, 3, 3) * (1.0 / (C * 9) ** 0.5))
+    spec = ops.ConvSpec(C, C, 3, 1, 1, 1)
+    gy = q(torch.randn(N, C, H, W))
+    _, dx64, _, dxi = references(x, w, None, gy, 3, 1, 1, 1)
+    _, dxa, _, _ = references(x.abs(), w.abs(), None, gy.abs(), 3, 1, 1, 1)
+    pc = ops.PackedConv(spec, w.permute(0, 2, 3, 1).contiguous().reshape(-1).to(DEV), None, ops.BF16)
+    pc.pack()
+    gyd = nhwc(gy)
+    folded = H % 16 == 0 and W % 16 == 0 and H >= 32 and W >= 32
+    for out_dt, r_out in ((torch.bfloat16, R_BF16), (torch.float32, 0.0)):
+        dx = torch.zeros(N, H, W, C, device=DEV, dtype=out_dt)
+        ops.conv_dgrad(pc, ops.Feat(gyd), ops.Feat(dx))
+        check(nchw64(dx), dx64, dxa, r_out, f"fold {out_dt}", partial=None if folded else dxi)
+    old = q(torch.randn(N, C, H, W))
+    dxb = torch.zeros(N, H, W, C + 8, device=DEV, dtype=torch.bfloat16)
+    dxb[..., 8:] = nhwc(old)
+    ops.conv_dgrad(pc, ops.Feat(gyd), ops.Feat(dxb, 8, C), accumulate=True)
+    check(nchw64(dxb[..., 8:]), dx64 + old.double(), dxa + old.double().abs(), R_BF16, "fold accumulate",
+          partial=None if folded else dxi + old.double())
+    assert not dxb[..., :8].any()

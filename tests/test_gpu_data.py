@@ -161,3 +161,22 @@ def test_train_kaist_on_kaist_directory(tmp_path):
     assert len(hist) == 1 and np.isfinite(hist[0]["loss_G"]) and np.isfinite(hist[0]["val_l1"])
     assert "Total pairs: 8, train: 7, val: 1" in logs   # val_size = max(1, int(8 * 0.1)) (ir:1565-1566)
     assert os.path.isfile(os.path.join(cfg.save_dir, "netG_epoch_001.pth"))
+
+
+@pytest.mark.parametrize("H,W,S", [(200, 160, 256), (300, 200, 256), (64, 80, 100)])
+def test_device_inter_area_upscale_bit_identical_to_host(H, W, S):
+    """img_size above the source (an upscaling axis): irgan_linear_area_resize_u8 (OpenCV's
+    linear path with area-mode coefficients, 8-bit fixed point) equals the host
+    restatement data.resize_linear_area_u8 bit for bit, with the flip and the IR max rule."""
+    D = pkg().data
+    rng = np.random.default_rng(5)
+    B = 3
+    ir = rng.integers(0, 256, size=(B, H, W), dtype=np.uint8)
+    ir[2] = rng.integers(0, 2, size=(H, W), dtype=np.uint8)
+    rgb = rng.integers(0, 256, size=(B, H + 8, W - 8, 3), dtype=np.uint8)   # modalities of different sizes
+    flip = torch.tensor([0, 1, 1], dtype=torch.uint8)
+    out = D.DeviceResizer(S, DEV)({"ir_u8": torch.from_numpy(ir), "rgb_u8": torch.from_numpy(rgb), "flip": flip})
+    for b in range(B):
+        hi, hr = _host_item(D, ir[b], rgb[b], bool(flip[b]), S)
+        assert torch.equal(out["ir"][b].cpu(), hi), b
+        assert torch.equal(out["rgb"][b].cpu(), hr), b

@@ -136,6 +136,12 @@ def test_run_test_outputs_and_csv(tmp_path):
     # collages: [IR | pred | GT] with 8-pixel gutters; no GT -> two panels
     c = np.asarray(Image.open(os.path.join(cfg.output_dir, "Comparisons", "set02", "V000", "I00000_cmp.png")))
     assert c.shape == (32, 32 * 3 + 16, 3)
+    # the IR panel is the reference's float01_to_uint8_rgb(load_ir_image(...)) bit for bit
+    # (ir:945-958, 1374: float32 v / 255 * 255 truncated), not rebuilt from the [-1, 1] tensor
+    ir_path0 = [e[0] for e in entries if e[0].endswith(os.path.join("set02", "V000", "lwir", "I00000.png"))][0]
+    ir01 = D.load_ir_image(ir_path0, img_size=cfg.img_size)
+    want_panel = np.repeat((np.clip(ir01, 0.0, 1.0) * 255.0).astype(np.uint8)[:, :, None], 3, axis=2)
+    assert np.array_equal(c[:, :32], want_panel)
     c4 = np.asarray(Image.open(os.path.join(cfg.output_dir, "Comparisons", "set02", "V000", "I00004_cmp.png")))
     assert c4.shape == (32, 32 * 2 + 8, 3)
     assert any(line.startswith("Mean SSIM  :") for line in logs)

@@ -6,11 +6,13 @@ ATen is allowed); post-step parameters use an absolute tolerance of 2*lr
 gradients may flip sign), and pre-InstanceNorm biases are excluded from
 gradient-value checks (their exact gradient is zero; fp32 values are noise).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
 
-from conftest import load_golden
+from conftest import GOLDEN, load_golden
 from oracle import step as O
 
 SEEDS = dict(G=1, D=2, V=3)
@@ -153,3 +155,72 @@ def test_oracle_as_written_equals_minimal_step():
     for P, Q in ((Ga, Gb), (Da, Db)):
         for k in P:
             assert torch.equal(P[k], Q[k]) or torch.allclose(P[k], Q[k], rtol=1e-12, atol=1e-15), k
+
+
+def _digest_ok(fx, prefix, named_grads, rtol=1e-9):
+    """Sampled gradient entries and the norm vs the golden digest; pre-InstanceNorm biases
+    are skipped (exactly-zero gradient: their fp64 values are rounding noise)."""
+    import numpy as np
+    skip = set(O.pre_in_bias_keys([k for k, _ in named_grads]))
+    for k, g in named_grads:
+        if k in skip:
+            continue
+        flat = g.reshape(-1).double().numpy()
+        idx = fx[f"{prefix}|{k}|idx"]
+        ref = fx[f"{prefix}|{k}|val"]
+        scale = max(float(fx[f"{prefix}|{k}|norm"]) / max(flat.size, 1) ** 0.5, 1e-300)
+        assert np.max(np.abs(flat[idx] - ref)) <= rtol * max(np.max(np.abs(ref)), scale), (prefix, k)
+        assert abs(np.linalg.norm(flat) - float(fx[f"{prefix}|{k}|norm"])) <= rtol * float(fx[f"{prefix}|{k}|norm"])
+
+
+def test_oracle_matches_reference_module_variants():
+    """The oracle's restatement of the NON-DEFAULT module options against goldens made by
+    executing the reference (tests/golden/make_module_golden.py, fp64): generator norm
+    'none' / padding 'replicate' / 'zero' / the Dropout layout in eval mode / ConvTranspose2d
+    without bias; PatchGAN n_layers 1, 2, 4 and norm 'none'; SSIM window sizes 3, 5, 7 with
+    size_average True / False.  Outputs, input gradients and parameter-gradient digests
+    agree to fp64 rounding."""
+    import numpy as np
+    import torch
+    from oracle import step as O
+    fx = dict(np.load(os.path.join(GOLDEN, "modules.npz")))
+    x = torch.from_numpy(fx["g_x"])
+    cases = {"g_none": ("none", "reflect", False, False), "g_replicate": ("instance", "replicate", False, False),
+             "g_zero": ("instance", "zero", False, False), "g_dropout_eval": ("instance", "reflect", True, False),
+             "g_none_zero_up": ("none", "zero", False, True)}
+    for name, (norm, pad, drop, noaaup) in cases.items():
+        shapes = O.g_param_shapes(no_antialias_up=noaaup, use_bias=norm == "instance", padding_type=pad,
+                                  use_dropout=drop)
+        P = {k: v.double().requires_grad_(not k.endswith(".filt"))
+             for k, v in O.seeded_params(shapes, 1, bias_std=0.02).items()}
+        if drop:   # eval mode: the Dropout is inactive; the conv keys follow the layout with it
+            k1, k2 = O.res_conv_keys(pad, True)
+            Q = {k.replace(f"conv_block.{k2}.", "conv_block.5."): v for k, v in P.items()}
+            out = O.g_forward(Q, x, no_antialias_up=noaaup, norm=norm, padding_type=pad)
+        else:
+            out = O.g_forward(P, x, no_antialias_up=noaaup, norm=norm, padding_type=pad)
+        assert np.max(np.abs(out.detach().numpy() - fx[f"{name}|out"])) <= 1e-10, name
+        Rw = torch.randn(out.shape, generator=torch.Generator().manual_seed(11), dtype=torch.float64)
+        (out * Rw).sum().backward()
+        _digest_ok(fx, name, [(k, v.grad) for k, v in P.items() if not k.endswith(".filt")])
+    xd = torch.from_numpy(fx["d_x"])
+    for name, (nl, norm) in {"d_n1": (1, "instance"), "d_n2": (2, "instance"), "d_n4": (4, "instance"),
+                             "d_none": (3, "none")}.items():
+        shapes = O.d_param_shapes(4, 64, nl, use_bias=norm == "instance")
+        P = {k: v.double().requires_grad_(True) for k, v in O.seeded_params(shapes, 2, bias_std=0.02).items()}
+        xi = xd.clone().requires_grad_(True)
+        out = O.d_forward(P, xi, n_layers=nl, norm=norm)
+        assert np.max(np.abs(out.detach().numpy() - fx[f"{name}|out"])) <= 1e-10, name
+        Rw = torch.randn(out.shape, generator=torch.Generator().manual_seed(12), dtype=torch.float64)
+        (out * Rw).sum().backward()
+        assert np.max(np.abs(xi.grad.numpy() - fx[f"{name}|dx"])) <= 1e-10 * max(1.0, np.abs(fx[f"{name}|dx"]).max())
+        _digest_ok(fx, name, [(k, v.grad) for k, v in P.items()])
+    a, b = torch.from_numpy(fx["ssim_a"]), torch.from_numpy(fx["ssim_b"])
+    for ws in (3, 5, 7):
+        for avg in (True, False):
+            aa = a.clone().requires_grad_(True)
+            loss = O.ssim_loss(aa, b, window_size=ws, size_average=avg)
+            w = torch.arange(1, loss.numel() + 1, dtype=torch.float64).reshape(loss.shape)
+            (loss * w).sum().backward()
+            assert np.allclose(loss.detach().numpy(), fx[f"ssim{ws}_{int(avg)}|loss"], rtol=1e-12, atol=1e-14)
+            assert np.allclose(aa.grad.numpy(), fx[f"ssim{ws}_{int(avg)}|grad"], rtol=1e-10, atol=1e-14)
