@@ -648,7 +648,9 @@ class GeneratorEngine:
             t = Feat(g.get(name + "_d", (x.N, 2 * x.H, 2 * x.W, dy.C), self.tdt))
             ops.resize_bwd(dy, t)
             dy = t
-        ops.channel_sum(dy, S.krsc(key + ".bias", S.grad))
+        db = self._bgrad(key + ".bias")
+        if db is not None:
+            ops.channel_sum(dy, db)
         ops.conv_wgrad(pc.spec, dy, x, S.krsc(key + ".weight", S.grad), self.dtype)
         ops.conv_fwd(pc, dy, dx, bias=False)
 

@@ -141,7 +141,8 @@ def test_run_test_outputs_and_csv(tmp_path):
     ir_path0 = [e[0] for e in entries if e[0].endswith(os.path.join("set02", "V000", "lwir", "I00000.png"))][0]
     ir01 = D.load_ir_image(ir_path0, img_size=cfg.img_size)
     want_panel = np.repeat((np.clip(ir01, 0.0, 1.0) * 255.0).astype(np.uint8)[:, :, None], 3, axis=2)
-    assert np.array_equal(c[:, :32], want_panel)
+    # (labels are drawn from x=10, y=10 on: compare the untouched left columns and top rows)
+    assert np.array_equal(c[:, :10], want_panel[:, :10]) and np.array_equal(c[:10, :32], want_panel[:10])
     c4 = np.asarray(Image.open(os.path.join(cfg.output_dir, "Comparisons", "set02", "V000", "I00004_cmp.png")))
     assert c4.shape == (32, 32 * 2 + 8, 3)
     assert any(line.startswith("Mean SSIM  :") for line in logs)

@@ -41,7 +41,7 @@ def test_dgrad_in_stats_matches_separate_reduce(H, act, acc):
     dx = ops.Feat(old.clone() if acc else torch.zeros(N, H, H, C, device=DEV, dtype=torch.bfloat16))
     work2 = torch.empty_like(work)
     nb = ops.conv_dgrad_in(pc, dy, dx, z, mr, act, work2, accumulate=acc)
-    assert nb > (H // 16) ** 2, "the fused kernel did not run"
+    assert nb >= (H // 16) ** 2, "the fused kernel did not run"   # ring folded in: exactly the patches
     red = torch.empty(N * C * 2, device=DEV)
     m._lib.call("irgan_in_bwd_finalize", ops.P(work2), N, H * H, C, nb, ops.P(red), ops.stream())
     torch.cuda.synchronize()
