@@ -11,7 +11,7 @@ Tolerances (north star: 1e-3 rel fp32):
                forward state (ReLU / LeakyReLU kinks, hinge, sign() in the L1 and
                perceptual-L1 terms): one activation that lands on the other side
                of a kink moves a whole layer's grads by ~1e-3..3e-2 (measured:
-               tools/diag_g.py shows a single-layer jump at one resblock while all
+               a per-layer diagnostic in round 1 showed a single-layer jump at one resblock while all
                other layers sit at ~7e-6 = 2.5x the CPU fp32 error), and the
                reference's OWN fp32 run is off by up to ~2e-2 max-rel on some
                tensors (err32 / err32l2 per tensor in the fixtures).  Criterion:
