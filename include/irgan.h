@@ -263,10 +263,11 @@ int irgan_reflect_dgrad_ring(const irgan_conv_desc* d, const void* dy, const voi
                              irgan_stream_t s);
 /* The whole backward-data of a reflect-padded stride-1 conv (ir:381-392, 401-411): the
  * interior correlation and the fold of its pad ring (d, w, p as irgan_reflect_dgrad_ring).
- * ResnetBlock shapes (bf16, 3x3, p = 1, dY channels % 64, dx channels % 256, H and W
- * multiples of 16 and >= 32, no mask / activation) run as ONE conv_pp launch with the
- * ring folded into its border patches (every dx pixel rounded once); other shapes run
- * irgan_conv_fwd + irgan_reflect_dgrad_ring (IRGAN_NO_RING_FOLD=1 forces that pair). */
+ * With the ring fold on (irgan_set_ring_fold), ResnetBlock shapes (bf16, 3x3, p = 1, dY
+ * channels % 64, dx channels % 256, H and W multiples of 16 and >= 32, no mask /
+ * activation) run as ONE conv_pp launch with the ring folded into its border patches
+ * (every dx pixel rounded once); otherwise (the default) irgan_conv_fwd +
+ * irgan_reflect_dgrad_ring. */
 int irgan_conv_dgrad_reflect(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p, void* dx,
                              irgan_stream_t s);
 /* out = (Wy (x) Wx) in on NHWC slices, tables from irgan_resample_table (device
@@ -414,6 +415,9 @@ int irgan_version(void);
  * faster (high split counts: up2 / down1-class layers at 256^2).  Loss VALUES are
  * fp64 atomic block sums in either mode (they feed no gradient).  Returns the old value. */
 int irgan_set_deterministic(int32_t on);
+/* Process-wide switch of irgan_conv_dgrad_reflect's one-launch ring fold (default off, or
+ * on with IRGAN_RING_FOLD set).  Returns the old value. */
+int irgan_set_ring_fold(int32_t on);
 
 #ifdef __cplusplus
 }

@@ -21,13 +21,24 @@ void launch_ring(const irgan_conv_desc* d, const void* dy, const void* w, void* 
 
 }  // namespace
 
+// Opt-in (irgan_set_ring_fold / IRGAN_RING_FOLD=1): on the bench step the fold measured no
+// faster than interior + ring (the border patches' extra K-loop rows and epilogue GEMM
+// lengthen the one-block-per-CU launch by about what the separate ring launch costs).
 // Shapes the one-launch fold takes (else the caller runs interior + ring): bf16, 3x3, stride
 // 1, p = 1, dY / dx channels % 64 / 256, an output the size of the input whose sides are
 // multiples of 16 with >= 2 patches each (a mirrored row / column then lies in its own
 // patch), plain (unstrided) output grid, no mask / activation / bias.
+static int g_ring_fold = -1;  // -1: not yet read from IRGAN_RING_FOLD
+
+extern "C" int irgan_set_ring_fold(int32_t on) {
+    const int old = g_ring_fold < 0 ? (getenv("IRGAN_RING_FOLD") != nullptr) : g_ring_fold;
+    g_ring_fold = on ? 1 : 0;
+    return old;
+}
+
 bool irgan_ring_fold_ok(const irgan_conv_desc* d, int p) {
-    static const bool off = getenv("IRGAN_NO_RING_FOLD") != nullptr;
-    return !off && p == 1 && d->dtype == IRGAN_BF16 && d->KH == 3 && d->KW == 3 && d->sy == 1 && d->sx == 1 &&
+    if (g_ring_fold < 0) g_ring_fold = getenv("IRGAN_RING_FOLD") != nullptr;
+    return g_ring_fold && p == 1 && d->dtype == IRGAN_BF16 && d->KH == 3 && d->KW == 3 && d->sy == 1 && d->sx == 1 &&
            d->Cin % 64 == 0 && d->Cout % 256 == 0 && d->ldx % 8 == 0 && d->xoff % 8 == 0 && d->Ho == d->H &&
            d->Wo == d->W && d->H % 16 == 0 && d->W % 16 == 0 && d->H >= 32 && d->W >= 32 && d->Ho == d->OH &&
            d->Wo == d->OW && d->omy == 1 && d->omx == 1 && d->ooy == 0 && d->oox == 0 &&

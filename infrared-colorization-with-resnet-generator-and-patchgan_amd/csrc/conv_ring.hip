@@ -107,7 +107,7 @@ __global__ __launch_bounds__(NWV * 64) void reflect_ring_kernel(const irgan_conv
     // block-uniform: which terms can occur.  Row segment: term 0 (Vy, x) for all
     // pixels; terms 1 (y, Vx) and 2 (Vy, Vx) only for pixels in band columns.
     // Column segment: term 1 only.
-    const int qlo = seg * NPIX, qhi = min(qlo + NPIX, rowseg ? W : H) - 1;
+    const int qlo = seg * NPIX, qhi = min(qlo + NPIX, rowseg ? W : H) - 1;   // the segment's pixels
     const bool has_bandcol = rowseg && (qlo <= p || qhi >= W - 1 - p);
     const int vby = rowseg ? mirror_pos(bpos, H, p) : 0;   // row segments: Vy (uniform)
     const int vbx = rowseg ? 0 : mirror_pos(bpos, W, p);   // column segments: Vx (uniform)
@@ -118,28 +118,50 @@ __global__ __launch_bounds__(NWV * 64) void reflect_ring_kernel(const irgan_conv
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[f][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // block-uniform list of the (term, ty, tx) taps that can touch dy
+    // block-uniform list of the DISTINCT (ty, tx) taps that can touch dy, each with the mask
+    // of the terms that use it: a tap's weight fragments are loaded once per 32-channel step
+    // and shared by its terms (row segments: term 0 needs the taps that reach dy from Vy,
+    // terms 1 / 2 only the taps that reach it from a band column's Vx -- 7 of the 15
+    // (term, tap) pairs of a 3x3 resblock ring share their weights)
+    const int fw0 = seg * NPIX;  // first pixel of the segment along its band line
     if (threadIdx.x == 0) {
         int nt = 0;
-        for (int term = 0; term < 3; ++term) {
-            if (rowseg ? (term > 0 && !has_bandcol) : term != 1) continue;
-            for (int ty = 0; ty < d.KH; ++ty) {
-                if (rowseg && term != 1 && (unsigned)(vby + ty + d.c0y) >= (unsigned)d.H) continue;
-                for (int tx = 0; tx < d.KW; ++tx) {
-                    if (!rowseg && (unsigned)(vbx + tx + d.c0x) >= (unsigned)d.W) continue;
-                    tap_list[nt++] = (term << 8) | (ty << 4) | tx;
+        for (int ty = 0; ty < d.KH; ++ty)
+            for (int tx = 0; tx < d.KW; ++tx) {
+                int m = 0;
+                if (rowseg) {
+                    const bool rv = (unsigned)(vby + ty + d.c0y) < (unsigned)d.H;       // term 0 / 2 rows
+                    const bool r1 = (unsigned)(bpos + ty + d.c0y) < (unsigned)d.H;      // term 1 row
+                    bool cv = false;  // some band column of this segment reaches dy through tx
+                    if (has_bandcol)
+                        for (int k = 0; k < 2 * p; ++k) {  // band columns 1..p, W-1-p..W-2
+                            const int q = k < p ? k + 1 : W - 1 - p + (k - p);
+                            const int vx = mirror_pos(q, W, p);
+                            if (q >= qlo && q <= qhi && (unsigned)(vx + tx + d.c0x) < (unsigned)d.W) cv = true;
+                        }
+                    if (rv) m |= 1;
+                    if (cv && r1) m |= 2;
+                    if (cv && rv) m |= 4;
+                } else if ((unsigned)(vbx + tx + d.c0x) < (unsigned)d.W) {
+                    m = 2;
                 }
+                if (m) tap_list[nt++] = (m << 8) | (ty << 4) | tx;
             }
-        }
         ntap_s = nt;
     }
     __syncthreads();
     const int ntap = ntap_s;
 
-    // mirrored column of fragment f's pixel (terms 1 and 2)
+    // mirrored column of fragment f's pixel (terms 1 and 2); fragments that hold no band
+    // column skip the term 1 / 2 loads and MFMAs of a row segment (wave-uniform)
     int mxf[NF];
+    bool fb[NF];
 #pragma unroll
-    for (int f = 0; f < NF; ++f) mxf[f] = rowseg ? mirror_pos(px[f], W, p) : vbx;
+    for (int f = 0; f < NF; ++f) {
+        mxf[f] = rowseg ? mirror_pos(px[f], W, p) : vbx;
+        const int f0 = fw0 + f * 16, f1 = f0 + 15;
+        fb[f] = !rowseg || (f0 <= p && f1 >= 1) || (f0 <= W - 2 && f1 >= W - 1 - p);
+    }
 
     const int kc = (lane >> 4) * 8;  // channel offset of this lane within a 32-deep k step
     const bf16_t* wrow[4];
@@ -152,46 +174,60 @@ __global__ __launch_bounds__(NWV * 64) void reflect_ring_kernel(const irgan_conv
     }
     const int nc = d.Cin / 32;
     const int total = ntap * nc;  // flattened K steps (tap, 32-channel step); wave wv takes s = wv mod NWV
-    auto load_step = [&](int q, uint4 (&a)[NF], uint4 (&b)[4]) {
+    // one K step: the tap's weight fragments once, the dy fragments of each term in its mask
+    auto load_step = [&](int q, uint4 (&a)[3][NF], uint4 (&b)[4], int& msk) {
         const int tp = q / nc, c = q - tp * nc;
         const int e = tap_list[tp];
-        const int term = e >> 8, ty = (e >> 4) & 15, tx = e & 15;
+        msk = e >> 8;
+        const int ty = (e >> 4) & 15, tx = e & 15;
         const int wb = (ty * d.KW + tx) * d.Cin + c * 32;
 #pragma unroll
         for (int j = 0; j < 4; ++j) b[j] = wok[j] ? *(const uint4*)(wrow[j] + wb) : uint4{0, 0, 0, 0};
 #pragma unroll
-        for (int f = 0; f < NF; ++f) {
-            // term 0: (Vy, x); term 1: (y, Vx); term 2: (Vy, Vx)  (term is wave-uniform)
-            const int vy = term == 1 ? py[f] : vby;
-            const int vx = term == 0 ? px[f] : mxf[f];
-            const bool tv = pv[f] && (term == 0 || mxf[f] != -0x40000000);
-            const int r = vy + ty + d.c0y, cc = vx + tx + d.c0x;
-            const bool ok = tv && (unsigned)r < (unsigned)d.H && (unsigned)cc < (unsigned)d.W;
-            a[f] = ok ? *(const uint4*)(dy + (((long)n * d.H + r) * d.W + cc) * d.ldx + d.xoff + kc + c * 32)
-                      : uint4{0, 0, 0, 0};
+        for (int term = 0; term < 3; ++term) {
+            if (!((msk >> term) & 1)) continue;
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                // term 0: (Vy, x); term 1: (y, Vx); term 2: (Vy, Vx)
+                if (term > 0 && !fb[f]) continue;
+                const int vy = term == 1 ? py[f] : vby;
+                const int vx = term == 0 ? px[f] : mxf[f];
+                const bool tv = pv[f] && (term == 0 || mxf[f] != -0x40000000);
+                const int r = vy + ty + d.c0y, cc = vx + tx + d.c0x;
+                const bool ok = tv && (unsigned)r < (unsigned)d.H && (unsigned)cc < (unsigned)d.W;
+                a[term][f] = ok ? *(const uint4*)(dy + (((long)n * d.H + r) * d.W + cc) * d.ldx + d.xoff + kc + c * 32)
+                                : uint4{0, 0, 0, 0};
+            }
         }
     };
-    auto mma = [&](const uint4 (&a)[NF], const uint4 (&b)[4]) {
+    auto mma = [&](const uint4 (&a)[3][NF], const uint4 (&b)[4], int msk) {
 #pragma unroll
-        for (int f = 0; f < NF; ++f)
+        for (int term = 0; term < 3; ++term) {
+            if (!((msk >> term) & 1)) continue;
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, b[j]),
-                                                                    __builtin_bit_cast(bf16x8_t, a[f]), acc[f][j], 0,
-                                                                    0, 0);
+            for (int f = 0; f < NF; ++f) {
+                if (term > 0 && !fb[f]) continue;
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, b[j]),
+                                                                        __builtin_bit_cast(bf16x8_t, a[term][f]),
+                                                                        acc[f][j], 0, 0, 0);
+            }
+        }
     };
     // two steps of operands in flight: step s+NWV loads while step s multiplies
-    uint4 a0[NF], b0[4], a1[NF], b1[4];
+    uint4 a0[3][NF], b0[4], a1[3][NF], b1[4];
+    int m0 = 0, m1 = 0;
     int ks = wv;
-    if (ks < total) load_step(ks, a0, b0);
+    if (ks < total) load_step(ks, a0, b0, m0);
     while (ks < total) {
         const int k1 = ks + NWV;
-        if (k1 < total) load_step(k1, a1, b1);
-        mma(a0, b0);
+        if (k1 < total) load_step(k1, a1, b1, m1);
+        mma(a0, b0, m0);
         if (k1 >= total) break;
         const int k2 = k1 + NWV;
-        if (k2 < total) load_step(k2, a0, b0);
-        mma(a1, b1);
+        if (k2 < total) load_step(k2, a0, b0, m0);
+        mma(a1, b1, m1);
         ks = k2;
     }
     // partial tiles -> LDS: lane holds pixel f*16 + (lane & 15), channels j*16 + 4*(lane>>4) + r

@@ -1,14 +1,16 @@
 // bf16 backward-weight convolution, producer/consumer form (3x3, stride 1,
-// Cout % 128 == 0, Cin % 64 == 0, Wo % 64 == 0): the ResnetBlock weight
+// Cout % 64 == 0, Cin % 64 == 0, Wo % 64 == 0): the ResnetBlock weight
 // gradients (ir:390, 411) and the encoder / decoder 3x3 convs that qualify
-// (down1, down2, up1_conv: ir:470, 478, 504).
+// (down1, down2, up1_conv, up2_conv: ir:470, 478, 504, 520).  co tiles of 128 (BMC 128,
+// Cout % 128 == 0) or 64 (BMC 64: up2_conv's 64 output channels; its dY rows are 128 B
+// and use the X span's swizzle).
 //
 //   dW[co][ty][tx][ci] += sum_p dY[p][co] * X[iy(p, ty)][ix(p, tx)][ci]
 //
-// Same work decomposition as conv_wgrad_halo.hip: a block owns (128-channel co
+// Same work decomposition as conv_wgrad_halo.hip: a block owns (BMC-channel co
 // tile, 64-channel ci chunk, kernel row ty, all three tx taps) and walks 64-pixel
 // row segments of dY (split-K over segments); per segment the dY tile
-// [64 px][128 co] and ONE input row span [66][64 ci] sit in LDS and the three tx
+// [64 px][BMC co] and ONE input row span [66][64 ci] sit in LDS and the three tx
 // taps are row shifts of the span.  What is different is who does what
 // (measured on the halo kernel: 5 VALU per MFMA, fragment reads and DMA issue
 // serialised with the MFMAs):
@@ -18,7 +20,7 @@
 //    precomputed per-lane offsets (dY: a lane-invariant offset + the segment's
 //    scalar soffset; X span: a few VALU per piece for the reflect / zero edge),
 //    so the compute waves issue no VMEM and almost no VALU;
-//  * 4-stage LDS ring (4 x 25 KiB), one s_barrier per segment, the DMA two
+//  * 4-stage LDS ring (4 x 25 KiB at BMC 128, 4 x 17 KiB at 64), one s_barrier per segment, the DMA two
 //    segments ahead of its consumer: the loaders retire segment k+1 with a
 //    counted vmcnt before barrier k, then issue segment k+3 into the stage that
 //    segment k-1 (fully consumed before barrier k) used;
@@ -29,8 +31,8 @@
 //    below do not change over those steps).
 //
 // LDS images (conflict-free ds_read_b64_tr_b16, as conv_wgrad_halo.hip):
-//   dY, 256-B rows: 16-B chunk XOR 2*((r&3)|((r>>3&1)<<2));
-//   X span, 128-B rows: chunk XOR 2*((r>>1&1)|((r>>3&1)<<1)).
+//   dY, 256-B rows (BMC 128): 16-B chunk XOR 2*((r&3)|((r>>3&1)<<2));
+//   X span and dY at BMC 64, 128-B rows: chunk XOR 2*((r>>1&1)|((r>>3&1)<<1)).
 // Split-K partials go to a caller slab (plain stores, ordered reduce) or, with
 // no slab, fp32 atomics into dW.
 #include "common.h"
@@ -50,22 +52,26 @@ typedef __attribute__((address_space(3))) s16x4 lds_s4;
 IRGAN_HD int pc_t128(int r) { return ((r >> 1) & 1) | (((r >> 3) & 1) << 1); }
 IRGAN_HD int pc_t256(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
 
-constexpr int BMC = 128;                 // co tile
 constexpr int KW = 3;
-constexpr int APIECES = 64 * BMC * 2 / 1024;  // dY tile: 16 pieces of 4 pixel rows
 constexpr int XPOS = 66;                 // X span positions (63 + KW)
 constexpr int XPIECES = 9;               // 72 positions, 8 per piece
-constexpr int TP = APIECES + XPIECES;    // 25 pieces per segment
-constexpr int STAGE = TP * 1024;
 constexpr int STAGES = 4;
 constexpr int NJ = 3;                    // 3 (tx, 16-ci) fragments per compute wave
-constexpr int PPL = (TP + 3) / 4;        // max pieces per loader wave (7)
-// CW compute waves: 4 -> 128 co x 48 n per wave (1 per SIMD); 8 -> 64 co x 48 n (2 per SIMD)
-template <int CW>
+// BMC: co tile (128 or 64).  CW compute waves: 4 -> BMC co x 48 n per wave (1 per SIMD);
+// 8 -> BMC/2 co x 48 n (2 per SIMD)
+template <int BMC, int CW>
 struct PC {
+    static constexpr int DYR = BMC * 2;             // dY tile row bytes
+    static constexpr int APIECES = 64 * DYR / 1024; // dY tile pieces (16 of 4 rows / 8 of 8 rows)
+    static constexpr int TP = APIECES + XPIECES;    // pieces per segment (25 / 17)
+    static constexpr int STAGE = TP * 1024;
+    static constexpr int PPL = (TP + 3) / 4;        // max pieces per loader wave (7 / 5)
     static constexpr int MI = BMC / 16 / (CW / 4);  // co fragments per compute wave
     static constexpr int NT = (CW + 4) * 64;        // threads: CW compute + 4 loader waves
+    static_assert(TP % 4 == 1, "loader 0 takes PPL pieces, loaders 1-3 PPL - 1");
 };
+template <int BMC>
+IRGAN_HD int pc_dsw(int r) { return BMC == 128 ? pc_t256(r) : pc_t128(r); }  // dY row swizzle
 
 IRGAN_HD uint4 ld_tr_pair(const char* lo, const char* hi) {
     const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)lo);
@@ -81,15 +87,18 @@ struct Frag {
     uint4 a[MI], b[NJ];
 };
 
-template <int CW>
-__global__ __launch_bounds__(PC<CW>::NT, 1) void wgrad_pc_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
+template <int BMC, int CW>
+__global__ __launch_bounds__((PC<BMC, CW>::NT), 1) void wgrad_pc_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
                                                           const bf16_t* __restrict__ dy, float* __restrict__ dw,
                                                           int segs_per_block, int nseg, int ntco, int nci, int swz,
                                                           float* __restrict__ slab) {
+    using Q = PC<BMC, CW>;
+    constexpr int APIECES = Q::APIECES, TP = Q::TP, STAGE = Q::STAGE, PPL = Q::PPL, DYR = Q::DYR;
+    constexpr int DROWS = 1024 / DYR;  // dY rows per piece
     __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    constexpr int MI = PC<CW>::MI;
+    constexpr int MI = Q::MI;
     const bool loader = wid >= CW;
     const int tiles = ntco * nci * d.KH;
     const int t = xcd_tile(blockIdx.x, gridDim.x, swz);
@@ -109,7 +118,7 @@ __global__ __launch_bounds__(PC<CW>::NT, 1) void wgrad_pc_kernel(const irgan_con
         // ------------------------------------------------------------------
         // loader wave l issues pieces j = l, l+4, ... (< TP) of every segment
         const int l = wid - CW;
-        const int np = (TP - l + 3) / 4;  // 7 for l = 0, else 6
+        const int np = (TP - l + 3) / 4;  // PPL for l = 0, else PPL - 1
         const bool reflect = d.pad_mode == IRGAN_PAD_REFLECT;
         // dY: buffer base at dy + yoff + co0; lane offset fixed per piece, the
         // segment's first pixel enters as the scalar soffset
@@ -126,8 +135,8 @@ __global__ __launch_bounds__(PC<CW>::NT, 1) void wgrad_pc_kernel(const irgan_con
             xpos[u] = 0;
             xc16[u] = 0;
             if (j < APIECES) {
-                const int pos = j * 4 + (lane >> 4), slot = lane & 15;
-                const int c16 = slot ^ (2 * pc_t256(pos));
+                const int pos = j * DROWS + lane / (64 / DROWS), slot = lane % (64 / DROWS);
+                const int c16 = slot ^ (2 * pc_dsw<BMC>(pos));
                 if (co0 + c16 * 8 < cout8) voff[u] = (uint32_t)((pos * d.ldy + c16 * 8) * 2);
             } else if (j < TP) {
                 const int pos = (j - APIECES) * 8 + (lane >> 3), slot = lane & 7;
@@ -164,9 +173,9 @@ __global__ __launch_bounds__(PC<CW>::NT, 1) void wgrad_pc_kernel(const irgan_con
         if (nk > 1) issue(s_beg + 1, 1);
         if (nk > 2) issue(s_beg + 2, 2);
         if (nk > 2) {
-            if (np == 7) wait_vmcnt<14>(); else wait_vmcnt<12>();
+            if (np == PPL) wait_vmcnt<2 * PPL>(); else wait_vmcnt<2 * PPL - 2>();
         } else if (nk > 1) {
-            if (np == 7) wait_vmcnt<7>(); else wait_vmcnt<6>();
+            if (np == PPL) wait_vmcnt<PPL>(); else wait_vmcnt<PPL - 1>();
         } else {
             wait_vmcnt<0>();
         }
@@ -175,7 +184,7 @@ __global__ __launch_bounds__(PC<CW>::NT, 1) void wgrad_pc_kernel(const irgan_con
             // retire segment kt+1 (segment kt+2 may stay in flight), then barrier kt
             if (kt + 1 < nk && !PCX(1)) {
                 if (kt + 2 < nk) {
-                    if (np == 7) wait_vmcnt<7>(); else wait_vmcnt<6>();
+                    if (np == PPL) wait_vmcnt<PPL>(); else wait_vmcnt<PPL - 1>();
                 } else {
                     wait_vmcnt<0>();
                 }
@@ -194,13 +203,13 @@ __global__ __launch_bounds__(PC<CW>::NT, 1) void wgrad_pc_kernel(const irgan_con
     const int wn = wid & 3, wm = wid >> 2;  // n group, co group (CW = 8)
     const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
     const int k_lo = 8 * g + q;  // pixel row of the lane's low 4-row half (k-step 0)
-    // per-lane byte offsets inside a stage (k-step 0, low half); +1024 / +512 for
-    // the high half (rows +4), +8192 / +4096 for k-step 1 (rows +32)
+    // per-lane byte offsets inside a stage (k-step 0, low half); +4 / +32 rows for the
+    // high half / k-step 1 (the row swizzles do not change over those steps)
     int aoff[MI];
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
         const int col = (wm * MI + i) * 16 + 4 * p, c16 = col >> 3, within = (col & 7) * 2;
-        aoff[i] = k_lo * 256 + ((c16 ^ (2 * pc_t256(k_lo))) << 4) + within;
+        aoff[i] = k_lo * DYR + ((c16 ^ (2 * pc_dsw<BMC>(k_lo))) << 4) + within;
     }
     int boff[NJ][2];
 #pragma unroll
@@ -222,7 +231,7 @@ __global__ __launch_bounds__(PC<CW>::NT, 1) void wgrad_pc_kernel(const irgan_con
     // interleaved one pair per MFMA: the first MFMA retires cur's reads with no
     // newer read in flight, every later one needs no wait (lgkmcnt counts 15).
     auto step = [&](const Frag<MI>& cur, Frag<MI>& nxt, int stage, int h) {
-        const char* S = smem + stage * STAGE + h * 8192;
+        const char* S = smem + stage * STAGE + h * 32 * DYR;
         const char* X = smem + stage * STAGE + h * 4096;
 #pragma unroll
         for (int idx = 0; idx < MI * NJ; ++idx) {
@@ -231,7 +240,7 @@ __global__ __launch_bounds__(PC<CW>::NT, 1) void wgrad_pc_kernel(const irgan_con
                                                                 __builtin_bit_cast(bf16x8_t, cur.b[j]), acc[i][j], 0,
                                                                 0, 0);
 #if !PCX(4)
-            if (idx < MI) nxt.a[idx] = ld_tr_pair(S + aoff[idx], S + aoff[idx] + 1024);
+            if (idx < MI) nxt.a[idx] = ld_tr_pair(S + aoff[idx], S + aoff[idx] + 4 * DYR);
             else if (idx < MI + NJ) nxt.b[idx - MI] = ld_tr_pair(X + boff[idx - MI][0], X + boff[idx - MI][1]);
 #else
             if (idx < MI) nxt.a[idx] = cur.a[idx] ^ make_uint4(idx, 1, 2, 3);
@@ -262,7 +271,7 @@ __global__ __launch_bounds__(PC<CW>::NT, 1) void wgrad_pc_kernel(const irgan_con
     {
         const char* S = smem;
 #pragma unroll
-        for (int i = 0; i < MI; ++i) f0.a[i] = ld_tr_pair(S + aoff[i], S + aoff[i] + 1024);
+        for (int i = 0; i < MI; ++i) f0.a[i] = ld_tr_pair(S + aoff[i], S + aoff[i] + 4 * DYR);
 #pragma unroll
         for (int j = 0; j < NJ; ++j) f0.b[j] = ld_tr_pair(S + boff[j][0], S + boff[j][1]);
     }
@@ -308,13 +317,15 @@ __global__ __launch_bounds__(256) void wgrad_pc_reduce(const float* __restrict__
 }  // namespace
 
 // Preconditions (else IRGAN_EUNSUPPORTED, nothing launched): bf16 operands, KH x 3
-// taps with KW == 3, stride 1, Cout % 128 == 0, Cin % 64 == 0, Wo % 64 == 0, ldx, xoff,
+// taps with KW == 3, stride 1, Cout % 64 == 0, Cin % 64 == 0, Wo % 64 == 0, ldx, xoff,
 // ldy, yoff % 8 == 0, byte extents < 2^31.
 extern "C" int irgan_conv_wgrad_pc(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, int splitk,
                                    float* ws, long ws_cap, hipStream_t st) {
     if ((long)d->N * d->Ho * d->Wo <= 0) return 0;
+    static const bool no64 = getenv("IRGAN_NO_WGRAD_PC64") != nullptr;
+    const int BMC = d->Cout % 128 == 0 ? 128 : 64;
     if (getenv("IRGAN_NO_WGRAD_PC") || d->dtype != IRGAN_BF16 || d->KW != 3 || d->sx != 1 || d->sy != 1 ||
-        d->Cout % BMC || d->Cin % 64 || d->Wo % 64 || d->ldx % 8 || d->xoff % 8 || d->ldy % 8 || d->yoff % 8 ||
+        d->Cout % BMC || (BMC == 64 && no64) || d->Cin % 64 || d->Wo % 64 || d->ldx % 8 || d->xoff % 8 || d->ldy % 8 || d->yoff % 8 ||
         (long)d->N * d->H * d->W * d->ldx * 2 >= (1L << 31) || (long)d->N * d->Ho * d->Wo * d->ldy * 2 >= (1L << 31))
         return IRGAN_EUNSUPPORTED;
     static int cus = 0;
@@ -328,8 +339,8 @@ extern "C" int irgan_conv_wgrad_pc(const irgan_conv_desc* d, const void* x, cons
     const int ntco = d->Cout / BMC, nci = d->Cin / 64;
     const int tiles = ntco * nci * d->KH;
     const int nseg = d->N * d->Ho * (d->Wo / 64);
-    if (splitk <= 0) {  // one block per CU: the largest split count whose grid fits one round
-        splitk = cus / tiles;
+    if (splitk <= 0) {  // one block per CU (BMC 64: two fit): the largest split count whose grid fits one round
+        splitk = (BMC == 64 ? 2 : 1) * cus / tiles;
         if (splitk < 1) splitk = 1;
         const int maxs = irgan_cdiv(nseg, 4);  // >= 4 segments per split
         if (splitk > maxs) splitk = maxs;
@@ -343,12 +354,13 @@ extern "C" int irgan_conv_wgrad_pc(const irgan_conv_desc* d, const void* x, cons
     const long n = (long)d->Cout * d->KH * d->KW * d->Cin;
     float* slab = (ws && splitk > 1 && n % 4 == 0 && (long)splitk * n <= ws_cap) ? ws : nullptr;
     static const int cw = getenv("IRGAN_WGPC_CW4") ? 4 : 8;
-    if (cw == 8)
-        wgrad_pc_kernel<8><<<tiles * splitk, PC<8>::NT, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)dy, dw, spb, nseg,
-                                                                 ntco, nci, swz, slab);
-    else
-        wgrad_pc_kernel<4><<<tiles * splitk, PC<4>::NT, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)dy, dw, spb, nseg,
-                                                                 ntco, nci, swz, slab);
+#define WPC(B, C)                                                                                                   \
+    wgrad_pc_kernel<B, C><<<tiles * splitk, PC<B, C>::NT, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)dy, dw, spb, \
+                                                                   nseg, ntco, nci, swz, slab)
+    if (BMC == 64) WPC(64, 4);   // 4 co fragments x 3 per compute wave (8 waves would hold 2 x 3)
+    else if (cw == 8) WPC(128, 8);
+    else WPC(128, 4);
+#undef WPC
     if (slab) {
         const int blocks = (int)std::min<long>(irgan_cdiv(n / 4, 256), 2048);
         wgrad_pc_reduce<<<blocks, 256, 0, st>>>(slab, splitk, n, dw);

@@ -278,7 +278,10 @@ IRGAN_HD void block_partials8(float* a0, float* a1, const Lay& L, bool on, int c
 }
 
 // All-bf16 fast path of rows_kernel<MODE, 8> for MODE 0 (stats), 1 (backward
-// reduce) and 2 (backward apply without db).  rows_kernel issues one row's
+// reduce) and 2 (backward apply without db), and MODE 4: the forward apply
+// y = act((x - mean) * rstd) [+ res] (res in the dy slot, nullable) -- apply_kernel's job
+// without its per-element index divisions and per-element {mean, rstd} reloads: a
+// thread's 8 channels and image are fixed, so their table entries are loaded once.  rows_kernel issues one row's
 // loads at a time at ~150 VGPRs (3 waves per SIMD), so only ~24 KB of loads are
 // in flight per CU and the backward reduce streams at ~2 TB/s.  Here each
 // thread walks its rows in batches of U and issues every 16-byte load of a
@@ -306,7 +309,7 @@ __global__ __launch_bounds__(TPB) void rows8_kernel(const bf16_t* x, int ldx, in
         float a0[8], a1[8], mean[8], rstd[8], mg[8], mgx[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) { a0[k] = 0.f; a1[k] = 0.f; }
-        if (on && MODE >= 1) {
+        if (on && MODE >= 1) {   // (MODE 4 as well)
             const float4* m4 = (const float4*)(mr + 2 * ((long)n * C + c));
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -330,7 +333,7 @@ __global__ __launch_bounds__(TPB) void rows8_kernel(const bf16_t* x, int ldx, in
                 for (int u = 0; u < U; ++u) {
                     const long p = pb + min(r + u * L.RP, r1 - 1);
                     xr[u] = *(const uint4*)(x + p * ldx + xoff + c);
-                    if (MODE != 0) gr[u] = *(const uint4*)(dy + p * lddy + dyoff + c);
+                    if (MODE != 0 && (MODE != 4 || dy)) gr[u] = *(const uint4*)(dy + p * lddy + dyoff + c);
                 }
                 if (MODE != 0 && dy2) {
 #pragma unroll
@@ -350,7 +353,7 @@ __global__ __launch_bounds__(TPB) void rows8_kernel(const bf16_t* x, int ldx, in
                         continue;
                     }
                     float gv[8];
-                    bf8f(gr[u], gv);
+                    if (MODE != 4 || dy) bf8f(gr[u], gv);
                     if (dy2) {
                         float hv[8];
                         bf8f(hr[u], hv);
@@ -358,14 +361,24 @@ __global__ __launch_bounds__(TPB) void rows8_kernel(const bf16_t* x, int ldx, in
                         for (int k = 0; k < 8; ++k) gv[k] += hv[k];
                     }
                     float o[8];
+                    if (MODE == 4) {   // forward apply (as apply_kernel, same float ops)
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        const float xh = (xv[k] - mean[k]) * rstd[k];
-                        const float g = gv[k] * act_grad(xh, act);
-                        if (MODE == 1) { a0[k] += g; a1[k] += g * xh; }
-                        else o[k] = rstd[k] * (g - mg[k] - xh * mgx[k]);
+                        for (int k = 0; k < 8; ++k) {
+                            float h = (xv[k] - mean[k]) * rstd[k];
+                            if (act == IRGAN_ACT_RELU) h = h > 0.f ? h : 0.f;
+                            else if (act == IRGAN_ACT_LRELU) h = h > 0.f ? h : 0.2f * h;
+                            o[k] = dy ? h + gv[k] : h;
+                        }
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) {
+                            const float xh = (xv[k] - mean[k]) * rstd[k];
+                            const float g = gv[k] * act_grad(xh, act);
+                            if (MODE == 1) { a0[k] += g; a1[k] += g * xh; }
+                            else o[k] = rstd[k] * (g - mg[k] - xh * mgx[k]);
+                        }
                     }
-                    if (MODE == 2) {
+                    if (MODE == 2 || MODE == 4) {
                         uint4 w;
                         w.x = pk_bf16(o[0], o[1]);
                         w.y = pk_bf16(o[2], o[3]);
@@ -383,7 +396,7 @@ __global__ __launch_bounds__(TPB) void rows8_kernel(const bf16_t* x, int ldx, in
                 }
             }
         }
-        if (MODE == 2) continue;  // uniform across the block
+        if (MODE == 2 || MODE == 4) continue;  // uniform across the block
         block_partials8(a0, a1, L, on, cb, c, C, n, s0, s1, part);
     }
     if constexpr (F8) fp8_block_amax(amx, q8.amax, blockIdx.y * gridDim.x + blockIdx.x);
@@ -551,10 +564,15 @@ int rp_of(int C, int VW) {
     return TPB / cl;
 }
 
-// blocks per image: ~4096 blocks over the grid, >= 8 rows per thread, <= IN_PARTS
-int blocks_per_image(long HW, int N, int RP) {
+// blocks per image: ~4096 blocks over the grid, >= rpt rows per thread, <= IN_PARTS.
+// rpt 16 for the reductions (stats, backward reduce: half the partials for the finalize)
+// and the plain forward apply, 8 for the three-stream passes (backward apply, apply +
+// residual) -- measured per pass at the resblock shape (tools/norm_sweep.sh, r03_e:
+// backward reduce + finalize 20.6 -> 17.2 us, apply + ReLU 17.4 -> 16.5, apply + residual
+// 18.1 -> 18.8, backward apply 18.4 -> 18.6; U = 2 / a 128-VGPR cap on the reduce: no gain)
+int blocks_per_image(long HW, int N, int RP, long rpt = 8) {
     long nb = (4096 + N - 1) / (N > 0 ? N : 1);
-    const long maxnb = (HW + 8L * RP - 1) / (8L * RP);
+    const long maxnb = (HW + rpt * RP - 1) / (rpt * RP);
     if (nb > maxnb) nb = maxnb;
     if (nb > IN_PARTS) nb = IN_PARTS;
     if (nb < 1) nb = 1;
@@ -566,7 +584,7 @@ int launch_rows(Slice X, Slice DY, Slice DY2, int act, const float* mr, const fl
                 int dxoff, int N, int HW, int C, float2* part, float* db, bool vec, hipStream_t st, int* nb_out,
                 const Q8* q8 = nullptr) {
     const int VW = vec ? V : 1;
-    int nb = blocks_per_image(HW, N, rp_of(C, VW));
+    int nb = blocks_per_image(HW, N, rp_of(C, VW), MODE == 2 ? 8 : 16);
     const int rows = irgan_cdiv(HW, nb);
     nb = irgan_cdiv(HW, rows);
     dim3 g(nb, N);
@@ -650,10 +668,38 @@ extern "C" int irgan_in_finalize_apply(const void* part, int32_t nb, const void*
     return 0;
 }
 
+// the forward apply as rows8_kernel<4> (bf16, 8-channel vectors, no xhat), grid as the
+// other row passes; q8: also the fp8 copy of y (irgan_in_apply_fp8)
+bool apply_rows(const void* x, int ldx, int xoff, int N, int HW, int C, const float* mr, int act, const void* res,
+                int ldr, int roff, void* y, int ldy, int yoff, hipStream_t st, const Q8* q8 = nullptr) {
+    static const bool off = getenv("IRGAN_NO_APPLY_ROWS") != nullptr;
+    if (off) return false;
+    int nb = blocks_per_image(HW, N, rp_of(C, 8), res ? 8 : 16);
+    const int rows = irgan_cdiv(HW, nb);
+    nb = irgan_cdiv(HW, rows);
+    dim3 g(nb, N);
+    const bf16_t *xp = (const bf16_t*)x, *rp = (const bf16_t*)res;
+    if (q8)
+        rows8_kernel<4, 4, true><<<g, TPB, 0, st>>>(xp, ldx, xoff, rp, ldr, roff, nullptr, 0, 0, act, mr, nullptr,
+                                                    (bf16_t*)y, ldy, yoff, HW, C, rows, nullptr, *q8);
+    else if (res)
+        rows8_kernel<4, 4><<<g, TPB, 0, st>>>(xp, ldx, xoff, rp, ldr, roff, nullptr, 0, 0, act, mr, nullptr,
+                                              (bf16_t*)y, ldy, yoff, HW, C, rows, nullptr);
+    else
+        rows8_kernel<4, 8><<<g, TPB, 0, st>>>(xp, ldx, xoff, nullptr, 0, 0, nullptr, 0, 0, act, mr, nullptr,
+                                              (bf16_t*)y, ldy, yoff, HW, C, rows, nullptr);
+    return true;
+}
+
 extern "C" int irgan_in_apply(const void* x, int32_t dtype, int32_t N, int32_t HW, int32_t C, int32_t ldx,
                               int32_t xoff, const float* mr, int32_t act, const void* res, int32_t ldr, int32_t roff,
                               void* y, int32_t ldy, int32_t yoff, void* xhat, irgan_stream_t s) {
     const bool vec = vec_ok(C, {ldx, xoff, ldy, yoff}) && (!res || vec_ok(C, {ldr, roff}));
+    if (vec && dtype == IRGAN_BF16 && !xhat && (long)N * HW * C > 0 &&
+        apply_rows(x, ldx, xoff, N, HW, C, mr, act, res, ldr, roff, y, ldy, yoff, (hipStream_t)s)) {
+        IRGAN_LAUNCH_CHECK();
+        return 0;
+    }
     const int VW = vec ? V : 1;
     long total = (long)N * HW * (C / VW);
     if (total <= 0) return 0;
@@ -727,10 +773,15 @@ extern "C" int irgan_in_apply_fp8(const void* x, int32_t N, int32_t HW, int32_t 
     if (!vec_ok(C, {ldx, xoff, ldy, yoff, ld8, off8}) || (res && !vec_ok(C, {ldr, roff}))) return IRGAN_EUNSUPPORTED;
     const long total = (long)N * HW * (C / V);
     if (total <= 0) return 0;
+    const Q8 q8v{(uint8_t*)y8, ld8, off8, q, amax};
+    if (apply_rows(x, ldx, xoff, N, HW, C, mr, act, res, ldr, roff, y, ldy, yoff, (hipStream_t)s, &q8v)) {
+        IRGAN_LAUNCH_CHECK();
+        return 0;
+    }
     const int blocks = (int)std::min<long>((total + TPB - 1) / TPB, 16384);
     Slice X{x, IRGAN_BF16, ldx, xoff}, R{res, IRGAN_BF16, ldr, roff};
     apply_kernel<V, true><<<blocks, TPB, 0, (hipStream_t)s>>>(X, HW, C, mr, act, R, y, ldy, yoff, nullptr, total,
-                                                               Q8{(uint8_t*)y8, ld8, off8, q, amax});
+                                                               q8v);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }

@@ -49,6 +49,12 @@ def set_deterministic(on: bool) -> bool:
     return bool(_lib.load().irgan_set_deterministic(int(bool(on))))
 
 
+def set_ring_fold(on: bool) -> bool:
+    """irgan_set_ring_fold: the resblock dgrad as one conv_pp launch with the reflect ring
+    folded in (opt-in) instead of interior + ring launches.  Returns the previous setting."""
+    return bool(_lib.load().irgan_set_ring_fold(int(bool(on))))
+
+
 class LaunchTimer:
     """Optional HIP-event timing of tagged conv launches (bench.py's live
     roofline).  Events are recorded on the launching stream around each launch."""

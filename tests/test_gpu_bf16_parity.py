@@ -49,11 +49,14 @@ EXTRA_CASES = [
     (1, 64, 7, 1, 3, 1, 37),
     (1, 64, 7, 1, 3, 1, 130),
     (4, 64, 4, 2, 1, 0, 258),
-    # Wo % 64 == 0, Cout % 128 == 0: the producer/consumer wgrad (conv_wgrad_pc.hip)
+    # Wo % 64 == 0, Cout % 128 == 0: the producer/consumer wgrad (conv_wgrad_pc.hip, 128-channel co tiles)
     (128, 256, 3, 1, 1, 0, 64),    # down2 shape, zero pad, 2 co tiles
     (384, 128, 3, 1, 1, 0, 64),    # up1_conv shape, 6 ci chunks
     (64, 128, 3, 1, 1, 0, 128),    # down1 shape, 2 segments per row
     (256, 256, 3, 1, 1, 1, 128),   # resblock conv, reflect, interior + edge segments
+    # Cout % 128 != 0 (Cout % 64 == 0): wgrad_pc with 64-channel co tiles (128-B dY rows)
+    (192, 64, 3, 1, 1, 0, 64),     # up2_conv shape, 3 ci chunks
+    (64, 64, 3, 1, 1, 1, 128),     # reflect, 2 segments per row
     # one 64-channel input chunk: the resident-weight persistent kernel (conv_res64) takes the
     # bf16 forward and every dgrad whose dY has 64 channels (ragged patches, reflect, 3 co tiles)
     (64, 64, 3, 1, 1, 1, 37),
@@ -240,7 +243,8 @@ def test_reflect_dgrad_ring_fold_tight(ops, N, H, W):
     the border patches' K loop, ring columns + corners as an epilogue GEMM), so every dx
     pixel is rounded to bf16 ONCE: held to the plain bound (no twice-rounded band), for
     plain / accumulating bf16 and fp32 outputs, non-square and multi-image shapes (every
-    corner / edge patch kind).  Sides that are not (16, 37) take interior + ring launch."""
+    corner / edge patch kind).  Sides that are not (16, 37) take interior + ring launch.
+    The fold is opt-in (ops.set_ring_fold): switched on for this test only."""
     C = 256
     torch.manual_seed(12)
     x = q(torch.randn(N, C, H, W))
@@ -252,7 +256,16 @@ def test_reflect_dgrad_ring_fold_tight(ops, N, H, W):
     pc = ops.PackedConv(spec, w.permute(0, 2, 3, 1).contiguous().reshape(-1).to(DEV), None, ops.BF16)
     pc.pack()
     gyd = nhwc(gy)
-    folded = H % 16 == 0 and W % 16 == 0 and H >= 32 and W >= 32
+    for fold in (True, False):   # fold on, then the default interior + reflect_ring_kernel pair
+        old_fold = ops.set_ring_fold(fold)
+        try:
+            _ring_fold_cases(ops, pc, gyd, dx64, dxa, dxi, N, H, W, C, fold)
+        finally:
+            ops.set_ring_fold(old_fold)
+
+
+def _ring_fold_cases(ops, pc, gyd, dx64, dxa, dxi, N, H, W, C, fold):
+    folded = fold and H % 16 == 0 and W % 16 == 0 and H >= 32 and W >= 32
     for out_dt, r_out in ((torch.bfloat16, R_BF16), (torch.float32, 0.0)):
         dx = torch.zeros(N, H, W, C, device=DEV, dtype=out_dt)
         ops.conv_dgrad(pc, ops.Feat(gyd), ops.Feat(dx))
