@@ -344,6 +344,13 @@ int irgan_ssim_ws(const float* a, const float* b, int32_t N, int32_t H, int32_t 
 /* step_size = lr/(1-beta1^t), bc2_sqrt = sqrt(1-beta2^t) (host, fp64 -> fp32). */
 int irgan_adam(float* p, const float* g, float* m, float* v, int64_t n, float step_size,
                float beta1, float beta2, float bc2_sqrt, float eps, irgan_stream_t s);
+/* The same update with the step count on the device (a captured train step replays with
+ * the right bias corrections): irgan_adam_prep advances *count (int32, device) and writes
+ * prm[0] = step_size, prm[1] = bc2_sqrt for the new count (the host formula above, fp64 on
+ * the device, then fp32); irgan_adam_dev reads them from prm. */
+int irgan_adam_prep(int32_t* count, double lr, double beta1, double beta2, float* prm, irgan_stream_t s);
+int irgan_adam_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* prm, float beta1,
+                   float beta2, float eps, irgan_stream_t s);
 
 /* ---- inference / evaluation ---- */
 /* out[p][c] = uint8(clip((x + 1) / 2, 0, 1) * 255) for every pixel p and

@@ -45,7 +45,8 @@ class ConvDesc(ctypes.Structure):
 
 
 _CTYPES = {
-    "int32_t": ctypes.c_int32, "int64_t": ctypes.c_int64, "float": ctypes.c_float, "uint32_t": ctypes.c_uint32,
+    "int32_t": ctypes.c_int32, "int64_t": ctypes.c_int64, "float": ctypes.c_float, "double": ctypes.c_double,
+    "uint32_t": ctypes.c_uint32,
     "uint64_t": ctypes.c_uint64,
     "irgan_stream_t": ctypes.c_void_p, "void": None,
 }

@@ -20,6 +20,12 @@
 // pixel (r, c) of tap t reads span pixel (2r + ty, 2c + tx).
 #include "conv_epilogue.h"
 
+#ifndef C8_EXP
+#define C8_EXP 0  // A/B timing experiments only (tools/build_variant.sh); 0 = the real kernel
+#endif
+// bits: 1 no output stores, 2 no MFMA, 4 no halo loads (zeros)
+#define C8X(b) ((C8_EXP & (b)) != 0)
+
 namespace {
 
 constexpr int PH = 16, PW = 16;
@@ -89,7 +95,7 @@ __global__ __launch_bounds__(256, 2) void conv_c8_kernel(const irgan_conv_desc d
                     iy = reflect_idx(iy, d.H);
                     ix = reflect_idx(ix, d.W);
                 }
-                if ((unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W)
+                if ((unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W && !C8X(4))
                     hv[u] = *(const uint4*)(x + (((long)img * d.H + iy) * d.W + ix) * d.ldx + d.xoff);
             }
         }
@@ -138,7 +144,7 @@ __global__ __launch_bounds__(256, 2) void conv_c8_kernel(const irgan_conv_desc d
             for (int i = 0; i < 4; ++i)
                 a[i] = *(const uint4*)(H + ((wid * 4 + i) * S * HWd + c16 * S + toff[s]) * 16);
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < 4 * !C8X(2); ++i)
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, b[j]),
@@ -152,7 +158,7 @@ __global__ __launch_bounds__(256, 2) void conv_c8_kernel(const irgan_conv_desc d
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int oy = pyi * PH + wid * 4 + i;
-                if (oy >= d.Ho || ox >= d.Wo) continue;
+                if (oy >= d.Ho || ox >= d.Wo || C8X(1)) continue;
                 const long pix = ((long)img * d.OH + oy * d.omy + d.ooy) * d.OW + ox * d.omx + d.oox;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {

@@ -302,6 +302,9 @@ void launch_narrow(const irgan_conv_desc* d, const void* x, const void* w, const
 
 }  // namespace
 
+extern "C" int irgan_conv_fwd_rowspan(const irgan_conv_desc* d, const void* x, const void* w, const float* bias,
+                                      void* y, const void* mask, hipStream_t st);
+
 // Preconditions (checked by the dispatcher in conv.hip): bf16, sy = sx = 1,
 // Cin % 64 == 0, ldx % 8 == 0, xoff % 8 == 0, 2 <= KH*KW, KH, KW <= 7 (taps
 // beyond 4x4 only for Cout <= 64).
@@ -318,6 +321,8 @@ extern "C" int irgan_conv_fwd_halo(const irgan_conv_desc* d, const void* x, cons
     static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
     static const bool narrow = !getenv("IRGAN_NO_NARROW");
     if (narrow && d->Cout <= 8) {
+        // one 64-channel chunk: the row-span GEMM (conv_rowspan.hip: outc, VGG conv1_1 dgrad)
+        if (irgan_conv_fwd_rowspan(d, x, w, bias, y, mask, st) == 0) return 0;
         if (d->KH == 7 && d->KW == 7) { launch_narrow<7, 7, 8, 1>(d, x, w, bias, y, mask, st, zero, swz); IRGAN_LAUNCH_CHECK(); return 0; }
         if (d->KH == 4 && d->KW == 4) { launch_narrow<4, 4, 6, 2>(d, x, w, bias, y, mask, st, zero, swz); IRGAN_LAUNCH_CHECK(); return 0; }
         if (d->KH == 3 && d->KW == 3) { launch_narrow<3, 3, 6, 2>(d, x, w, bias, y, mask, st, zero, swz); IRGAN_LAUNCH_CHECK(); return 0; }

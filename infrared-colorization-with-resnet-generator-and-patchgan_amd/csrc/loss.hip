@@ -341,9 +341,16 @@ __global__ __launch_bounds__(TPB) void ssim_grad_kernel(const float* __restrict_
     }
 }
 
+// prm (device, nullable): {step_size, bc2s} written by adam_prep_kernel in the same stream
+// (graph replay: the step count lives on the device, so a captured step stays valid)
 __global__ __launch_bounds__(TPB) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, long n,
-                                                   float step_size, float b1, float b2, float bc2s, float eps) {
+                                                   float step_size, float b1, float b2, float bc2s, float eps,
+                                                   const float* __restrict__ prm = nullptr) {
+    if (prm) {
+        step_size = prm[0];
+        bc2s = prm[1];
+    }
     const float w1 = 1.f - b1, w2 = 1.f - b2;
     for (long i = blockIdx.x * (long)TPB + threadIdx.x; i < n; i += (long)gridDim.x * TPB) {
         const float gi = g[i];
@@ -471,6 +478,33 @@ extern "C" int irgan_ssim_ws(const float* a, const float* b, int32_t N, int32_t 
 extern "C" int irgan_ssim(const float* a, const float* b, int32_t N, int32_t H, int32_t W, int32_t C, float w,
                           float* g, double* loss, float* work, irgan_stream_t s) {
     return irgan_ssim_ws(a, b, N, H, W, C, w, g, loss, work, 11, s);
+}
+
+// t = ++*count; prm = {lr / (1 - b1^t), sqrt(1 - b2^t)}: the host formula of irgan_adam's
+// arguments (ops.adam), in fp64 and then rounded to fp32, evaluated on the device
+__global__ void adam_prep_kernel(int32_t* count, double lr, double b1, double b2, float* prm) {
+    if (threadIdx.x != 0) return;
+    const int t = *count + 1;
+    *count = t;
+    const double bc1 = 1.0 - pow(b1, (double)t), bc2 = 1.0 - pow(b2, (double)t);
+    prm[0] = (float)(lr / bc1);
+    prm[1] = (float)sqrt(bc2);
+}
+
+extern "C" int irgan_adam_prep(int32_t* count, double lr, double beta1, double beta2, float* prm, irgan_stream_t s) {
+    if (!count || !prm) return IRGAN_EINVAL;
+    adam_prep_kernel<<<1, 64, 0, (hipStream_t)s>>>(count, lr, beta1, beta2, prm);
+    IRGAN_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int irgan_adam_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* prm, float beta1,
+                              float beta2, float eps, irgan_stream_t s) {
+    if (!prm) return IRGAN_EINVAL;
+    if (n <= 0) return 0;
+    adam_kernel<<<nblocks(n), TPB, 0, (hipStream_t)s>>>(p, g, m, v, n, 0.f, beta1, beta2, 1.f, eps, prm);
+    IRGAN_LAUNCH_CHECK();
+    return 0;
 }
 
 extern "C" int irgan_adam(float* p, const float* g, float* m, float* v, int64_t n, float step_size, float beta1,

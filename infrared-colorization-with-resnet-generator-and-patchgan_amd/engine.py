@@ -125,6 +125,9 @@ class ParamStore:
         self.m = torch.zeros(off, device=device) if with_adam else None
         self.v = torch.zeros(off, device=device) if with_adam else None
         self.step_count = 0
+        self.dev_adam = False   # GANStep: step count on the device (irgan_adam_prep)
+        self._count = self._prm = None
+        self._count_host = 0
 
     def krsc(self, k, buf=None):
         buf = self.flat if buf is None else buf
@@ -209,6 +212,21 @@ class ParamStore:
         bucket's gradient all-reduce completes (BucketedAllreduce.finish)."""
         self.step_count += 1
         t = self.step_count
+        if self.dev_adam:
+            # the count and the bias corrections on the device (a captured step replays with
+            # the right t); the device count is resynced to the host's after a state load
+            if self._count is None:
+                self._count = torch.zeros(1, dtype=torch.int32, device=self.device)
+                self._prm = torch.zeros(2, dtype=torch.float32, device=self.device)
+                self._count_host = 0
+            if self._count_host != t - 1:
+                self._count.fill_(t - 1)
+            ops.adam_prep(self._count, lr, b1, b2, self._prm)
+            self._count_host = t
+
+            def apply_dev(a, b):
+                ops.adam_dev(self.flat[a:b], self.grad[a:b], self.m[a:b], self.v[a:b], self._prm, b1, b2, eps)
+            return apply_dev
 
         def apply(a, b):
             ops.adam(self.flat[a:b], self.grad[a:b], self.m[a:b], self.v[a:b], t, lr, b1, b2, eps)
@@ -233,12 +251,14 @@ class Buffers:
 
     def __init__(self, device):
         self.device, self.d, self.state = device, {}, {}
+        self.allocs = 0   # (re)allocations so far: a captured step is valid while this is unchanged
 
     def get(self, name, shape, dtype):
         t = self.d.get(name)
         if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype:
             t = torch.empty(shape, dtype=dtype, device=self.device)
             self.d[name] = t
+            self.allocs += 1
         return t
 
     def zeros(self, name, shape, dtype):
@@ -247,6 +267,7 @@ class Buffers:
         if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype:
             t = torch.zeros(shape, dtype=dtype, device=self.device)
             self.d[name] = t
+            self.allocs += 1
         return t
 
     def flat(self, name, numel, dtype=torch.float32):
@@ -254,6 +275,7 @@ class Buffers:
         if t is None or t.numel() < numel or t.dtype != dtype:
             t = torch.empty(numel, dtype=dtype, device=self.device)
             self.d[name] = t
+            self.allocs += 1
         return t
 
 
@@ -1105,6 +1127,11 @@ class GANStep:
         self.side = None
         if G.device.type == "cuda" and not os.environ.get("IRGAN_NO_D_OVERLAP"):
             self.side = torch.cuda.Stream(device=G.device)
+        # the whole step as one HIP graph (captured on first use, replayed after): see _graph_ok
+        self.G.dev_adam = self.D.dev_adam = G.device.type == "cuda"
+        self._graph = self._graph_key = self._graph_L = None
+        self._static_in = None
+        self.eager_steps = 0
         self.vgg.pack()
         self.gen.pack()
         self.dis.pack()
@@ -1115,8 +1142,68 @@ class GANStep:
         ops.axpby(Feat(ir_t.t, 0, cin), 1.0, Feat(out.t, 0, cin))
         ops.axpby(Feat(img), 1.0, Feat(out.t, cin, img.shape[3]))
 
+    # ---- HIP graph of the whole step.  Eager, the host enqueues the D step's ~100 side-stream
+    # launches (~2.2 ms of Python) before the main stream's G-step terms, so the main stream
+    # idles behind the host while the D step runs alone (r03 trace: 2.23 ms per step).  A
+    # captured step carries both streams' launches with their event edges; a replay hands
+    # them to the device at once.  Everything that varies per step lives on the device
+    # (inputs copied into static buffers, the Adam step count: ParamStore.dev_adam); the
+    # learning rates and every buffer address are baked in, so the graph is re-captured when
+    # the LR scale changes or any buffer set (re)allocates.
+    def _graph_ok(self, ir):
+        return (self.side is not None and self.pg is None and self.dtype != ops.FP8 and not self.gen.use_dropout
+                and not ops.TIMER.enabled and self.eager_steps >= 1 and not os.environ.get("IRGAN_NO_GRAPH"))
+
+    def _bufsets(self):
+        return (self.bufs, self.dbufs, self.gen.bufs, self.dis.bufs, self.vgg.bufs)
+
+    def _key(self, ir, rgb):
+        c = self.cfg
+        return (tuple(ir.shape), tuple(rgb.shape), self.lr_scale, c.lr_G, c.lr_D, c.beta1, c.beta2,
+                tuple(id(x) for x in self._bufsets()), tuple(x.allocs for x in self._bufsets()))
+
+    def _graph_step(self, ir, rgb):
+        key = self._key(ir, rgb)
+        if self._graph is None or key != self._graph_key:
+            self._graph = None
+            self._static_in = (torch.empty_like(ir), torch.empty_like(rgb))
+            self._static_in[0].copy_(ir)
+            self._static_in[1].copy_(rgb)
+            for st in (self.G, self.D):   # the device counts must match the host's before capture
+                if st._count is not None and st._count_host != st.step_count:
+                    st._count.fill_(st.step_count)
+                    st._count_host = st.step_count
+            counts = (self.G.step_count, self.D.step_count, self.G._count_host, self.D._count_host)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                L = self._eager_step(*self._static_in)
+            # capture ran no kernel: put the host's step counts back
+            self.G.step_count, self.D.step_count, self.G._count_host, self.D._count_host = counts
+            self._graph, self._graph_L = g, L
+            self._graph_key = self._key(ir, rgb)
+        else:
+            if ir.data_ptr() != self._static_in[0].data_ptr():
+                self._static_in[0].copy_(ir)
+            if rgb.data_ptr() != self._static_in[1].data_ptr():
+                self._static_in[1].copy_(rgb)
+        for st in (self.G, self.D):
+            if st._count_host != st.step_count:   # a state load since the capture
+                st._count.fill_(st.step_count)
+            st.step_count += 1
+            st._count_host = st.step_count
+        self._graph.replay()
+        return self._graph_L
+
     def step(self, ir: torch.Tensor, rgb: torch.Tensor):
         """One train step on NCHW fp32 device tensors; returns the loss vector (device)."""
+        if self._graph_ok(ir):
+            return self._graph_step(ir, rgb)
+        L = self._eager_step(ir, rgb)   # (a reallocation it makes shows in _key: re-capture)
+        self.eager_steps += 1
+        return L
+
+    def _eager_step(self, ir: torch.Tensor, rgb: torch.Tensor):
         cfg, b, T = self.cfg, self.bufs, self.tdt
         B, _, H, W = ir.shape
         cin, cout = cfg.input_nc, cfg.output_nc

@@ -60,12 +60,12 @@ class LaunchTimer:
     roofline).  Events are recorded on the launching stream around each launch."""
 
     def __init__(self, tags):
-        self.tags = set(tags)
+        self.tags = set(tags)   # None: every tagged launch (tools/layer_times.py)
         self.pending = []
         self.enabled = False
 
     def wrap(self, tag, fn):
-        if not self.enabled or tag not in self.tags:
+        if not self.enabled or (self.tags is not None and tag not in self.tags):
             return fn()
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
@@ -97,7 +97,7 @@ def _timed(kind, x, fn):
 
 def conv_tag(kind, spec, x_hw, n=None):
     pad = "r" if spec.mode == PAD_REFLECT else "z"
-    nb = f"b{n}" if n is not None else ""
+    nb = f"b{n}/" if n is not None else ""
     return f"{kind}:{spec.cin}x{spec.cout}k{spec.k}s{spec.stride}{pad}@{nb}{x_hw[0]}x{x_hw[1]}"
 
 
@@ -773,6 +773,19 @@ def adam(p, g, m, v, step: int, lr: float, b1: float, b2: float, eps: float):
     bc2 = 1 - b2 ** step
     _lib.call("irgan_adam", P(p), P(g), P(m), P(v), p.numel(), ctypes.c_float(lr / bc1), ctypes.c_float(b1),
               ctypes.c_float(b2), ctypes.c_float(math.sqrt(bc2)), ctypes.c_float(eps), stream())
+
+
+def adam_prep(count: torch.Tensor, lr: float, b1: float, b2: float, prm: torch.Tensor):
+    """Device-side step count + bias corrections (irgan_adam_prep): count (int32[1]) += 1,
+    prm (fp32[2]) = {lr / (1 - b1^t), sqrt(1 - b2^t)} -- ops.adam's host formula."""
+    _lib.call("irgan_adam_prep", P(count), ctypes.c_double(lr), ctypes.c_double(b1), ctypes.c_double(b2), P(prm),
+              stream())
+
+
+def adam_dev(p, g, m, v, prm: torch.Tensor, b1: float, b2: float, eps: float):
+    """ops.adam with step_size / bc2_sqrt read from prm on the device (irgan_adam_dev)."""
+    _lib.call("irgan_adam_dev", P(p), P(g), P(m), P(v), p.numel(), P(prm), ctypes.c_float(b1), ctypes.c_float(b2),
+              ctypes.c_float(eps), stream())
 
 
 # ----------------------------------------------------------------------------

@@ -8,7 +8,7 @@ SRC=$2
 OBJ=$B/var_$1_$(basename $SRC .hip).o
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I include -I $P/csrc -Wno-unused-result $3 -c $P/csrc/$SRC -o $OBJ
 OBJS=""
-for s in conv conv_glds conv_halo conv_pp conv_wgrad_halo conv_wgrad_pc conv_wgrad_narrow conv_ring conv_c8 fp8 infer data norm resample loss; do
+for s in $(python3 -c "import sys; sys.path.insert(0, '$P'); import _build; print(' '.join(x[:-4] for x in _build.SOURCES))"); do
   if [ "$s.hip" = "$SRC" ]; then OBJS="$OBJS $OBJ"; else OBJS="$OBJS $B/$s.o"; fi
 done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $B/libirgan_$1.so $OBJS
