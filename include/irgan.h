@@ -55,6 +55,7 @@ typedef struct irgan_conv_desc {
     int32_t out_dtype;                    /* output dtype */
     int32_t mask_act;                     /* backward mask: 0 none, 1 relu, 2 lrelu(0.2) */
     int32_t ldm, moff;                    /* mask slice (same pixel grid as output) */
+    int32_t cin_real;                     /* nonzero input channels of a zero-padded input (0: Cin) */
 } irgan_conv_desc;
 
 /* y = act(conv(x, w) + bias) [* mask'(m)]   -- replaces nn.Conv2d forward

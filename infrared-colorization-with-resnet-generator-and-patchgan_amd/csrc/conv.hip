@@ -26,6 +26,8 @@ extern "C" int irgan_conv_fwd_c8(const irgan_conv_desc* d, const void* x, const 
                                  const void* mask, hipStream_t st);
 extern "C" int irgan_conv_wgrad_halo(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, int splitk,
                                      float* ws, long ws_cap, hipStream_t st);
+extern "C" int irgan_conv_wgrad_rowspan(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, float* ws,
+                                        long ws_cap, hipStream_t st);
 extern "C" int irgan_conv_wgrad_pc(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, int splitk,
                                    float* ws, long ws_cap, hipStream_t st);
 extern "C" int irgan_conv_wgrad_narrow(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, float* ws,
@@ -605,6 +607,10 @@ int launch_wgrad(const irgan_conv_desc* d, const void* x, const void* dy, float*
     if constexpr (sizeof(T) == 2) {
         {   // 8-channel inputs (G inc, D model.0): conv_wgrad_narrow.hip
             const int rc = irgan_conv_wgrad_narrow(d, x, dy, dw, ws, ws_cap, st);
+            if (rc != IRGAN_EUNSUPPORTED) return rc;
+        }
+        {   // Cout <= 8, 7x7, one 64-channel input chunk (G outc): row-span GEMM (conv_rowspan.hip)
+            const int rc = irgan_conv_wgrad_rowspan(d, x, dy, dw, ws, ws_cap, st);
             if (rc != IRGAN_EUNSUPPORTED) return rc;
         }
         {   // 3x3 stride-1, Cout % 128: producer/consumer row-segment kernel (conv_wgrad_pc.hip)

@@ -25,6 +25,9 @@
 #endif
 // bits: 1 no output stores, 2 no MFMA, 4 no halo loads (zeros)
 #define C8X(b) ((C8_EXP & (b)) != 0)
+#ifndef C8_MINB
+#define C8_MINB 2  // resident blocks per CU the register allocation is held to
+#endif
 
 namespace {
 
@@ -47,7 +50,7 @@ struct C8 {
 };
 
 template <int KH, int KW, int S>
-__global__ __launch_bounds__(256, 2) void conv_c8_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
+__global__ __launch_bounds__(256, C8_MINB) void conv_c8_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
                                                          const bf16_t* __restrict__ w, const float* __restrict__ bias,
                                                          void* __restrict__ y, int tpx, int tpy, int npatch) {
     using G = C8<KH, KW, S>;
@@ -223,6 +226,217 @@ void launch_c8(const irgan_conv_desc* d, const void* x, const void* w, const flo
     conv_c8_kernel<KH, KW, S><<<grid, 256, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, y, tpx, tpy, npatch);
 }
 
+
+// ---- dense-K variant: the REAL input channels only (d.cin_real = CR of the 8): G inc
+// (CR 1), VGG conv1_1 (3), D model.0 (4).  The
+// K axis is (tap, channel) over CR channels, padded to 32: inc 49 -> 64 instead of 392 ->
+// 416, conv1_1 27 -> 32 instead of 96.  Per patch the block builds the im2col tile
+// [256 pixels][64-deep K chunk] in LDS from the resident halo (one 8-byte halo read per
+// tap per pixel), multiplies it with the dense weight rows, and stages the bf16 output
+// tile [256][64] in the same LDS to store it as whole 128-byte pixel rows, 16 bytes per
+// lane: the plain kernel's 8-byte stores straight from the accumulators (16 pixels x 32 B
+// per instruction) held it at ~2 TB/s -- without them it ran 4-5x faster
+// (profiles/r03_k_c8_ablation.txt).  One halo buffer (the halo is dead once the last K
+// chunk's tile is built; the next one is staged through registers meanwhile).  No
+// accumulate (the staged tile is rounded to bf16 before it could be added).
+template <int KH, int KW, int S, int CR>
+struct C8R {
+    static constexpr int TAPS = KH * KW, HWd = PW * S + KW - S, HPIX = (PH * S + KH - S) * HWd;
+    static constexpr int KR = TAPS * CR, KP = (KR + 31) / 32 * 32, NCH = (KP + 63) / 64;
+    static constexpr int WS = KP * 2 + 16;           // weight row stride (bytes)
+    static constexpr int TS = 144;                   // tile row stride: 64 K (or 64 co) bf16 + 16 B
+    static constexpr int HBYTES = HPIX * 16;
+    static constexpr int HPT = (HPIX + 255) / 256;
+    static constexpr int LDS = 64 * WS + HBYTES + 256 * TS;
+    static_assert(2 * LDS <= 160 * 1024, "two resident blocks per CU");
+};
+
+template <int KH, int KW, int S, int CR>
+__global__ __launch_bounds__(256, 2) void conv_c8r_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
+                                                          const bf16_t* __restrict__ w,
+                                                          const float* __restrict__ bias, bf16_t* __restrict__ y,
+                                                          int tpx, int tpy, int npatch) {
+    using G = C8R<KH, KW, S, CR>;
+    constexpr int TAPS = G::TAPS, HWd = G::HWd, HPIX = G::HPIX, KR = G::KR, KP = G::KP, WS = G::WS, TS = G::TS;
+    __shared__ __attribute__((aligned(16))) char smem[G::LDS];
+    char* const sW = smem;
+    char* const sH = smem + 64 * WS;
+    char* const sT = sH + G::HBYTES;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, c16 = lane & 15;
+    const bool reflect = d.pad_mode == IRGAN_PAD_REFLECT;
+
+    // dense weight rows: k = tap * CR + c <- packed [co][tap][8] element tap*8 + c
+    {
+        constexpr int Kw = (TAPS * 8 + 63) / 64 * 64;
+        for (int e = tid; e < 64 * KP; e += 256) {
+            const int co = e / KP, k = e - co * KP;
+            bf16_t v = 0;
+            if (co < d.Cout && k < KR) v = w[(long)co * Kw + (k / CR) * 8 + (k % CR)];
+            *(bf16_t*)(sW + co * WS + k * 2) = v;
+        }
+    }
+    auto load_halo = [&](int p, uint4 (&hv)[G::HPT]) {
+        const int pxi = p % tpx, r = p / tpx, pyi = r % tpy, img = r / tpy;
+#pragma unroll
+        for (int u = 0; u < G::HPT; ++u) {
+            const int h = u * 256 + tid;
+            hv[u] = make_uint4(0u, 0u, 0u, 0u);
+            if (h < HPIX) {
+                const int hy = h / HWd, hx = h - hy * HWd;
+                int iy = pyi * PH * S + hy + d.c0y, ix = pxi * PW * S + hx + d.c0x;
+                if (reflect) {
+                    iy = reflect_idx(iy, d.H);
+                    ix = reflect_idx(ix, d.W);
+                }
+                if ((unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W)
+                    hv[u] = *(const uint4*)(x + (((long)img * d.H + iy) * d.W + ix) * d.ldx + d.xoff);
+            }
+        }
+    };
+    auto store_halo = [&](const uint4 (&hv)[G::HPT]) {
+#pragma unroll
+        for (int u = 0; u < G::HPT; ++u) {
+            const int h = u * 256 + tid;
+            if (h < HPIX) *(uint4*)(sH + h * 16) = hv[u];
+        }
+    };
+    // im2col row of this thread's pixel (patch row pr, column pc) for K chunk kc
+    const int pr = tid >> 4, pcol = tid & 15;
+    auto build = [&](int kc) {
+#pragma unroll
+        for (int k8 = 0; k8 < 8; ++k8) {
+            float v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int kk = kc * 64 + k8 * 8 + k;  // compile-time after unrolling
+                v[k] = 0.f;
+                if (kk < KR) {
+                    const int tap = kk / CR, c = kk % CR, ty = tap / KW, tx = tap % KW;
+                    const int h = (pr * S + ty) * HWd + pcol * S + tx;
+                    v[k] = bf2f(*(const bf16_t*)(sH + h * 16 + c * 2));
+                }
+            }
+            uint4 u;
+            u.x = pk_bf16(v[0], v[1]);
+            u.y = pk_bf16(v[2], v[3]);
+            u.z = pk_bf16(v[4], v[5]);
+            u.w = pk_bf16(v[6], v[7]);
+            if (kc * 64 + k8 * 8 < KP) *(uint4*)(sT + tid * TS + k8 * 16) = u;
+        }
+    };
+
+    float bv[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int co = j * 16 + 4 * g + r;
+            bv[j][r] = (bias && co < d.Cout) ? bias[co] : 0.f;
+        }
+    uint4 hv[G::HPT];
+    int p = blockIdx.x;
+    if (p < npatch) load_halo(p, hv);
+#pragma unroll 1
+    for (; p < npatch; p += gridDim.x) {
+        store_halo(hv);
+        __syncthreads();  // halo p in LDS (and the previous patch's output tile stored)
+        const int pn = p + gridDim.x;
+        if (pn < npatch) load_halo(pn, hv);  // in flight under this patch
+        f32x4 acc[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kc = 0; kc < G::NCH; ++kc) {
+            if (kc) __syncthreads();  // the previous chunk's tile consumed
+            build(kc);
+            __syncthreads();
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                if (kc * 64 + s * 32 >= KP) break;
+                uint4 a[4], b[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) b[j] = *(const uint4*)(sW + (j * 16 + c16) * WS + (kc * 64 + s * 32) * 2 + g * 16);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) a[i] = *(const uint4*)(sT + ((wid * 4 + i) * 16 + c16) * TS + s * 64 + g * 16);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, b[j]),
+                                                                            __builtin_bit_cast(bf16x8_t, a[i]),
+                                                                            acc[i][j], 0, 0, 0);
+            }
+        }
+        __syncthreads();  // every wave done with the tile: it becomes the output staging
+        // pixel (row wid*4+i, column c16), channels j*16 + 4g + r -> staging row (4w+i)*16 + c16
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float v[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = conv_act(acc[i][j][r] + bv[j][r], d.act);
+                uint2 o;
+                o.x = pk_bf16(v[0], v[1]);
+                o.y = pk_bf16(v[2], v[3]);
+                *(uint2*)(sT + ((wid * 4 + i) * 16 + c16) * TS + (j * 16 + 4 * g) * 2) = o;
+            }
+        __syncthreads();
+        // whole pixel rows: 8 lanes x 16 B per pixel, 8 pixels per wave instruction
+        {
+            const int pxi = p % tpx, r0 = p / tpx, pyi = r0 % tpy, img = r0 / tpy;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int e = u * 256 + tid, px = e >> 3, ch = e & 7;
+                const int oy = pyi * PH + (px >> 4), ox = pxi * PW + (px & 15);
+                if (oy >= d.Ho || ox >= d.Wo) continue;
+                const long pix = ((long)img * d.OH + oy * d.omy + d.ooy) * d.OW + ox * d.omx + d.oox;
+                *(uint4*)(y + pix * d.ldy + d.yoff + ch * 8) = *(const uint4*)(sT + px * TS + ch * 16);
+            }
+        }
+    }
+}
+
+template <int KH, int KW, int S, int CR>
+void launch_c8r(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y, hipStream_t st) {
+    static int slots = 0;
+    if (!slots) {
+        int b = 0, dev = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, conv_c8r_kernel<KH, KW, S, CR>, 256, 0) != hipSuccess ||
+            b < 1)
+            b = 1;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+            cus = 256;
+        slots = b * cus;
+    }
+    const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH);
+    const int npatch = d->N * tpx * tpy;
+    const int grid = npatch < slots ? npatch : slots;
+    conv_c8r_kernel<KH, KW, S, CR><<<grid, 256, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, (bf16_t*)y,
+                                                        tpx, tpy, npatch);
+}
+
+// the dense-K launch for (KH, KW, S, cin_real); false: no instance (the caller runs conv_c8)
+bool try_c8r(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y, hipStream_t st) {
+    static const bool off = getenv("IRGAN_NO_C8R") != nullptr;
+    // (accumulate: the staged bf16 tile would round before the add; outc's backward-data
+    // (7x7, 3 channels: 147-deep K in three im2col passes) measured slower than conv_c8)
+    if (off || d->cin_real <= 0 || d->cin_real >= 8 || d->Cout != 64 || d->out_dtype != IRGAN_BF16 || d->ldy % 8 ||
+        d->yoff % 8 || d->accumulate)
+        return false;
+    const int cr = d->cin_real, k = d->KH, s = d->sy;
+    if (k == 7 && s == 1 && cr == 1) launch_c8r<7, 7, 1, 1>(d, x, w, bias, y, st);
+    else if (k == 3 && s == 1 && cr == 3) launch_c8r<3, 3, 1, 3>(d, x, w, bias, y, st);
+    else if (k == 4 && s == 2 && cr == 4) launch_c8r<4, 4, 2, 4>(d, x, w, bias, y, st);
+    else return false;
+    return true;
+}
+
 }  // namespace
 
 // Preconditions: bf16 input and weights, Cin == 8, ldx % 8 == 0, xoff % 8 == 0,
@@ -234,6 +448,10 @@ extern "C" int irgan_conv_fwd_c8(const irgan_conv_desc* d, const void* x, const 
     if (d->dtype != IRGAN_BF16 || d->Cin != 8 || d->ldx % 8 || d->xoff % 8 || d->sy != d->sx || d->Cout > 64 ||
         mask)
         return IRGAN_EUNSUPPORTED;
+    if (d->KH == d->KW && try_c8r(d, x, w, bias, y, st)) {
+        IRGAN_LAUNCH_CHECK();
+        return 0;
+    }
     if (d->sy == 2) {
         if (d->KH == 4 && d->KW == 4) launch_c8<4, 4, 2>(d, x, w, bias, y, st);
         else return IRGAN_EUNSUPPORTED;

@@ -26,6 +26,12 @@
 // lds_off row swizzle (conflict-free 16-byte fragment reads).
 #include "conv_epilogue.h"
 
+#ifndef RS_EXP
+#define RS_EXP 0  // A/B timing experiments only (tools/build_variant.sh); 0 = the real kernels
+#endif
+// wgrad bits: 1 no MFMA phase, 2 no A build, 4 no loads in the loop
+#define RSX(b) ((RS_EXP & (b)) != 0)
+
 namespace {
 
 constexpr int RS_SEG = 32;     // output pixels per row segment
@@ -180,7 +186,262 @@ void launch_rowspan(const irgan_conv_desc* d, const void* x, const void* w, cons
                                                                  nsx, nrb);
 }
 
+// ---- weight gradient of the same layers (G outc, 7x7): the same row-span trick with the
+// shift moved onto dY.  For output row oy, segment x0 and kernel row ty:
+//
+//   dW[ty][n = tx*Cout + co][ci] += sum_q A[q][n] * X[oy + ty + c0y][x0 + q + c0x][ci],
+//   A[q][n] = dY[oy][x0 + q - tx][co]   (0 <= q - tx < 32, else 0)
+//
+// an MFMA GEMM with M = n (32 rows, 21 used), N = ci (64), K = q (64: 38 used; the rest
+// multiplies zeros of A).  Wave ty (< KH) owns the 2 x 4 accumulator tiles of kernel row
+// ty for the whole block (one A fragment feeds 4 MFMAs, one X fragment 2); both operands
+// are K-major in LDS ([q][n] and the [q][ci] ring) and are read with ds_read_b64_tr_b16
+// pairs (conv_wgrad_pc.hip's operand reads).  Per batch of 8 output rows every wave
+// builds its share of the 8 A tiles (64 q x 32 n bf16) from dY while the next 8 input
+// rows stream into the ring.  Block partials -> slab (ordered reduce) or fp32 atomics.
+typedef __attribute__((ext_vector_type(4))) short rs_s16x4;
+typedef __attribute__((address_space(3))) rs_s16x4 rs_lds_s4;
+IRGAN_HD uint4 rs_tr_pair(const char* lo, const char* hi) {
+    const rs_s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((rs_lds_s4*)lo);
+    const rs_s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((rs_lds_s4*)hi);
+    uint4 out;
+    __builtin_memcpy(&out, &a, 8);
+    __builtin_memcpy((char*)&out + 8, &b, 8);
+    return out;
+}
+
+// K-major operand images for the transposed reads, 128-B rows, 16-B chunk XOR 2*t(r)
+// (conv_wgrad_pc.hip's X-span swizzle: conflict-free ds_read_b64_tr_b16 pairs)
+IRGAN_HD int rs_t128(int r) { return ((r >> 1) & 1) | (((r >> 3) & 1) << 1); }
+IRGAN_HD int rs_tr_off(int row, int col) { return row * 128 + (((col >> 3) ^ (2 * rs_t128(row))) << 4) + (col & 7) * 2; }
+
+template <int KH, int KW>
+struct RSW {
+    static constexpr int RR = RS_NR + KH - 1;
+    static constexpr int RING = (RR * RS_QP + 32) * 128;          // + 32 rows: K-step 1 of the last slot
+    static constexpr int AB = RS_NR * 64 * 128;                   // 8 A tiles [64 q][32 n, padded to 64] bf16
+    static constexpr int DB = RS_NR * RS_SEG * 16;                // the batch's dY rows (8 channels)
+    static constexpr int LDS = RING + AB + DB;
+    static_assert(LDS <= 160 * 1024 && KH <= 8, "lds / one kernel row per wave");
+};
+
+template <int KH, int KW>
+__global__ __launch_bounds__(512, 1) void wgrad_rowspan_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
+                                                               const bf16_t* __restrict__ dy, float* __restrict__ dw,
+                                                               float* __restrict__ slab, int nsx, int nrb,
+                                                               int nchunk) {
+    using L = RSW<KH, KW>;
+    constexpr int RR = L::RR;
+    __shared__ __attribute__((aligned(1024))) char smem[L::LDS];
+    char* const sR = smem;
+    char* const sA = smem + L::RING;
+    char* const sD = sA + L::AB;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // block = (64-channel input chunk, image, strip, row block); a group (image, strip, row
+    // block) of nchunk blocks writes one slab partial, each block its chunk's columns
+    const int chunk = blockIdx.x % nchunk, grp = blockIdx.x / nchunk;
+    int t = grp;
+    const int sx = t % nsx;
+    t /= nsx;
+    const int rb = t % nrb;
+    const int img = t / nrb;
+    const int x0 = sx * RS_SEG, R0 = rb * RS_RB;
+    const int R1 = min(d.Ho, R0 + RS_RB);
+    const int Cout = d.Cout;
+    const bool reflect = d.pad_mode == IRGAN_PAD_REFLECT;
+
+    // the slack rows after the ring are read by K-step 1 of the last slot (times zeros of A):
+    // they must hold finite values
+    for (int e = tid; e < 32 * 8; e += 512) *(uint4*)(sR + (RR * RS_QP) * 128 + e * 16) = make_uint4(0u, 0u, 0u, 0u);
+    const i32x4 rs = make_rsrc(x, (uint32_t)((long)d.N * d.H * d.W * d.ldx * 2));
+    const int sub = lane >> 3, cl = lane & 7;
+    auto load_row = [&](int rel, int part) {
+        const int slot = rel % RR;
+        const int lrow = slot * RS_QP + part * 8 + sub;
+        const int q = part * 8 + sub;
+        int iy = R0 + d.c0y + rel, ix = x0 + q + d.c0x;
+        if (reflect) {
+            iy = reflect_idx(iy, d.H);
+            ix = reflect_idx(ix, d.W);
+        }
+        const bool ok = q < RS_SEG + KW - 1 && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+        const int ck = cl ^ (2 * rs_t128(lrow));
+        const uint32_t off =
+            ok ? (uint32_t)((((img * d.H + iy) * d.W + ix) * d.ldx + d.xoff) * 2 + chunk * 128 + ck * 16)
+               : IRGAN_OOB;
+        blds16(rs, off, sR + (slot * RS_QP + part * 8) * 128);
+    };
+    // the batch's dY rows -> sD [8 rows][32 px][8 channels] (4 wave-instructions; out of
+    // range -> zeros)
+    const i32x4 rsd = make_rsrc(dy, (uint32_t)((long)d.N * d.Ho * d.Wo * d.ldy * 2));
+    auto load_dy = [&](int it) {
+        if (wid < 4) {
+            const int r = wid * 2 + (lane >> 5), j = lane & 31, oy = R0 + it * RS_NR + r, ox = x0 + j;
+            const bool ok = oy < R1 && ox < d.Wo;
+            const uint32_t off = ok ? (uint32_t)((((long)img * d.Ho + oy) * d.Wo + ox) * d.ldy + d.yoff) * 2 : IRGAN_OOB;
+            blds16(rsd, off, sD + wid * 1024);
+        }
+    };
+    // A tiles of batch `it` (from sD): row r, q, 8 consecutive n -> one 16-byte LDS write
+    auto build_a = [&](int it) {
+        for (int e = tid; e < RS_NR * 64 * 4; e += 512) {
+            const int r = e >> 8, q = (e >> 2) & 63, n8 = (e & 3) * 8;
+            float v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int n = n8 + k, tx = n / Cout, co = n - tx * Cout, j = q - tx;
+                const bool ok = n < KW * Cout && j >= 0 && j < RS_SEG;
+                v[k] = ok ? bf2f(*(const bf16_t*)(sD + (r * RS_SEG + j) * 16 + co * 2)) : 0.f;
+            }
+            uint4 u;
+            u.x = pk_bf16(v[0], v[1]);
+            u.y = pk_bf16(v[2], v[3]);
+            u.z = pk_bf16(v[4], v[5]);
+            u.w = pk_bf16(v[6], v[7]);
+            *(uint4*)(sA + r * 8192 + rs_tr_off(q, n8)) = u;
+        }
+    };
+    for (int e = wid; e < RR * 5; e += 8) load_row(e / 5, e % 5);
+    load_dy(0);
+    wait_vmcnt<0>();
+    __syncthreads();
+    build_a(0);
+    __syncthreads();
+
+    // lane roles of the transposed operand reads (conv_wgrad_pc.hip): k row k_lo (+4 for the
+    // high half, +32 for K-step 1), 4 consecutive columns from 4p
+    const int g = lane >> 4, qq = (lane & 15) >> 2, p = lane & 3;
+    const int k_lo = 8 * g + qq;
+    const int ty = wid;  // waves >= KH only build / load
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int xo[4];  // X column byte terms of ci fragment j (swizzle applied per row below)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xo[j] = (16 * j + 4 * p);
+
+#pragma unroll 1
+    for (int it = 0; R0 + it * RS_NR < R1; ++it) {
+        if (ty < KH && !RSX(1)) {
+#pragma unroll 2
+            for (int r = 0; r < RS_NR; ++r) {
+                const int slot = (it * RS_NR + r + ty) % RR;
+                const char* Ar = sA + r * 8192;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    uint4 a[2], b[4];
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        const int q0 = 32 * h + k_lo, col = 16 * i + 4 * p;
+                        a[i] = rs_tr_pair(Ar + rs_tr_off(q0, col), Ar + rs_tr_off(q0 + 4, col));
+                    }
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int row = slot * RS_QP + 32 * h + k_lo;
+                        b[j] = rs_tr_pair(sR + rs_tr_off(row, xo[j]), sR + rs_tr_off(row + 4, xo[j]));
+                    }
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a[i]),
+                                                                                __builtin_bit_cast(bf16x8_t, b[j]),
+                                                                                acc[i][j], 0, 0, 0);
+                }
+            }
+        }
+        __syncthreads();  // ring rows of this batch and its A tiles consumed
+        if (R0 + (it + 1) * RS_NR < R1) {
+            if (!RSX(4)) {
+                for (int e = wid; e < RS_NR * 5; e += 8) load_row((it + 1) * RS_NR + KH - 1 + e / 5, e % 5);
+                load_dy(it + 1);
+                wait_vmcnt<0>();
+            }
+            __syncthreads();
+            if (!RSX(2)) build_a(it + 1);
+            __syncthreads();
+        }
+    }
+    if (ty >= KH) return;
+    // C[row = n][col = ci]: n = 16i + 4g + rr, ci = 16j + (lane & 15)
+    const int Kw = KH * KW * d.Cin;
+    float* const dst = slab ? slab + (long)grp * Cout * Kw : nullptr;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const int n = 16 * i + 4 * g + rr;
+            if (n >= KW * Cout) continue;
+            const int tx = n / Cout, co = n - tx * Cout;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const long o = (long)co * Kw + (ty * KW + tx) * d.Cin + chunk * 64 + 16 * j + (lane & 15);
+                if (dst) dst[o] = acc[i][j][rr];
+                else atomicAdd(dw + o, acc[i][j][rr]);
+            }
+        }
+}
+
+// Ordered two-level reduce of the nb group partials (n floats each; deterministic): level 1
+// sums slabs [part*per, (part+1)*per) of index i into tmp[part][i] -- n is small (outc 9408)
+// and nb large (512), so one thread per index would be a 512-long dependent load chain --
+// level 2 adds the parts into dw in order.
+__global__ __launch_bounds__(256) void wgrad_rowspan_reduce1(const float* __restrict__ slab, int nb, int per, long n,
+                                                             float* __restrict__ tmp) {
+    const long i = blockIdx.x * 256L + threadIdx.x;
+    if (i >= n) return;
+    const int b0 = blockIdx.y * per, b1 = min(nb, b0 + per);
+    float a = 0.f;
+    for (int b = b0; b < b1; ++b) a += slab[(long)b * n + i];
+    tmp[(long)blockIdx.y * n + i] = a;
+}
+__global__ __launch_bounds__(256) void wgrad_rowspan_reduce2(const float* __restrict__ tmp, int parts, long n,
+                                                             float* __restrict__ dw) {
+    const long i = blockIdx.x * 256L + threadIdx.x;
+    if (i >= n) return;
+    float a = dw[i];
+    for (int q = 0; q < parts; ++q) a += tmp[(long)q * n + i];
+    dw[i] = a;
+}
+
 }  // namespace
+
+// Weight gradient of narrow-output stride-1 convs: G outc (7x7, Cin 64) and D's last layer
+// (512 -> 1, 4x4: its 64-channel chunks are separate blocks of one group).  bf16, Cin % 64,
+// KW * Cout <= 32, ldx / xoff % 8.  dw += the gradient (fp32 [Cout][KH][KW][Cin]); the group
+// partials go through ws (ordered reduce) when groups * Cout * KH * KW * Cin <= ws_cap, else
+// fp32 atomics.
+extern "C" int irgan_conv_wgrad_rowspan(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, float* ws,
+                                        long ws_cap, hipStream_t st) {
+    if ((long)d->N * d->Ho * d->Wo <= 0 || d->Cout <= 0) return 0;
+    static const bool off = getenv("IRGAN_NO_ROWSPAN") != nullptr;
+    if (off || d->dtype != IRGAN_BF16 || d->sy != 1 || d->sx != 1 || d->Cin % 64 || d->Cout > 8 ||
+        d->KW * d->Cout > 32 || d->KH != d->KW || (d->KH != 7 && d->KH != 4) || d->ldx % 8 || d->xoff % 8 ||
+        d->ldy % 8 || d->yoff % 8 || (long)d->N * d->H * d->W * d->ldx * 2 >= (1L << 31) ||
+        (long)d->N * d->Ho * d->Wo * d->ldy * 2 >= (1L << 31))
+        return IRGAN_EUNSUPPORTED;
+    const int nsx = irgan_cdiv(d->Wo, RS_SEG), nrb = irgan_cdiv(d->Ho, RS_RB), nchunk = d->Cin / 64;
+    const int ng = d->N * nsx * nrb;
+    const long n = (long)d->Cout * d->KH * d->KW * d->Cin;
+    const int per = 16, parts = irgan_cdiv(ng, per);
+    float* slab = (ws && (long)(ng + parts) * n <= ws_cap) ? ws : nullptr;
+    if (d->KH == 7)
+        wgrad_rowspan_kernel<7, 7><<<ng * nchunk, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)dy, dw, slab, nsx,
+                                                                nrb, nchunk);
+    else
+        wgrad_rowspan_kernel<4, 4><<<ng * nchunk, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)dy, dw, slab, nsx,
+                                                                nrb, nchunk);
+    if (slab) {
+        float* tmp = slab + (long)ng * n;
+        wgrad_rowspan_reduce1<<<dim3((unsigned)irgan_cdiv(n, 256), parts), 256, 0, st>>>(slab, ng, per, n, tmp);
+        wgrad_rowspan_reduce2<<<(unsigned)irgan_cdiv(n, 256), 256, 0, st>>>(tmp, parts, n, dw);
+    }
+    IRGAN_LAUNCH_CHECK();
+    return 0;
+}
 
 // Shapes it takes (else IRGAN_EUNSUPPORTED, nothing launched): bf16 operands, stride 1,
 // Cin == 64, KW * Cout <= 32 (Cout <= 8), (KH, KW) in {(7,7), (3,3)}, ldx / xoff % 8,

@@ -1149,10 +1149,13 @@ class GANStep:
     # them to the device at once.  Everything that varies per step lives on the device
     # (inputs copied into static buffers, the Adam step count: ParamStore.dev_adam); the
     # learning rates and every buffer address are baked in, so the graph is re-captured when
-    # the LR scale changes or any buffer set (re)allocates.
+    # the LR scale changes or any buffer set (re)allocates.  Opt-in (IRGAN_GRAPH=1): on the
+    # bench step the replay measured no faster than eager (r03_h: 1119 / 1113 vs 1124 / 1128
+    # img/s on one box) -- the device runs the captured branches without the eager schedule's
+    # side-stream overlap gain, so the host-starvation gap is traded for lost concurrency.
     def _graph_ok(self, ir):
         return (self.side is not None and self.pg is None and self.dtype != ops.FP8 and not self.gen.use_dropout
-                and not ops.TIMER.enabled and self.eager_steps >= 1 and not os.environ.get("IRGAN_NO_GRAPH"))
+                and not ops.TIMER.enabled and self.eager_steps >= 1 and bool(os.environ.get("IRGAN_GRAPH")))
 
     def _bufsets(self):
         return (self.bufs, self.dbufs, self.gen.bufs, self.dis.bufs, self.vgg.bufs)

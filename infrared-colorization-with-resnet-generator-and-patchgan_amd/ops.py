@@ -259,7 +259,8 @@ def conv_fwd(pc: PackedConv, x: Feat, y: Feat, act=ACT_NONE, bias=True, accumula
     d = _desc(N=x.N, H=x.H, W=x.W, Cin=pc.cin_eff, ldx=x.ld, xoff=x.off, Ho=Ho, Wo=Wo, Cout=s.cout, ldy=y.ld,
               yoff=y.off, OH=Ho, OW=Wo, omy=1, ooy=0, omx=1, oox=0, KH=s.k, KW=s.k, sy=s.stride, sx=s.stride,
               c0y=-s.pad, c0x=-s.pad, pad_mode=s.mode, act=act, accumulate=int(accumulate), dtype=pc.dtype,
-              out_dtype=y.dt, mask_act=mask_act, ldm=mask.ld if mask else 0, moff=mask.off if mask else 0)
+              out_dtype=y.dt, mask_act=mask_act, ldm=mask.ld if mask else 0, moff=mask.off if mask else 0,
+              cin_real=s.cin if s.cin < pc.cin_eff else 0)
     assert x.dt == pc.dtype
     TIMER.wrap(conv_tag("fwd", s, (x.H, x.W), x.N), lambda: _lib.call(
         "irgan_conv_fwd", ctypes.byref(d), x.ptr, P(pc.fwd), P(pc.bias if bias else None), y.ptr,
@@ -318,7 +319,8 @@ def conv_dgrad(pc: PackedConv, dy: Feat, dx: Feat, accumulate=False, mask: Feat 
         assert mask is None
         (_, _, ay, c0y), (_, _, ax, c0x), buf = pc.dg[0]
         base = dict(N=dy.N, H=dy.H, W=dy.W, Cin=pc.cout_eff, ldx=dy.ld, xoff=dy.off, Cout=s.cin, KH=ay, KW=ax,
-                    pad_mode=PAD_ZERO, act=0, dtype=pc.dtype, mask_act=0, ldm=0, moff=0)
+                    pad_mode=PAD_ZERO, act=0, dtype=pc.dtype, mask_act=0, ldm=0, moff=0,
+                    cin_real=s.cout if s.cout < pc.cout_eff else 0)
         d = _desc(**base, Ho=H, Wo=W, ldy=dx.ld, yoff=dx.off, OH=H, OW=W, omy=1, ooy=0, omx=1, oox=0, sy=1, sx=1,
                   c0y=c0y + p, c0x=c0x + p, accumulate=int(accumulate), out_dtype=dx.dt)
         ring_mfma = (p > 0 and pc.dtype == BF16 and RING_MFMA and pc.cout_eff % 32 == 0 and H >= 2 * p + 2

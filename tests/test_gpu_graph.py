@@ -4,9 +4,9 @@ With the whole step in a graph, the host no longer feeds the two streams launch 
 launch; what differs from eager is only WHEN kernels are issued.  In deterministic mode
 (ops.set_deterministic) every kernel is run-to-run reproducible, so graph replays must
 give bit-identical losses-to-1e-12, grads, parameters and Adam moments to eager steps
-(IRGAN_NO_GRAPH=1) -- including across a learning-rate change (re-capture) and across a
-checkpoint save / load in the middle of a run (the Adam step count lives on the device
-and is resynced from the loaded state)."""
+(the default; IRGAN_GRAPH=1 turns the graph on) -- including across a learning-rate
+change (re-capture) and across a checkpoint save / load in the middle of a run (the Adam
+step count lives on the device and is resynced from the loaded state)."""
 import pytest
 import torch
 
@@ -34,9 +34,9 @@ def _same(ta, tb, what):
 
 def _run(monkeypatch, graph, batches, lr_change_after=None):
     if graph:
-        monkeypatch.delenv("IRGAN_NO_GRAPH", raising=False)
+        monkeypatch.setenv("IRGAN_GRAPH", "1")
     else:
-        monkeypatch.setenv("IRGAN_NO_GRAPH", "1")
+        monkeypatch.delenv("IRGAN_GRAPH", raising=False)
     tr, _ = make_trainer(load_golden("s64"), "bf16")
     losses, captures, last = [], 0, None
     for i, (ir, rgb) in enumerate(batches):
@@ -71,7 +71,7 @@ def test_graph_resume_from_checkpoint(monkeypatch, tmp_path):
     """4 graph steps in one run == 2 graph steps, checkpoint, a fresh trainer that loads it
     and runs 2 more graph steps: the device step count follows the loaded Adam state."""
     ops = pkg().ops
-    monkeypatch.delenv("IRGAN_NO_GRAPH", raising=False)
+    monkeypatch.setenv("IRGAN_GRAPH", "1")
     batches = _batches(4, seed=62)
     old = ops.set_deterministic(True)
     try:
