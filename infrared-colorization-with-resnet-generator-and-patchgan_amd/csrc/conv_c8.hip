@@ -18,6 +18,8 @@
 // 4 waves; wave w owns patch rows 4w..4w+3 (4 pixel fragments) x 64 channels.
 // Stride 2 (D's first layer, 4x4): the halo is the 34x34 input span and output
 // pixel (r, c) of tap t reads span pixel (2r + ty, 2c + tx).
+#include <type_traits>
+
 #include "conv_epilogue.h"
 
 #ifndef C8_EXP
@@ -228,7 +230,7 @@ void launch_c8(const irgan_conv_desc* d, const void* x, const void* w, const flo
 
 
 // ---- dense-K variant: the REAL input channels only (d.cin_real = CR of the 8): G inc
-// (CR 1), VGG conv1_1 (3), D model.0 (4).  The
+// (CR 1), VGG conv1_1 (3), D model.0 (4), G outc backward-data (dY of 3 channels).  The
 // K axis is (tap, channel) over CR channels, padded to 32: inc 49 -> 64 instead of 392 ->
 // 416, conv1_1 27 -> 32 instead of 96.  Per patch the block builds the im2col tile
 // [256 pixels][64-deep K chunk] in LDS from the resident halo (one 8-byte halo read per
@@ -302,28 +304,33 @@ __global__ __launch_bounds__(256, 2) void conv_c8r_kernel(const irgan_conv_desc 
             if (h < HPIX) *(uint4*)(sH + h * 16) = hv[u];
         }
     };
-    // im2col row of this thread's pixel (patch row pr, column pc) for K chunk kc
+    // im2col row of this thread's pixel (patch row pr, column pc) for K chunk kc: one 8-byte
+    // halo read (channels 0-3) per tap the chunk touches, the bf16 halves moved by bit ops
     const int pr = tid >> 4, pcol = tid & 15;
-    auto build = [&](int kc) {
+    auto build = [&](auto kcc) {
+        constexpr int kc = decltype(kcc)::value;
+        constexpr int k0 = kc * 64, k1 = (k0 + 64 < KR ? k0 + 64 : KR);
+        constexpr int t0 = k0 / CR, t1 = (k1 - 1) / CR;   // taps of this chunk
+        uint2 tv[t1 - t0 + 1];
+#pragma unroll
+        for (int t = t0; t <= t1; ++t) {
+            const int ty = t / KW, tx = t % KW;
+            tv[t - t0] = *(const uint2*)(sH + ((pr * S + ty) * HWd + pcol * S + tx) * 16);
+        }
+        auto half = [&](int kk) -> uint32_t {   // bf16 bits of K index kk (0 past KR)
+            if (kk >= KR) return 0u;
+            const int t = kk / CR, c = kk % CR;
+            const uint2 v = tv[t - t0];
+            const uint32_t wd = c < 2 ? v.x : v.y;
+            return (c & 1) ? (wd >> 16) : (wd & 0xffffu);
+        };
 #pragma unroll
         for (int k8 = 0; k8 < 8; ++k8) {
-            float v[8];
+            if (k0 + k8 * 8 >= KP) break;
+            uint32_t wds[4];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const int kk = kc * 64 + k8 * 8 + k;  // compile-time after unrolling
-                v[k] = 0.f;
-                if (kk < KR) {
-                    const int tap = kk / CR, c = kk % CR, ty = tap / KW, tx = tap % KW;
-                    const int h = (pr * S + ty) * HWd + pcol * S + tx;
-                    v[k] = bf2f(*(const bf16_t*)(sH + h * 16 + c * 2));
-                }
-            }
-            uint4 u;
-            u.x = pk_bf16(v[0], v[1]);
-            u.y = pk_bf16(v[2], v[3]);
-            u.z = pk_bf16(v[4], v[5]);
-            u.w = pk_bf16(v[6], v[7]);
-            if (kc * 64 + k8 * 8 < KP) *(uint4*)(sT + tid * TS + k8 * 16) = u;
+            for (int k = 0; k < 4; ++k) wds[k] = half(k0 + k8 * 8 + 2 * k) | (half(k0 + k8 * 8 + 2 * k + 1) << 16);
+            *(uint4*)(sT + tid * TS + k8 * 16) = make_uint4(wds[0], wds[1], wds[2], wds[3]);
         }
     };
 
@@ -349,10 +356,10 @@ __global__ __launch_bounds__(256, 2) void conv_c8r_kernel(const irgan_conv_desc 
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kc = 0; kc < G::NCH; ++kc) {
+        auto chunk = [&](auto kcc) {
+            constexpr int kc = decltype(kcc)::value;
             if (kc) __syncthreads();  // the previous chunk's tile consumed
-            build(kc);
+            build(kcc);
             __syncthreads();
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
@@ -370,7 +377,11 @@ __global__ __launch_bounds__(256, 2) void conv_c8r_kernel(const irgan_conv_desc 
                                                                             __builtin_bit_cast(bf16x8_t, a[i]),
                                                                             acc[i][j], 0, 0, 0);
             }
-        }
+        };
+        chunk(std::integral_constant<int, 0>());
+        if constexpr (G::NCH > 1) chunk(std::integral_constant<int, 1>());
+        if constexpr (G::NCH > 2) chunk(std::integral_constant<int, 2>());
+        static_assert(G::NCH <= 3, "K chunks");
         __syncthreads();  // every wave done with the tile: it becomes the output staging
         // pixel (row wid*4+i, column c16), channels j*16 + 4g + r -> staging row (4w+i)*16 + c16
 #pragma unroll
@@ -424,13 +435,13 @@ void launch_c8r(const irgan_conv_desc* d, const void* x, const void* w, const fl
 // the dense-K launch for (KH, KW, S, cin_real); false: no instance (the caller runs conv_c8)
 bool try_c8r(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y, hipStream_t st) {
     static const bool off = getenv("IRGAN_NO_C8R") != nullptr;
-    // (accumulate: the staged bf16 tile would round before the add; outc's backward-data
-    // (7x7, 3 channels: 147-deep K in three im2col passes) measured slower than conv_c8)
+    // (accumulate: the staged bf16 tile would round before the add)
     if (off || d->cin_real <= 0 || d->cin_real >= 8 || d->Cout != 64 || d->out_dtype != IRGAN_BF16 || d->ldy % 8 ||
         d->yoff % 8 || d->accumulate)
         return false;
     const int cr = d->cin_real, k = d->KH, s = d->sy;
     if (k == 7 && s == 1 && cr == 1) launch_c8r<7, 7, 1, 1>(d, x, w, bias, y, st);
+    else if (k == 7 && s == 1 && cr == 3) launch_c8r<7, 7, 1, 3>(d, x, w, bias, y, st);
     else if (k == 3 && s == 1 && cr == 3) launch_c8r<3, 3, 1, 3>(d, x, w, bias, y, st);
     else if (k == 4 && s == 2 && cr == 4) launch_c8r<4, 4, 2, 4>(d, x, w, bias, y, st);
     else return false;

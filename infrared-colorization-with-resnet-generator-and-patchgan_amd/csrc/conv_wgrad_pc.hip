@@ -52,11 +52,8 @@ typedef __attribute__((address_space(3))) s16x4 lds_s4;
 IRGAN_HD int pc_t128(int r) { return ((r >> 1) & 1) | (((r >> 3) & 1) << 1); }
 IRGAN_HD int pc_t256(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
 
-constexpr int KW = 3;
-constexpr int XPOS = 66;                 // X span positions (63 + KW)
-constexpr int XPIECES = 9;               // 72 positions, 8 per piece
+constexpr int XPIECES = 9;               // 72 X span positions, 8 per piece
 constexpr int STAGES = 4;
-constexpr int NJ = 3;                    // 3 (tx, 16-ci) fragments per compute wave
 // BMC: co tile (128 or 64).  CW compute waves: 4 -> BMC co x 48 n per wave (1 per SIMD);
 // 8 -> BMC/2 co x 48 n (2 per SIMD)
 template <int BMC, int CW>
@@ -82,12 +79,16 @@ IRGAN_HD uint4 ld_tr_pair(const char* lo, const char* hi) {
     return out;
 }
 
-template <int MI>
+template <int MI, int NJ>
 struct Frag {
     uint4 a[MI], b[NJ];
 };
 
-template <int BMC, int CW>
+// KW: 3 or 4 taps per kernel row (NJ = KW (tx, 16-ci) fragments per compute wave).
+// PAIR (Wo <= 32: D model.8, 31 wide): a 64-pixel segment is TWO output rows of 32 (pixel
+// 32 h + c of row oy0 + h), and the X span holds both input rows: positions [36 h, 36 h +
+// 35) are row h's, so k-step h reads position 36 h + k + tx.
+template <int BMC, int CW, int KW = 3, bool PAIR = false>
 __global__ __launch_bounds__((PC<BMC, CW>::NT), 1) void wgrad_pc_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
                                                           const bf16_t* __restrict__ dy, float* __restrict__ dw,
                                                           int segs_per_block, int nseg, int ntco, int nci, int swz,
@@ -95,6 +96,8 @@ __global__ __launch_bounds__((PC<BMC, CW>::NT), 1) void wgrad_pc_kernel(const ir
     using Q = PC<BMC, CW>;
     constexpr int APIECES = Q::APIECES, TP = Q::TP, STAGE = Q::STAGE, PPL = Q::PPL, DYR = Q::DYR;
     constexpr int DROWS = 1024 / DYR;  // dY rows per piece
+    constexpr int NJ = KW, XPOS = 63 + KW;
+    static_assert(KW == 3 || KW == 4, "taps per row");
     __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -128,6 +131,7 @@ __global__ __launch_bounds__((PC<BMC, CW>::NT), 1) void wgrad_pc_kernel(const ir
         const int cout8 = (d.Cout + 7) / 8 * 8;
         uint32_t voff[PPL];
         int xpos[PPL], xc16[PPL];
+        uint32_t second = 0;  // PAIR: bit u set when piece u's lane row is in the segment's 2nd output row
 #pragma unroll
         for (int u = 0; u < PPL; ++u) {
             const int j = l + 4 * u;
@@ -137,33 +141,55 @@ __global__ __launch_bounds__((PC<BMC, CW>::NT), 1) void wgrad_pc_kernel(const ir
             if (j < APIECES) {
                 const int pos = j * DROWS + lane / (64 / DROWS), slot = lane % (64 / DROWS);
                 const int c16 = slot ^ (2 * pc_dsw<BMC>(pos));
-                if (co0 + c16 * 8 < cout8) voff[u] = (uint32_t)((pos * d.ldy + c16 * 8) * 2);
+                // PAIR: tile row pos = pixel (pos & 31) of output row pos >> 5 (masked past Wo)
+                const int mpix = PAIR ? (pos >> 5) * d.Wo + (pos & 31) : pos;
+                const bool pix_ok = !PAIR || (pos & 31) < d.Wo;
+                if (PAIR && pos >= 32) second |= 1u << u;
+                if (co0 + c16 * 8 < cout8 && pix_ok) voff[u] = (uint32_t)((mpix * d.ldy + c16 * 8) * 2);
             } else if (j < TP) {
                 const int pos = (j - APIECES) * 8 + (lane >> 3), slot = lane & 7;
                 xpos[u] = pos;
                 xc16[u] = (slot ^ (2 * pc_t128(pos))) * 16;  // byte offset of the lane's 16-B chunk
             }
         }
+        const int hpair = (d.Ho + 1) >> 1;  // PAIR: row pairs per image
         auto issue = [&](int s, int stage) {
-            const int rowi = s / segs_row, x0 = (s - rowi * segs_row) * 64;
-            const int n = rowi / d.Ho, oy = rowi - n * d.Ho;
-            int iy = oy * d.sy + ty + d.c0y;
-            if (reflect) iy = reflect_idx(iy, d.H);
-            const bool row_ok = (unsigned)iy < (unsigned)d.H;
-            const uint32_t dy_soff = (uint32_t)(((long)rowi * d.Wo + x0) * d.ldy * 2);
-            const long xrow = ((long)n * d.H + iy) * d.W;
+            int n, oy, x0;
+            if (PAIR) {
+                n = s / hpair;
+                oy = (s - n * hpair) * 2;
+                x0 = 0;
+            } else {
+                const int rowi = s / segs_row;
+                x0 = (s - rowi * segs_row) * 64;
+                n = rowi / d.Ho;
+                oy = rowi - n * d.Ho;
+            }
+            const bool second_ok = !PAIR || oy + 1 < d.Ho;
+            int iy0 = oy * d.sy + ty + d.c0y, iy1 = (oy + 1) * d.sy + ty + d.c0y;
+            if (reflect) {
+                iy0 = reflect_idx(iy0, d.H);
+                iy1 = reflect_idx(iy1, d.H);
+            }
+            const bool row0_ok = (unsigned)iy0 < (unsigned)d.H, row1_ok = second_ok && (unsigned)iy1 < (unsigned)d.H;
+            const uint32_t dy_soff = (uint32_t)((((long)n * d.Ho + oy) * d.Wo + x0) * d.ldy * 2);
+            const long xrow0 = ((long)n * d.H + iy0) * d.W, xrow1 = ((long)n * d.H + iy1) * d.W;
             char* base = smem + stage * STAGE;
 #pragma unroll
             for (int u = 0; u < PPL; ++u) {
                 if (u >= np) break;
                 const int j = l + 4 * u;
                 if (j < APIECES) {
-                    blds16(rs_dy, voff[u], dy_soff, base + j * 1024);
+                    const uint32_t vo = (PAIR && !second_ok && ((second >> u) & 1)) ? IRGAN_OOB : voff[u];
+                    blds16(rs_dy, vo, dy_soff, base + j * 1024);
                 } else {
-                    int ix = x0 + d.c0x + xpos[u];
+                    const bool hi = PAIR && xpos[u] >= 36;
+                    const int xp = hi ? xpos[u] - 36 : xpos[u];
+                    int ix = x0 + d.c0x + xp;
                     if (reflect) ix = reflect_idx(ix, d.W);
-                    const bool ok = row_ok & (xpos[u] < XPOS) & ((unsigned)ix < (unsigned)d.W);
-                    const uint32_t off = ok ? (uint32_t)((xrow + ix) * d.ldx * 2) + xc16[u] : IRGAN_OOB;
+                    const bool ok = (hi ? row1_ok : row0_ok) & (xp < (PAIR ? 32 + KW - 1 : XPOS)) &
+                                    ((unsigned)ix < (unsigned)d.W);
+                    const uint32_t off = ok ? (uint32_t)(((hi ? xrow1 : xrow0) + ix) * d.ldx * 2) + xc16[u] : IRGAN_OOB;
                     blds16(rs_x, off, base + j * 1024);
                 }
             }
@@ -211,16 +237,21 @@ __global__ __launch_bounds__((PC<BMC, CW>::NT), 1) void wgrad_pc_kernel(const ir
         const int col = (wm * MI + i) * 16 + 4 * p, c16 = col >> 3, within = (col & 7) * 2;
         aoff[i] = k_lo * DYR + ((c16 ^ (2 * pc_dsw<BMC>(k_lo))) << 4) + within;
     }
-    int boff[NJ][2];
+    // [j][high half][k-step]: k-step 1 is the +32-row image of k-step 0 (the swizzle repeats)
+    // except in PAIR mode, where it starts at position 36 (its own swizzle phase)
+    constexpr int NH = PAIR ? 2 : 1;
+    int boff[NJ][2][NH];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
         const int jj = wn * NJ + j, tx = jj >> 2, col = (jj & 3) * 16 + 4 * p;
         const int c16 = col >> 3, within = (col & 7) * 2;
 #pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-            const int pos = k_lo + 4 * hh + tx;
-            boff[j][hh] = APIECES * 1024 + pos * 128 + ((c16 ^ (2 * pc_t128(pos))) << 4) + within;
-        }
+        for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+            for (int h = 0; h < NH; ++h) {
+                const int pos = 36 * h + k_lo + 4 * hh + tx;
+                boff[j][hh][h] = APIECES * 1024 + pos * 128 + ((c16 ^ (2 * pc_t128(pos))) << 4) + within;
+            }
     }
     f32x4 acc[MI][NJ];
 #pragma unroll
@@ -230,9 +261,10 @@ __global__ __launch_bounds__((PC<BMC, CW>::NT), 1) void wgrad_pc_kernel(const ir
     // MFMAs on `cur` with the 11 fragment-pair reads of `nxt` (stage, half h)
     // interleaved one pair per MFMA: the first MFMA retires cur's reads with no
     // newer read in flight, every later one needs no wait (lgkmcnt counts 15).
-    auto step = [&](const Frag<MI>& cur, Frag<MI>& nxt, int stage, int h) {
+    auto step = [&](const Frag<MI, NJ>& cur, Frag<MI, NJ>& nxt, int stage, int h) {
         const char* S = smem + stage * STAGE + h * 32 * DYR;
-        const char* X = smem + stage * STAGE + h * 4096;
+        const char* X = smem + stage * STAGE + (PAIR ? 0 : h * 4096);
+        const int hb = PAIR ? h : 0;
 #pragma unroll
         for (int idx = 0; idx < MI * NJ; ++idx) {
             const int i = idx / NJ, j = idx % NJ;
@@ -241,7 +273,8 @@ __global__ __launch_bounds__((PC<BMC, CW>::NT), 1) void wgrad_pc_kernel(const ir
                                                                 0, 0);
 #if !PCX(4)
             if (idx < MI) nxt.a[idx] = ld_tr_pair(S + aoff[idx], S + aoff[idx] + 4 * DYR);
-            else if (idx < MI + NJ) nxt.b[idx - MI] = ld_tr_pair(X + boff[idx - MI][0], X + boff[idx - MI][1]);
+            else if (idx < MI + NJ)
+                nxt.b[idx - MI] = ld_tr_pair(X + boff[idx - MI][0][hb], X + boff[idx - MI][1][hb]);
 #else
             if (idx < MI) nxt.a[idx] = cur.a[idx] ^ make_uint4(idx, 1, 2, 3);
             else if (idx < MI + NJ) nxt.b[idx - MI] = cur.b[idx - MI] ^ make_uint4(idx, 1, 2, 3);
@@ -263,7 +296,7 @@ __global__ __launch_bounds__((PC<BMC, CW>::NT), 1) void wgrad_pc_kernel(const ir
 #endif
         __builtin_amdgcn_sched_barrier(0);
     };
-    Frag<MI> f0, f1;
+    Frag<MI, NJ> f0, f1;
 #if PCX(32)
     __builtin_amdgcn_s_setprio(1);  // compute waves win issue arbitration over the loaders
 #endif
@@ -273,7 +306,7 @@ __global__ __launch_bounds__((PC<BMC, CW>::NT), 1) void wgrad_pc_kernel(const ir
 #pragma unroll
         for (int i = 0; i < MI; ++i) f0.a[i] = ld_tr_pair(S + aoff[i], S + aoff[i] + 4 * DYR);
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) f0.b[j] = ld_tr_pair(S + boff[j][0], S + boff[j][1]);
+        for (int j = 0; j < NJ; ++j) f0.b[j] = ld_tr_pair(S + boff[j][0][0], S + boff[j][1][0]);
     }
     for (int kt = 0; kt < nk; ++kt) {
         step(f0, f1, kt % STAGES, 1);        // segment kt, pixels 0-31 | read pixels 32-63
@@ -316,17 +349,21 @@ __global__ __launch_bounds__(256) void wgrad_pc_reduce(const float* __restrict__
 
 }  // namespace
 
-// Preconditions (else IRGAN_EUNSUPPORTED, nothing launched): bf16 operands, KH x 3
-// taps with KW == 3, stride 1, Cout % 64 == 0, Cin % 64 == 0, Wo % 64 == 0, ldx, xoff,
-// ldy, yoff % 8 == 0, byte extents < 2^31.
+// Preconditions (else IRGAN_EUNSUPPORTED, nothing launched): bf16 operands, stride 1,
+// Cin % 64 == 0, ldx, xoff, ldy, yoff % 8 == 0, byte extents < 2^31, and either KH x 3 taps,
+// Cout % 64 == 0, Wo % 64 == 0 (64-pixel row segments) or 4 x 4 taps, Cout % 128 == 0,
+// Wo <= 32 (paired-row segments: D model.8).
 extern "C" int irgan_conv_wgrad_pc(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, int splitk,
                                    float* ws, long ws_cap, hipStream_t st) {
     if ((long)d->N * d->Ho * d->Wo <= 0) return 0;
     static const bool no64 = getenv("IRGAN_NO_WGRAD_PC64") != nullptr;
+    static const bool nopair = getenv("IRGAN_NO_WGRAD_PC_PAIR") != nullptr;
     const int BMC = d->Cout % 128 == 0 ? 128 : 64;
-    if (getenv("IRGAN_NO_WGRAD_PC") || d->dtype != IRGAN_BF16 || d->KW != 3 || d->sx != 1 || d->sy != 1 ||
-        d->Cout % BMC || (BMC == 64 && no64) || d->Cin % 64 || d->Wo % 64 || d->ldx % 8 || d->xoff % 8 || d->ldy % 8 || d->yoff % 8 ||
-        (long)d->N * d->H * d->W * d->ldx * 2 >= (1L << 31) || (long)d->N * d->Ho * d->Wo * d->ldy * 2 >= (1L << 31))
+    const bool pair = d->KW == 4 && d->KH == 4 && d->Wo <= 32 && BMC == 128 && !nopair;
+    if (getenv("IRGAN_NO_WGRAD_PC") || d->dtype != IRGAN_BF16 || (d->KW != 3 && !pair) || d->sx != 1 || d->sy != 1 ||
+        d->Cout % BMC || (BMC == 64 && no64) || d->Cin % 64 || (d->Wo % 64 && !pair) || d->ldx % 8 || d->xoff % 8 ||
+        d->ldy % 8 || d->yoff % 8 || (long)d->N * d->H * d->W * d->ldx * 2 >= (1L << 31) ||
+        (long)d->N * d->Ho * d->Wo * d->ldy * 2 >= (1L << 31))
         return IRGAN_EUNSUPPORTED;
     static int cus = 0;
     if (!cus) {
@@ -338,7 +375,7 @@ extern "C" int irgan_conv_wgrad_pc(const irgan_conv_desc* d, const void* x, cons
     static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
     const int ntco = d->Cout / BMC, nci = d->Cin / 64;
     const int tiles = ntco * nci * d->KH;
-    const int nseg = d->N * d->Ho * (d->Wo / 64);
+    const int nseg = pair ? d->N * ((d->Ho + 1) / 2) : d->N * d->Ho * (d->Wo / 64);
     if (splitk <= 0) {  // one block per CU (BMC 64: two fit): the largest split count whose grid fits one round
         splitk = (BMC == 64 ? 2 : 1) * cus / tiles;
         if (splitk < 1) splitk = 1;
@@ -354,10 +391,11 @@ extern "C" int irgan_conv_wgrad_pc(const irgan_conv_desc* d, const void* x, cons
     const long n = (long)d->Cout * d->KH * d->KW * d->Cin;
     float* slab = (ws && splitk > 1 && n % 4 == 0 && (long)splitk * n <= ws_cap) ? ws : nullptr;
     static const int cw = getenv("IRGAN_WGPC_CW4") ? 4 : 8;
-#define WPC(B, C)                                                                                                   \
-    wgrad_pc_kernel<B, C><<<tiles * splitk, PC<B, C>::NT, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)dy, dw, spb, \
-                                                                   nseg, ntco, nci, swz, slab)
-    if (BMC == 64) WPC(64, 4);   // 4 co fragments x 3 per compute wave (8 waves would hold 2 x 3)
+#define WPC(B, C, ...)                                                                                          \
+    wgrad_pc_kernel<B, C, ##__VA_ARGS__><<<tiles * splitk, PC<B, C>::NT, 0, st>>>(                             \
+        *d, (const bf16_t*)x, (const bf16_t*)dy, dw, spb, nseg, ntco, nci, swz, slab)
+    if (pair) WPC(128, 8, 4, true);
+    else if (BMC == 64) WPC(64, 4);   // 4 co fragments x 3 per compute wave (8 waves would hold 2 x 3)
     else if (cw == 8) WPC(128, 8);
     else WPC(128, 4);
 #undef WPC

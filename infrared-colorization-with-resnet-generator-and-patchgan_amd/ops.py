@@ -360,17 +360,21 @@ def conv_dgrad(pc: PackedConv, dy: Feat, dx: Feat, accumulate=False, mask: Feat 
                   dx.ld, dx.off, stream())
         return
     st = s.stride
-    for (py, _, ay, c0y), (px, _, ax, c0x), buf in pc.dg:
-        Ho, Wo = -(-(dx.H - py) // st), -(-(dx.W - px) // st)
-        if Ho <= 0 or Wo <= 0:
-            continue
-        assert ay > 0 and ax > 0
-        d = _desc(N=dy.N, H=dy.H, W=dy.W, Cin=pc.cout_eff, ldx=dy.ld, xoff=dy.off, Ho=Ho, Wo=Wo, Cout=s.cin,
-                  ldy=dx.ld, yoff=dx.off, OH=dx.H, OW=dx.W, omy=st, ooy=py, omx=st, oox=px, KH=ay, KW=ax, sy=1,
-                  sx=1, c0y=c0y, c0x=c0x, pad_mode=PAD_ZERO, act=0, accumulate=int(accumulate), dtype=pc.dtype,
-                  out_dtype=dx.dt, mask_act=mask_act, ldm=mask.ld if mask else 0, moff=mask.off if mask else 0)
-        _lib.call("irgan_conv_fwd", ctypes.byref(d), dy.ptr, P(buf), P(pc.bias if bias else None), dx.ptr,
-                  mask.ptr if mask else None, stream())
+
+    def phases():
+        for (py, _, ay, c0y), (px, _, ax, c0x), buf in pc.dg:
+            Ho, Wo = -(-(dx.H - py) // st), -(-(dx.W - px) // st)
+            if Ho <= 0 or Wo <= 0:
+                continue
+            assert ay > 0 and ax > 0
+            d = _desc(N=dy.N, H=dy.H, W=dy.W, Cin=pc.cout_eff, ldx=dy.ld, xoff=dy.off, Ho=Ho, Wo=Wo, Cout=s.cin,
+                      ldy=dx.ld, yoff=dx.off, OH=dx.H, OW=dx.W, omy=st, ooy=py, omx=st, oox=px, KH=ay, KW=ax, sy=1,
+                      sx=1, c0y=c0y, c0x=c0x, pad_mode=PAD_ZERO, act=0, accumulate=int(accumulate), dtype=pc.dtype,
+                      out_dtype=dx.dt, mask_act=mask_act, ldm=mask.ld if mask else 0, moff=mask.off if mask else 0,
+                      cin_real=s.cout if s.cout < pc.cout_eff else 0)
+            _lib.call("irgan_conv_fwd", ctypes.byref(d), dy.ptr, P(buf), P(pc.bias if bias else None), dx.ptr,
+                      mask.ptr if mask else None, stream())
+    TIMER.wrap(conv_tag("dgrad", s, (dx.H, dx.W), dx.N), phases)
 
 
 def conv_wgrad(spec: ConvSpec, x: Feat, dy: Feat, dw: torch.Tensor, dtype: int, splitk=0):

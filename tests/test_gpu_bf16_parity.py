@@ -54,6 +54,10 @@ EXTRA_CASES = [
     (384, 128, 3, 1, 1, 0, 64),    # up1_conv shape, 6 ci chunks
     (64, 128, 3, 1, 1, 0, 128),    # down1 shape, 2 segments per row
     (256, 256, 3, 1, 1, 1, 128),   # resblock conv, reflect, interior + edge segments
+    # 4x4 stride 1 with Wo <= 32: wgrad_pc on paired-row segments (two output rows of 32 per
+    # 64-pixel segment; odd Ho masks the last pair's second row): D model.8 at its own shape
+    (256, 512, 4, 1, 1, 0, 32),
+    (128, 256, 4, 1, 1, 0, 33),
     # Cout % 128 != 0 (Cout % 64 == 0): wgrad_pc with 64-channel co tiles (128-B dY rows)
     (192, 64, 3, 1, 1, 0, 64),     # up2_conv shape, 3 ci chunks
     (64, 64, 3, 1, 1, 1, 128),     # reflect, 2 segments per row
