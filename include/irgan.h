@@ -262,6 +262,16 @@ int irgan_reflect_ring_fold(const float* rows, const float* cols, int32_t nsplit
  * border pixel of dx (one owner per pixel, no atomics). */
 int irgan_reflect_dgrad_ring(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p, void* dx,
                              irgan_stream_t s);
+/* irgan_reflect_dgrad_ring with a caller workspace ws of ws_floats floats.  ResnetBlock
+ * shapes (3x3, p = 1, 4 <= H, W <= 64, dY channels % 32 and <= 256, dx channels % 64, bf16,
+ * ws_floats >= N * 4 * 68 * dx channels) run as two launches: the four border lines as
+ * GEMMs with LDS-resident weights (at most max_blocks workgroups, each walking a group of
+ * images) into ws, then the fold onto dx (one read-modify-write per owned pixel); other
+ * shapes: irgan_reflect_dgrad_ring.  max_blocks bounds the first launch for a second stream
+ * beside a kernel that leaves that many CUs idle (the ResnetBlock weight gradient, ir:386-411's
+ * backward: engine.GeneratorEngine.backward). */
+int irgan_reflect_dgrad_ring_ws(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p, void* dx,
+                                float* ws, int64_t ws_floats, int32_t max_blocks, irgan_stream_t s);
 /* The whole backward-data of a reflect-padded stride-1 conv (ir:381-392, 401-411): the
  * interior correlation and the fold of its pad ring (d, w, p as irgan_reflect_dgrad_ring).
  * With the ring fold on (irgan_set_ring_fold), ResnetBlock shapes (bf16, 3x3, p = 1, dY

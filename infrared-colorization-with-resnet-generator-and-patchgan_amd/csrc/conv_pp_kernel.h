@@ -65,6 +65,9 @@
 #endif
 // bits: 1 no MFMA, 2 no weight DMA in the loop, 4 no fragment reads, 8 no barriers in the loop, 16 no epilogue
 #define PPX(b) ((PP_EXP & (b)) != 0)
+#ifndef RING_EXP
+#define RING_EXP 0  // A/B timing only: 1 skips the ring column terms, 2 the ring row terms
+#endif
 
 namespace {
 
@@ -130,86 +133,25 @@ IRGAN_HD float in_act_grad(float xh, int act) {  // as norm.hip's act_grad
 // tiles, profiles/r02_s5_pp_one_ab.txt).  With more than one channel chunk the next chunk's halo cannot be
 // prefetched: after the last window that reads chunk c (4k+3 of its last tap) every
 // wave issues its pieces of chunk c+1, retires them and meets at one extra barrier.
-// RING epilogue: the padded-domain ring COLUMN of a left / right border patch (ir:386-411:
-// backward-data of conv(ReflectionPad2d(1)(x)) is the fold of the zero-padded correlation g
-// over the (H+2) x (W+2) domain; the interior of g is the K loop's result).  Column -1
-// (left) reads only tap column tx = 2, column W (right) only tx = 0, so its 16 values
-// (rows py0..py0+15) plus the corner (row -1 of a top patch / H of a bottom one) are a
-// 17 x BN x (3 * Cin) GEMM.  The operand halos are gone by now, so it streams straight
-// from L2 / HBM: 8 waves x 32 output channels, two pixel fragments (the 16 rows; the
-// corner in lane 0 of the second), 3 * Cin / 32 K-steps with the next step's loads in
-// flight.  Result: fp32 table[17][BN] (row 16 = the corner), which emit() adds onto the
-// mirrored pixels before the single bf16 rounding of the output.
-IRGAN_HD void ring_col_epilogue(const irgan_conv_desc& d, const bf16_t* __restrict__ dy, const bf16_t* __restrict__ w,
-                                int img, int py0, bool left, bool top, bool bot, int n0, float* table) {
-    constexpr int BN = 256;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int Kw = 9 * d.Cin;
-    const int txr = left ? 2 : 0;
-    const int oc = left ? -1 : d.W;                      // padded-domain column (output coordinates)
-    const int dcol = oc + d.c0x + txr;                   // the dy column it reads
-    const int kc = (lane >> 4) * 8;
-    const bool corner = top || bot;                      // block-uniform
-    const int orow0 = py0 + (lane & 15);                 // pixel fragment 0: rows py0 .. py0+15
-    const int orow1 = top ? -1 : d.H;                    // fragment 1, lane 0: the corner row
-    const bool c_lane = corner && (lane & 15) == 0;
-    const bf16_t* wr[2];
-#pragma unroll
-    for (int nf = 0; nf < 2; ++nf) wr[nf] = w + (long)(n0 + wv * 32 + nf * 16 + (lane & 15)) * Kw + kc;
-    const long pixb = ((long)img * d.H) * d.W;
-    auto dy_at = [&](int orow, int ty, int cs, bool ok) -> uint4 {
-        const int r = orow + d.c0y + ty;
-        if (!ok || (unsigned)r >= (unsigned)d.H || (unsigned)dcol >= (unsigned)d.W) return uint4{0, 0, 0, 0};
-        return *(const uint4*)(dy + (pixb + (long)r * d.W + dcol) * d.ldx + d.xoff + cs * 32 + kc);
-    };
-    const int ncs = d.Cin / 32, nk = 3 * ncs;
-    auto load = [&](int k, uint4 (&a)[2], uint4 (&b)[2]) {
-        const int ty = k / ncs, cs = k - ty * ncs;
-        const int kcol = (ty * 3 + txr) * d.Cin + cs * 32;
-#pragma unroll
-        for (int nf = 0; nf < 2; ++nf) a[nf] = *(const uint4*)(wr[nf] + kcol);
-        b[0] = dy_at(orow0, ty, cs, true);
-        b[1] = dy_at(orow1, ty, cs, c_lane);
-    };
-    f32x4 ra[2][2];
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-        for (int nf = 0; nf < 2; ++nf) ra[m][nf] = f32x4{0.f, 0.f, 0.f, 0.f};
-    auto mma = [&](const uint4 (&a)[2], const uint4 (&b)[2]) {
-#pragma unroll
-        for (int nf = 0; nf < 2; ++nf) {
-            ra[0][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a[nf]),
-                                                                __builtin_bit_cast(bf16x8_t, b[0]), ra[0][nf], 0, 0, 0);
-            if (corner)
-                ra[1][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a[nf]),
-                                                                    __builtin_bit_cast(bf16x8_t, b[1]), ra[1][nf], 0, 0,
-                                                                    0);
-        }
-    };
-    uint4 a0[2], b0[2], a1[2], b1[2];
-    load(0, a0, b0);
-#pragma unroll 1
-    for (int k = 0; k < nk; k += 2) {
-        if (k + 1 < nk) load(k + 1, a1, b1);
-        mma(a0, b0);
-        if (k + 1 >= nk) break;
-        if (k + 2 < nk) load(k + 2, a0, b0);
-        mma(a1, b1);
-    }
-    // C^T fragments: lane = pixel (lane & 15), channels 4 * (lane >> 4) + r of the 16
-#pragma unroll
-    for (int nf = 0; nf < 2; ++nf) {
-        const int cl = wv * 32 + nf * 16 + 4 * (lane >> 4);
-        *(float4*)(table + (lane & 15) * BN + cl) = make_float4(ra[0][nf][0], ra[0][nf][1], ra[0][nf][2], ra[0][nf][3]);
-        if (c_lane)
-            *(float4*)(table + 16 * BN + cl) = make_float4(ra[1][nf][0], ra[1][nf][1], ra[1][nf][2], ra[1][nf][3]);
-    }
-}
-
 // RING (conv_pp_ring.hip: the reflect-padded ResnetBlock backward-data, ir:386-411, with
-// its pad ring folded in -- see ring_col_epilogue below): bf16, 3x3, BN 256, Ho == H and
-// Wo == W multiples of 16 with >= 2 patches per axis (host-checked).
+// its pad ring folded in): bf16, 3x3, BN 256, Ho == H and Wo == W multiples of 16 with >= 2
+// patches per axis (host-checked).  Backward-data of conv(ReflectionPad2d(1)(x)) is the fold
+// of the zero-padded correlation g over the (H+2) x (W+2) domain; the interior of g is the
+// K loop's result, the ring values fold onto the mirrored pixels.  Every ring term is read
+// from the operand halo already in LDS, inside the K loop:
+//  * ring ROW (padded row -1 of a top patch / H of a bottom one): reads only tap row ty = 2
+//    / 0, i.e. one extra pixel fragment (dy row 0 = halo row 1 / H-1 = halo row 16) whose
+//    MFMAs accumulate straight into the mirrored row's accumulators (dx row 1 / H-2: the
+//    same columns, so the same lanes);
+//  * ring COLUMN (padded column -1 of a left patch / W of a right one): reads only tap
+//    column tx = 2 / 0; its 16 pixels (the patch rows) are one fragment whose lane r reads
+//    halo row r + ty at column 1 / 16 (a per-lane row address), accumulated in accC;
+//  * the corner (padded (-1 | H, -1 | W)) folds onto the same dx pixel as the ring column's
+//    row 1 / 14 and reads one tap: a fragment with only that lane's operand nonzero, into
+//    accC as well.
+// One wave group takes the ring row (group 0 top, group 1 bottom), the other the column and
+// corner, so no wave carries both.  After the K loop accC goes to an fp32 LDS table past the
+// staging rows, and emit() adds it onto dx column 1 / W-2 before the single bf16 rounding.
 template <int KH, int KW, int BN, bool ACC, bool STATS = false, bool F8 = false, bool ONE = false,
           bool RING = false>
 __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
@@ -257,8 +199,15 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
     const bool reflect = d.pad_mode == IRGAN_PAD_REFLECT;
     static_assert(!RING || (KH == 3 && KW == 3 && BN == 256 && !F8 && !ONE), "ring fold: resblock dgrad tiles");
     // RING: which sides of the padded domain this patch borders (block-uniform)
-    const bool rtop = RING && pyi == 0, rbot = RING && pyi == tpy - 1;
+    const bool rtop = RING && !(RING_EXP & 2) && pyi == 0, rbot = RING && !(RING_EXP & 2) && pyi == tpy - 1;
     const bool rleft = RING && pxi == 0, rright = RING && pxi == tpx - 1;
+    // ring column: the wave group that does not take a ring row (bottom patches: group 0)
+    const bool rcol = !(RING_EXP & 1) && (rleft || rright) && grp == (rbot ? 0 : 1);
+    const int txc = rleft ? 2 : 0;          // the tap column the ring column reads
+    const int hxc = rleft ? 1 : PW;         // its dy column in halo coordinates
+    const int tyc = rtop ? 2 : 0;           // the tap row the corner reads
+    const int rcn = rtop ? 1 : PH - 2;      // ring-column pixel whose dx pixel the corner shares
+    const bool rcorner = rcol && (rtop || rbot);
 
     // DMA sources as byte offsets into buffer resources (out-of-range offsets
     // arrive as zeros: padding and Cout tails cost no address math in the loop)
@@ -317,7 +266,11 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     uint4 af[MI], bfr[NJ];
-    uint4 afr;  // RING: the ring-row fragment (padded-domain row -1 or H) of this K-step
+    uint4 afr;  // RING: the ring-row or ring-column fragment of this K-step
+    uint4 afk;  // RING: the corner fragment (one lane nonzero)
+    f32x4 accC[RING ? NJ : 1];  // RING: the ring column (lane = patch row)
+#pragma unroll
+    for (int j = 0; j < (RING ? NJ : 1); ++j) accC[j] = f32x4{0.f, 0.f, 0.f, 0.f};
     v8i_t af8[MS], bf8[NJ];  // fp8: 32-byte fragments (chunks g, g + 4)
     // prologue: W(0), halo(0), W(1); retire the first two
     issue_w(0, 0, 0);
@@ -395,6 +348,13 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
                         const int K = 8 * HWd + tx;
                         afr = *(const uint4*)(sH + (hbp + (tsw[K & 7] ^ (h * 64))) + K * 128);
                     }
+                    // ring column: lane r reads halo row r + ty at column hxc (the corner: the
+                    // halo row of dy row 0 / H-1, lane rcn only)
+                    if (rcol && tx == txc) {
+                        const char* hbuf = sH + (c & 1) * HBYTES;
+                        const int row = ((lane & 15) + ty) * HWd + hxc;
+                        afr = *(const uint4*)(hbuf + row * 128 + (((g0 + 4 * h) ^ (row & 7)) << 4));
+                    }
                 }
 #else
                 if (k == 0 && h == 0) {
@@ -459,6 +419,25 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
                                     __builtin_bit_cast(bf16x8_t, bfr[j]), __builtin_bit_cast(bf16x8_t, afr),
                                     acc[6][j], 0, 0, 0);
                         }
+                        if (rcol && tx == txc) {
+#pragma unroll
+                            for (int j = 0; j < NJ; ++j)
+                                accC[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                                    __builtin_bit_cast(bf16x8_t, bfr[j]), __builtin_bit_cast(bf16x8_t, afr), accC[j],
+                                    0, 0, 0);
+                            if (rcorner && ty == tyc) {
+                                // the corner operand, read here (after the main MFMAs freed af[])
+                                const char* hbuf = sH + (c & 1) * HBYTES;
+                                const int rowk = (rtop ? 1 : PH) * HWd + hxc;
+                                const uint4 v = *(const uint4*)(hbuf + rowk * 128 + (((g0 + 4 * h) ^ (rowk & 7)) << 4));
+                                afk = (lane & 15) == rcn ? v : uint4{0u, 0u, 0u, 0u};
+#pragma unroll
+                                for (int j = 0; j < NJ; ++j)
+                                    accC[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                                        __builtin_bit_cast(bf16x8_t, bfr[j]), __builtin_bit_cast(bf16x8_t, afk),
+                                        accC[j], 0, 0, 0);
+                            }
+                        }
                     }
                 }
                 if (h == HS - 1 && grp == 0 && !last_k) retire(halo_now);  // last window of step k
@@ -469,14 +448,19 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
     }
     if (grp == 0) phase_barrier();  // match group 1's extra barrier
     __syncthreads();                // all operand reads done: LDS becomes the staging buffer
-    // RING: the ring columns (padded col -1 / W, incl. the corner of a top / bottom patch)
-    // as a small GEMM from L2 into an fp32 LDS table past the staging rows; emit() adds
-    // them onto their mirrored pixels (dx col 1 / W-2)
-    constexpr int RING_OFF = 256 * PP<BN>::RSB;  // bytes: [17 rows][BN] fp32
+    // RING: the ring column (incl. the corner) into an fp32 LDS table past the staging rows;
+    // emit() adds it onto the mirrored pixels (dx col 1 / W-2)
+    constexpr int RING_OFF = 256 * PP<BN>::RSB;  // bytes: [16 rows][BN] fp32
     if constexpr (RING) {
-        static_assert(!RING || RING_OFF + 17 * BN * 4 <= LDS, "ring table fits past the staging rows");
-        if (rleft || rright) {
-            ring_col_epilogue(d, x, w, img, py0, rleft, rtop, rbot, n0, (float*)(smem + RING_OFF));
+        static_assert(!RING || RING_OFF + 16 * BN * 4 <= LDS, "ring table fits past the staging rows");
+        if (rleft || rright) {  // block-uniform
+            if (rcol) {
+                float* table = (float*)(smem + RING_OFF);
+#pragma unroll
+                for (int j = 0; j < NJ; ++j)
+                    *(float4*)(table + (lane & 15) * BN + cb + j * 16 + 4 * (lane >> 4)) =
+                        make_float4(accC[j][0], accC[j][1], accC[j][2], accC[j][3]);
+            }
             __syncthreads();
         }
     }
@@ -554,17 +538,11 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
                     v[3] = acc[i][j][3] * osc + b.w;
                 }
                 if constexpr (RING) {
-                    // ring column -> dx col 1 (left) / W-2 = patch col 14 (right, W % 16 == 0);
-                    // the corner ring value -> dx row 1 (top) / H-2 = patch row 14 (bottom)
+                    // ring column (+ corner) -> dx col 1 (left) / W-2 = patch col 14 (right, W % 16 == 0)
                     const int col = lane & 15, row = prow + i;
                     if ((rleft && col == 1) || (rright && col == 14)) {
-                        const float* rt = (const float*)(smem + RING_OFF);
-                        const float4 cv = *(const float4*)(rt + row * BN + cl);
+                        const float4 cv = *(const float4*)((const float*)(smem + RING_OFF) + row * BN + cl);
                         v[0] += cv.x; v[1] += cv.y; v[2] += cv.z; v[3] += cv.w;
-                        if ((rtop && row == 1) || (rbot && row == 14)) {
-                            const float4 kv = *(const float4*)(rt + 16 * BN + cl);
-                            v[0] += kv.x; v[1] += kv.y; v[2] += kv.z; v[3] += kv.w;
-                        }
                     }
                 }
 #pragma unroll

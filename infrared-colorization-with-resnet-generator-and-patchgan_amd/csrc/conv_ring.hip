@@ -25,6 +25,16 @@
 // and added into dx with 16-byte read-modify-writes.
 #include "common.h"
 
+#ifndef RING_TS
+#define RING_TS 0  // timing experiments only: per-block wall-clock stamps (irgan_debug_ring_ts)
+#endif
+#if RING_TS
+__device__ unsigned long long g_ring_ts[4096 * 6];
+#define RTS(i) do { if (threadIdx.x == 0) g_ring_ts[(blockIdx.y * gridDim.x + blockIdx.x) * 6 + (i)] = wall_clock64(); } while (0)
+#else
+#define RTS(i) do {} while (0)
+#endif
+
 namespace {
 
 // 64 band pixels per block: each block streams its (taps x Cin) weight slices from L2
@@ -66,6 +76,7 @@ __global__ __launch_bounds__(NWV * 64) void reflect_ring_kernel(const irgan_conv
     __shared__ __attribute__((aligned(16))) float red[NWV][NPIX][NCO + 4];  // +4: conflict-free row writes
     __shared__ int tap_list[MAXT];
     __shared__ int ntap_s;
+    RTS(0);
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int H = d.Ho, W = d.Wo;               // dx spatial size (stride 1)
@@ -150,6 +161,7 @@ __global__ __launch_bounds__(NWV * 64) void reflect_ring_kernel(const irgan_conv
         ntap_s = nt;
     }
     __syncthreads();
+    RTS(1);
     const int ntap = ntap_s;
 
     // mirrored column of fragment f's pixel (terms 1 and 2); fragments that hold no band
@@ -230,6 +242,7 @@ __global__ __launch_bounds__(NWV * 64) void reflect_ring_kernel(const irgan_conv
         mma(a1, b1, m1);
         ks = k2;
     }
+    RTS(2);
     // partial tiles -> LDS: lane holds pixel f*16 + (lane & 15), channels j*16 + 4*(lane>>4) + r
 #pragma unroll
     for (int f = 0; f < NF; ++f)
@@ -238,6 +251,7 @@ __global__ __launch_bounds__(NWV * 64) void reflect_ring_kernel(const irgan_conv
             *(float4*)&red[wv][f * 16 + (lane & 15)][j * 16 + 4 * (lane >> 4)] =
                 make_float4(acc[f][j][0], acc[f][j][1], acc[f][j][2], acc[f][j][3]);
     __syncthreads();
+    RTS(3);
     // thread -> (pixel, 8 channels): sum the NWV partials in order, add into dx
     static_assert(NPIX * NCO / 8 == NWV * 64, "one (pixel, 8 channels) per thread");
     const int pix_l = threadIdx.x >> 3, cg = (threadIdx.x & 7) * 8;
@@ -306,6 +320,10 @@ __global__ __launch_bounds__(NWV * 64) void reflect_ring_kernel(const irgan_conv
         }
     }
     }
+#if RING_TS
+    __syncthreads();
+    RTS(4);
+#endif
     if (!is.part) return;
     // per-channel sums over the block's NPIX pixels, fixed order (deterministic)
     __syncthreads();  // every wave is done reading red[][][]
@@ -325,8 +343,202 @@ __global__ __launch_bounds__(NWV * 64) void reflect_ring_kernel(const irgan_conv
     }
 }
 
+// ---- Line form of the same fold for the ResnetBlock case (3x3, p = 1, sides <= 64).
+// With p = 1 the ring is four 1-D convolutions along the border lines of dy: the padded
+// row -1 reads only dy row 0 through tap row ty = 2, row H only dy row H-1 (ty = 0),
+// column -1 only dy column 0 (tx = 2), column W only column W-1 (tx = 0):
+//   top    g(-1, u) = sum_tx Wd[2][tx] dy(0, u + tx - 1),    u in [-1, W]  -> dx(1, refl(u))
+//   bottom g(H, u)  = sum_tx Wd[0][tx] dy(H-1, u + tx - 1),  u in [-1, W]  -> dx(H-2, refl(u))
+//   left   g(y, -1) = sum_ty Wd[ty][2] dy(y + ty - 1, 0),    y in [0, H)   -> dx(y, 1)
+//   right  g(y, W)  = sum_ty Wd[ty][0] dy(y + ty - 1, W-1),  y in [0, H)   -> dx(y, W-2)
+// (the corners are the u = -1 / W ends of the top / bottom lines).  Two launches:
+//  * ring_line_gemm_kernel: workgroup = (line, 64 output channels, a group of images).  The
+//    line's 3 taps x Cin x 64 weights stay in LDS (96 KiB, loaded once), the image's dy line
+//    (<= 68 positions x Cin) beside them; per image a [64 co] x [80 positions] x [3 Cin]
+//    GEMM entirely from LDS (wave = 16 channels, 5 position fragments), the next image's
+//    line prefetched into registers meanwhile; g (fp32) -> the caller's workspace.
+//  * ring_line_fold_kernel: one thread per (owned dx pixel, 8 channels) adds the sum of its
+//    ring terms in a fixed order (one read-modify-write, deterministic): rows 1 / H-2 take
+//    their line's u plus, at columns 1 / W-2, the corner end and the column line's value.
+constexpr int RV_L = 64;            // longest line (H, W)
+constexpr int RV_ROWS = RV_L + 4;   // positions per line: dy coordinates -2 .. L+1 (g: u + 1 in [0, 68))
+constexpr int RV_CIN = 256;         // dy channels (LDS row = 512 B)
+
+IRGAN_HD int rv_off(int row, int chunk) { return row * 512 + ((chunk ^ (row & 15)) << 4); }
+IRGAN_HD int rv_tap(int line, int k) {  // dgrad-conv tap ty*3 + tx of along-line offset k
+    return line == 0 ? 6 + k : (line == 1 ? k : (line == 2 ? 3 * k + 2 : 3 * k));
+}
+
+__global__ __launch_bounds__(256, 1) void ring_line_gemm_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ dy,
+                                                                const bf16_t* __restrict__ w, float* __restrict__ gbuf,
+                                                                int ipb) {
+    __shared__ __attribute__((aligned(16))) char smem[3 * 64 * 512 + RV_ROWS * 512];
+    char* const sW = smem;                 // [3 taps][64 co] rows of Cin bf16
+    char* const sL = smem + 3 * 64 * 512;  // [RV_ROWS positions] rows of Cin bf16
+    RTS(0);
+    const int nct = d.Cout / 64;
+    const int line = blockIdx.x / nct, ct = blockIdx.x - line * nct;
+    const int n0 = blockIdx.y * ipb, n1 = min(d.N, n0 + ipb);
+    const int H = d.Ho, W = d.Wo, L = line < 2 ? W : H;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, l16 = lane & 15;
+    const int Kw = (9 * d.Cin + 63) / 64 * 64;
+    const int c32 = d.Cin / 8;  // 16-byte chunks per row
+
+    // weights: row (k * 64 + co), chunk c  <-  w[ct*64 + co][rv_tap(line, k) * Cin + 8c]
+    {
+        constexpr int PER = 3 * 64 * 32 / 256;
+        uint4 v[PER];
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int e = u * 256 + tid, row = e >> 5, c = e & 31, k = row >> 6, co = row & 63;
+            v[u] = c < c32 ? *(const uint4*)(w + (long)(ct * 64 + co) * Kw + rv_tap(line, k) * d.Cin + c * 8)
+                           : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int e = u * 256 + tid;
+            *(uint4*)(sW + rv_off(e >> 5, e & 31)) = v[u];
+        }
+    }
+    // the dy line of image n: position p = dy coordinate + 2 along the line
+    constexpr int LPER = (RV_ROWS * 32 + 255) / 256;
+    auto load_line = [&](int n, uint4 (&v)[LPER]) {
+#pragma unroll
+        for (int u = 0; u < LPER; ++u) {
+            const int e = u * 256 + tid, q = (e >> 5) - 2, c = e & 31;
+            v[u] = make_uint4(0u, 0u, 0u, 0u);
+            if (e < RV_ROWS * 32 && q >= 0 && q < L && c < c32) {
+                const int y = line == 0 ? 0 : (line == 1 ? H - 1 : q);
+                const int x = line < 2 ? q : (line == 2 ? 0 : W - 1);
+                v[u] = *(const uint4*)(dy + ((long)(n * d.H + y) * d.W + x) * d.ldx + d.xoff + c * 8);
+            }
+        }
+    };
+    uint4 lv[LPER];
+    if (n0 < n1) load_line(n0, lv);
+    const int ub = line < 2 ? -1 : 0;  // position of fragment 0, lane 0
+    const int ncs = d.Cin / 32;
+    const int co = ct * 64 + wv * 16 + 4 * g;  // this lane's 4 output channels (C^T rows)
+#pragma unroll 1
+    for (int n = n0; n < n1; ++n) {
+        __syncthreads();  // the previous image's GEMM is done with sL
+#pragma unroll
+        for (int u = 0; u < LPER; ++u) {
+            const int e = u * 256 + tid;
+            if (e < RV_ROWS * 32) *(uint4*)(sL + rv_off(e >> 5, e & 31)) = lv[u];
+        }
+        __syncthreads();
+        RTS(1);
+        if (n + 1 < n1) load_line(n + 1, lv);  // in flight under this image's GEMM
+        f32x4 acc[5];
+#pragma unroll
+        for (int f = 0; f < 5; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+#pragma unroll
+            for (int cs = 0; cs < RV_CIN / 32; ++cs) {
+                if (cs >= ncs) break;
+                const uint4 a = *(const uint4*)(sW + rv_off(k * 64 + wv * 16 + l16, cs * 4 + g));
+                uint4 b[5];
+#pragma unroll
+                for (int f = 0; f < 5; ++f)
+                    b[f] = *(const uint4*)(sL + rv_off(min(16 * f + l16 + ub + k + 1, RV_ROWS - 1), cs * 4 + g));
+#pragma unroll
+                for (int f = 0; f < 5; ++f)
+                    acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a),
+                                                                     __builtin_bit_cast(bf16x8_t, b[f]), acc[f], 0, 0, 0);
+            }
+        }
+        RTS(2);
+        // g[n][line][u + 1][co]: lane = position 16 f + l16 + ub, rows 4g + r = channels
+        float* gl = gbuf + ((long)n * 4 + line) * RV_ROWS * d.Cout;
+#pragma unroll
+        for (int f = 0; f < 5; ++f) {
+            const int pos = 16 * f + l16 + ub + 1;
+            if (pos < RV_ROWS) *(float4*)(gl + (long)pos * d.Cout + co) = make_float4(acc[f][0], acc[f][1], acc[f][2], acc[f][3]);
+        }
+    }
+#if RING_TS
+    RTS(3);
+    RTS(4);
+#endif
+}
+
+// one thread per (owned dx pixel, 8 channels); targets per image: row 1 (W), row H-2 (W),
+// column 1 and column W-2 without those rows (H-2 each)
+__global__ __launch_bounds__(256) void ring_line_fold_kernel(const irgan_conv_desc d, const float* __restrict__ gbuf,
+                                                             void* __restrict__ dx) {
+    const int H = d.Ho, W = d.Wo, C8 = d.Cout / 8;
+    const int per_img = (2 * W + 2 * (H - 2)) * C8;
+    const long i = blockIdx.x * 256L + threadIdx.x;
+    if (i >= (long)d.N * per_img) return;
+    const int n = (int)(i / per_img);
+    int r = (int)(i - (long)n * per_img);
+    const int c = (r % C8) * 8;
+    r /= C8;
+    int y, x;
+    float v[8];
+    auto add = [&](int line, int pos) {  // pos = u + 1 (top / bottom) or y + 1 (left / right)
+        const float4* q = (const float4*)(gbuf + (((long)n * 4 + line) * RV_ROWS + pos) * d.Cout + c);
+        const float4 a = q[0], b = q[1];
+        v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+        v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+    };
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = 0.f;
+    if (r < 2 * W) {  // rows 1 (top line) / H-2 (bottom line)
+        const int line = r / W;
+        x = r - line * W;
+        y = line == 0 ? 1 : H - 2;
+        add(line, x + 1);
+        if (x == 1) { add(line, 0); add(2, y + 1); }          // corner end u = -1, left line at y
+        if (x == W - 2) { add(line, W + 1); add(3, y + 1); }  // corner end u = W, right line at y
+    } else {          // columns 1 (left line) / W-2 (right line), rows other than 1 and H-2
+        r -= 2 * W;
+        const int side = r / (H - 2);
+        int k = r - side * (H - 2);
+        y = k == 0 ? 0 : k + 1;                  // rows 0, 2, 3, ..., H-3,
+        if (k == H - 3) y = H - 1;               // and H-1
+        x = side == 0 ? 1 : W - 2;
+        add(2 + side, y + 1);
+    }
+    const long o = (((long)n * d.OH + y) * d.OW + x) * d.ldy + d.yoff + c;
+    if (d.out_dtype == IRGAN_F32) {
+        float4* p = (float4*)((float*)dx + o);
+        float4 a = p[0], b = p[1];
+        a.x += v[0]; a.y += v[1]; a.z += v[2]; a.w += v[3];
+        b.x += v[4]; b.y += v[5]; b.z += v[6]; b.w += v[7];
+        p[0] = a;
+        p[1] = b;
+    } else {
+        uint4* p = (uint4*)((bf16_t*)dx + o);
+        const uint4 u = *p;
+        const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
+        uint32_t o4[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            o4[k] = pk_bf16(__uint_as_float(wd[k] << 16) + v[2 * k], __uint_as_float(wd[k] & 0xffff0000u) + v[2 * k + 1]);
+        *p = make_uint4(o4[0], o4[1], o4[2], o4[3]);
+    }
+}
+
 }  // namespace
 
+// the line launches' shapes (else the general reflect_ring_kernel): bf16, 3x3, p = 1, output
+// = input size with 4 <= H, W <= 64, dy channels % 32 and <= 256, dx channels % 64, 8-aligned
+// dy / dx slices, plain (unstrided) output grid, a workspace of N * 4 * 68 * Cout floats
+static long ring_line_ws(const irgan_conv_desc* d) { return (long)d->N * 4 * RV_ROWS * d->Cout; }
+static bool ring_line_ok(const irgan_conv_desc* d, int p, long ws_floats) {
+    static const bool off = getenv("IRGAN_NO_RING_LINE") != nullptr;
+    return !off && p == 1 && d->dtype == IRGAN_BF16 && d->KH == 3 && d->KW == 3 && d->c0y == -1 && d->c0x == -1 &&
+           d->Cin % 32 == 0 && d->Cin <= RV_CIN && d->Cout % 64 == 0 && d->ldx % 8 == 0 && d->xoff % 8 == 0 &&
+           d->ldy % 8 == 0 && d->yoff % 8 == 0 && d->H >= 4 && d->W >= 4 && d->H <= RV_L && d->W <= RV_L &&
+           d->Ho == d->H && d->Wo == d->W && d->Ho == d->OH && d->Wo == d->OW && d->omy == 1 && d->omx == 1 &&
+           d->ooy == 0 && d->oox == 0 && (d->out_dtype == IRGAN_BF16 || d->out_dtype == IRGAN_F32) &&
+           ws_floats >= ring_line_ws(d);
+}
 // conv_pp.hip's irgan_conv_dgrad_in_stats: the ring partial rows per image, and the
 // ring launch that writes them (bf16 output, Cout % 64 == 0, 8-aligned slices: checked there)
 int ring_in_slots(const irgan_conv_desc* d, int p) {
@@ -345,6 +557,12 @@ int ring_in_launch(const irgan_conv_desc* d, const void* dy, const void* w, int 
     return 0;
 }
 
+#if RING_TS
+extern "C" int irgan_debug_ring_ts(unsigned long long* host, int n) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ring_ts), sizeof(unsigned long long) * n * 6);
+}
+#endif
+
 extern "C" int irgan_reflect_dgrad_ring(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p, void* dx,
                                         irgan_stream_t s) {
     if (!d || !dy || !w || !dx) return IRGAN_EINVAL;
@@ -357,6 +575,30 @@ extern "C" int irgan_reflect_dgrad_ring(const irgan_conv_desc* d, const void* dy
     dim3 grid(d->N * 2 * p * (segs_row + segs_col), irgan_cdiv(d->Cout, NCO));
     reflect_ring_kernel<<<grid, NWV * 64, 0, (hipStream_t)s>>>(*d, (const bf16_t*)dy, (const bf16_t*)w, p, dx, segs_row,
                                                          segs_col);
+    IRGAN_LAUNCH_CHECK();
+    return 0;
+}
+
+// The same fold with a workspace: ResnetBlock shapes (ring_line_ok) run the two line
+// launches (GEMM with at most max_blocks workgroups -- for a launch on a second stream beside a
+// kernel that leaves that many CUs idle, the ResnetBlock weight gradient: 240 of 256 CUs --
+// then the fold); other shapes the general ring launch.
+extern "C" int irgan_reflect_dgrad_ring_ws(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p,
+                                           void* dx, float* ws, int64_t ws_floats, int32_t max_blocks,
+                                           irgan_stream_t s) {
+    if (!d || !dy || !w || !dx || max_blocks < 1) return IRGAN_EINVAL;
+    if ((long)d->N * d->Ho * d->Wo <= 0 || d->Cout <= 0 || p <= 0) return 0;
+    if (!ws || !ring_line_ok(d, p, ws_floats)) return irgan_reflect_dgrad_ring(d, dy, w, p, dx, s);
+    hipStream_t st = (hipStream_t)s;
+    const int tiles = 4 * (d->Cout / 64);             // (line, 64-channel tile)
+    int groups = max_blocks / tiles;                  // image groups
+    if (groups < 1) groups = 1;
+    if (groups > d->N) groups = d->N;
+    const int ipb = irgan_cdiv(d->N, groups);
+    groups = irgan_cdiv(d->N, ipb);
+    ring_line_gemm_kernel<<<dim3(tiles, groups), 256, 0, st>>>(*d, (const bf16_t*)dy, (const bf16_t*)w, ws, ipb);
+    const long threads = (long)d->N * (2 * d->Wo + 2 * (d->Ho - 2)) * (d->Cout / 8);
+    ring_line_fold_kernel<<<(unsigned)irgan_cdiv(threads, 256), 256, 0, st>>>(*d, ws, dx);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }

@@ -508,6 +508,8 @@ class GeneratorEngine:
                       [f"r{b}_{i}" for b in range(n_blocks) for i in (1, 2)]}
         assert len(self.norms) == n_in
         self.bufs = Buffers(store.device)
+        # a second stream for the ResnetBlock backward-data rings (set by GANStep; None: in line)
+        self.ring_stream = None
 
     def pack(self):
         if self._pack_batch is None:
@@ -529,14 +531,24 @@ class GeneratorEngine:
         ops.pad(x, xp, 1, "replicate")
         return xp
 
-    def _res_dgrad(self, g: Buffers, pc, dy: Feat, dx: Feat, accumulate, padbuf):
-        """dx (+)= backward-data of a ResnetBlock conv for the padding type."""
+    def _res_dgrad(self, g: Buffers, pc, dy: Feat, dx: Feat, accumulate, padbuf, ring_stream=None):
+        """dx (+)= backward-data of a ResnetBlock conv for the padding type.  With
+        ring_stream (reflect), the pad ring runs there: returns the event dx's consumer waits on."""
         if self.padding_type != "replicate":
-            ops.conv_dgrad(pc, dy, dx, accumulate=accumulate, pad_buf=padbuf)
-            return
+            return ops.conv_dgrad(pc, dy, dx, accumulate=accumulate, pad_buf=padbuf, ring_stream=ring_stream)
         dxp = Feat(g.get("res_dxp", (dx.N, dx.H + 2, dx.W + 2, dx.C), self.tdt))
         ops.conv_dgrad(pc, dy, dxp)
         ops.pad_fold(dxp, dx, 1, "replicate", accumulate=accumulate)
+        return None
+
+    def _res_dgrad_wgrad(self, g: Buffers, pc, dy: Feat, dx: Feat, accumulate, padbuf, wgrad):
+        """The backward-data of a ResnetBlock conv, then its weight gradient (``wgrad()``).
+        With self.ring_stream set, the reflect ring of the backward-data runs on that stream
+        beside the weight gradient (which leaves CUs idle), joined before dx is read."""
+        ev = self._res_dgrad(g, pc, dy, dx, accumulate, padbuf, ring_stream=self.ring_stream)
+        wgrad()
+        if ev is not None:
+            torch.cuda.current_stream().wait_event(ev)
 
     def _bgrad(self, key):
         """Flat-buffer slice of parameter ``key``'s gradient, None when the layout has no
@@ -753,10 +765,12 @@ class GeneratorEngine:
             # nb_h: dh's IN-backward partials for r{b}_2, written by the previous block's dgrad
             self.norms[f"r{b}_2"].bwd(g, f"r{b}_2", dh, r2, ACT_NONE, dt_, db=self._bgrad(f"{key}{k2}.bias"),
                                       q8=A.spec(s2, dy8) if self.fp8 else None, nb=nb_h)
-            wg(p2, f"{key}{k2}", xin2, dt_)
             dr = Feat(g.get("dtmp2", (B, H2, W2, c2), T))
             nb_r = 0
+            wg2 = lambda: wg(p2, f"{key}{k2}", xin2, dt_)  # noqa: E731
+            wg1 = lambda: wg(p1, f"{key}{k1}", xin1, dr)   # noqa: E731
             if self.fp8:
+                wg2()
                 A.ensure(s2, dt_, dy8)
                 ops.conv_dgrad_fp8(p2, *self._w8(4 * b + 3), dy8, A.dqp(s2), dt_, dr)
             else:
@@ -764,14 +778,16 @@ class GeneratorEngine:
                 if not drop:
                     nb_r = self.norms[f"r{b}_1"].dgrad_in(g, f"r{b}_1", p2, dt_, dr, r1, ACT_RELU)
                 if not nb_r:
-                    self._res_dgrad(g, p2, dt_, dr, False, padbuf)
+                    self._res_dgrad_wgrad(g, p2, dt_, dr, False, padbuf, wg2)
+                else:
+                    wg2()
                 if drop:   # backward of the dropout: the same mask and scale on the gradient
                     ops.dropout(dr, dr, g.state["dropout_seed"] + 2 * b)
             self.norms[f"r{b}_1"].bwd(g, f"r{b}_1", dr, r1, ACT_RELU, dr, db=self._bgrad(f"{key}{k1}.bias"),
                                       q8=A.spec(s1, dy8) if self.fp8 else None, nb=nb_r)
-            wg(p1, f"{key}{k1}", xin1, dr)
             nb_h = 0
             if self.fp8:
+                wg1()
                 A.ensure(s1, dr, dy8)
                 ops.conv_dgrad_fp8(p1, *self._w8(4 * b + 1), dy8, A.dqp(s1), dr, dh, accumulate=True)
             else:
@@ -780,7 +796,9 @@ class GeneratorEngine:
                     nb_h = self.norms[f"r{b - 1}_2"].dgrad_in(g, f"r{b - 1}_2", p1, dr, dh, Feat(g.d[f"r2_{b - 1}"]),
                                                               ACT_NONE, accumulate=True)
                 if not nb_h:
-                    self._res_dgrad(g, p1, dr, dh, True, padbuf)
+                    self._res_dgrad_wgrad(g, p1, dr, dh, True, padbuf, wg1)
+                else:
+                    wg1()
             ready(f"{key}{k1}.weight")
         if self.fp8:
             self.f8a.update(nb2, nb2)   # next step's backward-data scales
@@ -1127,6 +1145,10 @@ class GANStep:
         self.side = None
         if G.device.type == "cuda" and not os.environ.get("IRGAN_NO_D_OVERLAP"):
             self.side = torch.cuda.Stream(device=G.device)
+        # the G backward's ResnetBlock reflect rings on the (then idle) side stream, beside
+        # each conv's weight gradient (IRGAN_NO_RING_SIDE=1: in line on the main stream)
+        if self.side is not None and dtype == BF16 and not os.environ.get("IRGAN_NO_RING_SIDE"):
+            self.gen.ring_stream = self.side
         # the whole step as one HIP graph (captured on first use, replayed after): see _graph_ok
         self.G.dev_adam = self.D.dev_adam = G.device.type == "cuda"
         self._graph = self._graph_key = self._graph_L = None

@@ -49,10 +49,37 @@ def set_deterministic(on: bool) -> bool:
     return bool(_lib.load().irgan_set_deterministic(int(bool(on))))
 
 
+_RING_FOLD = [bool(os.environ.get("IRGAN_RING_FOLD"))]
+
+
 def set_ring_fold(on: bool) -> bool:
     """irgan_set_ring_fold: the resblock dgrad as one conv_pp launch with the reflect ring
     folded in (opt-in) instead of interior + ring launches.  Returns the previous setting."""
+    _RING_FOLD[0] = bool(on)
     return bool(_lib.load().irgan_set_ring_fold(int(bool(on))))
+
+
+# the reflect ring of a ResnetBlock backward-data beside the weight gradient: the ring's
+# line GEMM keeps to this many workgroups (conv_wgrad_pc leaves 16 of 256 CUs idle)
+RING_SIDE_BLOCKS = 16
+_RING_WS = {}
+
+
+def _ring_ws(dev, floats):
+    """Per-(device, stream) fp32 workspace of the ring's line GEMM (irgan_reflect_dgrad_ring_ws)."""
+    key = (dev, torch.cuda.current_stream(dev).cuda_stream)
+    w = _RING_WS.get(key)
+    if w is None or w.numel() < floats:
+        w = _RING_WS[key] = torch.empty(floats, dtype=torch.float32, device=dev)
+    return w
+
+
+def _ring(d, dy: "Feat", buf, p, dx: "Feat", max_blocks=1 << 20):
+    """The reflect-pad ring of a bf16 backward-data onto dx (after its interior): the line
+    GEMM + fold on ResnetBlock shapes, else the general ring launch (the library decides)."""
+    ws = _ring_ws(dx.t.device, dx.N * 4 * 68 * dx.C)
+    _lib.call("irgan_reflect_dgrad_ring_ws", ctypes.byref(d), dy.ptr, P(buf), p, dx.ptr, P(ws), ws.numel(),
+              max_blocks, stream())
 
 
 class LaunchTimer:
@@ -299,12 +326,17 @@ RING_MFMA = not os.environ.get("IRGAN_NO_RING_MFMA")
 
 
 def conv_dgrad(pc: PackedConv, dy: Feat, dx: Feat, accumulate=False, mask: Feat = None, mask_act=0,
-               pad_buf: torch.Tensor = None, bias=False):
+               pad_buf: torch.Tensor = None, bias=False, ring_stream=None):
     """dx = d(conv)/dx^T dy.  Reflect-padded layers: interior straight into dx and the
-    padded ring folded onto dx's border band -- bf16: irgan_conv_dgrad_reflect (one
-    launch with the ring folded in on the ResnetBlock shapes, else interior + the MFMA
-    ring launch); fp32: split-K ring partials in pad_buf (fp32 scratch) folded by
-    irgan_reflect_ring_fold; stride-2 layers launch per phase."""
+    padded ring folded onto dx's border band -- bf16: the interior launch, then the ring
+    (irgan_reflect_dgrad_ring_ws: line GEMM + fold on the ResnetBlock shapes), or with the
+    opt-in fold (set_ring_fold) one irgan_conv_dgrad_reflect launch; fp32: split-K ring
+    partials in pad_buf (fp32 scratch) folded by irgan_reflect_ring_fold; stride-2 layers
+    launch per phase.
+
+    ring_stream (bf16 reflect, fold off): the ring runs on that stream after the interior,
+    so it can overlap the caller's next launches (the weight gradient); returns an event
+    recorded on ring_stream that the consumer of dx must wait on.  Otherwise None."""
     s = pc.spec
     assert dy.C == pc.cout_eff and dx.C == s.cin and dy.dt == pc.dtype
     if pc.reflect:
@@ -326,18 +358,33 @@ def conv_dgrad(pc: PackedConv, dy: Feat, dx: Feat, accumulate=False, mask: Feat 
         ring_mfma = (p > 0 and pc.dtype == BF16 and RING_MFMA and pc.cout_eff % 32 == 0 and H >= 2 * p + 2
                      and W >= 2 * p + 2 and dy.ld % 8 == 0 and dy.off % 8 == 0)
 
-        def launch():
-            if ring_mfma:
-                # interior + ring fold: one conv_pp launch on the ResnetBlock shapes, else the
-                # interior launch + the MFMA ring launch (irgan_conv_dgrad_reflect decides)
-                _lib.call("irgan_conv_dgrad_reflect", ctypes.byref(d), dy.ptr, P(buf), p, dx.ptr, stream())
-            else:
-                _lib.call("irgan_conv_fwd", ctypes.byref(d), dy.ptr, P(buf), None, dx.ptr, None, stream())
+        fold = ring_mfma and _RING_FOLD[0]
+        side = ring_stream is not None and ring_mfma and not fold
 
-        # the timed dgrad op is the whole backward-data: interior + ring
+        def launch():
+            if fold:
+                # interior + ring in one conv_pp launch on the ResnetBlock shapes, else both
+                # launches (irgan_conv_dgrad_reflect decides)
+                _lib.call("irgan_conv_dgrad_reflect", ctypes.byref(d), dy.ptr, P(buf), p, dx.ptr, stream())
+                return
+            _lib.call("irgan_conv_fwd", ctypes.byref(d), dy.ptr, P(buf), None, dx.ptr, None, stream())
+            if ring_mfma and not side:
+                _ring(d, dy, buf, p, dx)
+
+        # the timed dgrad op is the whole backward-data (interior + ring) unless the ring runs
+        # on ring_stream: then the interior here and the ring as its own "ring" op there
         TIMER.wrap(conv_tag("dgrad", s, (H, W), dx.N), launch)
+        if side:
+            ev = torch.cuda.Event()
+            ev.record()
+            ring_stream.wait_event(ev)
+            with torch.cuda.stream(ring_stream):
+                TIMER.wrap(conv_tag("ring", s, (H, W), dx.N), lambda: _ring(d, dy, buf, p, dx, RING_SIDE_BLOCKS))
+                done = torch.cuda.Event()
+                done.record(ring_stream)
+            return done
         if p == 0 or ring_mfma:
-            return
+            return None
         # ring in split-K partials: rows[ks][N][2p][Wp][C], cols[ks][N][H][2p][C]
         rsz, csz = dx.N * 2 * p * Wp * s.cin, dx.N * H * 2 * p * s.cin
         nk = -(-(ay * ax * pc.cout_eff) // 64)
@@ -963,5 +1010,5 @@ def conv_dgrad_fp8(pc: PackedConv, wd8: torch.Tensor, dqw, dy8: Feat, dqx, dy: F
         _lib.call("irgan_conv_fwd_fp8", ctypes.byref(d8), dy8.ptr, P(wd8), dqx, dqw, None, dx.ptr, None,
                   ctypes.byref(nb), stream())
         if p > 0:
-            _lib.call("irgan_reflect_dgrad_ring", ctypes.byref(d), dy.ptr, P(buf), p, dx.ptr, stream())
+            _ring(d, dy, buf, p, dx)
     TIMER.wrap(conv_tag("dgrad8", s, (H, W), dx.N), launch)
