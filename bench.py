@@ -306,6 +306,9 @@ def main():
                    "rank_time_s": {"max": round(el, 4), "min": round(el_min, 4)},
                    "replicas_bit_identical": replicas_ok},
             "losses": {k: round(v, 5) for k, v in losses.items()},
+            **({"join_wait_ms": round(sum(a.elapsed_time(b) for a, b in irc.engine.JOIN_TIMES[-args.steps:]) /
+                                      max(1, len(irc.engine.JOIN_TIMES[-args.steps:])), 4)}
+               if irc.engine.JOIN_TIMES else {}),
         }
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(H, W, B, args.cpu_budget)

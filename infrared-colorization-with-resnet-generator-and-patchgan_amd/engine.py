@@ -1117,6 +1117,11 @@ class BucketedAllreduce:
         self.works, self.end = [], self.store.numel
 
 
+# IRGAN_JOIN_TIMING=1: (event, event) pairs around the main stream's wait for the side
+# stream's D step (tools: how much of the step is the D step on the critical path)
+JOIN_TIMES = [] if os.environ.get("IRGAN_JOIN_TIMING") else None
+
+
 class GANStep:
     """Buffers, engines and the fused step for one rank.
 
@@ -1145,9 +1150,12 @@ class GANStep:
         self.side = None
         if G.device.type == "cuda" and not os.environ.get("IRGAN_NO_D_OVERLAP"):
             self.side = torch.cuda.Stream(device=G.device)
-        # the G backward's ResnetBlock reflect rings on the (then idle) side stream, beside
-        # each conv's weight gradient (IRGAN_NO_RING_SIDE=1: in line on the main stream)
-        if self.side is not None and dtype == BF16 and not os.environ.get("IRGAN_NO_RING_SIDE"):
+        # opt-in (IRGAN_RING_SIDE=1): the G backward's ResnetBlock reflect rings on the (then
+        # idle) side stream beside each conv's weight gradient.  Measured slower than in line
+        # (1152 vs 1168 img/s, gpurun_out/r03_t): on the 16 CUs the weight gradient leaves idle
+        # the ring takes ~85 us, longer than the weight gradient, and the two event edges per
+        # conv cost ~4 us of main-stream bubble each
+        if self.side is not None and dtype == BF16 and os.environ.get("IRGAN_RING_SIDE"):
             self.gen.ring_stream = self.side
         # the whole step as one HIP graph (captured on first use, replayed after): see _graph_ok
         self.G.dev_adam = self.D.dev_adam = G.device.type == "cuda"
@@ -1301,7 +1309,14 @@ class GANStep:
         ssim_work = b.flat("ssim_work", 10 * fake.numel())
         ops.ssim(Feat(fake), Feat(rgb_h), cfg.lambda_ssim, dfake, L[5:6], ssim_work)
         if main is not None:
+            jt = JOIN_TIMES is not None and not torch.cuda.is_current_stream_capturing()
+            if jt:   # diagnostics: how long the main stream waits here for the side stream's D step
+                ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                ea.record(main)
             main.wait_stream(self.side)           # the GAN term's d fake
+            if jt:
+                eb.record(main)
+                JOIN_TIMES.append((ea, eb))
         ops.axpby(dd.sl(cin, cout), 1.0, Feat(dfake), 1.0)
         self.gen.backward(dfake, ready=self.g_reduce.ready)
         self.g_reduce.finish(self.G.adam_begin(cfg.lr_G * self.lr_scale, cfg.beta1, cfg.beta2))

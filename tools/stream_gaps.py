@@ -1,6 +1,6 @@
 """Per-stream busy time, idle gaps and overlap from a rocprofv3 kernel trace, over the last
 --steps steps (a step = the span between consecutive launches of --marker, default the
-generator's first conv: the narrow 7x7 kernel).
+generator's first conv: the dense-K 7x7 kernel).
 
     python tools/stream_gaps.py <run_kernel_trace.csv> [--steps 5]
 """
@@ -13,7 +13,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--marker", default="conv_narrow_kernel<7, 7, 8, 1>")
+    ap.add_argument("--marker", default="conv_c8r_kernel<7, 7, 1, 1>")
     a = ap.parse_args()
     rows = [r for r in csv.DictReader(open(a.trace))]
     ks = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Queue_Id"],
