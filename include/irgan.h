@@ -231,7 +231,7 @@ int irgan_in_bwd_apply_fp8(const void* dy, int32_t lddy, int32_t dyoff, const vo
                            int32_t dxoff, void* y8, int32_t ld8, int32_t off8, const float* q,
                            uint32_t* amax, irgan_stream_t s);
 /* db[c] += sum over pixels of g[p][c] (bias gradient), g slice (dtype, ld, off).
- * work: IRGAN_IN_PARTS*C doubles of scratch. */
+ * work: 16*IRGAN_IN_PARTS*C doubles of scratch. */
 int irgan_channel_sum(const void* g, int32_t dtype, int32_t P, int32_t C, int32_t ld,
                       int32_t off, float* db, double* work, irgan_stream_t s);
 
@@ -272,6 +272,14 @@ int irgan_reflect_dgrad_ring(const irgan_conv_desc* d, const void* dy, const voi
  * backward: engine.GeneratorEngine.backward). */
 int irgan_reflect_dgrad_ring_ws(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p, void* dx,
                                 float* ws, int64_t ws_floats, int32_t max_blocks, irgan_stream_t s);
+/* Backward-data of a 4x4 stride-2 pad-1 conv (PatchGAN model.0 / .3 / .6, ir:600-612) in
+ * ONE launch for all four output phases: d = the four per-phase descriptors (2x2 taps on
+ * dy, omy = omx = 2, (ooy, oox) the phase, c0y / c0x in {-1, 0}; otherwise identical), w =
+ * their four packed phase images.  dx (+)= result, with the optional backward mask as
+ * irgan_conv_fwd.  bf16, dy channels % 64, dx channels <= 16 or % 64, no bias / activation;
+ * else IRGAN_EUNSUPPORTED (nothing launched; the caller runs the four phase launches). */
+int irgan_conv_dgrad_s2(const irgan_conv_desc* d, const void* dy, const void* const* w, void* dx,
+                        const void* mask, irgan_stream_t s);
 /* The whole backward-data of a reflect-padded stride-1 conv (ir:381-392, 401-411): the
  * interior correlation and the fold of its pad ring (d, w, p as irgan_reflect_dgrad_ring).
  * With the ring fold on (irgan_set_ring_fold), ResnetBlock shapes (bf16, 3x3, p = 1, dY

@@ -409,6 +409,9 @@ def conv_dgrad(pc: PackedConv, dy: Feat, dx: Feat, accumulate=False, mask: Feat 
     st = s.stride
 
     def phases():
+        if st == 2 and len(pc.dg) == 4 and pc.dtype == BF16 and not bias and _dgrad_s2(pc, dy, dx, accumulate, mask,
+                                                                                        mask_act):
+            return   # all four phases in one launch (irgan_conv_dgrad_s2)
         for (py, _, ay, c0y), (px, _, ax, c0x), buf in pc.dg:
             Ho, Wo = -(-(dx.H - py) // st), -(-(dx.W - px) // st)
             if Ho <= 0 or Wo <= 0:
@@ -422,6 +425,27 @@ def conv_dgrad(pc: PackedConv, dy: Feat, dx: Feat, accumulate=False, mask: Feat 
             _lib.call("irgan_conv_fwd", ctypes.byref(d), dy.ptr, P(buf), P(pc.bias if bias else None), dx.ptr,
                       mask.ptr if mask else None, stream())
     TIMER.wrap(conv_tag("dgrad", s, (dx.H, dx.W), dx.N), phases)
+
+
+def _dgrad_s2(pc: PackedConv, dy: Feat, dx: Feat, accumulate, mask, mask_act) -> bool:
+    """The four phase launches of a 4x4 stride-2 backward-data as one irgan_conv_dgrad_s2
+    launch; False (nothing ran) when the library does not take the shapes."""
+    s = pc.spec
+    descs, ws = (_lib.ConvDesc * 4)(), (ctypes.c_void_p * 4)()
+    for k, ((py, _, ay, c0y), (px, _, ax, c0x), buf) in enumerate(pc.dg):
+        Ho, Wo = -(-(dx.H - py) // 2), -(-(dx.W - px) // 2)
+        descs[k] = _desc(N=dy.N, H=dy.H, W=dy.W, Cin=pc.cout_eff, ldx=dy.ld, xoff=dy.off, Ho=Ho, Wo=Wo, Cout=s.cin,
+                         ldy=dx.ld, yoff=dx.off, OH=dx.H, OW=dx.W, omy=2, ooy=py, omx=2, oox=px, KH=ay, KW=ax, sy=1,
+                         sx=1, c0y=c0y, c0x=c0x, pad_mode=PAD_ZERO, act=0, accumulate=int(accumulate),
+                         dtype=pc.dtype, out_dtype=dx.dt, mask_act=mask_act, ldm=mask.ld if mask else 0,
+                         moff=mask.off if mask else 0, cin_real=s.cout if s.cout < pc.cout_eff else 0)
+        ws[k] = buf.data_ptr()
+    rc = _lib.load().irgan_conv_dgrad_s2(descs, dy.ptr, ws, dx.ptr, mask.ptr if mask else None, stream())
+    if rc == IRGAN_EUNSUPPORTED:
+        return False
+    if rc != 0:
+        raise _lib.IrganError(f"irgan_conv_dgrad_s2 failed with code {rc}")
+    return True
 
 
 def conv_wgrad(spec: ConvSpec, x: Feat, dy: Feat, dw: torch.Tensor, dtype: int, splitk=0):
@@ -540,7 +564,7 @@ def channel_sum(g: Feat, db: torch.Tensor):
     key = (db.device, g.C, torch.cuda.current_stream(db.device).cuda_stream)
     w = _CS_WORK.get(key)
     if w is None:
-        w = _CS_WORK[key] = torch.empty(IN_PARTS * g.C, dtype=torch.float64, device=db.device)
+        w = _CS_WORK[key] = torch.empty(16 * IN_PARTS * g.C, dtype=torch.float64, device=db.device)
     _lib.call("irgan_channel_sum", g.ptr, g.dt, g.P, g.C, g.ld, g.off, P(db), P(w), stream())
 
 
