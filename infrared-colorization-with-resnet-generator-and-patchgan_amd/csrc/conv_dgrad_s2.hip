@@ -157,6 +157,7 @@ __global__ __launch_bounds__(512, 1) void dgrad_s2_kernel(const irgan_conv_desc 
     const bool vec = co + 8 <= d.Cout &&
                      (out_f32 ? (d.ldy % 4 == 0 && d.yoff % 4 == 0) : (d.ldy % 8 == 0 && d.yoff % 8 == 0)) &&
                      (!mask || (d.ldm % 8 == 0 && d.moff % 8 == 0));
+    const bool quad = d.Cout == 4 && out_f32 && !mask && d.ldy % 4 == 0 && d.yoff % 4 == 0;
 #pragma unroll 1
     for (int p = 0; p < 4; ++p) {
         if (p) __syncthreads();  // the previous phase's tile is stored
@@ -178,6 +179,16 @@ __global__ __launch_bounds__(512, 1) void dgrad_s2_kernel(const irgan_conv_desc 
             if (oy >= d.OH || ox >= d.OW) continue;
             const long pix = ((long)img * d.OH + oy) * d.OW + ox;
             const float4 a0 = *(const float4*)(st + q * RS + ch), a1 = *(const float4*)(st + q * RS + ch + 4);
+            if (quad) {  // 4-channel fp32 output (the D input gradient): one 16-byte store
+                float4* yp = (float4*)((float*)dx + pix * d.ldy + d.yoff);
+                float4 o = a0;
+                if (d.accumulate) {
+                    const float4 p0 = *yp;
+                    o.x += p0.x; o.y += p0.y; o.z += p0.z; o.w += p0.w;
+                }
+                *yp = o;
+                continue;
+            }
             float v[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
             conv_store8(d, v, pix, co, vec, out_f32, dx, mask);
         }

@@ -35,6 +35,16 @@ bool split128(int cin) {
     return cin / 64 <= mx;
 }
 
+// Output-channel tile for a Cout % 256 == 0 layer: 256 unless that leaves most CUs idle
+// (the PatchGAN 4x4 layers at 32x32: D model.8 backward-data at B = 16 is 64 BN-256 blocks
+// for 256 CUs) -- then 128 or the 64-channel single-halo tile (two blocks per CU)
+int narrow_bn(const irgan_conv_desc* d) {
+    static const bool off = getenv("IRGAN_NO_PP_NARROW_BN") != nullptr;
+    const long patches = (long)d->N * irgan_cdiv(d->Ho, PH) * irgan_cdiv(d->Wo, PW);
+    if (off || patches * (d->Cout / 256) >= 160) return 256;
+    return patches * (d->Cout / 128) >= 160 ? 128 : 64;
+}
+
 template <int KH, int KW, int BN>
 void launch_pp(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y, const void* mask,
                hipStream_t st, int swz) {
@@ -80,10 +90,11 @@ extern "C" int irgan_conv_fwd_pp(const irgan_conv_desc* d, const void* x, const 
         IRGAN_LAUNCH_CHECK();
         return 0;
     }
-    if (d->Cout % 256 == 0) {
+    const int nbn = d->Cout % 256 == 0 ? narrow_bn(d) : 0;
+    if (nbn == 256) {
         if (k33) launch_pp<3, 3, 256>(d, x, w, bias, y, mask, st, swz);
         else launch_pp<4, 4, 256>(d, x, w, bias, y, mask, st, swz);
-    } else if (d->Cout % 128 == 0 && !split128(d->Cin)) {
+    } else if (nbn == 128 || (nbn == 0 && d->Cout % 128 == 0 && !split128(d->Cin))) {
         if (!pp128) return IRGAN_EUNSUPPORTED;
         if (k33) launch_pp<3, 3, 128>(d, x, w, bias, y, mask, st, swz);
         else launch_pp<4, 4, 128>(d, x, w, bias, y, mask, st, swz);
@@ -122,7 +133,8 @@ extern "C" int irgan_conv_fwd_stats(const irgan_conv_desc* d, const void* x, con
     if (tpx * tpy > IRGAN_IN_PARTS) return IRGAN_EUNSUPPORTED;
     if ((long)d->N * d->Ho * d->Wo <= 0) return IRGAN_EUNSUPPORTED;
     static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
-    const int bn = d->Cout % 256 == 0 ? 256 : (d->Cout % 128 == 0 && !split128(d->Cin) ? 128 : 64);  // as irgan_conv_fwd_pp
+    const int bn = d->Cout % 256 == 0 ? narrow_bn(d)
+                                      : (d->Cout % 128 == 0 && !split128(d->Cin) ? 128 : 64);  // as irgan_conv_fwd_pp
     const int ntn = d->Cout / bn;
     const int blocks = d->N * tpy * tpx * ntn;
     hipStream_t st = (hipStream_t)s;
