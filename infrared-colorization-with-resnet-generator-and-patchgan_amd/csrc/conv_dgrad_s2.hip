@@ -36,7 +36,7 @@ struct S2Phases {
     int c0y[4], c0x[4];  // dy offset of tap (0, 0)
 };
 
-template <int BN>
+template <int BN, bool ONEC>
 struct S2 {
     static constexpr int WM = BN >= 32 ? 4 : 8, WN = 8 / WM;  // wave rows x columns
     static constexpr int MI = 4 * S2P * S2P / WM / 16;        // pixel fragments per wave
@@ -44,22 +44,22 @@ struct S2 {
     static constexpr int BB = BN * 128;                       // one phase's weight tile
     static constexpr int STAGE = 4 * BB;
     static constexpr int RS = BN + 4;                         // epilogue row stride (floats)
-    static constexpr int LOOP = 2 * S2HB + 2 * STAGE;
+    static constexpr int LOOP = (ONEC ? 1 : 2) * S2HB + 2 * STAGE;  // ONEC: one 64-channel chunk, one halo
     static constexpr int EPI = S2P * S2P * RS * 4;            // one phase, fp32
     static constexpr int LDS = LOOP > EPI ? LOOP : EPI;
     static_assert(NJ >= 1 && NJ * 16 * WN == BN && LDS <= 160 * 1024, "tile");
 };
 
-template <int BN>
-__global__ __launch_bounds__(512, 1) void dgrad_s2_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ dy,
+template <int BN, bool ONEC>
+__global__ __launch_bounds__(512, ONEC ? 2 : 1) void dgrad_s2_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ dy,
                                                           const S2Phases ph, void* __restrict__ dx,
                                                           const void* __restrict__ mask, int tpx, int tpy, int ntn,
                                                           int swz) {
-    using G = S2<BN>;
+    using G = S2<BN, ONEC>;
     constexpr int WM = G::WM, WN = G::WN, MI = G::MI, NJ = G::NJ, BB = G::BB, STAGE = G::STAGE;
     __shared__ __attribute__((aligned(1024))) char smem[G::LDS];
     char* const sH = smem;
-    char* const sW = smem + 2 * S2HB;
+    char* const sW = smem + (ONEC ? 1 : 2) * S2HB;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wid / WN, wn = wid % WN;
@@ -80,7 +80,7 @@ __global__ __launch_bounds__(512, 1) void dgrad_s2_kernel(const irgan_conv_desc 
     const int sub = lane >> 3;
     auto issue_halo = [&](int c) {
         const i32x4 rs = make_rsrc(dy + c * 64, dybytes - c * 128);
-        char* dst = sH + (c & 1) * S2HB;
+        char* dst = sH + (ONEC ? 0 : (c & 1) * S2HB);
         for (int u = wid; u < S2PIECES; u += 8) {
             const int r = u * 8 + sub, hy = r / S2H, hx = r - hy * S2H;
             const int iy = I0 - 1 + hy, ix = J0 - 1 + hx;
@@ -126,7 +126,7 @@ __global__ __launch_bounds__(512, 1) void dgrad_s2_kernel(const irgan_conv_desc 
         const int c = k >> 2, tp = k & 3;
         if (k + 1 < nk) issue_w(k + 1);
         if (tp == 0 && c + 1 < nchunk) issue_halo(c + 1);
-        const char* H = sH + (c & 1) * S2HB;
+        const char* H = sH + (ONEC ? 0 : (c & 1) * S2HB);
         const char* Wt = sW + (k & 1) * STAGE + phs * BB;
         const int tap = (tp >> 1) * S2H + (tp & 1);
 #pragma unroll
@@ -237,13 +237,18 @@ extern "C" int irgan_conv_dgrad_s2(const irgan_conv_desc* d, const void* dy, con
     static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
     const int tpy = irgan_cdiv((a.OH + 1) / 2, S2P), tpx = irgan_cdiv((a.OW + 1) / 2, S2P);
     hipStream_t st = (hipStream_t)s;
+    const bool one = a.Cin == 64;  // one chunk: a single halo buffer (BN 16: two blocks per CU)
+#define S2L(BNV, ONEV, NTN) \
+    dgrad_s2_kernel<BNV, ONEV><<<a.N * tpy * tpx * (NTN), 512, 0, st>>>(a, (const bf16_t*)dy, ph, dx, mask, tpx, tpy, \
+                                                                        NTN, swz)
     if (a.Cout <= 16) {
-        dgrad_s2_kernel<16><<<a.N * tpy * tpx, 512, 0, st>>>(a, (const bf16_t*)dy, ph, dx, mask, tpx, tpy, 1, swz);
+        if (one) S2L(16, true, 1);
+        else S2L(16, false, 1);
     } else {
-        const int ntn = a.Cout / 64;
-        dgrad_s2_kernel<64><<<a.N * tpy * tpx * ntn, 512, 0, st>>>(a, (const bf16_t*)dy, ph, dx, mask, tpx, tpy, ntn,
-                                                                     swz);
+        if (one) S2L(64, true, a.Cout / 64);
+        else S2L(64, false, a.Cout / 64);
     }
+#undef S2L
     IRGAN_LAUNCH_CHECK();
     return 0;
 }

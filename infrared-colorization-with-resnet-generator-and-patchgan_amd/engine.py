@@ -879,30 +879,59 @@ class DiscriminatorEngine:
             x = y
         return x.t
 
-    def backward(self, dout: torch.Tensor, want_wgrad=True, want_dinput=False, tag="", bufs: Buffers = None):
+    def backward(self, dout: torch.Tensor, want_wgrad=True, want_dinput=False, tag="", bufs: Buffers = None,
+                 wgrad_stream=None):
         """dout: dL/dlogits fp32 (same shape as forward output).  Weight grads
-        accumulate into store.grad; returns d input (fp32 NHWC) if asked."""
+        accumulate into store.grad; returns d input (fp32 NHWC) if asked.
+
+        wgrad_stream: run each layer's weight (and bias) gradient on that stream, beside the
+        backward-data chain on the current one (they read the same dY, which nothing rewrites
+        afterwards); the current stream waits for it before returning."""
         g, T, S = bufs or self.bufs, self.tdt, self.store
         acts, pre = g.state[tag]
         G = S.grad
         n = len(self.packs)
+        if wgrad_stream is not None and torch.cuda.is_current_stream_capturing():
+            wgrad_stream = None   # (a third stream inside the opt-in HIP graph capture crashed capture_end)
+        cur = torch.cuda.current_stream() if wgrad_stream is not None else None
+
+        def off_stream(fn):
+            if cur is None:
+                fn()
+                return
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            wgrad_stream.wait_event(ev)
+            with torch.cuda.stream(wgrad_stream):
+                fn()
+
+        def join():
+            if cur is not None:
+                cur.wait_stream(wgrad_stream)
         dbuf = g.zeros(f"{tag}dout_t", tuple(dout.shape[:3]) + (8,), T)   # 1-ch logits grad, padded to 8
         ops.axpby(Feat(dout), 1.0, Feat(dbuf, 0, dout.shape[3]))
         dy = Feat(dbuf, 0, self.packs[-1].cout_eff)
         for i in reversed(range(n)):
             pc, key = self.packs[i], self.LAYERS[i][0]
             x = acts[i]
+            bias_sum = None
             if i == n - 1:
                 if want_wgrad:
-                    ops.channel_sum(Feat(dout), S.krsc(key + ".bias", G))
+                    bias_sum = Feat(dout)
             elif self.norms[i] is not None:
                 self.norms[i].bwd(g, f"{tag}n{i}", dy, pre[i], ACT_LRELU, dy,
                                   db=S.krsc(key + ".bias", G) if want_wgrad and key + ".bias" in S.shapes else None)
             elif want_wgrad:  # layer 0: LReLU mask already folded into dy by the layer-1 dgrad
-                ops.channel_sum(dy, S.krsc(key + ".bias", G))
+                bias_sum = dy
             if want_wgrad:
-                ops.conv_wgrad(pc.spec, x, Feat(dy.t, dy.off, pc.spec.cout), S.krsc(key + ".weight", G), self.dtype)
+                def wgrad(pc=pc, key=key, x=x, dy=dy, bias_sum=bias_sum):
+                    if bias_sum is not None:
+                        ops.channel_sum(bias_sum, S.krsc(key + ".bias", G))
+                    ops.conv_wgrad(pc.spec, x, Feat(dy.t, dy.off, pc.spec.cout), S.krsc(key + ".weight", G),
+                                   self.dtype)
+                off_stream(wgrad)
             if i == 0:
+                join()
                 if not want_dinput:
                     return None
                 dx = Feat(g.get(f"{tag}dinput", (x.N, x.H, x.W, pc.spec.cin), torch.float32))
@@ -914,6 +943,7 @@ class DiscriminatorEngine:
             else:
                 ops.conv_dgrad(pc, dy, dx)
             dy = dx
+        join()
         return None
 
 
@@ -1157,6 +1187,13 @@ class GANStep:
         # conv cost ~4 us of main-stream bubble each
         if self.side is not None and dtype == BF16 and os.environ.get("IRGAN_RING_SIDE"):
             self.gen.ring_stream = self.side
+        # opt-in (IRGAN_DWG_STREAM=1): the D step's weight gradients on a third stream beside its
+        # backward-data chain.  The main stream's wait for the D step drops 0.84 -> 0.62 ms, but
+        # the step does not gain (1169 vs 1173 img/s, gpurun_out/r03_z): the GPU is busy 99 % of
+        # the step either way, the third stream only takes CUs from the main stream's G-step terms
+        self.side2 = None
+        if self.side is not None and os.environ.get("IRGAN_DWG_STREAM"):
+            self.side2 = torch.cuda.Stream(device=G.device)
         # the whole step as one HIP graph (captured on first use, replayed after): see _graph_ok
         self.G.dev_adam = self.D.dev_adam = G.device.type == "cuda"
         self._graph = self._graph_key = self._graph_L = None
@@ -1278,7 +1315,7 @@ class GANStep:
             pred = self.dis.forward(din, tag="d")
             dpred = b.get("dpred", tuple(pred.shape), torch.float32)
             ops.hinge(pred, pred[:B].numel(), 0, 1.0, dpred, L[0:1])
-            self.dis.backward(dpred, want_wgrad=True, want_dinput=False, tag="d")
+            self.dis.backward(dpred, want_wgrad=True, want_dinput=False, tag="d", wgrad_stream=self.side2)
             self.d_reduce.start()
             # D Adam, then the G-step GAN term through the updated D (ir:1651, 1659-1662),
             # still on the side stream: the main stream meanwhile runs the G-step terms
