@@ -74,12 +74,23 @@ def _ring_ws(dev, floats):
     return w
 
 
+RING_LINE = [True]
+
+
+def set_ring_line(on: bool) -> bool:
+    """The line-GEMM ring launches (default) or the general reflect_ring_kernel for the
+    ResnetBlock shapes -- the latter is the ring of the opt-in fused IN-backward dgrad
+    (irgan_conv_dgrad_in_stats), so its bit-identity test references it.  Returns the previous setting."""
+    old, RING_LINE[0] = RING_LINE[0], bool(on)
+    return old
+
+
 def _ring(d, dy: "Feat", buf, p, dx: "Feat", max_blocks=1 << 20):
     """The reflect-pad ring of a bf16 backward-data onto dx (after its interior): the line
     GEMM + fold on ResnetBlock shapes, else the general ring launch (the library decides)."""
     ws = _ring_ws(dx.t.device, dx.N * 4 * 68 * dx.C)
-    _lib.call("irgan_reflect_dgrad_ring_ws", ctypes.byref(d), dy.ptr, P(buf), p, dx.ptr, P(ws), ws.numel(),
-              max_blocks, stream())
+    _lib.call("irgan_reflect_dgrad_ring_ws", ctypes.byref(d), dy.ptr, P(buf), p, dx.ptr, P(ws),
+              ws.numel() if RING_LINE[0] else 0, max_blocks, stream())
 
 
 class LaunchTimer:

@@ -33,7 +33,13 @@ def test_dgrad_in_stats_matches_separate_reduce(H, act, acc):
     pad = torch.empty(N * (H + 2) ** 2 * C, device=DEV)
 
     dx_ref = ops.Feat(old.clone() if acc else torch.zeros(N, H, H, C, device=DEV, dtype=torch.bfloat16))
-    ops.conv_dgrad(pc, dy, dx_ref, accumulate=acc, pad_buf=pad)
+    # the fused launch carries the general ring kernel (its IN partials): reference the plain
+    # dgrad with that same ring, not the default line-GEMM ring (another fp32 summation order)
+    prev = ops.set_ring_line(False)
+    try:
+        ops.conv_dgrad(pc, dy, dx_ref, accumulate=acc, pad_buf=pad)
+    finally:
+        ops.set_ring_line(prev)
     red_ref = torch.empty(N * C * 2, device=DEV)
     m._lib.call("irgan_in_bwd_reduce", dx_ref.ptr, dx_ref.dt, dx_ref.ld, dx_ref.off, None, 0, 0, 0, z.ptr, z.dt,
                 z.ld, z.off, act, N, H * H, C, ops.P(mr), ops.P(work), ops.P(red_ref), ops.stream())
