@@ -114,8 +114,8 @@ __global__ __launch_bounds__(TPB) void sep_kernel(const void* __restrict__ in, i
 // the Downsample / UpsampleAA that consumes it, so the normalised tensor is never stored.
 // LTPB % G == 0, so a thread's channel group (and its 8 (mean, rstd) pairs) is fixed.
 constexpr int LTPB = 1024;
-template <int TM, bool NORM = false>
-__global__ __launch_bounds__(LTPB) void sep_lds_kernel(const void* __restrict__ in, int idt, int Hin, int Win,
+template <int TM, bool NORM = false, int NT = LTPB>
+__global__ __launch_bounds__(NT) void sep_lds_kernel(const void* __restrict__ in, int idt, int Hin, int Win,
                                                        int ldi, int offi, void* __restrict__ out, int odt, int Hout,
                                                        int Wout, int ldo, int offo, const int* __restrict__ ty,
                                                        const float* __restrict__ wy, int Ty,
@@ -147,7 +147,7 @@ __global__ __launch_bounds__(LTPB) void sep_lds_kernel(const void* __restrict__ 
         wyv[i] = i < Ty ? wy[oy * Ty + i] : 0.f;
         rb[i] = i < Ty ? (long)(n * Hin + ty[oy * Ty + i]) * Win : 0;
     }
-    for (int v = threadIdx.x; v < Win * G; v += LTPB) {
+    for (int v = threadIdx.x; v < Win * G; v += NT) {
         const int col = v / G, g = v - col * G;
         float acc[8];
 #pragma unroll
@@ -172,7 +172,7 @@ __global__ __launch_bounds__(LTPB) void sep_lds_kernel(const void* __restrict__ 
         d[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
     }
     __syncthreads();
-    for (int v = threadIdx.x; v < Wout * G; v += LTPB) {
+    for (int v = threadIdx.x; v < Wout * G; v += NT) {
         const int ox = v / G, g = v - ox * G;
         float wxv[TM];
         int ix[TM];
@@ -204,10 +204,25 @@ __global__ __launch_bounds__(LTPB) void sep_lds_kernel(const void* __restrict__ 
     }
 }
 
-// XCD-aware row order for sep_lds_kernel (A/B knob IRGAN_SEP_SWZ=0/1)
+// Threads per block of sep_lds_kernel and the LDS row cap (floats) that sizes its channel
+// group: 512 threads with CB <= 8192 / Win (A/B knob IRGAN_SEP_NT=1024: CB <= 16384 / Win,
+// 256: a quarter).  Half-size groups double the blocks and let two resident blocks per CU
+// overlap one's load with the other's taps: the six resample launches of a step sum
+// 659 -> 576 us standalone and the step goes 1191 -> 1204 img/s (same box, 3 reps each).
+int sep_nt() {
+    static int v = -1;
+    if (v < 0) v = getenv("IRGAN_SEP_NT") ? atoi(getenv("IRGAN_SEP_NT")) : 512;
+    if (v != 256 && v != 1024) v = 512;
+    return v;
+}
+
+// XCD-aware row order for sep_lds_kernel, on by default (A/B knob IRGAN_SEP_SWZ=0): each
+// XCD takes a contiguous range of output rows, so the input rows their vertical taps share
+// stay in that XCD's L2
+
 int sep_swz() {
     static int v = -1;
-    if (v < 0) v = getenv("IRGAN_SEP_SWZ") ? atoi(getenv("IRGAN_SEP_SWZ")) : 0;
+    if (v < 0) v = getenv("IRGAN_SEP_SWZ") ? atoi(getenv("IRGAN_SEP_SWZ")) : 1;
     return v;
 }
 
@@ -519,21 +534,26 @@ extern "C" int irgan_sep_resample(const void* in, int32_t in_dtype, int32_t N, i
     static const bool use_lds = !getenv("IRGAN_NO_SEP_LDS");
     const int TM = Ty > Tx ? Ty : Tx;
     if (vec && use_lds && TM <= 8) {
-        // channel group: the widest of 128..8 dividing C whose fp32 row [Win][CB] fits 64 KiB
+        // channel group: the widest of 128..8 dividing C whose fp32 row [Win][CB] fits the cap
+        const int nt = sep_nt();
         int CB = 0;
         for (int cb = 128; cb >= 8 && !CB; cb >>= 1)
-            if (C % cb == 0 && (long)Win * cb <= 16384) CB = cb;
+            if (C % cb == 0 && (long)Win * cb <= 16384 * nt / 1024) CB = cb;
         if (CB) {
             dim3 g(N * Hout, C / CB);
             const size_t sh = (size_t)Win * CB * 4;
             hipStream_t st = (hipStream_t)s;
-#define SEPL(T)                                                                                                      \
-    sep_lds_kernel<T><<<g, LTPB, sh, st>>>(in, in_dtype, Hin, Win, ldi, offi, out, out_dtype, Hout, Wout, ldo, offo, \
-                                           ty, wy, Ty, tx, wx, Tx, accumulate, CB, nullptr, 0, 0, sep_swz())
-            if (TM <= 2) SEPL(2);
-            else if (TM <= 4) SEPL(4);
-            else if (TM <= 6) SEPL(6);
-            else SEPL(8);
+#define SEPL(T, NTV)                                                                                                 \
+    sep_lds_kernel<T, false, NTV><<<g, NTV, sh, st>>>(in, in_dtype, Hin, Win, ldi, offi, out, out_dtype, Hout, Wout,   \
+                                                      ldo, offo, ty, wy, Ty, tx, wx, Tx, accumulate, CB, nullptr, 0,   \
+                                                      0, sep_swz())
+#define SEPT(NTV)                          \
+    if (TM <= 2) SEPL(2, NTV);             \
+    else if (TM <= 4) SEPL(4, NTV);        \
+    else if (TM <= 6) SEPL(6, NTV);        \
+    else SEPL(8, NTV);
+            if (nt == 256) { SEPT(256) } else if (nt == 512) { SEPT(512) } else { SEPT(1024) }
+#undef SEPT
 #undef SEPL
             IRGAN_LAUNCH_CHECK();
             return 0;
@@ -565,20 +585,24 @@ extern "C" int irgan_sep_resample_in(const void* in, int32_t in_dtype, int32_t N
     if (Ty < 1 || Tx < 1) return IRGAN_EINVAL;
     const int TM = Ty > Tx ? Ty : Tx;
     if (!vec || TM > 8 || getenv("IRGAN_NO_SEP_LDS") || getenv("IRGAN_NO_IN_RESAMPLE")) return IRGAN_EUNSUPPORTED;
+    const int nt = sep_nt();
     int CB = 0;
     for (int cb = 128; cb >= 8 && !CB; cb >>= 1)
-        if (C % cb == 0 && (long)Win * cb <= 16384) CB = cb;
+        if (C % cb == 0 && (long)Win * cb <= 16384 * nt / 1024) CB = cb;
     if (!CB) return IRGAN_EUNSUPPORTED;
     dim3 g(N * Hout, C / CB);
     const size_t sh = (size_t)Win * CB * 4;
     hipStream_t st = (hipStream_t)s;
-#define SEPN(T)                                                                                                   \
-    sep_lds_kernel<T, true><<<g, LTPB, sh, st>>>(in, in_dtype, Hin, Win, ldi, offi, out, out_dtype, Hout, Wout, ldo, \
-                                                 offo, ty, wy, Ty, tx, wx, Tx, 0, CB, mr, C, act, sep_swz())
-    if (TM <= 2) SEPN(2);
-    else if (TM <= 4) SEPN(4);
-    else if (TM <= 6) SEPN(6);
-    else SEPN(8);
+#define SEPN(T, NTV)                                                                                               \
+    sep_lds_kernel<T, true, NTV><<<g, NTV, sh, st>>>(in, in_dtype, Hin, Win, ldi, offi, out, out_dtype, Hout, Wout, \
+                                                     ldo, offo, ty, wy, Ty, tx, wx, Tx, 0, CB, mr, C, act, sep_swz())
+#define SEPT(NTV)                          \
+    if (TM <= 2) SEPN(2, NTV);             \
+    else if (TM <= 4) SEPN(4, NTV);        \
+    else if (TM <= 6) SEPN(6, NTV);        \
+    else SEPN(8, NTV);
+    if (nt == 256) { SEPT(256) } else if (nt == 512) { SEPT(512) } else { SEPT(1024) }
+#undef SEPT
 #undef SEPN
     IRGAN_LAUNCH_CHECK();
     return 0;
