@@ -272,6 +272,16 @@ int irgan_reflect_dgrad_ring(const irgan_conv_desc* d, const void* dy, const voi
  * backward: engine.GeneratorEngine.backward). */
 int irgan_reflect_dgrad_ring_ws(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p, void* dx,
                                 float* ws, int64_t ws_floats, int32_t max_blocks, irgan_stream_t s);
+/* Reflect-padded ResnetBlock backward-data (ir:386-411; replaces torch autograd's
+ * ReflectionPad2d + Conv2d backward) in two launches: the ring's line GEMM into ws (as
+ * irgan_reflect_dgrad_ring_ws), then the interior conv whose store pass adds the ring terms
+ * onto dx's border band -- the same dx, bit for bit, as irgan_conv_fwd (interior) followed by
+ * irgan_reflect_dgrad_ring_ws, one launch and one dx read-modify-write fewer.  d: the interior
+ * descriptor (ops.conv_dgrad).  IRGAN_EUNSUPPORTED (nothing launched) unless the line-ring
+ * shapes hold (irgan_reflect_dgrad_ring_ws), dx is bf16 without activation, and dx channels
+ * % 256 == 0 take the 256-channel conv tile. */
+int irgan_conv_dgrad_reflect_line(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p, void* dx,
+                                  float* ws, int64_t ws_floats, irgan_stream_t s);
 /* Backward-data of a 4x4 stride-2 pad-1 conv (PatchGAN model.0 / .3 / .6, ir:600-612) in
  * ONE launch for all four output phases: d = the four per-phase descriptors (2x2 taps on
  * dy, omy = omx = 2, (ooy, oox) the phase, c0y / c0x in {-1, 0}; otherwise identical), w =

@@ -75,6 +75,9 @@ IRGAN_HD i32x4 make_rsrc(const void* base, uint32_t bytes) {
     return r;
 }
 constexpr uint32_t IRGAN_OOB = 0x80000000u;  // byte offset that is out of range (num_records < 2^31)
+// positions per border line of the line-form reflect ring workspace (conv_ring.hip: dy
+// coordinates -2 .. 65 of a <= 64-long line), shared with conv_pp_kernel.h's epilogue fold
+constexpr int IRGAN_RING_ROWS = 68;
 // buffer_load_dwordx4 ... lds: 16 bytes per lane from rsrc.base + voff into
 // lds + 16*lane (same M0 contract as glds16); no 64-bit address math per lane.
 IRGAN_HD void blds16(i32x4 rsrc, uint32_t voff, const void* lds) {

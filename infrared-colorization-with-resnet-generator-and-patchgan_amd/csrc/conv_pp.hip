@@ -112,6 +112,40 @@ extern "C" int irgan_conv_fwd_pp(const irgan_conv_desc* d, const void* x, const 
     return 0;
 }
 
+// conv_ring.hip: the line-form reflect ring's shape check and its GEMM launch
+bool ring_line_check(const irgan_conv_desc* d, int p, long ws_floats);
+void ring_line_gemm_launch(const irgan_conv_desc* d, const void* dy, const void* w, float* ws, hipStream_t st);
+
+// Reflect-padded ResnetBlock backward-data (ir:386-411) as the ring's line GEMM into ws, then
+// the interior conv_pp launch whose store pass adds the ring terms onto dx's rows 1 / H-2 and
+// columns 1 / W-2 (ring_line_add): the fold launch of irgan_reflect_dgrad_ring_ws and its
+// read-modify-write of dx's border band are gone, dx is bit-identical.
+extern "C" int irgan_conv_dgrad_reflect_line(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p,
+                                             void* dx, float* ws, int64_t ws_floats, irgan_stream_t s) {
+    if (!d || !dy || !w || !dx || !ws) return IRGAN_EINVAL;
+    if ((long)d->N * d->Ho * d->Wo <= 0 || d->Cout <= 0) return 0;
+    static const bool off = getenv("IRGAN_NO_RING_EPI") != nullptr;
+    if (off || !ring_line_check(d, p, ws_floats) || d->out_dtype != IRGAN_BF16 || d->act != IRGAN_ACT_NONE ||
+        d->sy != 1 || d->sx != 1 || d->Cin % 64 || d->Cout % 256 || narrow_bn(d) != 256 || irgan_res64::ok(d) ||
+        (long)d->N * d->H * d->W * d->ldx >= (1L << 30) || (long)d->Cout * 9 * d->Cin >= (1L << 30))
+        return IRGAN_EUNSUPPORTED;
+    hipStream_t st = (hipStream_t)s;
+    ring_line_gemm_launch(d, dy, w, ws, st);
+    static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
+    const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH), ntn = d->Cout / 256;
+    const int nb = d->N * tpy * tpx * ntn;
+    if (d->accumulate)
+        conv_pp_kernel<3, 3, 256, true><<<nb, 512, 0, st>>>(*d, (const bf16_t*)dy, (const bf16_t*)w, nullptr, dx,
+                                                            nullptr, ntn, tpx, tpy, swz, nullptr, nullptr, nullptr,
+                                                            InBwdStats{}, ws);
+    else
+        conv_pp_kernel<3, 3, 256, false><<<nb, 512, 0, st>>>(*d, (const bf16_t*)dy, (const bf16_t*)w, nullptr, dx,
+                                                             nullptr, ntn, tpx, tpy, swz, nullptr, nullptr, nullptr,
+                                                             InBwdStats{}, ws);
+    IRGAN_LAUNCH_CHECK();
+    return 0;
+}
+
 // Forward conv with the InstanceNorm statistics of its output fused into the
 // epilogue (replaces the separate irgan_in_stats pass over y; ir:154-165, 392, 417).
 // part: float2[N * nb * Cout] partials, nb (out) = 16x16 patches per image; reduce

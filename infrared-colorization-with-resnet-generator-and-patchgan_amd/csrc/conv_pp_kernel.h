@@ -127,6 +127,40 @@ IRGAN_HD float in_act_grad(float xh, int act) {  // as norm.hip's act_grad
     return 1.f;
 }
 
+// rg (irgan_conv_dgrad_reflect_line): the line-form reflect ring of a ResnetBlock backward-data
+// (conv_ring.hip: g[n][line][pos][c], lines top / bottom / left / right) folded onto the stored
+// bf16 dx in the store pass -- ring_line_fold_kernel's terms, order and roundings, so dx is
+// bit-identical to the interior launch + fold launch
+IRGAN_HD void ring_line_add(const irgan_conv_desc& d, const float* __restrict__ g, int n, int y, int x, int c,
+                            uint4& o) {
+    const int H = d.Ho, W = d.Wo;
+    const bool row = y == 1 || y == H - 2;
+    if (!row && x != 1 && x != W - 2) return;
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = 0.f;
+    auto add = [&](int line, int pos) {
+        const float4* q = (const float4*)(g + (((long)n * 4 + line) * IRGAN_RING_ROWS + pos) * d.Cout + c);
+        const float4 a = q[0], b = q[1];
+        v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+        v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+    };
+    if (row) {
+        const int line = y == 1 ? 0 : 1;
+        add(line, x + 1);
+        if (x == 1) { add(line, 0); add(2, y + 1); }
+        if (x == W - 2) { add(line, W + 1); add(3, y + 1); }
+    } else {
+        add(x == 1 ? 2 : 3, y + 1);
+    }
+    const uint32_t wd[4] = {o.x, o.y, o.z, o.w};
+    uint32_t o4[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        o4[k] = pk_bf16(__uint_as_float(wd[k] << 16) + v[2 * k], __uint_as_float(wd[k] & 0xffff0000u) + v[2 * k + 1]);
+    o = make_uint4(o4[0], o4[1], o4[2], o4[3]);
+}
+
 // ONE: a single halo buffer, so at BN = 64 the block fits twice per CU (LDS 62 KiB,
 // <= 128 VGPRs) and one block's halo loads / epilogue overlap the other's MFMA loop
 // (BN = 128 would need 159 VGPRs: at 128 it spills 30 and runs slower than two BN-64
@@ -161,7 +195,8 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
                                                          float2* __restrict__ part = nullptr,
                                                          const float* __restrict__ dqx = nullptr,
                                                          const float* __restrict__ dqw = nullptr,
-                                                         const InBwdStats ib = InBwdStats{}) {
+                                                         const InBwdStats ib = InBwdStats{},
+                                                         const float* __restrict__ rg = nullptr) {
     constexpr int ESZ = F8 ? 1 : 2, CHN = 128 / ESZ;  // operand bytes, channels per 128-byte chunk
     const char* const xb = (const char*)x;
     const char* const wb = (const char*)w;
@@ -689,7 +724,9 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
         bf16_t* yp = (bf16_t*)y + pix * d.ldy + d.yoff + co8;
         const char* sp = smem + m * RSB + c8 * 2;
         if (vec) {
-            *(uint4*)yp = *(const uint4*)sp;
+            uint4 o = *(const uint4*)sp;
+            if (rg) ring_line_add(d, rg, img, py0 + (m >> 4), px0 + (m & 15), co8, o);  // block-uniform test
+            *(uint4*)yp = o;
         } else {
             for (int q = 0; q < 8 && co8 + q < d.Cout; ++q) yp[q] = ((const bf16_t*)sp)[q];
         }

@@ -362,6 +362,7 @@ __global__ __launch_bounds__(NWV * 64) void reflect_ring_kernel(const irgan_conv
 //    their line's u plus, at columns 1 / W-2, the corner end and the column line's value.
 constexpr int RV_L = 64;            // longest line (H, W)
 constexpr int RV_ROWS = RV_L + 4;   // positions per line: dy coordinates -2 .. L+1 (g: u + 1 in [0, 68))
+static_assert(RV_ROWS == IRGAN_RING_ROWS, "workspace layout shared with conv_pp_kernel.h");
 constexpr int RV_CIN = 256;         // dy channels (LDS row = 512 B)
 
 IRGAN_HD int rv_off(int row, int chunk) { return row * 512 + ((chunk ^ (row & 15)) << 4); }
@@ -538,6 +539,12 @@ static bool ring_line_ok(const irgan_conv_desc* d, int p, long ws_floats) {
            d->Ho == d->H && d->Wo == d->W && d->Ho == d->OH && d->Wo == d->OW && d->omy == 1 && d->omx == 1 &&
            d->ooy == 0 && d->oox == 0 && (d->out_dtype == IRGAN_BF16 || d->out_dtype == IRGAN_F32) &&
            ws_floats >= ring_line_ws(d);
+}
+// conv_pp.hip's irgan_conv_dgrad_reflect_line: the check, then the line GEMM alone (one
+// image per workgroup row); the fold runs in the interior launch's store pass
+bool ring_line_check(const irgan_conv_desc* d, int p, long ws_floats) { return ring_line_ok(d, p, ws_floats); }
+void ring_line_gemm_launch(const irgan_conv_desc* d, const void* dy, const void* w, float* ws, hipStream_t st) {
+    ring_line_gemm_kernel<<<dim3(4 * (d->Cout / 64), d->N), 256, 0, st>>>(*d, (const bf16_t*)dy, (const bf16_t*)w, ws, 1);
 }
 // conv_pp.hip's irgan_conv_dgrad_in_stats: the ring partial rows per image, and the
 // ring launch that writes them (bf16 output, Cout % 64 == 0, 8-aligned slices: checked there)

@@ -85,6 +85,17 @@ def set_ring_line(on: bool) -> bool:
     return old
 
 
+RING_EPI = [True]
+
+
+def set_ring_epi(on: bool) -> bool:
+    """The ResnetBlock ring folded into the interior launch's store pass
+    (irgan_conv_dgrad_reflect_line, default) or the separate fold launch after it -- the
+    same dx bit for bit (tests/test_gpu_ring_epi.py).  Returns the previous setting."""
+    old, RING_EPI[0] = RING_EPI[0], bool(on)
+    return old
+
+
 def _ring(d, dy: "Feat", buf, p, dx: "Feat", max_blocks=1 << 20):
     """The reflect-pad ring of a bf16 backward-data onto dx (after its interior): the line
     GEMM + fold on ResnetBlock shapes, else the general ring launch (the library decides)."""
@@ -378,6 +389,15 @@ def conv_dgrad(pc: PackedConv, dy: Feat, dx: Feat, accumulate=False, mask: Feat 
                 # launches (irgan_conv_dgrad_reflect decides)
                 _lib.call("irgan_conv_dgrad_reflect", ctypes.byref(d), dy.ptr, P(buf), p, dx.ptr, stream())
                 return
+            if ring_mfma and not side and RING_LINE[0] and RING_EPI[0] and dx.dt == BF16:
+                # line GEMM, then the interior with the ring folded into its store pass
+                ws = _ring_ws(dx.t.device, dx.N * 4 * 68 * dx.C)
+                rc = _lib.load().irgan_conv_dgrad_reflect_line(ctypes.byref(d), dy.ptr, P(buf), p, dx.ptr, P(ws),
+                                                              ws.numel(), stream())
+                if rc == 0:
+                    return
+                if rc != IRGAN_EUNSUPPORTED:
+                    raise _lib.IrganError(f"irgan_conv_dgrad_reflect_line failed with code {rc}")
             _lib.call("irgan_conv_fwd", ctypes.byref(d), dy.ptr, P(buf), None, dx.ptr, None, stream())
             if ring_mfma and not side:
                 _ring(d, dy, buf, p, dx)

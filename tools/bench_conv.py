@@ -15,6 +15,8 @@ CASES = [  # name, cin, cout, k, s, p, mode, H
     ("vgg12_64-64@256", 64, 64, 3, 1, 1, 0, 256),
     ("vgg21_64-128@128", 64, 128, 3, 1, 1, 0, 128),
     ("vgg22_128-128@128", 128, 128, 3, 1, 1, 0, 128),
+    ("vgg31_128-256@64", 128, 256, 3, 1, 1, 0, 64),
+    ("vgg33_256-256@64", 256, 256, 3, 1, 1, 0, 64),
     ("D2_128-256s2@64", 128, 256, 4, 2, 1, 0, 64),
     ("D3_256-512s1@32", 256, 512, 4, 1, 1, 0, 32),
 ]
@@ -49,6 +51,7 @@ for name, cin, cout, k, s, p, mode, H in CASES:
     flop = 2.0 * B * Ho * Wo * cout * cin * k * k
     part = torch.empty(B * 256 * cout * 2, device=DEV)
     fns = {"fwd": lambda: ops.conv_fwd(pc, ops.Feat(x), ops.Feat(y)),
+           "fwdr": lambda: ops.conv_fwd(pc, ops.Feat(x), ops.Feat(y), act=ops.ACT_RELU),
            "fwds": lambda: ops.conv_fwd_stats(pc, ops.Feat(x), ops.Feat(y), part),
            "dgrad": lambda: ops.conv_dgrad(pc, ops.Feat(dy), ops.Feat(dx), pad_buf=pad),
            "wgrad": lambda: ops.conv_wgrad(spec, ops.Feat(x), ops.Feat(dy), dw, ops.BF16)}
