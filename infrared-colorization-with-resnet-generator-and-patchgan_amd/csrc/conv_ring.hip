@@ -353,10 +353,10 @@ __global__ __launch_bounds__(NWV * 64) void reflect_ring_kernel(const irgan_conv
 //   right  g(y, W)  = sum_ty Wd[ty][0] dy(y + ty - 1, W-1),  y in [0, H)   -> dx(y, W-2)
 // (the corners are the u = -1 / W ends of the top / bottom lines).  Two launches:
 //  * ring_line_gemm_kernel: workgroup = (line, 64 output channels, a group of images).  The
-//    line's 3 taps x Cin x 64 weights stay in LDS (96 KiB, loaded once), the image's dy line
-//    (<= 68 positions x Cin) beside them; per image a [64 co] x [80 positions] x [3 Cin]
-//    GEMM entirely from LDS (wave = 16 channels, 5 position fragments), the next image's
-//    line prefetched into registers meanwhile; g (fp32) -> the caller's workspace.
+//    line's 3 taps x Cin x 64 weights are loaded once as MFMA fragments into registers (wave =
+//    16 channels), the image's dy line (<= 68 positions x Cin) into LDS; per image a [64 co] x
+//    [80 positions] x [3 Cin] GEMM (5 position fragments per wave), the next image's line
+//    prefetched into registers meanwhile; g (fp32) -> the caller's workspace.
 //  * ring_line_fold_kernel: one thread per (owned dx pixel, 8 channels) adds the sum of its
 //    ring terms in a fixed order (one read-modify-write, deterministic): rows 1 / H-2 take
 //    their line's u plus, at columns 1 / W-2, the corner end and the column line's value.
@@ -370,12 +370,16 @@ IRGAN_HD int rv_tap(int line, int k) {  // dgrad-conv tap ty*3 + tx of along-lin
     return line == 0 ? 6 + k : (line == 1 ? k : (line == 2 ? 3 * k + 2 : 3 * k));
 }
 
+// WREG: weight fragments straight into registers (default); else staged through LDS
+// (A/B knob IRGAN_RING_WLDS=1: 3 x 64 rows of Cin, 96 KiB, one barrier)
+template <bool WREG>
 __global__ __launch_bounds__(256, 1) void ring_line_gemm_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ dy,
                                                                 const bf16_t* __restrict__ w, float* __restrict__ gbuf,
                                                                 int ipb) {
-    __shared__ __attribute__((aligned(16))) char smem[3 * 64 * 512 + RV_ROWS * 512];
-    char* const sW = smem;                 // [3 taps][64 co] rows of Cin bf16
-    char* const sL = smem + 3 * 64 * 512;  // [RV_ROWS positions] rows of Cin bf16
+    constexpr int WB = WREG ? 0 : 3 * 64 * 512;
+    __shared__ __attribute__((aligned(16))) char smem[WB + RV_ROWS * 512];
+    char* const sW = smem;       // !WREG: [3 taps][64 co] rows of Cin bf16
+    char* const sL = smem + WB;  // [RV_ROWS positions] rows of Cin bf16
     RTS(0);
     const int nct = d.Cout / 64;
     const int line = blockIdx.x / nct, ct = blockIdx.x - line * nct;
@@ -386,9 +390,20 @@ __global__ __launch_bounds__(256, 1) void ring_line_gemm_kernel(const irgan_conv
     const int g = lane >> 4, l16 = lane & 15;
     const int Kw = (9 * d.Cin + 63) / 64 * 64;
     const int c32 = d.Cin / 8;  // 16-byte chunks per row
+    const int ncs = d.Cin / 32;
 
-    // weights: row (k * 64 + co), chunk c  <-  w[ct*64 + co][rv_tap(line, k) * Cin + 8c]
-    {
+    // this wave's weight fragments straight into registers (16 channels x 32 dy channels per
+    // (tap k, channel step cs)): w[ct*64 + wv*16 + l16][rv_tap(line, k) * Cin + 32 cs + 8 g ..],
+    // all 24 loads in flight at once -- no LDS staging, no barrier before the first MFMA
+    uint4 af[3][WREG ? RV_CIN / 32 : 1];
+    if constexpr (WREG) {
+        const bf16_t* wr = w + (long)(ct * 64 + wv * 16 + l16) * Kw + g * 8;
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+#pragma unroll
+            for (int cs = 0; cs < RV_CIN / 32; ++cs)
+                af[k][cs] = cs < ncs ? *(const uint4*)(wr + rv_tap(line, k) * d.Cin + cs * 32) : make_uint4(0u, 0u, 0u, 0u);
+    } else {  // row (k * 64 + co), chunk c  <-  w[ct*64 + co][rv_tap(line, k) * Cin + 8c]
         constexpr int PER = 3 * 64 * 32 / 256;
         uint4 v[PER];
 #pragma unroll
@@ -420,7 +435,6 @@ __global__ __launch_bounds__(256, 1) void ring_line_gemm_kernel(const irgan_conv
     uint4 lv[LPER];
     if (n0 < n1) load_line(n0, lv);
     const int ub = line < 2 ? -1 : 0;  // position of fragment 0, lane 0
-    const int ncs = d.Cin / 32;
     const int co = ct * 64 + wv * 16 + 4 * g;  // this lane's 4 output channels (C^T rows)
 #pragma unroll 1
     for (int n = n0; n < n1; ++n) {
@@ -441,7 +455,9 @@ __global__ __launch_bounds__(256, 1) void ring_line_gemm_kernel(const irgan_conv
 #pragma unroll
             for (int cs = 0; cs < RV_CIN / 32; ++cs) {
                 if (cs >= ncs) break;
-                const uint4 a = *(const uint4*)(sW + rv_off(k * 64 + wv * 16 + l16, cs * 4 + g));
+                uint4 a;
+                if constexpr (WREG) a = af[k][cs];
+                else a = *(const uint4*)(sW + rv_off(k * 64 + wv * 16 + l16, cs * 4 + g));
                 uint4 b[5];
 #pragma unroll
                 for (int f = 0; f < 5; ++f)
@@ -544,7 +560,15 @@ static bool ring_line_ok(const irgan_conv_desc* d, int p, long ws_floats) {
 // image per workgroup row); the fold runs in the interior launch's store pass
 bool ring_line_check(const irgan_conv_desc* d, int p, long ws_floats) { return ring_line_ok(d, p, ws_floats); }
 void ring_line_gemm_launch(const irgan_conv_desc* d, const void* dy, const void* w, float* ws, hipStream_t st) {
-    ring_line_gemm_kernel<<<dim3(4 * (d->Cout / 64), d->N), 256, 0, st>>>(*d, (const bf16_t*)dy, (const bf16_t*)w, ws, 1);
+    static const int ipb = getenv("IRGAN_RING_IPB") ? std::max(1, atoi(getenv("IRGAN_RING_IPB"))) : 1;
+    const int groups = irgan_cdiv(d->N, ipb);
+    static const bool wlds = getenv("IRGAN_RING_WLDS") != nullptr;
+    if (wlds)
+        ring_line_gemm_kernel<false><<<dim3(4 * (d->Cout / 64), groups), 256, 0, st>>>(*d, (const bf16_t*)dy,
+                                                                                      (const bf16_t*)w, ws, ipb);
+    else
+        ring_line_gemm_kernel<true><<<dim3(4 * (d->Cout / 64), groups), 256, 0, st>>>(*d, (const bf16_t*)dy,
+                                                                                     (const bf16_t*)w, ws, ipb);
 }
 // conv_pp.hip's irgan_conv_dgrad_in_stats: the ring partial rows per image, and the
 // ring launch that writes them (bf16 output, Cout % 64 == 0, 8-aligned slices: checked there)
@@ -603,7 +627,7 @@ extern "C" int irgan_reflect_dgrad_ring_ws(const irgan_conv_desc* d, const void*
     if (groups > d->N) groups = d->N;
     const int ipb = irgan_cdiv(d->N, groups);
     groups = irgan_cdiv(d->N, ipb);
-    ring_line_gemm_kernel<<<dim3(tiles, groups), 256, 0, st>>>(*d, (const bf16_t*)dy, (const bf16_t*)w, ws, ipb);
+    ring_line_gemm_kernel<true><<<dim3(tiles, groups), 256, 0, st>>>(*d, (const bf16_t*)dy, (const bf16_t*)w, ws, ipb);
     const long threads = (long)d->N * (2 * d->Wo + 2 * (d->Ho - 2)) * (d->Cout / 8);
     ring_line_fold_kernel<<<(unsigned)irgan_cdiv(threads, 256), 256, 0, st>>>(*d, ws, dx);
     IRGAN_LAUNCH_CHECK();
