@@ -45,7 +45,9 @@ constexpr int R64_HB = R64_HP * 1024;
 constexpr int R64_WB = 9 * 64 * 128;
 constexpr int R64_LDS = R64_WB + 2 * R64_HB + 8 * 64 * 8;
 
-template <bool ACC, bool STATS>
+// ONEB (no STATS): one barrier per patch -- the next-but-one halo is issued at the top of the
+// following iteration instead of after a second, post-K-loop barrier
+template <bool ACC, bool STATS, bool ONEB = false>
 __global__ __launch_bounds__(512, 1) void conv_res64_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
                                                            const bf16_t* __restrict__ w,
                                                            const float* __restrict__ bias, bf16_t* __restrict__ y,
@@ -53,6 +55,7 @@ __global__ __launch_bounds__(512, 1) void conv_res64_kernel(const irgan_conv_des
                                                            int tpy, float2* __restrict__ part, int xcdg) {
     constexpr int TAPS = 9, HWd = PW + 2, HROWS = (PH + 2) * HWd, MI = 2, NJ = 4, Kw = TAPS * 64;
     static_assert(HROWS <= R64_HP * 8 && R64_HP * 8 - HROWS < 8, "halo pieces");
+    static_assert(!(ONEB && STATS), "the stats rows need the post-loop barrier");
     __shared__ __attribute__((aligned(1024))) char smem[R64_LDS];
     char* const sW = smem;
     char* const sH = smem + R64_WB;
@@ -143,12 +146,18 @@ __global__ __launch_bounds__(512, 1) void conv_res64_kernel(const irgan_conv_des
         // VMEM ops issued after this patch's halo, in issue order: (it >= 2) the stats
         // store of patch it-2 (made at the top of it-1), the stores of patch it-1, the halo
         // of patch it+1 (it == 0: only that halo)
+        // (ONEB: halo it+1 was issued at the top of iteration it-1, so only patch it-1's stores
+        // are younger from it == 1 on)
         {
             const int nxt = p + qs < P ? nh : 0;
-            const int younger = it == 0 ? nxt : (it == 1 ? NST + nxt : (STATS ? 1 : 0) + NST + nxt);
+            const int younger = it == 0 ? nxt
+                                        : (ONEB ? NST : (it == 1 ? NST + nxt : (STATS ? 1 : 0) + NST + nxt));
             wait_vm_dyn(__builtin_amdgcn_readfirstlane(younger));
         }
         lds_barrier();  // every wave's pieces of this patch's halo (and the weights) landed
+        // ONEB: every wave has also finished patch it-1 (K loop and stores), so its halo buffer
+        // takes patch it+1's halo now
+        if (ONEB && it > 0 && p + qs < P) issue_halo(p + qs, buf ^ 1);
         if constexpr (STATS) {
             // patch it-1's partials: its 8 wave rows are complete (written before this barrier)
             if (it > 0 && lane < 8) {
@@ -192,7 +201,9 @@ __global__ __launch_bounds__(512, 1) void conv_res64_kernel(const irgan_conv_des
                                                                             acc[i][j], 0, 0, 0);
             }
         }
-        lds_barrier();  // every wave is done with this halo buffer; the stats rows were read
+        // every wave is done with this halo buffer; the stats rows were read.  ONEB: no barrier
+        // here -- a wave that finishes its MFMAs stores while the others still multiply
+        if (!ONEB) lds_barrier();
 
         // ---- epilogue from the accumulators
         const int pxi = p % tpx, pyi = (p / tpx) % tpy, img = p / (tpx * tpy);
@@ -272,7 +283,7 @@ __global__ __launch_bounds__(512, 1) void conv_res64_kernel(const irgan_conv_des
             const int k = lane & 15;
             sR[wid * 64 + (k >> 2) * 16 + cl0 + (k & 3)] = make_float2(st[0], st[1]);
         }
-        if (p + 2 * qs < P) issue_halo(p + 2 * qs, buf);
+        if (!ONEB && p + 2 * qs < P) issue_halo(p + 2 * qs, buf);
     }
     if constexpr (STATS) {
         lds_barrier();  // the last patch's stats rows
@@ -322,12 +333,13 @@ void launch(const irgan_conv_desc* d, const void* x, const void* w, const float*
     const int grid = grid_for(ntn, d->N * tpx * tpy * ntn);
     static const int xg = getenv("IRGAN_RES64_NO_XCDG") ? 0 : 1;
     const int xcdg = xg && ntn > 1 && grid % (8 * ntn) == 0;
-#define R64(ACCV, STV)                                                                                    \
-    conv_res64_kernel<ACCV, STV><<<grid, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, (bf16_t*)y, \
-                                                       (const bf16_t*)mask, ntn, tpx, tpy, part, xcdg)
-    if (part) R64(false, true);
-    else if (d->accumulate) R64(true, false);
-    else R64(false, false);
+    static const bool oneb = !getenv("IRGAN_RES64_TWOB");
+#define R64(ACCV, STV, OB)                                                                                          \
+    conv_res64_kernel<ACCV, STV, OB><<<grid, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias,             \
+                                                           (bf16_t*)y, (const bf16_t*)mask, ntn, tpx, tpy, part, xcdg)
+    if (part) R64(false, true, false);
+    else if (d->accumulate) { if (oneb) R64(true, false, true); else R64(true, false, false); }
+    else { if (oneb) R64(false, false, true); else R64(false, false, false); }
 #undef R64
 }
 
