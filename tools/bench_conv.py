@@ -10,6 +10,7 @@ B = 16
 CASES = [  # name, cin, cout, k, s, p, mode, H
     ("res3x3_256@64", 256, 256, 3, 1, 1, 1, 64),
     ("down1_64-128@256", 64, 128, 3, 1, 1, 0, 256),
+    ("down2_128-256@128", 128, 256, 3, 1, 1, 0, 128),
     ("up2_192-64@256", 192, 64, 3, 1, 1, 0, 256),
     ("up1_384-128@128", 384, 128, 3, 1, 1, 0, 128),
     ("vgg12_64-64@256", 64, 64, 3, 1, 1, 0, 256),
