@@ -1149,6 +1149,10 @@ class BucketedAllreduce:
 
 # IRGAN_JOIN_TIMING=1: (event, event) pairs around the main stream's wait for the side
 # stream's D step (tools: how much of the step is the D step on the critical path)
+# host enqueue order of the two streams' work after the G forward: the main stream's G-step
+# terms first, then the side stream's D step (1204 vs 1199 img/s, 3 same-box pairs,
+# profiles/r03_terms_first_ab.txt); IRGAN_D_FIRST=1 restores the D step first
+TERMS_FIRST = not os.environ.get("IRGAN_D_FIRST")
 JOIN_TIMES = [] if os.environ.get("IRGAN_JOIN_TIMING") else None
 
 
@@ -1306,9 +1310,40 @@ class GANStep:
         # ---- D step on [real; fake] as one 2B batch (ir:1636-1651), on the side stream
         dpad = max(8, cin + cout)   # D input zero-padded to 8 channels (narrow-input conv path)
         din = Feat(b.zeros("din2", (2 * B, H, W, dpad), T), 0, self.dis.packs[0].cin_eff)
+        dinf = Feat(b.zeros("din1", (B, H, W, dpad), T), 0, self.dis.packs[0].cin_eff)
+        dfake = b.get("dfake", (B, H, W, cout), torch.float32)
+
+        def g_terms():
+            # ---- G step terms that do not read D (ir:1656-1681)
+            self.G.zero_grad()
+            dfake.zero_()
+            ops.l1(fake, rgb_h, cfg.lambda_L1, dfake, L[2:3], accumulate=True)
+            # perceptual (ir:1667-1669): VGG on the fake half; the real half ran on the side stream
+            ops.affine(Feat(fake), self.vgg.scale, self.vgg.shift, vin.batch(0, B))
+            feat = self.vgg.forward(vin, part=(0, B))
+            if ev_vgg is not None:
+                main.wait_event(ev_vgg)
+            dfeat = b.get("dfeat", (B, feat.H, feat.W, feat.C), T)
+            ops.l1(feat.t[:B], feat.t[B:], cfg.lambda_perc, dfeat, L[3:4])
+            dv = self.vgg.backward_input(Feat(dfeat), B)
+            ops.affine(dv, self.vgg.scale, None, Feat(dfake), accumulate=True)
+            ops.tv(Feat(fake), cfg.lambda_tv, dfake, L[4:5])
+            ssim_work = b.flat("ssim_work", 10 * fake.numel())
+            ops.ssim(Feat(fake), Feat(rgb_h), cfg.lambda_ssim, dfake, L[5:6], ssim_work)
+
+        # host enqueue order (TERMS_FIRST): the main stream's G-step terms before the side
+        # stream's D step -- the dependencies are the event edges either way; enqueued first,
+        # the terms start right behind the G forward instead of after ~90 D-step launches
+        terms_first = main is not None and TERMS_FIRST
+        ev_fwd = None
         if main is not None:
-            self.side.wait_stream(main)           # G output, the zeroed losses
+            ev_fwd = torch.cuda.Event()
+            ev_fwd.record(main)                   # G output, the zeroed losses and D inputs
+        if terms_first:
+            g_terms()
         with side_ctx():
+            if ev_fwd is not None:
+                self.side.wait_event(ev_fwd)
             self.D.zero_grad()
             self._din(ir_t, rgb_h, din.batch(0, B))
             self._din(ir_t, fake if fake_d is None else fake_d, din.batch(B, B))
@@ -1322,29 +1357,13 @@ class GANStep:
             # that do not read D (L1, VGG, TV, SSIM)
             self.d_reduce.finish(self.D.adam_begin(cfg.lr_D * self.lr_scale, cfg.beta1, cfg.beta2))
             self.dis.pack()
-            dinf = Feat(b.zeros("din1", (B, H, W, dpad), T), 0, self.dis.packs[0].cin_eff)
             self._din(ir_t, fake, dinf)
             predg = self.dis.forward(dinf, tag="g")
             dpg = b.get("dpredg", tuple(predg.shape), torch.float32)
             ops.hinge(predg, predg.numel(), 1, cfg.lambda_gan, dpg, L[1:2])
             dd = self.dis.backward(dpg, want_wgrad=False, want_dinput=True, tag="g")
-        # ---- G step (ir:1656-1681)
-        self.G.zero_grad()
-        dfake = b.get("dfake", (B, H, W, cout), torch.float32)
-        dfake.zero_()
-        ops.l1(fake, rgb_h, cfg.lambda_L1, dfake, L[2:3], accumulate=True)
-        # perceptual (ir:1667-1669): VGG on the fake half; the real half ran on the side stream
-        ops.affine(Feat(fake), self.vgg.scale, self.vgg.shift, vin.batch(0, B))
-        feat = self.vgg.forward(vin, part=(0, B))
-        if ev_vgg is not None:
-            main.wait_event(ev_vgg)
-        dfeat = b.get("dfeat", (B, feat.H, feat.W, feat.C), T)
-        ops.l1(feat.t[:B], feat.t[B:], cfg.lambda_perc, dfeat, L[3:4])
-        dv = self.vgg.backward_input(Feat(dfeat), B)
-        ops.affine(dv, self.vgg.scale, None, Feat(dfake), accumulate=True)
-        ops.tv(Feat(fake), cfg.lambda_tv, dfake, L[4:5])
-        ssim_work = b.flat("ssim_work", 10 * fake.numel())
-        ops.ssim(Feat(fake), Feat(rgb_h), cfg.lambda_ssim, dfake, L[5:6], ssim_work)
+        if not terms_first:
+            g_terms()
         if main is not None:
             jt = JOIN_TIMES is not None and not torch.cuda.is_current_stream_capturing()
             if jt:   # diagnostics: how long the main stream waits here for the side stream's D step
