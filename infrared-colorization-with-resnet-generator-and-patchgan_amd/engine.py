@@ -1153,6 +1153,7 @@ class BucketedAllreduce:
 # terms first, then the side stream's D step (1204 vs 1199 img/s, 3 same-box pairs,
 # profiles/r03_terms_first_ab.txt); IRGAN_D_FIRST=1 restores the D step first
 TERMS_FIRST = not os.environ.get("IRGAN_D_FIRST")
+VGG_AFTER_GFWD = bool(os.environ.get("IRGAN_VGG_AFTER_GFWD"))
 JOIN_TIMES = [] if os.environ.get("IRGAN_JOIN_TIMING") else None
 
 
@@ -1291,15 +1292,27 @@ class GANStep:
         # concurrent with the G forward
         vin = Feat(b.zeros("vin", (2 * B, H, W, max(8, cout)), T), 0, self.vgg.packs[0].cin_eff)
         vgg_side = main is not None and not os.environ.get("IRGAN_NO_VGG_OVERLAP")
+        ev_in = None
         if vgg_side:
-            self.side.wait_stream(main)
-        with side_ctx() if vgg_side else _nullcontext():
-            ops.affine(Feat(rgb_h), self.vgg.scale, self.vgg.shift, vin.batch(B, B))
-            self.vgg.forward(vin, part=(B, B))
-        ev_vgg = None
-        if vgg_side:
-            ev_vgg = torch.cuda.Event()
-            ev_vgg.record(self.side)
+            ev_in = torch.cuda.Event()
+            ev_in.record(main)                    # the real images in NHWC, the zeroed VGG input
+
+        def vgg_real():
+            with side_ctx() if vgg_side else _nullcontext():
+                if ev_in is not None:
+                    self.side.wait_event(ev_in)
+                ops.affine(Feat(rgb_h), self.vgg.scale, self.vgg.shift, vin.batch(B, B))
+                self.vgg.forward(vin, part=(B, B))
+            if vgg_side:
+                ev = torch.cuda.Event()
+                ev.record(self.side)
+                return ev
+            return None
+
+        # host enqueue order (A/B knob IRGAN_VGG_AFTER_GFWD=1: the real half's VGG after the G
+        # forward's launches instead of before them)
+        vgg_late = vgg_side and VGG_AFTER_GFWD
+        ev_vgg = None if vgg_late else vgg_real()
         # ---- G forward once: ir:1638 and ir:1657 compute the same image -- unless G has
         # dropout, whose two calls draw two masks: then the D step gets its own forward
         # (ir:1638-1639, under no_grad: its activations are never read back)
@@ -1307,6 +1320,8 @@ class GANStep:
         fake_d = self.gen.forward(ir, bufs=self.dbufs) if self.gen.use_dropout else None
         fake = self.gen.forward(ir)
         ir_t = Feat(self.gen.bufs.d["ir"])
+        if vgg_late:
+            ev_vgg = vgg_real()
         # ---- D step on [real; fake] as one 2B batch (ir:1636-1651), on the side stream
         dpad = max(8, cin + cout)   # D input zero-padded to 8 channels (narrow-input conv path)
         din = Feat(b.zeros("din2", (2 * B, H, W, dpad), T), 0, self.dis.packs[0].cin_eff)
