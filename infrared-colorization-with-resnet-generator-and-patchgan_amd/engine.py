@@ -561,15 +561,19 @@ class GeneratorEngine:
         H2, W2 = (H1 - 1) // 2 + 1, (W1 - 1) // 2 + 1
         return H1, W1, H2, W2
 
-    def forward(self, ir_nchw: torch.Tensor, bufs: Buffers = None) -> torch.Tensor:
+    def forward(self, ir_nchw: torch.Tensor, bufs: Buffers = None, training: bool = None) -> torch.Tensor:
         """ir (B, input_nc, H, W) fp32 in [-1,1] -> fake NHWC fp32 (B, H, W, 3).
-        Activations land in ``bufs`` (default: the engine's own set)."""
+        Activations land in ``bufs`` (default: the engine's own set).  ``training``
+        (default: self.training) decides nn.Dropout's mode (ir:394-395): callers outside
+        the module forward / GANStep pass the module's train()/eval() state."""
         B, _, H, W = ir_nchw.shape
         g, T = bufs or self.bufs, self.tdt
+        train = self.training if training is None else bool(training)
         c0, c1, c2 = self.ngf, 2 * self.ngf, 4 * self.ngf
         H1, W1, H2, W2 = self._dims(H, W)
         g.state["shape"] = (B, H, W)
-        if self.use_dropout and self.training:   # a fresh mask per forward call; the backward reuses it
+        g.state.pop("dropout_seed", None)
+        if self.use_dropout and train:   # a fresh mask per forward call; the backward reuses it
             self.dropout_calls += 1
             g.state["dropout_seed"] = (self.dropout_seed << 32) ^ (self.dropout_calls << 8)
         ir_buf = g.zeros("ir", (B, H, W, max(8, self.input_nc)), T)   # narrow input zero-padded to 8 ch
@@ -629,7 +633,7 @@ class GeneratorEngine:
                     A.ensure(nxt, hn, x8)
             else:
                 t2 = t
-                if self.use_dropout and self.training:   # nn.Dropout(0.5) after the ReLU (ir:394-395)
+                if self.use_dropout and train:   # nn.Dropout(0.5) after the ReLU (ir:394-395)
                     t2 = Feat(g.get(f"td{b}", (B, H2, W2, c2), T))
                     ops.dropout(t, t2, g.state["dropout_seed"] + 2 * b)
                 self.norms[f"r{b}_2"].conv_fwd(g, f"r{b}_2", p2, self._res_in(g, f"xp2_{b}", t2), r2, hn, ACT_NONE,

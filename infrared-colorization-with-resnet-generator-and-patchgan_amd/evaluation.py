@@ -192,7 +192,7 @@ def run_test(cfg, model=None, log=print):
         B = ir8.shape[0]
         zero = torch.zeros(B, dtype=torch.uint8, device=device)
         ir_t, ir8r = resizer._one(ir8, 1, zero, True, keep_u8=True)   # load_ir_image + ir_to_tensor
-        fake = netG.engine.forward(ir_t)                              # (B, S, S, 3) NHWC fp32
+        fake = netG.engine.forward(ir_t, training=False)              # eval mode (ir:1357); NHWC fp32
         pred8 = rgb_u8(Feat(fake))                                    # tensor_to_rgb_image, per frame
         # ground truth: <seq>/visible/<file> (ir:1401-1404), resized on the device
         gts = []

@@ -65,7 +65,7 @@ def colorize_u8(model, ir_bchw: torch.Tensor) -> torch.Tensor:
     conversion launch straight from the engine's NHWC fp32 output."""
     netG = getattr(model, "netG", model)
     netG._maybe_repack()
-    fake = netG.engine.forward(ir_bchw.float())
+    fake = netG.engine.forward(ir_bchw.float(), training=netG.training)   # nn.Dropout follows train()/eval()
     return rgb_u8(Feat(fake))
 
 

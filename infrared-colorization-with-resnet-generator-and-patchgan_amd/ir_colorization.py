@@ -683,12 +683,18 @@ def validate_kaist(model: IRColorizationModel, val_loader, device):
     vs rgb.  Under data parallelism each rank scores its val shard (disjoint, no
     padding duplicates: dp_loaders) and (sum, count) is all-reduced."""
     total, count = 0.0, 0
-    for batch in val_loader:
-        ir = batch["ir"].to(device)
-        rgb = batch["rgb"].to(device)
-        fake = model(ir)
-        total += float((fake - rgb).abs().mean()) * ir.size(0)
-        count += ir.size(0)
+    mode = hasattr(model, "eval")   # an nn.Module (a bare callable has no train/eval state)
+    if mode:
+        model.eval()   # ir:1527
+    with torch.no_grad():
+        for batch in val_loader:
+            ir = batch["ir"].to(device)
+            rgb = batch["rgb"].to(device)
+            fake = model(ir)
+            total += float((fake - rgb).abs().mean()) * ir.size(0)
+            count += ir.size(0)
+    if mode:
+        model.train()  # ir:1541
     rank, world = _dp()
     if world > 1:
         import torch.distributed as dist

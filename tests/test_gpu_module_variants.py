@@ -179,6 +179,37 @@ def test_generator_dropout_training_vs_oracle_with_the_same_masks():
     assert not torch.equal(fake, fake2), "a second training forward must draw new masks"
 
 
+def test_generator_dropout_eval_mode_is_deterministic_on_every_entry():
+    """use_dropout=True after model.eval(): nn.Dropout is the identity (ir:394-395, 1357), so
+    the module forward, colorize_u8 (direct engine call) and validate_kaist all give the
+    no-dropout output, twice in a row; validate_kaist returns the model in train mode (ir:1541)."""
+    irc = pkg()
+    cfg = irc.Config()
+    cfg.device, cfg.compute_dtype = DEV, "fp32"
+    model = irc.IRColorizationModel(cfg)
+    model.netG = irc.ResnetUNetGenerator(1, 3, 64, norm_layer=irc.get_norm_layer("instance"), use_dropout=True,
+                                         n_blocks=9, device=DEV, compute_dtype="fp32")
+    P = O.seeded_params(O.g_param_shapes(use_dropout=True), 1, bias_std=0.02)
+    model.netG.load_state_dict(P)
+    x = (torch.rand(2, 1, 32, 32, generator=torch.Generator().manual_seed(5)) * 2 - 1).to(DEV)
+    ref = O.g_forward({k: v.clone() for k, v in P.items()}, x.cpu()).detach()
+    model.eval()
+    with torch.no_grad():
+        a, b = model(x).cpu(), model(x).cpu()
+    assert torch.equal(a, b) and float((a - ref).abs().max()) < 1e-4
+    u1 = irc.inference.colorize_u8(model, x)
+    u2 = irc.inference.colorize_u8(model, x)
+    assert torch.equal(u1, u2)
+    assert torch.equal(u1, irc.inference.rgb_u8(a.to(DEV)))
+    rgb = (torch.rand(2, 3, 32, 32, generator=torch.Generator().manual_seed(6)) * 2 - 1)
+    loader = [{"ir": x.cpu(), "rgb": rgb}]
+    model.train()
+    v1 = irc.validate_kaist(model, loader, DEV)
+    assert model.training and model.netG.training
+    v2 = irc.validate_kaist(model, loader, DEV)
+    assert v1 == v2 and abs(v1 - float((ref - rgb).abs().mean())) < 1e-5
+
+
 @pytest.mark.parametrize("variant", ["norm_none", "replicate", "zero", "dropout"])
 def test_train_step_variants_bf16_finite_and_close_to_fp32(variant):
     """The fused bf16 train step (GANTrainer) with a non-default generator / D: every loss,
