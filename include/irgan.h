@@ -23,6 +23,14 @@
 #include <stdint.h>
 #include <stddef.h>
 
+/* Every entry point below is exported from libirgan.so; everything else in the library is
+ * hidden (built with -fvisibility=hidden). */
+#if defined(__GNUC__) || defined(__clang__)
+#define IRGAN_API __attribute__((visibility("default")))
+#else
+#define IRGAN_API
+#endif
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -56,12 +64,20 @@ typedef struct irgan_conv_desc {
     int32_t mask_act;                     /* backward mask: 0 none, 1 relu, 2 lrelu(0.2) */
     int32_t ldm, moff;                    /* mask slice (same pixel grid as output) */
     int32_t cin_real;                     /* nonzero input channels of a zero-padded input (0: Cin) */
+    int32_t flags;                        /* IRGAN_CONV_* bits */
 } irgan_conv_desc;
+/* flags: IRGAN_CONV_DETERMINISTIC -- a split-K weight gradient (irgan_conv_wgrad_ws) reduces
+ * its partials through the caller's workspace in a fixed order and never through fp32
+ * atomics: it lowers its split count to what the workspace holds (torch's
+ * use_deterministic_algorithms analogue; bit-identical gradients run to run and under any
+ * stream schedule).  Without it the atomics are kept where they are faster (high split
+ * counts: up2 / down1-class layers at 256^2). */
+enum { IRGAN_CONV_DETERMINISTIC = 1 };
 
 /* y = act(conv(x, w) + bias) [* mask'(m)]   -- replaces nn.Conv2d forward
  * (ir:460, 470, 478, 390, 411, 504, 521, 529, 600-629, vgg 664) and, on
  * re-packed weights, conv backward-data and nn.ConvTranspose2d (ir:496, 513). */
-int irgan_conv_fwd(const irgan_conv_desc* d, const void* x, const void* w,
+IRGAN_API int irgan_conv_fwd(const irgan_conv_desc* d, const void* x, const void* w,
                    const float* bias, void* y, const void* mask, irgan_stream_t s);
 
 /* irgan_conv_fwd (bf16, stride 1, 3x3 / 4x4, no activation) that
@@ -71,21 +87,9 @@ int irgan_conv_fwd(const irgan_conv_desc* d, const void* x, const void* w,
  * image, <= IRGAN_IN_PARTS; Cout % 64 == 0 except 192); irgan_in_finalize turns them
  * into {mean, rstd}.
  * Returns IRGAN_EUNSUPPORTED (nothing launched) for other layers. */
-int irgan_conv_fwd_stats(const irgan_conv_desc* d, const void* x, const void* w,
+IRGAN_API int irgan_conv_fwd_stats(const irgan_conv_desc* d, const void* x, const void* w,
                          const float* bias, void* y, void* part, int32_t* nb, irgan_stream_t s);
 
-/* Backward-data of a reflect-padded 3x3 stride-1 ResnetBlock conv (ir:381-392, 401-411:
- * the interior by the bf16 conv_pp kernel, then the reflect-pad ring as
- * irgan_reflect_dgrad_ring; d = the interior descriptor ops.conv_dgrad builds, p = 1) that
- * also writes the InstanceNorm-backward partials (sum g, sum g*xhat) of its bf16 output
- * dx for the IN that produced the forward input of this conv's layer: z = that IN's
- * pre-norm input, mr its {mean, rstd}, act the activation after it; g = dx * act'(xhat).
- * *nb (out) = partial rows per image; reduce with irgan_in_bwd_finalize.  Replaces the
- * separate irgan_in_bwd_reduce pass over dx.  IRGAN_EUNSUPPORTED (nothing launched)
- * unless bf16, Cout % 256 == 0, 8-aligned slices, an output the size of the input. */
-int irgan_conv_dgrad_in_stats(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p,
-                              void* dx, const void* z, int32_t ldz, int32_t zoff, const float* mr,
-                              int32_t act, void* part, int32_t* nb, irgan_stream_t s);
 /* irgan_conv_fwd_stats / irgan_conv_fwd on fp8 operands (BASELINE config 5): x and
  * w OCP e4m3 (d->dtype = IRGAN_FP8; x NHWC with ldx, xoff % 16 == 0, w the packed
  * [Cout][3][3][Cin] image), 3x3, stride 1, Cin % 128 == 0, Cout % 64 == 0 (not
@@ -94,7 +98,7 @@ int irgan_conv_dgrad_in_stats(const irgan_conv_desc* d, const void* dy, const vo
  * InstanceNorm partials of y (as irgan_conv_fwd_stats; act none, no accumulate).
  * Replaces the ResnetBlock convs (ir:386-411) forward and backward-data in the fp8
  * path.  IRGAN_EUNSUPPORTED (nothing launched) for other layers. */
-int irgan_conv_fwd_fp8(const irgan_conv_desc* d, const void* x, const void* w, const float* dqx,
+IRGAN_API int irgan_conv_fwd_fp8(const irgan_conv_desc* d, const void* x, const void* w, const float* dqx,
                        const float* dqw, const float* bias, void* y, void* part, int32_t* nb,
                        irgan_stream_t s);
 
@@ -107,13 +111,13 @@ enum { IRGAN_FP8_AMAX_PARTS = 256 };
  * (round to nearest even; x bf16 or fp32 by dt; C, ld, off % 8 == 0), and the
  * max |x| recorded into the amax slot when amax != NULL.  y == NULL: the max only.
  * q == NULL: q = 1. */
-int irgan_fp8_quant(const void* x, int32_t dt, int64_t P, int32_t C, int32_t ldx, int32_t xoff,
+IRGAN_API int irgan_fp8_quant(const void* x, int32_t dt, int64_t P, int32_t C, int32_t ldx, int32_t xoff,
                     void* y, int32_t ldy, int32_t yoff, const float* q, uint32_t* amax,
                     irgan_stream_t s);
 /* Per-tensor scales from recorded maxima, for n slots (amax: n x IRGAN_FP8_AMAX_PARTS):
  * q = 2^floor(log2(448 / amax)) (1 if amax is 0), dq = 1 / q; reset != 0 clears the
  * slots afterwards. */
-int irgan_fp8_scale(uint32_t* amax, int32_t n, float* q, float* dq, int32_t reset, irgan_stream_t s);
+IRGAN_API int irgan_fp8_scale(uint32_t* amax, int32_t n, float* q, float* dq, int32_t reset, irgan_stream_t s);
 /* A table of njobs irgan_fp8_job records (device memory; n % 8 == 0, bf16 src,
  * n <= max_n): amax != NULL -> max |src| into amax slot `slot` only; otherwise
  * dst = e4m3(clamp(src * q[slot], +-448)).  The per-step re-quantisation of the
@@ -124,21 +128,21 @@ typedef struct irgan_fp8_job {
     int64_t n;
     int32_t slot, reserved;
 } irgan_fp8_job;
-int irgan_fp8_quant_batch(const void* jobs, int32_t njobs, int64_t max_n, const float* q,
+IRGAN_API int irgan_fp8_quant_batch(const void* jobs, int32_t njobs, int64_t max_n, const float* q,
                           uint32_t* amax, irgan_stream_t s);
 
 /* Split-K partial sums of irgan_conv_fwd (fp32 out; no bias, activation, mask or
  * accumulate): the K range is cut into ksplit parts and part ks lands at
  * y + ks*split_stride.  The consumer sums the parts (e.g. irgan_reflect_ring_fold).
  * bf16 LDS-DMA path; other dtypes support ksplit == 1 only. */
-int irgan_conv_fwd_splitk(const irgan_conv_desc* d, const void* x, const void* w, float* y,
+IRGAN_API int irgan_conv_fwd_splitk(const irgan_conv_desc* d, const void* x, const void* w, float* y,
                           int32_t ksplit, int64_t split_stride, irgan_stream_t s);
 
 /* dw[cout][ky][kx][cin] += sum_pixels dy * im2col(x)  (fp32 atomics, split-K
  * over pixels) -- replaces the weight half of convolution_backward.  d is the
  * FORWARD descriptor (x = forward input, dy = grad at the forward output with
  * slice ldy/yoff); dw must be zeroed by the caller for a fresh gradient. */
-int irgan_conv_wgrad(const irgan_conv_desc* d, const void* x, const void* dy,
+IRGAN_API int irgan_conv_wgrad(const irgan_conv_desc* d, const void* x, const void* dy,
                      float* dw, int32_t splitk, irgan_stream_t s);
 
 /* Same as irgan_conv_wgrad with a caller-owned fp32 workspace of ws_floats
@@ -146,7 +150,7 @@ int irgan_conv_wgrad(const irgan_conv_desc* d, const void* x, const void* dy,
  * are written there with plain stores and summed into dw by a second launch in
  * a fixed order (deterministic, no atomics); otherwise identical to
  * irgan_conv_wgrad.  ws may be NULL. */
-int irgan_conv_wgrad_ws(const irgan_conv_desc* d, const void* x, const void* dy, float* dw,
+IRGAN_API int irgan_conv_wgrad_ws(const irgan_conv_desc* d, const void* x, const void* dy, float* dw,
                         int32_t splitk, float* ws, int64_t ws_floats, irgan_stream_t s);
 
 /* Weight re-pack: dst rows [R][Kp] (dtype) from the fp32 KRSC master
@@ -158,7 +162,7 @@ int irgan_conv_wgrad_ws(const irgan_conv_desc* d, const void* x, const void* dy,
  * [Cin][Cout][K][K] is handed over as the KRSC master of the conv it transposes.
  * Narrow inputs (1/3/4 channels) are zero-padded to cpad = 8 so the bf16
  * LDS-DMA conv takes 64/8 = 8 taps per K-tile (kalign = 64). */
-int irgan_weight_pack(const float* src, void* dst, int32_t dtype, int32_t Cout, int32_t KH,
+IRGAN_API int irgan_weight_pack(const float* src, void* dst, int32_t dtype, int32_t Cout, int32_t KH,
                       int32_t KW, int32_t Cin, int32_t transpose, int32_t s, int32_t tyr,
                       int32_t Ay, int32_t txr, int32_t Ax, int32_t cpad, int32_t kalign,
                       irgan_stream_t st);
@@ -171,7 +175,7 @@ typedef struct irgan_pack_desc {
 } irgan_pack_desc;
 /* n irgan_weight_pack jobs in ONE launch (a network's post-Adam re-pack: ~50
  * small launches -> 1).  descs: device array of n records. */
-int irgan_weight_pack_batch(const irgan_pack_desc* descs, int32_t n, irgan_stream_t st);
+IRGAN_API int irgan_weight_pack_batch(const irgan_pack_desc* descs, int32_t n, irgan_stream_t st);
 
 /* ---- InstanceNorm (ir:154-165), per-(n,c) over H*W, eps 1e-5, no affine ---- */
 /* Reductions are two-level and atomic-free: <= IRGAN_IN_PARTS block partials per
@@ -179,37 +183,26 @@ int irgan_weight_pack_batch(const irgan_pack_desc* descs, int32_t n, irgan_strea
 enum { IRGAN_IN_PARTS = 256 };
 /* mr[n][c] = {mean, rstd} from nb float2 (sum, sum of squares) partials per (n, c)
  * written by irgan_conv_fwd_stats (the reduction half of irgan_in_stats). */
-int irgan_in_finalize(const void* part, int32_t N, int32_t HW, int32_t C, int32_t nb, float* mr,
+IRGAN_API int irgan_in_finalize(const void* part, int32_t N, int32_t HW, int32_t C, int32_t nb, float* mr,
                       irgan_stream_t s);
-/* irgan_in_finalize + irgan_in_apply in one launch (bf16 x / res / y, C <= 1024, slices
- * 8-aligned; else IRGAN_EUNSUPPORTED, nothing launched): mr (out, bit-identical to
- * irgan_in_finalize's) and y = act(IN(x)) [+ res] (ir:392, 417-418). */
-int irgan_in_finalize_apply(const void* part, int32_t nb, const void* x, int32_t N, int32_t HW,
-                            int32_t C, int32_t ldx, int32_t xoff, float* mr, int32_t act,
-                            const void* res, int32_t ldr, int32_t roff, void* y, int32_t ldy,
-                            int32_t yoff, irgan_stream_t s);
-/* red[n][c] = {mean g, mean g*xhat} from nb per-image partial rows (the reduce half of
- * irgan_in_bwd_reduce) written by irgan_conv_dgrad_in_stats. */
-int irgan_in_bwd_finalize(const void* part, int32_t N, int32_t HW, int32_t C, int32_t nb, float* red,
-                          irgan_stream_t s);
 /* mr[n][c] = {mean, rstd}; work: IRGAN_IN_PARTS*N*C doubles of scratch. */
-int irgan_in_stats(const void* x, int32_t dtype, int32_t N, int32_t HW, int32_t C,
+IRGAN_API int irgan_in_stats(const void* x, int32_t dtype, int32_t N, int32_t HW, int32_t C,
                    int32_t ld, int32_t off, double* work, float* mr, irgan_stream_t s);
 /* y = act((x - mean) * rstd) [+ res];  optional xhat output ([P][C], dtype). */
-int irgan_in_apply(const void* x, int32_t dtype, int32_t N, int32_t HW, int32_t C, int32_t ldx,
+IRGAN_API int irgan_in_apply(const void* x, int32_t dtype, int32_t N, int32_t HW, int32_t C, int32_t ldx,
                    int32_t xoff, const float* mr, int32_t act, const void* res, int32_t ldr,
                    int32_t roff, void* y, int32_t ldy, int32_t yoff, void* xhat, irgan_stream_t s);
 /* Backward of y = act(IN(x)) [+ res] given the PRE-norm input x and its
  * (mean, rstd): xhat = (x - mean)*rstd, g = (dy [+ dy2]) * act'(xhat),
  * red[n][c] = {mean g, mean g*xhat}.  work: IRGAN_IN_PARTS*N*C doubles of scratch. */
-int irgan_in_bwd_reduce(const void* dy, int32_t dy_dtype, int32_t lddy, int32_t dyoff,
+IRGAN_API int irgan_in_bwd_reduce(const void* dy, int32_t dy_dtype, int32_t lddy, int32_t dyoff,
                         const void* dy2, int32_t dy2_dtype, int32_t lddy2, int32_t dy2off,
                         const void* x, int32_t x_dtype, int32_t ldx, int32_t xoff, int32_t act,
                         int32_t N, int32_t HW, int32_t C, const float* mr, double* work, float* red,
                         irgan_stream_t s);
 /* dx = rstd*(g - mean(g) - xhat*mean(g*xhat)); also db[c] += sum dx (fp32 bias
  * grad of the producing conv, caller zeroes) when db != NULL.  dx may alias dy. */
-int irgan_in_bwd_apply(const void* dy, int32_t dy_dtype, int32_t lddy, int32_t dyoff,
+IRGAN_API int irgan_in_bwd_apply(const void* dy, int32_t dy_dtype, int32_t lddy, int32_t dyoff,
                        const void* dy2, int32_t dy2_dtype, int32_t lddy2, int32_t dy2off,
                        const void* x, int32_t x_dtype, int32_t ldx, int32_t xoff, int32_t act,
                        int32_t N, int32_t HW, int32_t C, const float* mr, const float* red,
@@ -221,18 +214,18 @@ int irgan_in_bwd_apply(const void* dy, int32_t dy_dtype, int32_t lddy, int32_t d
  * max |bf16(y)| into the amax slot (IRGAN_FP8_AMAX_PARTS partials): the producers
  * of the fp8 path's ResnetBlock conv operands, so no separate quantise pass runs.
  * IRGAN_EUNSUPPORTED when C, the strides or offsets are not multiples of 8. */
-int irgan_in_apply_fp8(const void* x, int32_t N, int32_t HW, int32_t C, int32_t ldx, int32_t xoff,
+IRGAN_API int irgan_in_apply_fp8(const void* x, int32_t N, int32_t HW, int32_t C, int32_t ldx, int32_t xoff,
                        const float* mr, int32_t act, const void* res, int32_t ldr, int32_t roff, void* y,
                        int32_t ldy, int32_t yoff, void* y8, int32_t ld8, int32_t off8, const float* q,
                        uint32_t* amax, irgan_stream_t s);
-int irgan_in_bwd_apply_fp8(const void* dy, int32_t lddy, int32_t dyoff, const void* dy2, int32_t lddy2,
+IRGAN_API int irgan_in_bwd_apply_fp8(const void* dy, int32_t lddy, int32_t dyoff, const void* dy2, int32_t lddy2,
                            int32_t dy2off, const void* x, int32_t ldx, int32_t xoff, int32_t act, int32_t N,
                            int32_t HW, int32_t C, const float* mr, const float* red, void* dx, int32_t lddx,
                            int32_t dxoff, void* y8, int32_t ld8, int32_t off8, const float* q,
                            uint32_t* amax, irgan_stream_t s);
 /* db[c] += sum over pixels of g[p][c] (bias gradient), g slice (dtype, ld, off).
  * work: 16*IRGAN_IN_PARTS*C doubles of scratch. */
-int irgan_channel_sum(const void* g, int32_t dtype, int32_t P, int32_t C, int32_t ld,
+IRGAN_API int irgan_channel_sum(const void* g, int32_t dtype, int32_t P, int32_t C, int32_t ld,
                       int32_t off, float* db, double* work, irgan_stream_t s);
 
 /* ---- resampling (ir:269-355 and reflection-pad backward) ---- */
@@ -242,7 +235,7 @@ int irgan_channel_sum(const void* g, int32_t dtype, int32_t P, int32_t C, int32_
  * kind 2: nn.ReflectionPad2d(p).  transpose=1 gives the adjoint (rows = the
  * forward map's input coordinates).  Fills idx/w [rows][tmax] and returns rows,
  * or a negative IRGAN_E* code. */
-int irgan_resample_table(int32_t kind, int32_t n_in, int32_t p, int32_t transpose, int32_t* idx,
+IRGAN_API int irgan_resample_table(int32_t kind, int32_t n_in, int32_t p, int32_t transpose, int32_t* idx,
                          float* w, int32_t tmax, int32_t rows_cap);
 /* Border half of the nn.ReflectionPad2d(p) backward (ir:381, 402, 459, 528).
  * The backward-data result g over the padded (H+2p) x (W+2p) domain has its
@@ -251,7 +244,7 @@ int irgan_resample_table(int32_t kind, int32_t n_in, int32_t p, int32_t transpos
  * k and H+p+k at compact rows k and p+k) and cols[ks][N][H][2p][C] (padded
  * columns k and W+p+k of the interior rows).  dx[band] += every mirrored ring
  * value (a gather: deterministic).  Together: dx = fold(g). */
-int irgan_reflect_ring_fold(const float* rows, const float* cols, int32_t nsplit, int32_t N, int32_t H,
+IRGAN_API int irgan_reflect_ring_fold(const float* rows, const float* cols, int32_t nsplit, int32_t N, int32_t H,
                             int32_t W, int32_t C, int32_t p, void* dx, int32_t dx_dtype, int32_t lddx,
                             int32_t dxoff, irgan_stream_t s);
 /* Same fold in one launch, without the fp32 partials (bf16, stride-1 reflect
@@ -260,7 +253,7 @@ int irgan_reflect_ring_fold(const float* rows, const float* cols, int32_t nsplit
  * Ho = H, Wo = W, c0 shifted by p), which must already have written dx; this
  * evaluates every ring value of g with MFMA and adds it onto its mirrored
  * border pixel of dx (one owner per pixel, no atomics). */
-int irgan_reflect_dgrad_ring(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p, void* dx,
+IRGAN_API int irgan_reflect_dgrad_ring(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p, void* dx,
                              irgan_stream_t s);
 /* irgan_reflect_dgrad_ring with a caller workspace ws of ws_floats floats.  ResnetBlock
  * shapes (3x3, p = 1, 4 <= H, W <= 64, dY channels % 32 and <= 256, dx channels % 64, bf16,
@@ -268,9 +261,8 @@ int irgan_reflect_dgrad_ring(const irgan_conv_desc* d, const void* dy, const voi
  * GEMMs with LDS-resident weights (at most max_blocks workgroups, each walking a group of
  * images) into ws, then the fold onto dx (one read-modify-write per owned pixel); other
  * shapes: irgan_reflect_dgrad_ring.  max_blocks bounds the first launch for a second stream
- * beside a kernel that leaves that many CUs idle (the ResnetBlock weight gradient, ir:386-411's
- * backward: engine.GeneratorEngine.backward). */
-int irgan_reflect_dgrad_ring_ws(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p, void* dx,
+ * beside a kernel that leaves that many CUs idle). */
+IRGAN_API int irgan_reflect_dgrad_ring_ws(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p, void* dx,
                                 float* ws, int64_t ws_floats, int32_t max_blocks, irgan_stream_t s);
 /* Reflect-padded ResnetBlock backward-data (ir:386-411; replaces torch autograd's
  * ReflectionPad2d + Conv2d backward) in two launches: the ring's line GEMM into ws (as
@@ -280,7 +272,7 @@ int irgan_reflect_dgrad_ring_ws(const irgan_conv_desc* d, const void* dy, const 
  * descriptor (ops.conv_dgrad).  IRGAN_EUNSUPPORTED (nothing launched) unless the line-ring
  * shapes hold (irgan_reflect_dgrad_ring_ws), dx is bf16 without activation, and dx channels
  * % 256 == 0 take the 256-channel conv tile. */
-int irgan_conv_dgrad_reflect_line(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p, void* dx,
+IRGAN_API int irgan_conv_dgrad_reflect_line(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p, void* dx,
                                   float* ws, int64_t ws_floats, irgan_stream_t s);
 /* Backward-data of a 4x4 stride-2 pad-1 conv (PatchGAN model.0 / .3 / .6, ir:600-612) in
  * ONE launch for all four output phases: d = the four per-phase descriptors (2x2 taps on
@@ -288,22 +280,13 @@ int irgan_conv_dgrad_reflect_line(const irgan_conv_desc* d, const void* dy, cons
  * their four packed phase images.  dx (+)= result, with the optional backward mask as
  * irgan_conv_fwd.  bf16, dy channels % 64, dx channels <= 16 or % 64, no bias / activation;
  * else IRGAN_EUNSUPPORTED (nothing launched; the caller runs the four phase launches). */
-int irgan_conv_dgrad_s2(const irgan_conv_desc* d, const void* dy, const void* const* w, void* dx,
+IRGAN_API int irgan_conv_dgrad_s2(const irgan_conv_desc* d, const void* dy, const void* const* w, void* dx,
                         const void* mask, irgan_stream_t s);
-/* The whole backward-data of a reflect-padded stride-1 conv (ir:381-392, 401-411): the
- * interior correlation and the fold of its pad ring (d, w, p as irgan_reflect_dgrad_ring).
- * With the ring fold on (irgan_set_ring_fold), ResnetBlock shapes (bf16, 3x3, p = 1, dY
- * channels % 64, dx channels % 256, H and W multiples of 16 and >= 32, no mask /
- * activation) run as ONE conv_pp launch with the ring folded into its border patches
- * (every dx pixel rounded once); otherwise (the default) irgan_conv_fwd +
- * irgan_reflect_dgrad_ring. */
-int irgan_conv_dgrad_reflect(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p, void* dx,
-                             irgan_stream_t s);
 /* out = (Wy (x) Wx) in on NHWC slices, tables from irgan_resample_table (device
  * copies, rows [Hout][Ty] and [Wout][Tx]: the host may drop trailing all-zero
  * tap columns); accumulate: out += result.  Downsample / UpsampleAA forward
  * and backward, and the reflect-pad fold, are all this one launch. */
-int irgan_sep_resample(const void* in, int32_t in_dtype, int32_t N, int32_t Hin, int32_t Win,
+IRGAN_API int irgan_sep_resample(const void* in, int32_t in_dtype, int32_t N, int32_t Hin, int32_t Win,
                        int32_t C, int32_t ldi, int32_t offi, void* out, int32_t out_dtype,
                        int32_t Hout, int32_t Wout, int32_t ldo, int32_t offo, const int32_t* ty,
                        const float* wy, int32_t Ty, const int32_t* tx, const float* wx,
@@ -313,37 +296,37 @@ int irgan_sep_resample(const void* in, int32_t in_dtype, int32_t N, int32_t Hin,
  * The IN apply + ReLU of down1 / down2 / up1_conv (ir:469-482, 557-558) fused into the
  * Downsample / UpsampleAA that consumes it.  IRGAN_EUNSUPPORTED unless 8-channel-aligned
  * slices and at most 8 taps per axis (then apply + resample separately). */
-int irgan_sep_resample_in(const void* in, int32_t in_dtype, int32_t N, int32_t Hin, int32_t Win,
+IRGAN_API int irgan_sep_resample_in(const void* in, int32_t in_dtype, int32_t N, int32_t Hin, int32_t Win,
                           int32_t C, int32_t ldi, int32_t offi, const float* mr, int32_t act,
                           void* out, int32_t out_dtype, int32_t Hout, int32_t Wout, int32_t ldo,
                           int32_t offo, const int32_t* ty, const float* wy, int32_t Ty,
                           const int32_t* tx, const float* wx, int32_t Tx, irgan_stream_t s);
 /* 2x2 max pool (VGG features) forward / backward (first max wins, as ATen). */
-int irgan_maxpool_fwd(const void* x, int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t C,
+IRGAN_API int irgan_maxpool_fwd(const void* x, int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t C,
                       void* y, irgan_stream_t s);
-int irgan_maxpool_bwd(const void* x, const void* dy, int32_t dtype, int32_t N, int32_t H,
+IRGAN_API int irgan_maxpool_bwd(const void* x, const void* dy, int32_t dtype, int32_t N, int32_t H,
                       int32_t W, int32_t C, void* dx, int32_t relu_mask, irgan_stream_t s);
 
 /* ---- layout / elementwise ---- */
 /* NCHW fp32 -> NHWC slice (dtype), optional affine y = x*scale[c] + shift[c]. */
-int irgan_nchw_to_nhwc(const float* x, int32_t N, int32_t C, int32_t H, int32_t W, void* y,
+IRGAN_API int irgan_nchw_to_nhwc(const float* x, int32_t N, int32_t C, int32_t H, int32_t W, void* y,
                        int32_t dtype, int32_t ldy, int32_t yoff, const float* scale,
                        const float* shift, irgan_stream_t s);
 /* NHWC slice (dtype) -> NCHW fp32, y = x*scale (+= when accumulate). */
-int irgan_nhwc_to_nchw(const void* x, int32_t dtype, int32_t ldx, int32_t xoff, int32_t N,
+IRGAN_API int irgan_nhwc_to_nchw(const void* x, int32_t dtype, int32_t ldx, int32_t xoff, int32_t N,
                        int32_t C, int32_t H, int32_t W, float* y, float scale, int32_t accumulate,
                        irgan_stream_t s);
 /* y[p][c] = a*x[p][c] (+ b*y) on slices; dtype conversion allowed. */
-int irgan_axpby(const void* x, int32_t xdtype, int32_t ldx, int32_t xoff, float a, void* y,
+IRGAN_API int irgan_axpby(const void* x, int32_t xdtype, int32_t ldx, int32_t xoff, float a, void* y,
                 int32_t ydtype, int32_t ldy, int32_t yoff, float b, int32_t P, int32_t C,
                 irgan_stream_t s);
 /* y[p][c] = x[p][c]*scale[c] (+ shift[c]) (+ y when accumulate): VGG input
  * normalisation (ir:679-682) and its backward. */
-int irgan_affine(const void* x, int32_t xdt, int32_t ldx, int32_t xoff, const float* scale,
+IRGAN_API int irgan_affine(const void* x, int32_t xdt, int32_t ldx, int32_t xoff, const float* scale,
                  const float* shift, void* y, int32_t ydt, int32_t ldy, int32_t yoff,
                  int32_t accumulate, int32_t P, int32_t C, irgan_stream_t s);
 /* dx = dy * act'(a): 1 relu (a>0), 2 lrelu (a>0 ? 1 : 0.2), 3 tanh (1 - a^2). */
-int irgan_act_bwd(const void* dy, int32_t dy_dtype, int32_t lddy, int32_t dyoff, const void* a,
+IRGAN_API int irgan_act_bwd(const void* dy, int32_t dy_dtype, int32_t lddy, int32_t dyoff, const void* a,
                   int32_t a_dtype, int32_t lda, int32_t aoff, int32_t act, void* dx,
                   int32_t dx_dtype, int32_t lddx, int32_t dxoff, int32_t P, int32_t C,
                   irgan_stream_t s);
@@ -352,33 +335,33 @@ int irgan_act_bwd(const void* dy, int32_t dy_dtype, int32_t lddy, int32_t dyoff,
 /* Hinge for D on a [real; fake] patch map (ir:1647-1649) and for G (ir:1662).
  * mode 0: loss = 0.5*(mean relu(1-p[:n]) + mean relu(1+p[n:])), grad written;
  * mode 1: loss = -mean p, grad = -scale/cnt. loss accumulated into *loss (fp64). */
-int irgan_hinge(const float* pred, int32_t n_half, int32_t mode, float scale, float* grad,
+IRGAN_API int irgan_hinge(const float* pred, int32_t n_half, int32_t mode, float scale, float* grad,
                 double* loss, irgan_stream_t s);
 /* Pixel / feature L1: loss += w*mean|a-b|; ga = w*sign(a-b)/cnt (dtype of ga). */
-int irgan_l1(const void* a, const void* b, int32_t dtype, int64_t count, float w, void* ga,
+IRGAN_API int irgan_l1(const void* a, const void* b, int32_t dtype, int64_t count, float w, void* ga,
              int32_t ga_dtype, int32_t accumulate, double* loss, irgan_stream_t s);
 /* TV (ir:686-694) on NHWC fp32 x: loss += w*tv(x), g += grad. */
-int irgan_tv(const float* x, int32_t N, int32_t H, int32_t W, int32_t C, float w, float* g,
+IRGAN_API int irgan_tv(const float* x, int32_t N, int32_t H, int32_t W, int32_t C, float w, float* g,
              double* loss, irgan_stream_t s);
 /* SSIM loss w*(1 - mean ssim((a+1)/2, (b+1)/2)) (ir:714-750, 1675-1677);
  * grad wrt a accumulated into g.  work: 10*N*H*W*C floats of scratch. */
-int irgan_ssim(const float* a, const float* b, int32_t N, int32_t H, int32_t W, int32_t C, float w,
+IRGAN_API int irgan_ssim(const float* a, const float* b, int32_t N, int32_t H, int32_t W, int32_t C, float w,
                float* g, double* loss, float* work, irgan_stream_t s);
 /* irgan_ssim with ssim_loss_torch's window_size (ir:714-736): any odd size 1..15
  * (Gaussian sigma 1.5, zero padding window / 2); IRGAN_EUNSUPPORTED otherwise. */
-int irgan_ssim_ws(const float* a, const float* b, int32_t N, int32_t H, int32_t W, int32_t C, float w,
+IRGAN_API int irgan_ssim_ws(const float* a, const float* b, int32_t N, int32_t H, int32_t W, int32_t C, float w,
                   float* g, double* loss, float* work, int32_t window, irgan_stream_t s);
 
 /* ---- optimizer (torch.optim.Adam, ir:1601-1604) over a flat fp32 buffer ---- */
 /* step_size = lr/(1-beta1^t), bc2_sqrt = sqrt(1-beta2^t) (host, fp64 -> fp32). */
-int irgan_adam(float* p, const float* g, float* m, float* v, int64_t n, float step_size,
+IRGAN_API int irgan_adam(float* p, const float* g, float* m, float* v, int64_t n, float step_size,
                float beta1, float beta2, float bc2_sqrt, float eps, irgan_stream_t s);
 /* The same update with the step count on the device (a captured train step replays with
  * the right bias corrections): irgan_adam_prep advances *count (int32, device) and writes
  * prm[0] = step_size, prm[1] = bc2_sqrt for the new count (the host formula above, fp64 on
  * the device, then fp32); irgan_adam_dev reads them from prm. */
-int irgan_adam_prep(int32_t* count, double lr, double beta1, double beta2, float* prm, irgan_stream_t s);
-int irgan_adam_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* prm, float beta1,
+IRGAN_API int irgan_adam_prep(int32_t* count, double lr, double beta1, double beta2, float* prm, irgan_stream_t s);
+IRGAN_API int irgan_adam_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* prm, float beta1,
                    float beta2, float eps, irgan_stream_t s);
 
 /* ---- inference / evaluation ---- */
@@ -386,14 +369,14 @@ int irgan_adam_dev(float* p, const float* g, float* m, float* v, int64_t n, cons
  * channel c of an NHWC fp32 slice (x, ldx, xoff), out dense [N][H][W][C]
  * (16-byte aligned) -- the float32 pipeline of tensor_to_rgb_image
  * (ir:865-876) for a whole batch, on the device; truncation as numpy astype. */
-int irgan_to_rgb_u8(const float* x, int32_t N, int32_t H, int32_t W, int32_t C, int32_t ldx,
+IRGAN_API int irgan_to_rgb_u8(const float* x, int32_t N, int32_t H, int32_t W, int32_t C, int32_t ldx,
                     int32_t xoff, void* out, irgan_stream_t s);
 /* Per-image error sums of compute_metrics (ir:1184-1206) over uint8 images
  * (as run_test feeds it, ir:1412-1415): d = pred/255 - gt/255 in fp32,
  * sums[2n] = sum |d|, sums[2n+1] = sum d^2 over the per_image bytes of image n
  * (MAE = sums[2n]/per_image, MSE = sums[2n+1]/per_image).  work: >= 128*N
  * doubles of scratch (work_cap = its size in doubles). */
-int irgan_image_metrics_u8(const void* pred, const void* gt, int32_t N, int64_t per_image,
+IRGAN_API int irgan_image_metrics_u8(const void* pred, const void* gt, int32_t N, int64_t per_image,
                            double* work, int64_t work_cap, double* sums, irgan_stream_t s);
 
 /* ---- KAIST data pipeline (KAISTPairDataset ir:1132-1177) ---- */
@@ -406,7 +389,7 @@ int irgan_image_metrics_u8(const void* pred, const void* gt, int32_t N, int64_t 
  * the same for x (host: computeResizeAreaTab's recurrence).  flip (nullable,
  * uint8 per image): 1 = horizontal flip (np.fliplr, ir:1166-1168).  img_max
  * (nullable, zeroed int32 per image): max destination byte of each image. */
-int irgan_area_resize_u8(const void* src, int32_t N, int32_t Hin, int32_t Win, int32_t C, int64_t img_stride,
+IRGAN_API int irgan_area_resize_u8(const void* src, int32_t N, int32_t Hin, int32_t Win, int32_t C, int64_t img_stride,
                          const int32_t* yptr, const int32_t* ysrc, const float* yw, int32_t Hout,
                          const int32_t* xptr, const int32_t* xsrc, const float* xw, int32_t Wout,
                          const void* flip, void* out_u8, int32_t* img_max, irgan_stream_t s);
@@ -415,14 +398,14 @@ int irgan_area_resize_u8(const void* src, int32_t N, int32_t Hin, int32_t Win, i
  * point.  Tables (data.linear_area_table): yofs [Hout], ycoef [Hout][2], xofs [Wout],
  * xcoef [Wout][2] (int, x 2048), xlim = first destination column with a single tap.
  * Layouts, flip and img_max as irgan_area_resize_u8. */
-int irgan_linear_area_resize_u8(const void* src, int32_t N, int32_t Hin, int32_t Win, int32_t C,
+IRGAN_API int irgan_linear_area_resize_u8(const void* src, int32_t N, int32_t Hin, int32_t Win, int32_t C,
                                 int64_t img_stride, const int32_t* yofs, const int32_t* ycoef, int32_t Hout,
                                 const int32_t* xofs, const int32_t* xcoef, int32_t xlim, int32_t Wout,
                                 const void* flip, void* out_u8, int32_t* img_max, irgan_stream_t s);
 /* out[n][i] = float32(in[n][i]) / 255 * 2 - 1 for per_image bytes per image (the
  * [-1, 1] tensors of ir:1157, 1175-1176); max_rule = 1: the IR rule of ir:1142 --
  * images whose img_max[n] <= 1 are not divided by 255. */
-int irgan_u8_to_unit(const void* in, int32_t N, int64_t per_image, const int32_t* img_max, int32_t max_rule,
+IRGAN_API int irgan_u8_to_unit(const void* in, int32_t N, int64_t per_image, const int32_t* img_max, int32_t max_rule,
                      float* out, irgan_stream_t s);
 
 /* The SSIM of compute_metrics (ir:1208-1213): skimage.metrics.structural_similarity(
@@ -430,30 +413,18 @@ int irgan_u8_to_unit(const void* in, int32_t N, int64_t per_image, const int32_t
  * standing for v / 255 -- per channel 7x7 uniform windows, sample covariance,
  * C1 = 0.01^2, C2 = 0.03^2, map averaged over pixels >= 3 from the border, then over
  * channels; fp64.  ssim[n] out.  work: >= N doubles (more = more blocks). */
-int irgan_ssim_eval_u8(const void* pred, const void* gt, int32_t N, int32_t H, int32_t W, int32_t C,
+IRGAN_API int irgan_ssim_eval_u8(const void* pred, const void* gt, int32_t N, int32_t H, int32_t W, int32_t C,
                        double* work, int64_t work_cap, double* ssim, irgan_stream_t s);
 
-/* Version / capability probe (no GPU work). */
 /* nn.Dropout(p) in training mode (ResnetBlock use_dropout, ir:394-395) on NHWC slices:
  * y = keep ? x / (1 - p) : 0, keep decided per element (pixel * C + channel) by a
  * counter-based hash of seed; the backward is the same call on the gradient (same seed).
  * x and y may alias. */
-int irgan_dropout(const void* x, int32_t xdt, int32_t P, int32_t C, int32_t ldx, int32_t xoff, void* y,
+IRGAN_API int irgan_dropout(const void* x, int32_t xdt, int32_t P, int32_t C, int32_t ldx, int32_t xoff, void* y,
                   int32_t ydt, int32_t ldy, int32_t yoff, uint64_t seed, float p, irgan_stream_t s);
 
-int irgan_version(void);
-
-/* Deterministic mode (process-wide, default off).  On: every split-K weight gradient
- * (wgrad_halo, wgrad_pc, wgrad_glds) reduces its partials through the caller's slab
- * workspace in a fixed order, never through fp32 atomics, so a step gives bit-identical
- * gradients run to run and under any stream schedule (torch's
- * use_deterministic_algorithms analogue).  Off: the atomics are kept where they are
- * faster (high split counts: up2 / down1-class layers at 256^2).  Loss VALUES are
- * fp64 atomic block sums in either mode (they feed no gradient).  Returns the old value. */
-int irgan_set_deterministic(int32_t on);
-/* Process-wide switch of irgan_conv_dgrad_reflect's one-launch ring fold (default off, or
- * on with IRGAN_RING_FOLD set).  Returns the old value. */
-int irgan_set_ring_fold(int32_t on);
+/* Version / capability probe (no GPU work). */
+IRGAN_API int irgan_version(void);
 
 #ifdef __cplusplus
 }

@@ -10,8 +10,6 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 #define IRGAN_HD __device__ __forceinline__
 
-// irgan_set_deterministic (conv.hip): host-side switch read by the split-K wgrad launchers
-int irgan_deterministic_mode();
 
 IRGAN_HD float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 // fp32 -> bf16, round to nearest even (NaN stays NaN): gfx950's v_cvt_pk_bf16_f32
@@ -113,3 +111,35 @@ IRGAN_HD int xcd_tile(int b, int nb, int swz) {
     } while (0)
 
 static inline int irgan_cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+// Per-device host caches (a process may drive several GPUs): the CU count and the address
+// of a __device__ symbol (a module global has one instance per device).  Lazily filled; two
+// threads racing on a slot store the same value.
+constexpr int IRGAN_MAX_DEVICES = 64;
+static inline int irgan_device() {
+    int d = 0;
+    return (hipGetDevice(&d) == hipSuccess && d >= 0 && d < IRGAN_MAX_DEVICES) ? d : -1;
+}
+static inline int irgan_cu_count() {
+    static int cache[IRGAN_MAX_DEVICES];
+    const int dev = irgan_device();
+    if (dev < 0) return 256;
+    int c = __atomic_load_n(&cache[dev], __ATOMIC_RELAXED);
+    if (!c) {
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c < 1) c = 256;
+        __atomic_store_n(&cache[dev], c, __ATOMIC_RELAXED);
+    }
+    return c;
+}
+// address of `sym` on the current device; nullptr on failure
+static inline void* irgan_symbol(const void* sym, void** cache) {
+    const int dev = irgan_device();
+    if (dev < 0) return nullptr;
+    void* p = __atomic_load_n(&cache[dev], __ATOMIC_ACQUIRE);
+    if (!p) {
+        if (hipGetSymbolAddress(&p, sym) != hipSuccess) return nullptr;
+        __atomic_store_n(&cache[dev], p, __ATOMIC_RELEASE);
+    }
+    return p;
+}
+static inline bool irgan_det(const irgan_conv_desc* d) { return (d->flags & IRGAN_CONV_DETERMINISTIC) != 0; }

@@ -675,10 +675,9 @@ extern "C" int irgan_conv_wgrad(const irgan_conv_desc* d, const void* x, const v
 extern "C" int irgan_conv_wgrad_ws(const irgan_conv_desc* d, const void* x, const void* dy, float* dw,
                                    int32_t splitk, float* ws, int64_t ws_floats, irgan_stream_t s) {
     if (!d || !x || !dy || !dw) return IRGAN_EINVAL;
-    static const bool use_slab = !getenv("IRGAN_NO_WGRAD_SLAB");
     hipStream_t st = (hipStream_t)s;
     if (d->dtype == IRGAN_BF16)
-        return launch_wgrad<bf16_t>(d, x, dy, dw, splitk, st, use_slab ? ws : nullptr, ws_floats);
+        return launch_wgrad<bf16_t>(d, x, dy, dw, splitk, st, ws, ws_floats);
     if (d->dtype == IRGAN_F32) return launch_wgrad<float>(d, x, dy, dw, splitk, st);
     return IRGAN_EUNSUPPORTED;
 }
@@ -714,11 +713,6 @@ extern "C" int irgan_weight_pack_batch(const irgan_pack_desc* descs, int32_t n, 
 
 extern "C" int irgan_version(void) { return 1; }
 
-static int g_irgan_deterministic = 0;
-int irgan_deterministic_mode() { return __atomic_load_n(&g_irgan_deterministic, __ATOMIC_RELAXED); }
-extern "C" int irgan_set_deterministic(int32_t on) {
-    return __atomic_exchange_n(&g_irgan_deterministic, on ? 1 : 0, __ATOMIC_RELAXED);
-}
 
 // Split-K partial sums (no bias / activation / mask): partial ks of the
 // fp32 output lands at y + ks*split_stride.  Used for thin output domains

@@ -212,16 +212,10 @@ __global__ __launch_bounds__(256, C8_MINB) void conv_c8_kernel(const irgan_conv_
 
 template <int KH, int KW, int S>
 void launch_c8(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y, hipStream_t st) {
-    static int slots = 0;
-    if (!slots) {
-        int b = 0, dev = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, conv_c8_kernel<KH, KW, S>, 256, 0) != hipSuccess || b < 1)
-            b = 1;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-            cus = 256;
-        slots = b * cus;
-    }
+    static int occ = 0;  // resident blocks per CU (a property of the kernel on gfx950)
+    if (!occ && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv_c8_kernel<KH, KW, S>, 256, 0) != hipSuccess || occ < 1))
+        occ = 1;
+    const int slots = occ * irgan_cu_count();
     const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH);
     const int npatch = d->N * tpx * tpy;
     const int grid = npatch < slots ? npatch : slots;
@@ -414,17 +408,10 @@ __global__ __launch_bounds__(256, 2) void conv_c8r_kernel(const irgan_conv_desc 
 
 template <int KH, int KW, int S, int CR>
 void launch_c8r(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y, hipStream_t st) {
-    static int slots = 0;
-    if (!slots) {
-        int b = 0, dev = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, conv_c8r_kernel<KH, KW, S, CR>, 256, 0) != hipSuccess ||
-            b < 1)
-            b = 1;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-            cus = 256;
-        slots = b * cus;
-    }
+    static int occ = 0;  // resident blocks per CU (a property of the kernel on gfx950)
+    if (!occ && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv_c8r_kernel<KH, KW, S, CR>, 256, 0) != hipSuccess || occ < 1))
+        occ = 1;
+    const int slots = occ * irgan_cu_count();
     const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH);
     const int npatch = d->N * tpx * tpy;
     const int grid = npatch < slots ? npatch : slots;

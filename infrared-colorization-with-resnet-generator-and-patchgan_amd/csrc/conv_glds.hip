@@ -161,9 +161,9 @@ extern "C" int irgan_conv_fwd_glds_split(const irgan_conv_desc* d, const void* x
                                          void* y, const void* mask, int ksplit, long sstride, hipStream_t st) {
     const long M = (long)d->N * d->Ho * d->Wo;
     if (M <= 0 || d->Cout <= 0) return 0;
-    static bf16_t* zero = nullptr;  // immutable after first lookup
-    if (!zero && hipGetSymbolAddress((void**)&zero, HIP_SYMBOL(g_irgan_zero_page)) != hipSuccess)
-        return IRGAN_EUNSUPPORTED;
+    static void* zero_cache[IRGAN_MAX_DEVICES];  // the zero page's address per device
+    const bf16_t* zero = (const bf16_t*)irgan_symbol(HIP_SYMBOL(g_irgan_zero_page), zero_cache);
+    if (!zero) return IRGAN_EUNSUPPORTED;
     static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
     if (ksplit < 1) ksplit = 1;
     if (d->Cout > 64) {
@@ -368,9 +368,9 @@ extern "C" int irgan_conv_wgrad_glds(const irgan_conv_desc* d, const void* x, co
     const long P = (long)d->N * d->Ho * d->Wo;
     const int K = d->KH * d->KW * d->Cin;
     if (P <= 0) return 0;
-    static bf16_t* zero = nullptr;
-    if (!zero && hipGetSymbolAddress((void**)&zero, HIP_SYMBOL(g_irgan_zero_page)) != hipSuccess)
-        return IRGAN_EUNSUPPORTED;
+    static void* zero_cache[IRGAN_MAX_DEVICES];  // the zero page's address per device
+    const bf16_t* zero = (const bf16_t*)irgan_symbol(HIP_SYMBOL(g_irgan_zero_page), zero_cache);
+    if (!zero) return IRGAN_EUNSUPPORTED;
     const int BMC = d->Cout % 128 == 0 ? 128 : 64;
     const int BNC = d->Cin % 128 == 0 ? 128 : 64;
     const int tiles = irgan_cdiv(d->Cout, BMC) * (K / BNC);
@@ -385,6 +385,10 @@ extern "C" int irgan_conv_wgrad_glds(const irgan_conv_desc* d, const void* x, co
     if (swz && splitk > 1 && (tiles * splitk) % 8) {
         for (int s2 = splitk; s2 >= 1 && s2 >= splitk - 7; --s2)
             if ((tiles * s2) % 8 == 0) { splitk = s2; break; }
+    }
+    if (irgan_det(d)) {  // deterministic: no atomics -- at most the splits the workspace holds
+        const long fit = ws ? ws_cap / ((long)d->Cout * d->KH * d->KW * d->Cin) : 1;
+        if (splitk > fit) splitk = (int)(fit > 1 ? fit : 1);
     }
     long kc = (P + splitk - 1) / splitk;
     kc = (kc + 63) / 64 * 64;

@@ -315,9 +315,9 @@ extern "C" int irgan_conv_fwd_halo(const irgan_conv_desc* d, const void* x, cons
         return IRGAN_EUNSUPPORTED;
     const bool big = d->KH > 4 || d->KW > 4;
     if (big && d->Cout > 64) return IRGAN_EUNSUPPORTED;
-    static bf16_t* zero = nullptr;
-    if (!zero && hipGetSymbolAddress((void**)&zero, HIP_SYMBOL(g_halo_zero_page)) != hipSuccess)
-        return IRGAN_EUNSUPPORTED;
+    static void* zero_cache[IRGAN_MAX_DEVICES];  // the zero page's address per device
+    const bf16_t* zero = (const bf16_t*)irgan_symbol(HIP_SYMBOL(g_halo_zero_page), zero_cache);
+    if (!zero) return IRGAN_EUNSUPPORTED;
     static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
     static const bool narrow = !getenv("IRGAN_NO_NARROW");
     if (narrow && d->Cout <= 8) {

@@ -136,12 +136,10 @@ extern "C" int irgan_conv_dgrad_reflect_line(const irgan_conv_desc* d, const voi
     const int nb = d->N * tpy * tpx * ntn;
     if (d->accumulate)
         conv_pp_kernel<3, 3, 256, true><<<nb, 512, 0, st>>>(*d, (const bf16_t*)dy, (const bf16_t*)w, nullptr, dx,
-                                                            nullptr, ntn, tpx, tpy, swz, nullptr, nullptr, nullptr,
-                                                            InBwdStats{}, ws);
+                                                            nullptr, ntn, tpx, tpy, swz, nullptr, nullptr, nullptr, ws);
     else
         conv_pp_kernel<3, 3, 256, false><<<nb, 512, 0, st>>>(*d, (const bf16_t*)dy, (const bf16_t*)w, nullptr, dx,
-                                                             nullptr, ntn, tpx, tpy, swz, nullptr, nullptr, nullptr,
-                                                             InBwdStats{}, ws);
+                                                             nullptr, ntn, tpx, tpy, swz, nullptr, nullptr, nullptr, ws);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }
@@ -194,61 +192,6 @@ extern "C" int irgan_conv_fwd_stats(const irgan_conv_desc* d, const void* x, con
 #undef PPS
     IRGAN_LAUNCH_CHECK();
     *nb = tpx * tpy;
-    return 0;
-}
-
-// Reflect-padded resblock backward-data (interior conv_pp + the ring, as ops.conv_dgrad)
-// that also writes the InstanceNorm-backward partials of its bf16 output for the layer
-// whose gradient it is: z / mr / act of that IN (ir:386-392, 401-411).  The interior's
-// partials fill rows [0, tpx*tpy) of each image, the ring kernel (irgan_reflect_dgrad_ring_in)
-// adds the change it makes to the border pixels in rows [tpx*tpy, *nb).  Reduce them with
-// irgan_in_bwd_finalize.  IRGAN_EUNSUPPORTED (nothing launched) unless BN-256 tiles.
-int ring_in_launch(const irgan_conv_desc* d, const void* dy, const void* w, int p, void* dx, const void* z, int ldz,
-                   int zoff, const float* mr, int act, void* part, int pstride, int slot0, hipStream_t st);
-int ring_in_slots(const irgan_conv_desc* d, int p);
-bool irgan_ring_fold_ok(const irgan_conv_desc* d, int p);  // conv_pp_ring.hip
-int irgan_ring_fold_in_stats(const irgan_conv_desc* d, const void* dy, const void* w, void* dx, const void* z,
-                             int ldz, int zoff, int act, int pstride, const float* mr, void* part, hipStream_t st);
-
-extern "C" int irgan_conv_dgrad_in_stats(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p, void* dx,
-                                         const void* z, int32_t ldz, int32_t zoff, const float* mr, int32_t act,
-                                         void* part, int32_t* nb, irgan_stream_t s) {
-    if (!d || !dy || !w || !dx || !z || !mr || !part || !nb) return IRGAN_EINVAL;
-    if (d->dtype != IRGAN_BF16 || d->out_dtype != IRGAN_BF16 || d->act != IRGAN_ACT_NONE || d->KH != 3 ||
-        d->KW != 3 || d->sy != 1 || d->sx != 1 || d->Cin % 64 || d->Cout % 256 || d->ldx % 8 || d->xoff % 8 ||
-        d->ldy % 8 || d->yoff % 8 || ldz % 8 || zoff % 8 || d->Ho != d->OH || d->Wo != d->OW || d->omy != 1 ||
-        d->omx != 1 || d->ooy || d->oox || p != 1 || d->Ho != d->H || d->Wo != d->W ||
-        (long)d->N * d->H * d->W * d->ldx >= (1L << 30) || (long)d->Cout * 9 * d->Cin >= (1L << 30) ||
-        getenv("IRGAN_NO_FUSED_IN_BWD"))
-        return IRGAN_EUNSUPPORTED;
-    const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH);
-    if (irgan_ring_fold_ok(d, p) && tpx * tpy <= IRGAN_IN_PARTS) {
-        // one launch: the ring folded in, so the epilogue's partials are those of the final dx
-        const int rc = irgan_ring_fold_in_stats(d, dy, w, dx, z, ldz, zoff, act, tpx * tpy, mr, part, (hipStream_t)s);
-        if (rc) return rc;
-        *nb = tpx * tpy;
-        return 0;
-    }
-    const int nr = ring_in_slots(d, p);
-    if (nr <= 0 || tpx * tpy + nr > IRGAN_IN_PARTS) return IRGAN_EUNSUPPORTED;
-    if ((long)d->N * d->Ho * d->Wo <= 0) return IRGAN_EUNSUPPORTED;
-    static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
-    const int ntn = d->Cout / 256;
-    const int blocks = d->N * tpy * tpx * ntn;
-    const int pstride = tpx * tpy + nr;
-    hipStream_t st = (hipStream_t)s;
-    const InBwdStats ib{(const bf16_t*)z, ldz, zoff, act, pstride, mr};
-#define PPB(ACCV)                                                                                                 \
-    conv_pp_kernel<3, 3, 256, ACCV, true, false, false><<<blocks, 512, 0, st>>>(                                   \
-        *d, (const bf16_t*)dy, (const bf16_t*)w, nullptr, dx, nullptr, ntn, tpx, tpy, swz, (float2*)part, nullptr, \
-        nullptr, ib)
-    if (d->accumulate) PPB(true);
-    else PPB(false);
-#undef PPB
-    IRGAN_LAUNCH_CHECK();
-    const int rc = ring_in_launch(d, dy, w, p, dx, z, ldz, zoff, mr, act, part, pstride, tpx * tpy, st);
-    if (rc) return rc;
-    *nb = pstride;
     return 0;
 }
 

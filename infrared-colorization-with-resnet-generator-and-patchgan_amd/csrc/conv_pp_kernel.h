@@ -1,6 +1,5 @@
-// bf16 / fp8 stride-1 convolution kernel template (conv_pp_kernel), shared by conv_pp.hip
-// (forward, backward-data, fused statistics) and conv_pp_ring.hip (the reflect-pad
-// backward-data with its ring folded in).  Design notes:
+// bf16 / fp8 stride-1 convolution kernel template (conv_pp_kernel), launched by conv_pp.hip
+// (forward, backward-data, fused statistics, the fp8 ResnetBlock path).  Design notes:
 //
 // bf16 stride-1 convolution, resident input halo, ping-pong wave groups.
 //
@@ -65,9 +64,6 @@
 #endif
 // bits: 1 no MFMA, 2 no weight DMA in the loop, 4 no fragment reads, 8 no barriers in the loop, 16 no epilogue
 #define PPX(b) ((PP_EXP & (b)) != 0)
-#ifndef RING_EXP
-#define RING_EXP 0  // A/B timing only: 1 skips the ring column terms, 2 the ring row terms
-#endif
 
 namespace {
 
@@ -111,22 +107,6 @@ struct PP {
 typedef int v8i_t __attribute__((ext_vector_type(8)));
 IRGAN_HD v8i_t cat8(i32x4 a, i32x4 b) { return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7); }
 
-// InstanceNorm-backward statistics in the STATS epilogue (irgan_conv_dgrad_in_stats):
-// with z set, the partials of the stored output v are (sum g, sum g*xhat) with
-// xhat = (z - mean) * rstd and g = v * act'(xhat) -- the reduce half of the IN backward
-// of the layer whose gradient this dgrad produces -- instead of (sum v, sum v^2).
-// pstride: partial rows per image (0: the patch count; > it leaves slots for the ring).
-struct InBwdStats {
-    const bf16_t* z;
-    int ldz, zoff, act, pstride;
-    const float* mr;
-};
-IRGAN_HD float in_act_grad(float xh, int act) {  // as norm.hip's act_grad
-    if (act == IRGAN_ACT_RELU) return xh > 0.f ? 1.f : 0.f;
-    if (act == IRGAN_ACT_LRELU) return xh > 0.f ? 1.f : 0.2f;
-    return 1.f;
-}
-
 // rg (irgan_conv_dgrad_reflect_line): the line-form reflect ring of a ResnetBlock backward-data
 // (conv_ring.hip: g[n][line][pos][c], lines top / bottom / left / right) folded onto the stored
 // bf16 dx in the store pass -- ring_line_fold_kernel's terms, order and roundings, so dx is
@@ -167,27 +147,7 @@ IRGAN_HD void ring_line_add(const irgan_conv_desc& d, const float* __restrict__ 
 // tiles, profiles/r02_s5_pp_one_ab.txt).  With more than one channel chunk the next chunk's halo cannot be
 // prefetched: after the last window that reads chunk c (4k+3 of its last tap) every
 // wave issues its pieces of chunk c+1, retires them and meets at one extra barrier.
-// RING (conv_pp_ring.hip: the reflect-padded ResnetBlock backward-data, ir:386-411, with
-// its pad ring folded in): bf16, 3x3, BN 256, Ho == H and Wo == W multiples of 16 with >= 2
-// patches per axis (host-checked).  Backward-data of conv(ReflectionPad2d(1)(x)) is the fold
-// of the zero-padded correlation g over the (H+2) x (W+2) domain; the interior of g is the
-// K loop's result, the ring values fold onto the mirrored pixels.  Every ring term is read
-// from the operand halo already in LDS, inside the K loop:
-//  * ring ROW (padded row -1 of a top patch / H of a bottom one): reads only tap row ty = 2
-//    / 0, i.e. one extra pixel fragment (dy row 0 = halo row 1 / H-1 = halo row 16) whose
-//    MFMAs accumulate straight into the mirrored row's accumulators (dx row 1 / H-2: the
-//    same columns, so the same lanes);
-//  * ring COLUMN (padded column -1 of a left patch / W of a right one): reads only tap
-//    column tx = 2 / 0; its 16 pixels (the patch rows) are one fragment whose lane r reads
-//    halo row r + ty at column 1 / 16 (a per-lane row address), accumulated in accC;
-//  * the corner (padded (-1 | H, -1 | W)) folds onto the same dx pixel as the ring column's
-//    row 1 / 14 and reads one tap: a fragment with only that lane's operand nonzero, into
-//    accC as well.
-// One wave group takes the ring row (group 0 top, group 1 bottom), the other the column and
-// corner, so no wave carries both.  After the K loop accC goes to an fp32 LDS table past the
-// staging rows, and emit() adds it onto dx column 1 / W-2 before the single bf16 rounding.
-template <int KH, int KW, int BN, bool ACC, bool STATS = false, bool F8 = false, bool ONE = false,
-          bool RING = false>
+template <int KH, int KW, int BN, bool ACC, bool STATS = false, bool F8 = false, bool ONE = false>
 __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
                                                          const bf16_t* __restrict__ w, const float* __restrict__ bias,
                                                          void* __restrict__ y, const void* __restrict__ mask,
@@ -195,7 +155,6 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
                                                          float2* __restrict__ part = nullptr,
                                                          const float* __restrict__ dqx = nullptr,
                                                          const float* __restrict__ dqw = nullptr,
-                                                         const InBwdStats ib = InBwdStats{},
                                                          const float* __restrict__ rg = nullptr) {
     constexpr int ESZ = F8 ? 1 : 2, CHN = 128 / ESZ;  // operand bytes, channels per 128-byte chunk
     const char* const xb = (const char*)x;
@@ -232,17 +191,6 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
     const int sub = lane >> 3;
     const int chunk = (lane & 7) ^ sub;  // source chunk for this lane's LDS slot (row & 7 == sub)
     const bool reflect = d.pad_mode == IRGAN_PAD_REFLECT;
-    static_assert(!RING || (KH == 3 && KW == 3 && BN == 256 && !F8 && !ONE), "ring fold: resblock dgrad tiles");
-    // RING: which sides of the padded domain this patch borders (block-uniform)
-    const bool rtop = RING && !(RING_EXP & 2) && pyi == 0, rbot = RING && !(RING_EXP & 2) && pyi == tpy - 1;
-    const bool rleft = RING && pxi == 0, rright = RING && pxi == tpx - 1;
-    // ring column: the wave group that does not take a ring row (bottom patches: group 0)
-    const bool rcol = !(RING_EXP & 1) && (rleft || rright) && grp == (rbot ? 0 : 1);
-    const int txc = rleft ? 2 : 0;          // the tap column the ring column reads
-    const int hxc = rleft ? 1 : PW;         // its dy column in halo coordinates
-    const int tyc = rtop ? 2 : 0;           // the tap row the corner reads
-    const int rcn = rtop ? 1 : PH - 2;      // ring-column pixel whose dx pixel the corner shares
-    const bool rcorner = rcol && (rtop || rbot);
 
     // DMA sources as byte offsets into buffer resources (out-of-range offsets
     // arrive as zeros: padding and Cout tails cost no address math in the loop)
@@ -301,11 +249,6 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     uint4 af[MI], bfr[NJ];
-    uint4 afr;  // RING: the ring-row or ring-column fragment of this K-step
-    uint4 afk;  // RING: the corner fragment (one lane nonzero)
-    f32x4 accC[RING ? NJ : 1];  // RING: the ring column (lane = patch row)
-#pragma unroll
-    for (int j = 0; j < (RING ? NJ : 1); ++j) accC[j] = f32x4{0.f, 0.f, 0.f, 0.f};
     v8i_t af8[MS], bf8[NJ];  // fp8: 32-byte fragments (chunks g, g + 4)
     // prologue: W(0), halo(0), W(1); retire the first two
     issue_w(0, 0, 0);
@@ -371,26 +314,6 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
                     const int K = (i + ty) * HWd + tx;
                     af[i] = *(const uint4*)(sH + (hbp + (tsw[K & 7] ^ (h * 64))) + K * 128);
                 }
-                if constexpr (RING) {
-                    // padded-domain ring rows: row -1 (top patches, group 0) reads only tap
-                    // row ty = 2 (dy row 0 = halo row 1), row H (bottom, group 1: fragment row
-                    // i = 8 of its 8) only ty = 0 (dy row H-1 = halo row 16)
-                    if (ty == 2 && grp == 0 && rtop) {
-                        const int K = HWd + tx;
-                        afr = *(const uint4*)(sH + (hbp + (tsw[K & 7] ^ (h * 64))) + K * 128);
-                    }
-                    if (ty == 0 && grp == 1 && rbot) {
-                        const int K = 8 * HWd + tx;
-                        afr = *(const uint4*)(sH + (hbp + (tsw[K & 7] ^ (h * 64))) + K * 128);
-                    }
-                    // ring column: lane r reads halo row r + ty at column hxc (the corner: the
-                    // halo row of dy row 0 / H-1, lane rcn only)
-                    if (rcol && tx == txc) {
-                        const char* hbuf = sH + (c & 1) * HBYTES;
-                        const int row = ((lane & 15) + ty) * HWd + hxc;
-                        afr = *(const uint4*)(hbuf + row * 128 + (((g0 + 4 * h) ^ (row & 7)) << 4));
-                    }
-                }
 #else
                 if (k == 0 && h == 0) {
 #pragma unroll
@@ -436,44 +359,6 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
                             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                                 __builtin_bit_cast(bf16x8_t, bfr[j]), __builtin_bit_cast(bf16x8_t, af[i]), acc[i][j],
                                 0, 0, 0);
-                    if constexpr (RING) {
-                        // the reflect fold of the ring rows: padded row -1 lands on dx row 1,
-                        // row H on row H-2 -- the same columns, so straight into those
-                        // fragments' accumulators (acc[1] of group 0, acc[6] of group 1)
-                        if (ty == 2 && grp == 0 && rtop) {
-#pragma unroll
-                            for (int j = 0; j < NJ; ++j)
-                                acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                                    __builtin_bit_cast(bf16x8_t, bfr[j]), __builtin_bit_cast(bf16x8_t, afr),
-                                    acc[1][j], 0, 0, 0);
-                        }
-                        if (ty == 0 && grp == 1 && rbot) {
-#pragma unroll
-                            for (int j = 0; j < NJ; ++j)
-                                acc[6][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                                    __builtin_bit_cast(bf16x8_t, bfr[j]), __builtin_bit_cast(bf16x8_t, afr),
-                                    acc[6][j], 0, 0, 0);
-                        }
-                        if (rcol && tx == txc) {
-#pragma unroll
-                            for (int j = 0; j < NJ; ++j)
-                                accC[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                                    __builtin_bit_cast(bf16x8_t, bfr[j]), __builtin_bit_cast(bf16x8_t, afr), accC[j],
-                                    0, 0, 0);
-                            if (rcorner && ty == tyc) {
-                                // the corner operand, read here (after the main MFMAs freed af[])
-                                const char* hbuf = sH + (c & 1) * HBYTES;
-                                const int rowk = (rtop ? 1 : PH) * HWd + hxc;
-                                const uint4 v = *(const uint4*)(hbuf + rowk * 128 + (((g0 + 4 * h) ^ (rowk & 7)) << 4));
-                                afk = (lane & 15) == rcn ? v : uint4{0u, 0u, 0u, 0u};
-#pragma unroll
-                                for (int j = 0; j < NJ; ++j)
-                                    accC[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                                        __builtin_bit_cast(bf16x8_t, bfr[j]), __builtin_bit_cast(bf16x8_t, afk),
-                                        accC[j], 0, 0, 0);
-                            }
-                        }
-                    }
                 }
                 if (h == HS - 1 && grp == 0 && !last_k) retire(halo_now);  // last window of step k
                 phase_barrier();
@@ -483,22 +368,6 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
     }
     if (grp == 0) phase_barrier();  // match group 1's extra barrier
     __syncthreads();                // all operand reads done: LDS becomes the staging buffer
-    // RING: the ring column (incl. the corner) into an fp32 LDS table past the staging rows;
-    // emit() adds it onto the mirrored pixels (dx col 1 / W-2)
-    constexpr int RING_OFF = 256 * PP<BN>::RSB;  // bytes: [16 rows][BN] fp32
-    if constexpr (RING) {
-        static_assert(!RING || RING_OFF + 16 * BN * 4 <= LDS, "ring table fits past the staging rows");
-        if (rleft || rright) {  // block-uniform
-            if (rcol) {
-                float* table = (float*)(smem + RING_OFF);
-#pragma unroll
-                for (int j = 0; j < NJ; ++j)
-                    *(float4*)(table + (lane & 15) * BN + cb + j * 16 + 4 * (lane >> 4)) =
-                        make_float4(accC[j][0], accC[j][1], accC[j][2], accC[j][3]);
-            }
-            __syncthreads();
-        }
-    }
 #if PPX(16)
     {
         float s = 0.f;
@@ -572,14 +441,6 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
                     v[2] = acc[i][j][2] * osc + b.z;
                     v[3] = acc[i][j][3] * osc + b.w;
                 }
-                if constexpr (RING) {
-                    // ring column (+ corner) -> dx col 1 (left) / W-2 = patch col 14 (right, W % 16 == 0)
-                    const int col = lane & 15, row = prow + i;
-                    if ((rleft && col == 1) || (rright && col == 14)) {
-                        const float4 cv = *(const float4*)((const float*)(smem + RING_OFF) + row * BN + cl);
-                        v[0] += cv.x; v[1] += cv.y; v[2] += cv.z; v[3] += cv.w;
-                    }
-                }
 #pragma unroll
                 for (int r = 0; r < 4; ++r) v[r] = conv_act(v[r], A);
                 const bool full = co + 4 <= d.Cout;
@@ -641,41 +502,17 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
         float s1[8], s2[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.f;
-        const bool bw = ib.z != nullptr;  // IN-backward statistics (block-uniform)
-        float mn[8], rs[8];
-        if (bw) {
-            const float4* m4 = (const float4*)(ib.mr + 2 * ((long)img * d.Cout + co8));
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float4 t4 = m4[k];
-                mn[2 * k] = t4.x; rs[2 * k] = t4.y; mn[2 * k + 1] = t4.z; rs[2 * k + 1] = t4.w;
-            }
-        }
         for (int m = tid / LPP; m < 256; m += PPASS) {
             const long pix = pix_of(m);
             if (pix < 0) continue;
             const uint4 v = *(const uint4*)(smem + m * RSB + c8 * 2);
             *(uint4*)((bf16_t*)y + pix * d.ldy + d.yoff + co8) = v;
             const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
-            if (bw) {
-                const uint4 zz = *(const uint4*)(ib.z + pix * ib.ldz + ib.zoff + co8);
-                const uint32_t zw[4] = {zz.x, zz.y, zz.z, zz.w};
 #pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const float f = __uint_as_float((k & 1) ? (wv[k / 2] & 0xffff0000u) : (wv[k / 2] << 16));
-                    const float zf = __uint_as_float((k & 1) ? (zw[k / 2] & 0xffff0000u) : (zw[k / 2] << 16));
-                    const float xh = (zf - mn[k]) * rs[k];
-                    const float g = f * in_act_grad(xh, ib.act);
-                    s1[k] += g;
-                    s2[k] += g * xh;
-                }
-            } else {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const float lo = __uint_as_float(wv[k] << 16), hi = __uint_as_float(wv[k] & 0xffff0000u);
-                    s1[2 * k] += lo; s2[2 * k] += lo * lo;
-                    s1[2 * k + 1] += hi; s2[2 * k + 1] += hi * hi;
-                }
+            for (int k = 0; k < 4; ++k) {
+                const float lo = __uint_as_float(wv[k] << 16), hi = __uint_as_float(wv[k] & 0xffff0000u);
+                s1[2 * k] += lo; s2[2 * k] += lo * lo;
+                s1[2 * k + 1] += hi; s2[2 * k + 1] += hi * hi;
             }
         }
         __syncthreads();  // staging reads done: reuse LDS for the cross-row reduction
@@ -709,7 +546,7 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
                 a += e.x;
                 b += e.y;
             }
-            const long patch = (long)img * (ib.pstride > 0 ? ib.pstride : tpx * tpy) + pyi * tpx + pxi;
+            const long patch = (long)img * (tpx * tpy) + pyi * tpx + pxi;
             part[patch * d.Cout + n0 + tid] = make_float2(a, b);
         }
         return;

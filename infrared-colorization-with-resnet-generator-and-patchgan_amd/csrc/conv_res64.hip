@@ -315,13 +315,7 @@ bool ok(const irgan_conv_desc* d) {
 }
 
 static int grid_for(int ntn, int tiles) {
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-            cus = 256;
-    }
+    const int cus = irgan_cu_count();
     const int g = (cus / ntn) * ntn;
     return g < tiles ? (g > 0 ? g : ntn) : tiles;
 }

@@ -25,16 +25,6 @@
 // and added into dx with 16-byte read-modify-writes.
 #include "common.h"
 
-#ifndef RING_TS
-#define RING_TS 0  // timing experiments only: per-block wall-clock stamps (irgan_debug_ring_ts)
-#endif
-#if RING_TS
-__device__ unsigned long long g_ring_ts[4096 * 6];
-#define RTS(i) do { if (threadIdx.x == 0) g_ring_ts[(blockIdx.y * gridDim.x + blockIdx.x) * 6 + (i)] = wall_clock64(); } while (0)
-#else
-#define RTS(i) do {} while (0)
-#endif
-
 namespace {
 
 // 64 band pixels per block: each block streams its (taps x Cin) weight slices from L2
@@ -52,31 +42,12 @@ IRGAN_HD int mirror_pos(int i, int n, int p) {  // virtual position folding onto
     return -0x40000000;
 }
 
-// IN-backward statistics of the band pixels this launch changes (irgan_conv_dgrad_in_stats):
-// with part set, block (image n, segment slot s, channel tile) writes the sums over its
-// pixels of (delta g, delta g * xhat), delta = the stored bf16 value after the add minus
-// the one before, g and xhat as conv_pp's InBwdStats -- so the interior partials plus
-// these equal the partials of the final tensor.  Row n*pstride + slot0 + s of part.
-struct RingInStats {
-    const bf16_t* z;
-    int ldz, zoff, act, pstride, slot0;
-    const float* mr;
-    float2* part;
-};
-IRGAN_HD float ring_act_grad(float xh, int act) {  // as norm.hip's act_grad
-    if (act == IRGAN_ACT_RELU) return xh > 0.f ? 1.f : 0.f;
-    if (act == IRGAN_ACT_LRELU) return xh > 0.f ? 1.f : 0.2f;
-    return 1.f;
-}
-
 __global__ __launch_bounds__(NWV * 64) void reflect_ring_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ dy,
                                                            const bf16_t* __restrict__ w, int p, void* __restrict__ dx,
-                                                           int segs_row, int segs_col,
-                                                           const RingInStats is = RingInStats{}) {
+                                                           int segs_row, int segs_col) {
     __shared__ __attribute__((aligned(16))) float red[NWV][NPIX][NCO + 4];  // +4: conflict-free row writes
     __shared__ int tap_list[MAXT];
     __shared__ int ntap_s;
-    RTS(0);
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int H = d.Ho, W = d.Wo;               // dx spatial size (stride 1)
@@ -161,7 +132,6 @@ __global__ __launch_bounds__(NWV * 64) void reflect_ring_kernel(const irgan_conv
         ntap_s = nt;
     }
     __syncthreads();
-    RTS(1);
     const int ntap = ntap_s;
 
     // mirrored column of fragment f's pixel (terms 1 and 2); fragments that hold no band
@@ -242,7 +212,6 @@ __global__ __launch_bounds__(NWV * 64) void reflect_ring_kernel(const irgan_conv
         mma(a1, b1, m1);
         ks = k2;
     }
-    RTS(2);
     // partial tiles -> LDS: lane holds pixel f*16 + (lane & 15), channels j*16 + 4*(lane>>4) + r
 #pragma unroll
     for (int f = 0; f < NF; ++f)
@@ -251,7 +220,6 @@ __global__ __launch_bounds__(NWV * 64) void reflect_ring_kernel(const irgan_conv
             *(float4*)&red[wv][f * 16 + (lane & 15)][j * 16 + 4 * (lane >> 4)] =
                 make_float4(acc[f][j][0], acc[f][j][1], acc[f][j][2], acc[f][j][3]);
     __syncthreads();
-    RTS(3);
     // thread -> (pixel, 8 channels): sum the NWV partials in order, add into dx
     static_assert(NPIX * NCO / 8 == NWV * 64, "one (pixel, 8 channels) per thread");
     const int pix_l = threadIdx.x >> 3, cg = (threadIdx.x & 7) * 8;
@@ -259,10 +227,7 @@ __global__ __launch_bounds__(NWV * 64) void reflect_ring_kernel(const irgan_conv
     const int yy = rowseg ? bpos : q, xx = rowseg ? q : bpos;
     const bool own = rowseg ? q < W : (q < H && mirror_pos(q, H, p) == -0x40000000);
     const int co = co0 + cg;
-    float st1[8], st2[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) st1[k] = st2[k] = 0.f;
-    if (own && co < d.Cout) {
+    if (!own || co >= d.Cout) return;
     float v[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = 0.f;
@@ -291,55 +256,15 @@ __global__ __launch_bounds__(NWV * 64) void reflect_ring_kernel(const irgan_conv
         if (full && (o & 7) == 0) {
             uint4 u = *(uint4*)yp;
             uint32_t wds[4] = {u.x, u.y, u.z, u.w};
-            float dlt[8];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const float o0 = __uint_as_float(wds[k] << 16), o1 = __uint_as_float(wds[k] & 0xffff0000u);
                 wds[k] = pk_bf16(o0 + v[2 * k], o1 + v[2 * k + 1]);
-                dlt[2 * k] = __uint_as_float(wds[k] << 16) - o0;
-                dlt[2 * k + 1] = __uint_as_float(wds[k] & 0xffff0000u) - o1;
             }
             *(uint4*)yp = uint4{wds[0], wds[1], wds[2], wds[3]};
-            if (is.part) {  // host guarantees the aligned bf16 path for every owned pixel
-                const uint4 zz = *(const uint4*)(is.z + pix * is.ldz + is.zoff + co);
-                const uint32_t zw[4] = {zz.x, zz.y, zz.z, zz.w};
-                const float4* m4 = (const float4*)(is.mr + 2 * ((long)n * d.Cout + co));
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const float4 t4 = m4[k];
-                    const float x0 = (__uint_as_float(zw[k] << 16) - t4.x) * t4.y;
-                    const float x1 = (__uint_as_float(zw[k] & 0xffff0000u) - t4.z) * t4.w;
-                    const float g0 = dlt[2 * k] * ring_act_grad(x0, is.act);
-                    const float g1 = dlt[2 * k + 1] * ring_act_grad(x1, is.act);
-                    st1[2 * k] = g0; st2[2 * k] = g0 * x0;
-                    st1[2 * k + 1] = g1; st2[2 * k + 1] = g1 * x1;
-                }
-            }
         } else {
             for (int k = 0; k < 8 && co + k < d.Cout; ++k) yp[k] = f2bf(bf2f(yp[k]) + v[k]);
         }
-    }
-    }
-#if RING_TS
-    __syncthreads();
-    RTS(4);
-#endif
-    if (!is.part) return;
-    // per-channel sums over the block's NPIX pixels, fixed order (deterministic)
-    __syncthreads();  // every wave is done reading red[][][]
-    float2* sr = (float2*)&red[0][0][0];  // [NPIX][NCO]
-#pragma unroll
-    for (int k = 0; k < 8; ++k) sr[pix_l * NCO + cg + k] = make_float2(st1[k], st2[k]);
-    __syncthreads();
-    if (threadIdx.x < NCO && co0 + (int)threadIdx.x < d.Cout) {
-        float a = 0.f, b = 0.f;
-        for (int r = 0; r < NPIX; ++r) {
-            const float2 e = sr[r * NCO + threadIdx.x];
-            a += e.x;
-            b += e.y;
-        }
-        const int slot = blockIdx.x - n * per_img;
-        is.part[((long)n * is.pstride + is.slot0 + slot) * d.Cout + co0 + threadIdx.x] = make_float2(a, b);
     }
 }
 
@@ -380,7 +305,6 @@ __global__ __launch_bounds__(256, 1) void ring_line_gemm_kernel(const irgan_conv
     __shared__ __attribute__((aligned(16))) char smem[WB + RV_ROWS * 512];
     char* const sW = smem;       // !WREG: [3 taps][64 co] rows of Cin bf16
     char* const sL = smem + WB;  // [RV_ROWS positions] rows of Cin bf16
-    RTS(0);
     const int nct = d.Cout / 64;
     const int line = blockIdx.x / nct, ct = blockIdx.x - line * nct;
     const int n0 = blockIdx.y * ipb, n1 = min(d.N, n0 + ipb);
@@ -445,8 +369,7 @@ __global__ __launch_bounds__(256, 1) void ring_line_gemm_kernel(const irgan_conv
             if (e < RV_ROWS * 32) *(uint4*)(sL + rv_off(e >> 5, e & 31)) = lv[u];
         }
         __syncthreads();
-        RTS(1);
-        if (n + 1 < n1) load_line(n + 1, lv);  // in flight under this image's GEMM
+            if (n + 1 < n1) load_line(n + 1, lv);  // in flight under this image's GEMM
         f32x4 acc[5];
 #pragma unroll
         for (int f = 0; f < 5; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -468,8 +391,7 @@ __global__ __launch_bounds__(256, 1) void ring_line_gemm_kernel(const irgan_conv
                                                                      __builtin_bit_cast(bf16x8_t, b[f]), acc[f], 0, 0, 0);
             }
         }
-        RTS(2);
-        // g[n][line][u + 1][co]: lane = position 16 f + l16 + ub, rows 4g + r = channels
+            // g[n][line][u + 1][co]: lane = position 16 f + l16 + ub, rows 4g + r = channels
         float* gl = gbuf + ((long)n * 4 + line) * RV_ROWS * d.Cout;
 #pragma unroll
         for (int f = 0; f < 5; ++f) {
@@ -477,10 +399,6 @@ __global__ __launch_bounds__(256, 1) void ring_line_gemm_kernel(const irgan_conv
             if (pos < RV_ROWS) *(float4*)(gl + (long)pos * d.Cout + co) = make_float4(acc[f][0], acc[f][1], acc[f][2], acc[f][3]);
         }
     }
-#if RING_TS
-    RTS(3);
-    RTS(4);
-#endif
 }
 
 // one thread per (owned dx pixel, 8 channels); targets per image: row 1 (W), row H-2 (W),
@@ -560,39 +478,11 @@ static bool ring_line_ok(const irgan_conv_desc* d, int p, long ws_floats) {
 // image per workgroup row); the fold runs in the interior launch's store pass
 bool ring_line_check(const irgan_conv_desc* d, int p, long ws_floats) { return ring_line_ok(d, p, ws_floats); }
 void ring_line_gemm_launch(const irgan_conv_desc* d, const void* dy, const void* w, float* ws, hipStream_t st) {
-    static const int ipb = getenv("IRGAN_RING_IPB") ? std::max(1, atoi(getenv("IRGAN_RING_IPB"))) : 1;
-    const int groups = irgan_cdiv(d->N, ipb);
-    static const bool wlds = getenv("IRGAN_RING_WLDS") != nullptr;
-    if (wlds)
-        ring_line_gemm_kernel<false><<<dim3(4 * (d->Cout / 64), groups), 256, 0, st>>>(*d, (const bf16_t*)dy,
-                                                                                      (const bf16_t*)w, ws, ipb);
-    else
-        ring_line_gemm_kernel<true><<<dim3(4 * (d->Cout / 64), groups), 256, 0, st>>>(*d, (const bf16_t*)dy,
-                                                                                     (const bf16_t*)w, ws, ipb);
+    // one image per workgroup row (2 / 4 images per workgroup measured slower: the launch
+    // is latency-bound, profiles/r03_ring_gemm_wreg_ab.txt)
+    ring_line_gemm_kernel<true><<<dim3(4 * (d->Cout / 64), d->N), 256, 0, st>>>(*d, (const bf16_t*)dy,
+                                                                              (const bf16_t*)w, ws, 1);
 }
-// conv_pp.hip's irgan_conv_dgrad_in_stats: the ring partial rows per image, and the
-// ring launch that writes them (bf16 output, Cout % 64 == 0, 8-aligned slices: checked there)
-int ring_in_slots(const irgan_conv_desc* d, int p) {
-    return 2 * p * (irgan_cdiv(d->Wo, NPIX) + irgan_cdiv(d->Ho, NPIX));
-}
-int ring_in_launch(const irgan_conv_desc* d, const void* dy, const void* w, int p, void* dx, const void* z, int ldz,
-                   int zoff, const float* mr, int act, void* part, int pstride, int slot0, hipStream_t st) {
-    if (d->dtype != IRGAN_BF16 || d->Cin % 32 || d->Cout % NCO || d->H < 2 * p + 2 || d->W < 2 * p + 2)
-        return IRGAN_EUNSUPPORTED;
-    const int segs_row = irgan_cdiv(d->Wo, NPIX), segs_col = irgan_cdiv(d->Ho, NPIX);
-    dim3 grid(d->N * 2 * p * (segs_row + segs_col), irgan_cdiv(d->Cout, NCO));
-    const RingInStats is{(const bf16_t*)z, ldz, zoff, act, pstride, slot0, mr, (float2*)part};
-    reflect_ring_kernel<<<grid, NWV * 64, 0, st>>>(*d, (const bf16_t*)dy, (const bf16_t*)w, p, dx, segs_row, segs_col,
-                                                   is);
-    IRGAN_LAUNCH_CHECK();
-    return 0;
-}
-
-#if RING_TS
-extern "C" int irgan_debug_ring_ts(unsigned long long* host, int n) {
-    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ring_ts), sizeof(unsigned long long) * n * 6);
-}
-#endif
 
 extern "C" int irgan_reflect_dgrad_ring(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p, void* dx,
                                         irgan_stream_t s) {

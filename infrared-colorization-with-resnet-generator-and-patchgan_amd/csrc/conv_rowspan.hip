@@ -428,6 +428,7 @@ extern "C" int irgan_conv_wgrad_rowspan(const irgan_conv_desc* d, const void* x,
     const long n = (long)d->Cout * d->KH * d->KW * d->Cin;
     const int per = 16, parts = irgan_cdiv(ng, per);
     float* slab = (ws && (long)(ng + parts) * n <= ws_cap) ? ws : nullptr;
+    if (!slab && irgan_det(d)) return IRGAN_EUNSUPPORTED;  // deterministic: the split kernels cap their splits
     if (d->KH == 7)
         wgrad_rowspan_kernel<7, 7><<<ng * nchunk, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)dy, dw, slab, nsx,
                                                                 nrb, nchunk);

@@ -261,17 +261,10 @@ void launch_t(const irgan_conv_desc* d, const void* x, const void* dy, float* dw
     // resident blocks per CU (LDS and VGPR limits, from the runtime) x 256 CUs: the
     // grid is sized to at most one full round -- a grid just above the resident
     // capacity runs a second, nearly empty round
-    static int slots = 0;
-    if (!slots) {
-        int b = 0, dev = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, wgrad_halo_kernel<BMC, KW, SX, WM, WN>, NW * 64, 0) !=
-                hipSuccess || b < 1)
-            b = 1;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-            cus = 256;
-        slots = b * cus;
-    }
+    static int occ = 0;  // resident blocks per CU (a property of the kernel on gfx950)
+    if (!occ && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, wgrad_halo_kernel<BMC, KW, SX, WM, WN>, NW * 64, 0) != hipSuccess || occ < 1))
+        occ = 1;
+    const int slots = occ * irgan_cu_count();
     const int ntco = irgan_cdiv(d->Cout, BMC), nci = d->Cin / 64;
     const int tiles = ntco * nci * d->KH;
     const int nseg = d->N * d->Ho * (d->Wo / 64);
@@ -286,6 +279,10 @@ void launch_t(const irgan_conv_desc* d, const void* x, const void* dy, float* dw
                 if ((tiles * s2) % 8 == 0) { splitk = s2; break; }
         }
     }
+    if (irgan_det(d)) {  // deterministic: no atomics -- at most the splits the workspace holds
+        const long fit = ws ? ws_cap / ((long)d->Cout * d->KH * d->KW * d->Cin) : 1;
+        if (splitk > fit) splitk = (int)(fit > 1 ? fit : 1);
+    }
     const int spb = irgan_cdiv(nseg, splitk);
     splitk = irgan_cdiv(nseg, spb);
     const long n = (long)d->Cout * d->KH * d->KW * d->Cin;
@@ -293,7 +290,7 @@ void launch_t(const irgan_conv_desc* d, const void* x, const void* dy, float* dw
     // fp32 atomics only at low split counts (resblock 3x3: 21 splits, -7 %), and
     // lose at 56-170 splits (down1 / up2 at 256^2: +3..12 %)
     // (deterministic mode: slabs at any split count)
-    float* slab = (ws && splitk > 1 && (splitk <= 24 || irgan_deterministic_mode()) && n % 4 == 0 &&
+    float* slab = (ws && splitk > 1 && (splitk <= 24 || irgan_det(d)) && n % 4 == 0 &&
                    (long)splitk * n <= ws_cap) ? ws : nullptr;
     wgrad_halo_kernel<BMC, KW, SX, WM, WN><<<tiles * splitk, WM * WN * 64, 0, st>>>(
         *d, (const bf16_t*)x, (const bf16_t*)dy, dw, spb, nseg, ntco, nci, zero, swz, slab);
@@ -313,9 +310,9 @@ extern "C" int irgan_conv_wgrad_halo(const irgan_conv_desc* d, const void* x, co
     if (d->Cin % 64 || d->ldx % 8 || d->xoff % 8 || d->ldy % 8 || d->yoff % 8 || d->Wo % 64 || d->sx != d->sy ||
         (d->sx != 1 && d->sx != 2))
         return IRGAN_EUNSUPPORTED;
-    static bf16_t* zero = nullptr;
-    if (!zero && hipGetSymbolAddress((void**)&zero, HIP_SYMBOL(g_wgh_zero_page)) != hipSuccess)
-        return IRGAN_EUNSUPPORTED;
+    static void* zero_cache[IRGAN_MAX_DEVICES];  // the zero page's address per device
+    const bf16_t* zero = (const bf16_t*)irgan_symbol(HIP_SYMBOL(g_wgh_zero_page), zero_cache);
+    if (!zero) return IRGAN_EUNSUPPORTED;
     static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
     const int s2 = d->sx == 2;
     static const bool wide = getenv("IRGAN_WGH_256") != nullptr;

@@ -53,7 +53,30 @@ IRGAN_HD int pc_t128(int r) { return ((r >> 1) & 1) | (((r >> 3) & 1) << 1); }
 IRGAN_HD int pc_t256(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
 
 constexpr int XPIECES = 9;               // 72 X span positions, 8 per piece
-constexpr int STAGES = 4;
+#ifndef WGPC_STAGES
+#define WGPC_STAGES 4
+#endif
+// LDS ring depth: segment k + STAGES - 1 is issued after barrier k, so STAGES - 2
+// segments are in flight while segment k + 1 is read (4: 100 KiB at BMC 128; 6: 150 KiB)
+// (BMC 64 keeps 4 stages: two of its blocks share a CU)
+template <int BMC>
+constexpr int stages_of() { return BMC == 128 ? WGPC_STAGES : 4; }
+static_assert(WGPC_STAGES >= 4, "the schedule needs segment k-1's stage free after barrier k");
+
+// wait until at most c segments of this loader's pieces (np per segment: PPL or PPL - 1)
+// are outstanding, c wave-uniform in [0, C]
+template <int PPL, int C>
+IRGAN_HD void wait_segs(int c, bool full) {
+    if constexpr (C == 0) {
+        wait_vmcnt<0>();
+    } else {
+        if (c >= C) {
+            if (full) wait_vmcnt<C * PPL>(); else wait_vmcnt<C * (PPL - 1)>();
+        } else {
+            wait_segs<PPL, C - 1>(c, full);
+        }
+    }
+}
 // BMC: co tile (128 or 64).  CW compute waves: 4 -> BMC co x 48 n per wave (1 per SIMD);
 // 8 -> BMC/2 co x 48 n (2 per SIMD)
 template <int BMC, int CW>
@@ -94,6 +117,7 @@ __global__ __launch_bounds__((PC<BMC, CW>::NT), 1) void wgrad_pc_kernel(const ir
                                                           int segs_per_block, int nseg, int ntco, int nci, int swz,
                                                           float* __restrict__ slab) {
     using Q = PC<BMC, CW>;
+    constexpr int STAGES = stages_of<BMC>();
     constexpr int APIECES = Q::APIECES, TP = Q::TP, STAGE = Q::STAGE, PPL = Q::PPL, DYR = Q::DYR;
     constexpr int DROWS = 1024 / DYR;  // dY rows per piece
     constexpr int NJ = KW, XPOS = 63 + KW;
@@ -194,31 +218,18 @@ __global__ __launch_bounds__((PC<BMC, CW>::NT), 1) void wgrad_pc_kernel(const ir
                 }
             }
         };
-        // prologue: segments 0..2 in flight, retire segment 0
-        issue(s_beg, 0);
-        if (nk > 1) issue(s_beg + 1, 1);
-        if (nk > 2) issue(s_beg + 2, 2);
-        if (nk > 2) {
-            if (np == PPL) wait_vmcnt<2 * PPL>(); else wait_vmcnt<2 * PPL - 2>();
-        } else if (nk > 1) {
-            if (np == PPL) wait_vmcnt<PPL>(); else wait_vmcnt<PPL - 1>();
-        } else {
-            wait_vmcnt<0>();
-        }
+        // prologue: segments 0..STAGES-2 in flight, retire segment 0
+        for (int k = 0; k < STAGES - 1; ++k)
+            if (k < nk) issue(s_beg + k, k);
+        wait_segs<PPL, STAGES - 2>(min(nk - 1, STAGES - 2), np == PPL);
         lds_barrier();
         for (int kt = 0; kt < nk; ++kt) {
-            // retire segment kt+1 (segment kt+2 may stay in flight), then barrier kt
-            if (kt + 1 < nk && !PCX(1)) {
-                if (kt + 2 < nk) {
-                    if (np == PPL) wait_vmcnt<PPL>(); else wait_vmcnt<PPL - 1>();
-                } else {
-                    wait_vmcnt<0>();
-                }
-            }
+            // retire segment kt+1 (segments kt+2 .. kt+STAGES-2 may stay in flight), then barrier kt
+            if (kt + 1 < nk && !PCX(1)) wait_segs<PPL, STAGES - 3>(min(nk - kt - 2, STAGES - 3), np == PPL);
 #if !PCX(8)
             lds_barrier();
 #endif
-            if (kt + 3 < nk && !PCX(2)) issue(s_beg + kt + 3, (kt + 3) % STAGES);
+            if (kt + STAGES - 1 < nk && !PCX(2)) issue(s_beg + kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
         }
         return;
     }
@@ -365,13 +376,7 @@ extern "C" int irgan_conv_wgrad_pc(const irgan_conv_desc* d, const void* x, cons
         d->ldy % 8 || d->yoff % 8 || (long)d->N * d->H * d->W * d->ldx * 2 >= (1L << 31) ||
         (long)d->N * d->Ho * d->Wo * d->ldy * 2 >= (1L << 31))
         return IRGAN_EUNSUPPORTED;
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-            cus = 256;
-    }
+    const int cus = irgan_cu_count();
     static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
     const int ntco = d->Cout / BMC, nci = d->Cin / 64;
     const int tiles = ntco * nci * d->KH;
@@ -385,6 +390,10 @@ extern "C" int irgan_conv_wgrad_pc(const irgan_conv_desc* d, const void* x, cons
             for (int s2 = splitk - 1; s2 >= 1 && s2 >= splitk - 8; --s2)
                 if ((tiles * s2) % 8 == 0) { splitk = s2; break; }
         }
+    }
+    if (irgan_det(d)) {  // deterministic: no atomics -- at most the splits the workspace holds
+        const long fit = ws ? ws_cap / ((long)d->Cout * d->KH * d->KW * d->Cin) : 1;
+        if (splitk > fit) splitk = (int)(fit > 1 ? fit : 1);
     }
     const int spb = irgan_cdiv(nseg, splitk);
     splitk = irgan_cdiv(nseg, spb);

@@ -482,7 +482,7 @@ extern "C" int irgan_ssim(const float* a, const float* b, int32_t N, int32_t H, 
 
 // t = ++*count; prm = {lr / (1 - b1^t), sqrt(1 - b2^t)}: the host formula of irgan_adam's
 // arguments (ops.adam), in fp64 and then rounded to fp32, evaluated on the device
-__global__ void adam_prep_kernel(int32_t* count, double lr, double b1, double b2, float* prm) {
+static __global__ void adam_prep_kernel(int32_t* count, double lr, double b1, double b2, float* prm) {
     if (threadIdx.x != 0) return;
     const int t = *count + 1;
     *count = t;

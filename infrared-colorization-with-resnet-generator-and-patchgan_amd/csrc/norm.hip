@@ -492,64 +492,6 @@ __global__ __launch_bounds__(TPB) void apply_kernel(Slice X, int HW, int C, cons
     if constexpr (F8) fp8_block_amax(amx, q8.amax, blockIdx.x);
 }
 
-// finalize_kernel + apply_kernel in one launch (bf16, 8 channels per thread): each block
-// first reduces the conv epilogue's partials of its image into (mean, rstd) for every
-// channel -- in finalize_kernel's exact fp64 order (lanes b mod 32, then the 32 lanes in
-// order), so mr is bit-identical -- keeps them in LDS (block 0 of each image also stores
-// them for the backward), then normalises its pixel range: y = act((x - mean) * rstd) [+ res].
-constexpr int AF_T = 1024;
-__global__ __launch_bounds__(AF_T) void apply_fin_kernel(const float2* __restrict__ part, int nb,
-                                                         const bf16_t* __restrict__ x, int ldx, int xoff, int HW,
-                                                         int C, float* __restrict__ mr, int act,
-                                                         const bf16_t* __restrict__ res, int ldr, int roff,
-                                                         bf16_t* __restrict__ y, int ldy, int yoff, int ppb) {
-    __shared__ float2 smr[AF_T];
-    const int n = blockIdx.y;
-    for (int c = threadIdx.x; c < C; c += AF_T) {
-        double s = 0.0, q = 0.0;
-        for (int k = 0; k < FS; ++k) {
-            double a = 0.0, b = 0.0;
-            for (int j = k; j < nb; j += FS) {
-                const float2 v = part[((long)n * nb + j) * C + c];
-                a += v.x;
-                b += v.y;
-            }
-            s += a;
-            q += b;
-        }
-        const double mean = s / HW;
-        double var = q / HW - mean * mean;
-        if (var < 0) var = 0;
-        const float m = (float)mean, r = (float)(1.0 / sqrt(var + 1e-5));
-        smr[c] = make_float2(m, r);
-        if (blockIdx.x == 0) {
-            mr[2 * ((long)n * C + c)] = m;
-            mr[2 * ((long)n * C + c) + 1] = r;
-        }
-    }
-    __syncthreads();
-    const int CG = C / 8;
-    const int p0 = blockIdx.x * ppb, np = min(HW - p0, ppb);
-    const int items = np * CG;
-#pragma unroll 4
-    for (int i = threadIdx.x; i < items; i += AF_T) {
-        const int pl = i / CG, c = (i - pl * CG) * 8;
-        const long p = (long)n * HW + p0 + pl;
-        float v[8];
-        ld8(x, IRGAN_BF16, p * ldx + xoff + c, v);
-        float rv[8];
-        if (res) ld8(res, IRGAN_BF16, p * ldr + roff + c, rv);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const float2 t = smr[c + k];
-            float h = (v[k] - t.x) * t.y;
-            if (act == IRGAN_ACT_RELU) h = h > 0.f ? h : 0.f;
-            else if (act == IRGAN_ACT_LRELU) h = h > 0.f ? h : 0.2f * h;
-            v[k] = res ? h + rv[k] : h;
-        }
-        st8(y, IRGAN_BF16, p * ldy + yoff + c, v);
-    }
-}
 
 bool vec_ok(int C, std::initializer_list<int> lds) {
     if (C % V) return false;
@@ -638,35 +580,7 @@ extern "C" int irgan_in_finalize(const void* part, int32_t N, int32_t HW, int32_
     return 0;
 }
 
-extern "C" int irgan_in_bwd_finalize(const void* part, int32_t N, int32_t HW, int32_t C, int32_t nb, float* red,
-                                     irgan_stream_t s) {
-    if ((long)N * HW * C <= 0) return 0;
-    if (!part || !red || nb < 1 || nb > IRGAN_IN_PARTS) return IRGAN_EINVAL;
-    finalize_kernel<<<dim3(irgan_cdiv(C, FC), N), 256, 0, (hipStream_t)s>>>((const float2*)part, red, N, C, nb, HW, 1);
-    IRGAN_LAUNCH_CHECK();
-    return 0;
-}
 
-extern "C" int irgan_in_finalize_apply(const void* part, int32_t nb, const void* x, int32_t N, int32_t HW, int32_t C,
-                                       int32_t ldx, int32_t xoff, float* mr, int32_t act, const void* res,
-                                       int32_t ldr, int32_t roff, void* y, int32_t ldy, int32_t yoff,
-                                       irgan_stream_t s) {
-    if ((long)N * HW * C <= 0) return 0;
-    if (!part || !x || !mr || !y || nb < 1 || nb > IRGAN_IN_PARTS) return IRGAN_EINVAL;
-    if (C > AF_T || !vec_ok(C, {ldx, xoff, ldy, yoff}) || (res && !vec_ok(C, {ldr, roff})) ||
-        getenv("IRGAN_NO_FIN_APPLY"))
-        return IRGAN_EUNSUPPORTED;
-    // ~512 blocks over the grid (two per CU), whole images per block row
-    int bpi = (512 + N - 1) / N;
-    if (bpi > HW) bpi = HW;
-    const int ppb = irgan_cdiv(HW, bpi);
-    bpi = irgan_cdiv(HW, ppb);
-    apply_fin_kernel<<<dim3(bpi, N), AF_T, 0, (hipStream_t)s>>>(
-        (const float2*)part, nb, (const bf16_t*)x, ldx, xoff, HW, C, mr, act, (const bf16_t*)res, ldr, roff,
-        (bf16_t*)y, ldy, yoff, ppb);
-    IRGAN_LAUNCH_CHECK();
-    return 0;
-}
 
 // the forward apply as rows8_kernel<4> (bf16, 8-channel vectors, no xhat), grid as the
 // other row passes; q8: also the fp8 copy of y (irgan_in_apply_fp8)
@@ -743,7 +657,7 @@ extern "C" int irgan_in_bwd_apply(const void* dy, int32_t dy_dtype, int32_t lddy
 
 // db[c] += sum of the nb partials' .x: FC channels x FS partial lanes per block (lane k adds
 // partials k, k + FS, ...), then the FS lanes of a channel in order (deterministic)
-__global__ __launch_bounds__(256) void colsum_finalize_kernel(const float2* __restrict__ part, float* __restrict__ db,
+static __global__ __launch_bounds__(256) void colsum_finalize_kernel(const float2* __restrict__ part, float* __restrict__ db,
                                                               int nb, int C) {
     __shared__ double sp[FS][FC];
     const int cl = threadIdx.x % FC, sub = threadIdx.x / FC, c = blockIdx.x * FC + cl;

@@ -251,14 +251,12 @@ class Buffers:
 
     def __init__(self, device):
         self.device, self.d, self.state = device, {}, {}
-        self.allocs = 0   # (re)allocations so far: a captured step is valid while this is unchanged
 
     def get(self, name, shape, dtype):
         t = self.d.get(name)
         if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype:
             t = torch.empty(shape, dtype=dtype, device=self.device)
             self.d[name] = t
-            self.allocs += 1
         return t
 
     def zeros(self, name, shape, dtype):
@@ -267,7 +265,6 @@ class Buffers:
         if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype:
             t = torch.zeros(shape, dtype=dtype, device=self.device)
             self.d[name] = t
-            self.allocs += 1
         return t
 
     def flat(self, name, numel, dtype=torch.float32):
@@ -275,7 +272,6 @@ class Buffers:
         if t is None or t.numel() < numel or t.dtype != dtype:
             t = torch.empty(numel, dtype=dtype, device=self.device)
             self.d[name] = t
-            self.allocs += 1
         return t
 
 
@@ -291,14 +287,7 @@ class INLayer:
     where a fused kernel exists (irgan_conv_fwd_stats) instead of a separate pass.
     """
     fused_stats = True
-    fused_resample = not os.environ.get("IRGAN_NO_IN_RESAMPLE")
-    # finalize + apply in one launch (irgan_in_finalize_apply): bit-identical, but the step is
-    # unchanged (1062 vs 1062 img/s, DESIGN.md 8): opt-in IRGAN_FIN_APPLY=1
-    fused_fin_apply = bool(os.environ.get("IRGAN_FIN_APPLY"))
-    # measured (DESIGN.md 8): the fused reduce adds ~16 us to each resblock dgrad (its
-    # epilogue reads z at one block per CU) against ~19 us for the separate reduce pass:
-    # +0.2 % per step, within box noise -- opt-in (IRGAN_FUSED_IN_BWD=1)
-    fused_in_bwd = bool(os.environ.get("IRGAN_FUSED_IN_BWD"))
+    fused_resample = True
     sum_bias_grad = False
 
     def fwd(self, bufs: Buffers, name: str, x: Feat, y: Feat, act, res: Feat = None, xhat=None, nb=0, q8=None):
@@ -309,9 +298,6 @@ class INLayer:
         N, C = x.N, x.C
         work = bufs.flat("in_work", ops.IN_PARTS * N * C, torch.float64)
         mr = bufs.get("mr_" + name, (N * C * 2,), torch.float32)
-        if nb and xhat is None and q8 is None and INLayer.fused_fin_apply and \
-                ops.in_finalize_apply(x, work, nb, mr, y, act=act, res=res):
-            return
         if nb:
             ops.in_finalize(x, work, nb, mr)
         else:
@@ -357,28 +343,15 @@ class INLayer:
         ops.in_apply(z, mr, a, act=act)
         plain(a, y)
 
-    def bwd(self, bufs: Buffers, name: str, dy: Feat, z: Feat, act, dx: Feat, db=None, dy2: Feat = None, q8=None,
-            nb=0):
+    def bwd(self, bufs: Buffers, name: str, dy: Feat, z: Feat, act, dx: Feat, db=None, dy2: Feat = None, q8=None):
         """z: the PRE-norm input kept from forward; act: the activation after IN.
-        q8: also write dx's fp8 copy (ops.in_backward).  nb > 0: dy's reduce partials
-        are already in the work buffer (ops.conv_dgrad_in wrote them with dy)."""
+        q8: also write dx's fp8 copy (ops.in_backward)."""
         N, C = z.N, z.C
         work = bufs.flat("in_work", ops.IN_PARTS * N * C, torch.float64)
         red = bufs.flat("in_red", 2 * N * C)
         mr = bufs.d["mr_" + name]
         ops.in_backward(dy, z, act, mr, work, red, dx, db=db if INLayer.sum_bias_grad else None, dy2=dy2,
-                        q8=q8 if not INLayer.sum_bias_grad else None, nb=nb)
-
-    @staticmethod
-    def dgrad_in(bufs: Buffers, name: str, pc, dy: Feat, dx: Feat, z: Feat, act, accumulate=False):
-        """Reflect-padded resblock backward-data that also writes the IN-backward partials of
-        dx for the IN ``name`` (pre-norm input z): returns nb for bwd(nb=...), 0 if it did
-        not run (INLayer.fused_in_bwd off, bias-grad mode, or a layer the kernel does not take)."""
-        if not INLayer.fused_in_bwd or INLayer.sum_bias_grad:
-            return 0
-        work = bufs.flat("in_work", ops.IN_PARTS * z.N * z.C, torch.float64)
-        return ops.conv_dgrad_in(pc, dy, dx, z, bufs.d["mr_" + name], act, work, accumulate=accumulate)
-
+                        q8=q8 if not INLayer.sum_bias_grad else None)
 
 class NoNorm(INLayer):
     """norm='none' (ir:162-163: ``lambda num_features: Identity()``): the layer is just its
@@ -411,20 +384,15 @@ class NoNorm(INLayer):
         ops.conv_fwd(pc, x, z, bias=pc.bias is not None)
         return self._ident(bufs, name, z.N, z.C)
 
-    def bwd(self, bufs, name, dy, z, act, dx, db=None, dy2=None, q8=None, nb=0):
-        if dy2 is not None or q8 is not None or nb:
-            raise NotImplementedError("NoNorm.bwd: dy2 / q8 / nb are InstanceNorm-path features")
+    def bwd(self, bufs, name, dy, z, act, dx, db=None, dy2=None, q8=None):
+        if dy2 is not None or q8 is not None:
+            raise NotImplementedError("NoNorm.bwd: dy2 / q8 are InstanceNorm-path features")
         if act == ACT_NONE and dx.t.data_ptr() == dy.t.data_ptr() and dx.off == dy.off:
             pass                                   # identity, in place
         else:
             ops.act_bwd(dy, z, act, dx)            # z > 0 <=> act(z) > 0 for ReLU / LeakyReLU
         if db is not None:
             ops.channel_sum(dx, db)
-
-    @staticmethod
-    def dgrad_in(*a, **kw):
-        return 0
-
 
 def make_norm(norm: str) -> INLayer:
     """The engine's per-layer norm for Config.norm (ir:154-165): 'instance' or 'none'
@@ -508,8 +476,6 @@ class GeneratorEngine:
                       [f"r{b}_{i}" for b in range(n_blocks) for i in (1, 2)]}
         assert len(self.norms) == n_in
         self.bufs = Buffers(store.device)
-        # a second stream for the ResnetBlock backward-data rings (set by GANStep; None: in line)
-        self.ring_stream = None
 
     def pack(self):
         if self._pack_batch is None:
@@ -531,24 +497,14 @@ class GeneratorEngine:
         ops.pad(x, xp, 1, "replicate")
         return xp
 
-    def _res_dgrad(self, g: Buffers, pc, dy: Feat, dx: Feat, accumulate, padbuf, ring_stream=None):
-        """dx (+)= backward-data of a ResnetBlock conv for the padding type.  With
-        ring_stream (reflect), the pad ring runs there: returns the event dx's consumer waits on."""
+    def _res_dgrad(self, g: Buffers, pc, dy: Feat, dx: Feat, accumulate, padbuf):
+        """dx (+)= backward-data of a ResnetBlock conv for the padding type."""
         if self.padding_type != "replicate":
-            return ops.conv_dgrad(pc, dy, dx, accumulate=accumulate, pad_buf=padbuf, ring_stream=ring_stream)
+            ops.conv_dgrad(pc, dy, dx, accumulate=accumulate, pad_buf=padbuf)
+            return
         dxp = Feat(g.get("res_dxp", (dx.N, dx.H + 2, dx.W + 2, dx.C), self.tdt))
         ops.conv_dgrad(pc, dy, dxp)
         ops.pad_fold(dxp, dx, 1, "replicate", accumulate=accumulate)
-        return None
-
-    def _res_dgrad_wgrad(self, g: Buffers, pc, dy: Feat, dx: Feat, accumulate, padbuf, wgrad):
-        """The backward-data of a ResnetBlock conv, then its weight gradient (``wgrad()``).
-        With self.ring_stream set, the reflect ring of the backward-data runs on that stream
-        beside the weight gradient (which leaves CUs idle), joined before dx is read."""
-        ev = self._res_dgrad(g, pc, dy, dx, accumulate, padbuf, ring_stream=self.ring_stream)
-        wgrad()
-        if ev is not None:
-            torch.cuda.current_stream().wait_event(ev)
 
     def _bgrad(self, key):
         """Flat-buffer slice of parameter ``key``'s gradient, None when the layout has no
@@ -752,7 +708,6 @@ class GeneratorEngine:
         dt_ = Feat(g.get("dtmp", (B, H2, W2, c2), T))
         nb2 = 2 * self.n_blocks
         dy8 = Feat(g.get("dy8", (B, H2, W2, c2), torch.float8_e4m3fn)) if self.fp8 else None
-        nb_h = 0
         k1, k2 = self.res_keys
         for b in reversed(range(self.n_blocks)):
             p1, p2 = self.res[b]
@@ -766,43 +721,27 @@ class GeneratorEngine:
             xin2 = Feat(g.d[f"xp2_{b}"]) if self.padding_type == "replicate" else t2
             A = self.f8a if self.fp8 else None
             s2, s1 = nb2 + 2 * b, nb2 + 2 * b + 1
-            # nb_h: dh's IN-backward partials for r{b}_2, written by the previous block's dgrad
             self.norms[f"r{b}_2"].bwd(g, f"r{b}_2", dh, r2, ACT_NONE, dt_, db=self._bgrad(f"{key}{k2}.bias"),
-                                      q8=A.spec(s2, dy8) if self.fp8 else None, nb=nb_h)
+                                      q8=A.spec(s2, dy8) if self.fp8 else None)
             dr = Feat(g.get("dtmp2", (B, H2, W2, c2), T))
-            nb_r = 0
-            wg2 = lambda: wg(p2, f"{key}{k2}", xin2, dt_)  # noqa: E731
-            wg1 = lambda: wg(p1, f"{key}{k1}", xin1, dr)   # noqa: E731
             if self.fp8:
-                wg2()
+                wg(p2, f"{key}{k2}", xin2, dt_)
                 A.ensure(s2, dt_, dy8)
                 ops.conv_dgrad_fp8(p2, *self._w8(4 * b + 3), dy8, A.dqp(s2), dt_, dr)
             else:
-                # the reduce of r{b}_1's IN backward rides in this dgrad's epilogue (not through a dropout)
-                if not drop:
-                    nb_r = self.norms[f"r{b}_1"].dgrad_in(g, f"r{b}_1", p2, dt_, dr, r1, ACT_RELU)
-                if not nb_r:
-                    self._res_dgrad_wgrad(g, p2, dt_, dr, False, padbuf, wg2)
-                else:
-                    wg2()
+                self._res_dgrad(g, p2, dt_, dr, False, padbuf)
+                wg(p2, f"{key}{k2}", xin2, dt_)
                 if drop:   # backward of the dropout: the same mask and scale on the gradient
                     ops.dropout(dr, dr, g.state["dropout_seed"] + 2 * b)
             self.norms[f"r{b}_1"].bwd(g, f"r{b}_1", dr, r1, ACT_RELU, dr, db=self._bgrad(f"{key}{k1}.bias"),
-                                      q8=A.spec(s1, dy8) if self.fp8 else None, nb=nb_r)
-            nb_h = 0
+                                      q8=A.spec(s1, dy8) if self.fp8 else None)
             if self.fp8:
-                wg1()
+                wg(p1, f"{key}{k1}", xin1, dr)
                 A.ensure(s1, dr, dy8)
                 ops.conv_dgrad_fp8(p1, *self._w8(4 * b + 1), dy8, A.dqp(s1), dr, dh, accumulate=True)
             else:
-                # ... and the reduce of block b-1's r2 IN backward in this one (dh = d h_b)
-                if b > 0:
-                    nb_h = self.norms[f"r{b - 1}_2"].dgrad_in(g, f"r{b - 1}_2", p1, dr, dh, Feat(g.d[f"r2_{b - 1}"]),
-                                                              ACT_NONE, accumulate=True)
-                if not nb_h:
-                    self._res_dgrad_wgrad(g, p1, dr, dh, True, padbuf, wg1)
-                else:
-                    wg1()
+                self._res_dgrad(g, p1, dr, dh, True, padbuf)
+                wg(p1, f"{key}{k1}", xin1, dr)
             ready(f"{key}{k1}.weight")
         if self.fp8:
             self.f8a.update(nb2, nb2)   # next step's backward-data scales
@@ -883,35 +822,13 @@ class DiscriminatorEngine:
             x = y
         return x.t
 
-    def backward(self, dout: torch.Tensor, want_wgrad=True, want_dinput=False, tag="", bufs: Buffers = None,
-                 wgrad_stream=None):
+    def backward(self, dout: torch.Tensor, want_wgrad=True, want_dinput=False, tag="", bufs: Buffers = None):
         """dout: dL/dlogits fp32 (same shape as forward output).  Weight grads
-        accumulate into store.grad; returns d input (fp32 NHWC) if asked.
-
-        wgrad_stream: run each layer's weight (and bias) gradient on that stream, beside the
-        backward-data chain on the current one (they read the same dY, which nothing rewrites
-        afterwards); the current stream waits for it before returning."""
+        accumulate into store.grad; returns d input (fp32 NHWC) if asked."""
         g, T, S = bufs or self.bufs, self.tdt, self.store
         acts, pre = g.state[tag]
         G = S.grad
         n = len(self.packs)
-        if wgrad_stream is not None and torch.cuda.is_current_stream_capturing():
-            wgrad_stream = None   # (a third stream inside the opt-in HIP graph capture crashed capture_end)
-        cur = torch.cuda.current_stream() if wgrad_stream is not None else None
-
-        def off_stream(fn):
-            if cur is None:
-                fn()
-                return
-            ev = torch.cuda.Event()
-            ev.record(cur)
-            wgrad_stream.wait_event(ev)
-            with torch.cuda.stream(wgrad_stream):
-                fn()
-
-        def join():
-            if cur is not None:
-                cur.wait_stream(wgrad_stream)
         dbuf = g.zeros(f"{tag}dout_t", tuple(dout.shape[:3]) + (8,), T)   # 1-ch logits grad, padded to 8
         ops.axpby(Feat(dout), 1.0, Feat(dbuf, 0, dout.shape[3]))
         dy = Feat(dbuf, 0, self.packs[-1].cout_eff)
@@ -928,14 +845,10 @@ class DiscriminatorEngine:
             elif want_wgrad:  # layer 0: LReLU mask already folded into dy by the layer-1 dgrad
                 bias_sum = dy
             if want_wgrad:
-                def wgrad(pc=pc, key=key, x=x, dy=dy, bias_sum=bias_sum):
-                    if bias_sum is not None:
-                        ops.channel_sum(bias_sum, S.krsc(key + ".bias", G))
-                    ops.conv_wgrad(pc.spec, x, Feat(dy.t, dy.off, pc.spec.cout), S.krsc(key + ".weight", G),
-                                   self.dtype)
-                off_stream(wgrad)
+                if bias_sum is not None:
+                    ops.channel_sum(bias_sum, S.krsc(key + ".bias", G))
+                ops.conv_wgrad(pc.spec, x, Feat(dy.t, dy.off, pc.spec.cout), S.krsc(key + ".weight", G), self.dtype)
             if i == 0:
-                join()
                 if not want_dinput:
                     return None
                 dx = Feat(g.get(f"{tag}dinput", (x.N, x.H, x.W, pc.spec.cin), torch.float32))
@@ -1068,12 +981,13 @@ def replica_digest(tensors) -> torch.Tensor:
     return torch.stack(out)
 
 
-def replicas_identical(tensors, group=None) -> bool:
+def replicas_identical(tensors, group=None, force=False) -> bool:
     """True when every rank of ``group`` holds bit-identical ``tensors`` (max == min of
-    the digests over ranks); True without a process group."""
+    the digests over ranks); True without a process group (and at world size 1 unless
+    ``force``: then the MAX / MIN collectives run anyway)."""
     import torch.distributed as dist
     d = replica_digest(tensors)
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+    if not (dist.is_available() and dist.is_initialized()) or (dist.get_world_size(group) == 1 and not force):
         return True
     if dist.get_backend(group) != "nccl":
         d = d.cpu()
@@ -1097,17 +1011,21 @@ class BucketedAllreduce:
     same element-wise mean as one whole-buffer all-reduce.
     """
 
-    def __init__(self, store: ParamStore, group=None, bucket_bytes=8 << 20):
+    def __init__(self, store: ParamStore, group=None, bucket_bytes=8 << 20, force=False):
+        """force: issue the collectives even at world size 1 (a process group must be
+        initialised) -- the RCCL path exercised on one GPU (tests/test_gpu_dp.py)."""
         self.store, self.group, self.bucket_bytes = store, group, bucket_bytes
         self.end, self.works, self.world, self.avg = store.numel, [], 1, True
         import torch.distributed as dist
+        self.force = False
         if dist.is_available() and dist.is_initialized():
             self.world = dist.get_world_size(group)
             self.avg = dist.get_backend(group) == "nccl"
+            self.force = bool(force)
 
     @property
     def active(self):
-        return self.world > 1
+        return self.world > 1 or self.force
 
     def _launch(self, start):
         import torch.distributed as dist
@@ -1153,11 +1071,6 @@ class BucketedAllreduce:
 
 # IRGAN_JOIN_TIMING=1: (event, event) pairs around the main stream's wait for the side
 # stream's D step (tools: how much of the step is the D step on the critical path)
-# host enqueue order of the two streams' work after the G forward: the main stream's G-step
-# terms first, then the side stream's D step (1204 vs 1199 img/s, 3 same-box pairs,
-# profiles/r03_terms_first_ab.txt); IRGAN_D_FIRST=1 restores the D step first
-TERMS_FIRST = not os.environ.get("IRGAN_D_FIRST")
-VGG_AFTER_GFWD = bool(os.environ.get("IRGAN_VGG_AFTER_GFWD"))
 JOIN_TIMES = [] if os.environ.get("IRGAN_JOIN_TIMING") else None
 
 
@@ -1168,7 +1081,10 @@ class GANStep:
     """
 
     def __init__(self, G: ParamStore, D: ParamStore, V: ParamStore, cfg, dtype=BF16, process_group=None,
-                 gen: GeneratorEngine = None, dis: DiscriminatorEngine = None, vgg: VGGEngine = None):
+                 gen: GeneratorEngine = None, dis: DiscriminatorEngine = None, vgg: VGGEngine = None,
+                 force_reduce=False):
+        """force_reduce: run the gradient collectives even at world size 1 (see
+        BucketedAllreduce): the DP schedule on one device."""
         self.G, self.D, self.V, self.cfg, self.dtype = G, D, V, cfg, dtype
         self.tdt = ops.TORCH_DT[dtype]
         self.gen = gen or GeneratorEngine(G, dtype, ngf=cfg.ngf, input_nc=cfg.input_nc, output_nc=cfg.output_nc,
@@ -1180,8 +1096,8 @@ class GANStep:
         self.bufs = Buffers(G.device)
         self.losses = torch.zeros(8, dtype=torch.float64, device=G.device)
         self.pg = process_group
-        self.g_reduce = BucketedAllreduce(G, process_group)
-        self.d_reduce = BucketedAllreduce(D, process_group)
+        self.g_reduce = BucketedAllreduce(G, process_group, force=force_reduce)
+        self.d_reduce = BucketedAllreduce(D, process_group, force=force_reduce)
         self.lr_scale = 1.0
         # the D step (D forward/backward on [real; fake] and its all-reduce) runs on a
         # side stream, concurrently with the G-step terms that do not read D (L1,
@@ -1189,25 +1105,7 @@ class GANStep:
         self.side = None
         if G.device.type == "cuda" and not os.environ.get("IRGAN_NO_D_OVERLAP"):
             self.side = torch.cuda.Stream(device=G.device)
-        # opt-in (IRGAN_RING_SIDE=1): the G backward's ResnetBlock reflect rings on the (then
-        # idle) side stream beside each conv's weight gradient.  Measured slower than in line
-        # (1152 vs 1168 img/s, gpurun_out/r03_t): on the 16 CUs the weight gradient leaves idle
-        # the ring takes ~85 us, longer than the weight gradient, and the two event edges per
-        # conv cost ~4 us of main-stream bubble each
-        if self.side is not None and dtype == BF16 and os.environ.get("IRGAN_RING_SIDE"):
-            self.gen.ring_stream = self.side
-        # opt-in (IRGAN_DWG_STREAM=1): the D step's weight gradients on a third stream beside its
-        # backward-data chain.  The main stream's wait for the D step drops 0.84 -> 0.62 ms, but
-        # the step does not gain (1169 vs 1173 img/s, gpurun_out/r03_z): the GPU is busy 99 % of
-        # the step either way, the third stream only takes CUs from the main stream's G-step terms
-        self.side2 = None
-        if self.side is not None and os.environ.get("IRGAN_DWG_STREAM"):
-            self.side2 = torch.cuda.Stream(device=G.device)
-        # the whole step as one HIP graph (captured on first use, replayed after): see _graph_ok
         self.G.dev_adam = self.D.dev_adam = G.device.type == "cuda"
-        self._graph = self._graph_key = self._graph_L = None
-        self._static_in = None
-        self.eager_steps = 0
         self.vgg.pack()
         self.gen.pack()
         self.dis.pack()
@@ -1218,71 +1116,8 @@ class GANStep:
         ops.axpby(Feat(ir_t.t, 0, cin), 1.0, Feat(out.t, 0, cin))
         ops.axpby(Feat(img), 1.0, Feat(out.t, cin, img.shape[3]))
 
-    # ---- HIP graph of the whole step.  Eager, the host enqueues the D step's ~100 side-stream
-    # launches (~2.2 ms of Python) before the main stream's G-step terms, so the main stream
-    # idles behind the host while the D step runs alone (r03 trace: 2.23 ms per step).  A
-    # captured step carries both streams' launches with their event edges; a replay hands
-    # them to the device at once.  Everything that varies per step lives on the device
-    # (inputs copied into static buffers, the Adam step count: ParamStore.dev_adam); the
-    # learning rates and every buffer address are baked in, so the graph is re-captured when
-    # the LR scale changes or any buffer set (re)allocates.  Opt-in (IRGAN_GRAPH=1): on the
-    # bench step the replay measured no faster than eager (r03_h: 1119 / 1113 vs 1124 / 1128
-    # img/s on one box) -- the device runs the captured branches without the eager schedule's
-    # side-stream overlap gain, so the host-starvation gap is traded for lost concurrency.
-    def _graph_ok(self, ir):
-        return (self.side is not None and self.pg is None and self.dtype != ops.FP8 and not self.gen.use_dropout
-                and not ops.TIMER.enabled and self.eager_steps >= 1 and bool(os.environ.get("IRGAN_GRAPH")))
-
-    def _bufsets(self):
-        return (self.bufs, self.dbufs, self.gen.bufs, self.dis.bufs, self.vgg.bufs)
-
-    def _key(self, ir, rgb):
-        c = self.cfg
-        return (tuple(ir.shape), tuple(rgb.shape), self.lr_scale, c.lr_G, c.lr_D, c.beta1, c.beta2,
-                tuple(id(x) for x in self._bufsets()), tuple(x.allocs for x in self._bufsets()))
-
-    def _graph_step(self, ir, rgb):
-        key = self._key(ir, rgb)
-        if self._graph is None or key != self._graph_key:
-            self._graph = None
-            self._static_in = (torch.empty_like(ir), torch.empty_like(rgb))
-            self._static_in[0].copy_(ir)
-            self._static_in[1].copy_(rgb)
-            for st in (self.G, self.D):   # the device counts must match the host's before capture
-                if st._count is not None and st._count_host != st.step_count:
-                    st._count.fill_(st.step_count)
-                    st._count_host = st.step_count
-            counts = (self.G.step_count, self.D.step_count, self.G._count_host, self.D._count_host)
-            torch.cuda.synchronize()
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                L = self._eager_step(*self._static_in)
-            # capture ran no kernel: put the host's step counts back
-            self.G.step_count, self.D.step_count, self.G._count_host, self.D._count_host = counts
-            self._graph, self._graph_L = g, L
-            self._graph_key = self._key(ir, rgb)
-        else:
-            if ir.data_ptr() != self._static_in[0].data_ptr():
-                self._static_in[0].copy_(ir)
-            if rgb.data_ptr() != self._static_in[1].data_ptr():
-                self._static_in[1].copy_(rgb)
-        for st in (self.G, self.D):
-            if st._count_host != st.step_count:   # a state load since the capture
-                st._count.fill_(st.step_count)
-            st.step_count += 1
-            st._count_host = st.step_count
-        self._graph.replay()
-        return self._graph_L
-
     def step(self, ir: torch.Tensor, rgb: torch.Tensor):
         """One train step on NCHW fp32 device tensors; returns the loss vector (device)."""
-        if self._graph_ok(ir):
-            return self._graph_step(ir, rgb)
-        L = self._eager_step(ir, rgb)   # (a reallocation it makes shows in _key: re-capture)
-        self.eager_steps += 1
-        return L
-
-    def _eager_step(self, ir: torch.Tensor, rgb: torch.Tensor):
         cfg, b, T = self.cfg, self.bufs, self.tdt
         B, _, H, W = ir.shape
         cin, cout = cfg.input_nc, cfg.output_nc
@@ -1313,10 +1148,9 @@ class GANStep:
                 return ev
             return None
 
-        # host enqueue order (A/B knob IRGAN_VGG_AFTER_GFWD=1: the real half's VGG after the G
-        # forward's launches instead of before them)
-        vgg_late = vgg_side and VGG_AFTER_GFWD
-        ev_vgg = None if vgg_late else vgg_real()
+        # enqueued before the G forward's launches (after them measured neutral,
+        # profiles/r03_vgg_after_gfwd_ab.txt)
+        ev_vgg = vgg_real()
         # ---- G forward once: ir:1638 and ir:1657 compute the same image -- unless G has
         # dropout, whose two calls draw two masks: then the D step gets its own forward
         # (ir:1638-1639, under no_grad: its activations are never read back)
@@ -1324,8 +1158,6 @@ class GANStep:
         fake_d = self.gen.forward(ir, bufs=self.dbufs) if self.gen.use_dropout else None
         fake = self.gen.forward(ir)
         ir_t = Feat(self.gen.bufs.d["ir"])
-        if vgg_late:
-            ev_vgg = vgg_real()
         # ---- D step on [real; fake] as one 2B batch (ir:1636-1651), on the side stream
         dpad = max(8, cin + cout)   # D input zero-padded to 8 channels (narrow-input conv path)
         din = Feat(b.zeros("din2", (2 * B, H, W, dpad), T), 0, self.dis.packs[0].cin_eff)
@@ -1350,10 +1182,11 @@ class GANStep:
             ssim_work = b.flat("ssim_work", 10 * fake.numel())
             ops.ssim(Feat(fake), Feat(rgb_h), cfg.lambda_ssim, dfake, L[5:6], ssim_work)
 
-        # host enqueue order (TERMS_FIRST): the main stream's G-step terms before the side
-        # stream's D step -- the dependencies are the event edges either way; enqueued first,
-        # the terms start right behind the G forward instead of after ~90 D-step launches
-        terms_first = main is not None and TERMS_FIRST
+        # host enqueue order: the main stream's G-step terms before the side stream's D step --
+        # the dependencies are the event edges either way; enqueued first, the terms start
+        # right behind the G forward instead of after ~90 D-step launches (1204 vs 1199 img/s,
+        # profiles/r03_terms_first_ab.txt)
+        terms_first = main is not None
         ev_fwd = None
         if main is not None:
             ev_fwd = torch.cuda.Event()
@@ -1369,7 +1202,7 @@ class GANStep:
             pred = self.dis.forward(din, tag="d")
             dpred = b.get("dpred", tuple(pred.shape), torch.float32)
             ops.hinge(pred, pred[:B].numel(), 0, 1.0, dpred, L[0:1])
-            self.dis.backward(dpred, want_wgrad=True, want_dinput=False, tag="d", wgrad_stream=self.side2)
+            self.dis.backward(dpred, want_wgrad=True, want_dinput=False, tag="d")
             self.d_reduce.start()
             # D Adam, then the G-step GAN term through the updated D (ir:1651, 1659-1662),
             # still on the side stream: the main stream meanwhile runs the G-step terms
@@ -1384,7 +1217,7 @@ class GANStep:
         if not terms_first:
             g_terms()
         if main is not None:
-            jt = JOIN_TIMES is not None and not torch.cuda.is_current_stream_capturing()
+            jt = JOIN_TIMES is not None
             if jt:   # diagnostics: how long the main stream waits here for the side stream's D step
                 ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 ea.record(main)

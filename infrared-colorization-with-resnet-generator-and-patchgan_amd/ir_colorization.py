@@ -603,7 +603,9 @@ class GANTrainer:
     the fused HIP train step and returns the device loss vector (no host sync)."""
 
     def __init__(self, cfg: Config, model: IRColorizationModel = None, netD: NLayerDiscriminator = None,
-                 vgg: VGGPerceptual = None, process_group=None):
+                 vgg: VGGPerceptual = None, process_group=None, force_reduce=False):
+        """force_reduce: the data-parallel gradient collectives run even at world size 1
+        (engine.BucketedAllreduce; needs an initialised process group)."""
         self.cfg = cfg
         dev = torch.device(cfg.device)
         dt = getattr(cfg, "compute_dtype", "bf16")
@@ -621,7 +623,7 @@ class GANTrainer:
         # the fused step drives the networks' own engines (shared packed weights / buffers)
         self.core = GANStep(self.netG.store, self.netD.store, self.vgg.store, cfg, _dtype_code(dt),
                             process_group=process_group, gen=self.netG.engine, dis=self.netD.engine,
-                            vgg=self.vgg.engine)
+                            vgg=self.vgg.engine, force_reduce=force_reduce)
         self.lr_lambda = get_lr_lambda(cfg)
         self.epoch_index = 0
 

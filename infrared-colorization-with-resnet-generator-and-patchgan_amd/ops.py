@@ -42,26 +42,19 @@ def Pi(t, i):
     return ctypes.c_void_p(t.data_ptr() + i * t.element_size())
 
 
+_DET = [False]
+CONV_DETERMINISTIC = _lib.header_enum("IRGAN_CONV_DETERMINISTIC")
+
+
 def set_deterministic(on: bool) -> bool:
-    """Process-wide deterministic mode (irgan_set_deterministic): every split-K weight
-    gradient reduces through ordered slabs, so the step is bitwise reproducible under any
-    stream schedule.  Returns the previous setting."""
-    return bool(_lib.load().irgan_set_deterministic(int(bool(on))))
+    """Deterministic mode for the launches this module makes: every split-K weight gradient
+    carries IRGAN_CONV_DETERMINISTIC in its descriptor (ordered slab reduction, never fp32
+    atomics), so the step is bitwise reproducible under any stream schedule.  Host-side
+    state of this module (the library keeps none).  Returns the previous setting."""
+    old, _DET[0] = _DET[0], bool(on)
+    return old
 
 
-_RING_FOLD = [bool(os.environ.get("IRGAN_RING_FOLD"))]
-
-
-def set_ring_fold(on: bool) -> bool:
-    """irgan_set_ring_fold: the resblock dgrad as one conv_pp launch with the reflect ring
-    folded in (opt-in) instead of interior + ring launches.  Returns the previous setting."""
-    _RING_FOLD[0] = bool(on)
-    return bool(_lib.load().irgan_set_ring_fold(int(bool(on))))
-
-
-# the reflect ring of a ResnetBlock backward-data beside the weight gradient: the ring's
-# line GEMM keeps to this many workgroups (conv_wgrad_pc leaves 16 of 256 CUs idle)
-RING_SIDE_BLOCKS = 16
 _RING_WS = {}
 
 
@@ -79,8 +72,7 @@ RING_LINE = [True]
 
 def set_ring_line(on: bool) -> bool:
     """The line-GEMM ring launches (default) or the general reflect_ring_kernel for the
-    ResnetBlock shapes -- the latter is the ring of the opt-in fused IN-backward dgrad
-    (irgan_conv_dgrad_in_stats), so its bit-identity test references it.  Returns the previous setting."""
+    ResnetBlock shapes (the A/B reference of the line form).  Returns the previous setting."""
     old, RING_LINE[0] = RING_LINE[0], bool(on)
     return old
 
@@ -96,12 +88,12 @@ def set_ring_epi(on: bool) -> bool:
     return old
 
 
-def _ring(d, dy: "Feat", buf, p, dx: "Feat", max_blocks=1 << 20):
+def _ring(d, dy: "Feat", buf, p, dx: "Feat"):
     """The reflect-pad ring of a bf16 backward-data onto dx (after its interior): the line
     GEMM + fold on ResnetBlock shapes, else the general ring launch (the library decides)."""
     ws = _ring_ws(dx.t.device, dx.N * 4 * 68 * dx.C)
     _lib.call("irgan_reflect_dgrad_ring_ws", ctypes.byref(d), dy.ptr, P(buf), p, dx.ptr, P(ws),
-              ws.numel() if RING_LINE[0] else 0, max_blocks, stream())
+              ws.numel() if RING_LINE[0] else 0, 1 << 20, stream())
 
 
 class LaunchTimer:
@@ -350,29 +342,23 @@ def conv_fwd_stats(pc: PackedConv, x: Feat, y: Feat, part: torch.Tensor) -> int:
     return int(nb.value)
 
 
-RING_MFMA = not os.environ.get("IRGAN_NO_RING_MFMA")
 
 
 def conv_dgrad(pc: PackedConv, dy: Feat, dx: Feat, accumulate=False, mask: Feat = None, mask_act=0,
-               pad_buf: torch.Tensor = None, bias=False, ring_stream=None):
+               pad_buf: torch.Tensor = None, bias=False):
     """dx = d(conv)/dx^T dy.  Reflect-padded layers: interior straight into dx and the
-    padded ring folded onto dx's border band -- bf16: the interior launch, then the ring
-    (irgan_reflect_dgrad_ring_ws: line GEMM + fold on the ResnetBlock shapes), or with the
-    opt-in fold (set_ring_fold) one irgan_conv_dgrad_reflect launch; fp32: split-K ring
-    partials in pad_buf (fp32 scratch) folded by irgan_reflect_ring_fold; stride-2 layers
-    launch per phase.
-
-    ring_stream (bf16 reflect, fold off): the ring runs on that stream after the interior,
-    so it can overlap the caller's next launches (the weight gradient); returns an event
-    recorded on ring_stream that the consumer of dx must wait on.  Otherwise None."""
+    padded ring folded onto dx's border band -- bf16 ResnetBlock shapes: the ring's line
+    GEMM, then the interior launch whose store pass adds the ring terms
+    (irgan_conv_dgrad_reflect_line); other bf16 shapes: the interior launch, then the ring
+    (irgan_reflect_dgrad_ring_ws); fp32: split-K ring partials in pad_buf (fp32 scratch)
+    folded by irgan_reflect_ring_fold; stride-2 layers launch per phase (or all four
+    phases in one irgan_conv_dgrad_s2 launch)."""
     s = pc.spec
     assert dy.C == pc.cout_eff and dx.C == s.cin and dy.dt == pc.dtype
     if pc.reflect:
         # Backward-data over the reflect-padded domain g (Hp x Wp) folded back:
         # the interior u in [p, H+p) maps 1:1 onto dx and is written there
-        # directly; only the ring of width p is computed separately (2p strided
-        # split-K launches into pad_buf), and irgan_reflect_ring_fold adds it
-        # onto dx's border band.
+        # directly; only the ring of width p is computed separately.
         p = s.pad
         H, W = dx.H, dx.W
         Hp, Wp = H + 2 * p, W + 2 * p
@@ -383,19 +369,11 @@ def conv_dgrad(pc: PackedConv, dy: Feat, dx: Feat, accumulate=False, mask: Feat 
                     cin_real=s.cout if s.cout < pc.cout_eff else 0)
         d = _desc(**base, Ho=H, Wo=W, ldy=dx.ld, yoff=dx.off, OH=H, OW=W, omy=1, ooy=0, omx=1, oox=0, sy=1, sx=1,
                   c0y=c0y + p, c0x=c0x + p, accumulate=int(accumulate), out_dtype=dx.dt)
-        ring_mfma = (p > 0 and pc.dtype == BF16 and RING_MFMA and pc.cout_eff % 32 == 0 and H >= 2 * p + 2
+        ring_mfma = (p > 0 and pc.dtype == BF16 and pc.cout_eff % 32 == 0 and H >= 2 * p + 2
                      and W >= 2 * p + 2 and dy.ld % 8 == 0 and dy.off % 8 == 0)
 
-        fold = ring_mfma and _RING_FOLD[0]
-        side = ring_stream is not None and ring_mfma and not fold
-
         def launch():
-            if fold:
-                # interior + ring in one conv_pp launch on the ResnetBlock shapes, else both
-                # launches (irgan_conv_dgrad_reflect decides)
-                _lib.call("irgan_conv_dgrad_reflect", ctypes.byref(d), dy.ptr, P(buf), p, dx.ptr, stream())
-                return
-            if ring_mfma and not side and RING_LINE[0] and RING_EPI[0] and dx.dt == BF16:
+            if ring_mfma and RING_LINE[0] and RING_EPI[0] and dx.dt == BF16:
                 # line GEMM, then the interior with the ring folded into its store pass
                 ws = _ring_ws(dx.t.device, dx.N * 4 * 68 * dx.C)
                 rc = _lib.load().irgan_conv_dgrad_reflect_line(ctypes.byref(d), dy.ptr, P(buf), p, dx.ptr, P(ws),
@@ -405,23 +383,12 @@ def conv_dgrad(pc: PackedConv, dy: Feat, dx: Feat, accumulate=False, mask: Feat 
                 if rc != IRGAN_EUNSUPPORTED:
                     raise _lib.IrganError(f"irgan_conv_dgrad_reflect_line failed with code {rc}")
             _lib.call("irgan_conv_fwd", ctypes.byref(d), dy.ptr, P(buf), None, dx.ptr, None, stream())
-            if ring_mfma and not side:
+            if ring_mfma:
                 _ring(d, dy, buf, p, dx)
 
-        # the timed dgrad op is the whole backward-data (interior + ring) unless the ring runs
-        # on ring_stream: then the interior here and the ring as its own "ring" op there
         TIMER.wrap(conv_tag("dgrad", s, (H, W), dx.N), launch)
-        if side:
-            ev = torch.cuda.Event()
-            ev.record()
-            ring_stream.wait_event(ev)
-            with torch.cuda.stream(ring_stream):
-                TIMER.wrap(conv_tag("ring", s, (H, W), dx.N), lambda: _ring(d, dy, buf, p, dx, RING_SIDE_BLOCKS))
-                done = torch.cuda.Event()
-                done.record(ring_stream)
-            return done
         if p == 0 or ring_mfma:
-            return None
+            return
         # ring in split-K partials: rows[ks][N][2p][Wp][C], cols[ks][N][H][2p][C]
         rsz, csz = dx.N * 2 * p * Wp * s.cin, dx.N * H * 2 * p * s.cin
         nk = -(-(ay * ax * pc.cout_eff) // 64)
@@ -493,7 +460,7 @@ def conv_wgrad(spec: ConvSpec, x: Feat, dy: Feat, dw: torch.Tensor, dtype: int, 
     d = _desc(N=x.N, H=x.H, W=x.W, Cin=spec.cin, ldx=x.ld, xoff=x.off, Ho=Ho, Wo=Wo, Cout=spec.cout, ldy=dy.ld,
               yoff=dy.off, OH=Ho, OW=Wo, omy=1, ooy=0, omx=1, oox=0, KH=spec.k, KW=spec.k, sy=spec.stride,
               sx=spec.stride, c0y=-spec.pad, c0x=-spec.pad, pad_mode=spec.mode, act=0, accumulate=1, dtype=dtype,
-              out_dtype=F32, mask_act=0, ldm=0, moff=0)
+              out_dtype=F32, mask_act=0, ldm=0, moff=0, flags=CONV_DETERMINISTIC if _DET[0] else 0)
     ws = _wgrad_ws(dw.device) if dtype == BF16 else None
     TIMER.wrap(conv_tag("wgrad", spec, (x.H, x.W), x.N), lambda: _lib.call(
         "irgan_conv_wgrad_ws", ctypes.byref(d), x.ptr, dy.ptr, P(dw), splitk, P(ws), 0 if ws is None else ws.numel(),
@@ -526,22 +493,6 @@ def in_stats(x: Feat, work: torch.Tensor, mr: torch.Tensor):
 def in_finalize(x: Feat, part: torch.Tensor, nb: int, mr: torch.Tensor):
     """{mean, rstd} of x from the nb per-image partials irgan_conv_fwd_stats wrote."""
     _lib.call("irgan_in_finalize", P(part), x.N, x.H * x.W, x.C, nb, P(mr), stream())
-
-
-def in_finalize_apply(x: Feat, part: torch.Tensor, nb: int, mr: torch.Tensor, y: Feat, act=ACT_NONE,
-                      res: Feat = None) -> bool:
-    """in_finalize + in_apply as one launch (irgan_in_finalize_apply; bf16).  False when
-    the kernel does not take the shapes -- then NOTHING ran."""
-    if x.dt != BF16 or y.dt != BF16 or (res is not None and res.dt != BF16):
-        return False
-    rc = getattr(_lib.load(), "irgan_in_finalize_apply")(
-        P(part), nb, x.ptr, x.N, x.H * x.W, x.C, x.ld, x.off, P(mr), act, res.ptr if res else None,
-        res.ld if res else 0, res.off if res else 0, y.ptr, y.ld, y.off, stream())
-    if rc == IRGAN_EUNSUPPORTED:
-        return False
-    if rc != 0:
-        raise _lib.IrganError(f"irgan_in_finalize_apply failed with code {rc}")
-    return True
 
 
 def in_apply(x: Feat, mr, y: Feat, act=ACT_NONE, res: Feat = None, xhat: torch.Tensor = None, q8=None):
@@ -582,15 +533,10 @@ def in_bwd_parts(dy: Feat, x: Feat, act: int, mr, work, red, dx: Feat, db=None, 
     return reduce, apply
 
 
-def in_backward(dy: Feat, x: Feat, act: int, mr, work, red, dx: Feat, db=None, dy2: Feat = None, q8=None, nb=0):
-    """dx = backward of act(IN(x)) applied to (dy [+ dy2]); x = PRE-norm input.
-    nb > 0: the reduce's partials (nb rows per image) are already in ``work``
-    (conv_dgrad_in wrote them with dy): only their finalize runs before the apply."""
+def in_backward(dy: Feat, x: Feat, act: int, mr, work, red, dx: Feat, db=None, dy2: Feat = None, q8=None):
+    """dx = backward of act(IN(x)) applied to (dy [+ dy2]); x = PRE-norm input."""
     reduce, apply = in_bwd_parts(dy, x, act, mr, work, red, dx, db, dy2, q8)
-    if nb:
-        _lib.call("irgan_in_bwd_finalize", P(work), x.N, x.H * x.W, x.C, nb, P(red), stream())
-    else:
-        _timed("in_bwd_reduce", x, reduce)
+    _timed("in_bwd_reduce", x, reduce)
     _timed("in_bwd_apply", x, apply)
 
 
@@ -1017,38 +963,6 @@ def conv_fwd_fp8(pc: PackedConv, w8: torch.Tensor, dqw, x8: Feat, dqx, y: Feat, 
         "irgan_conv_fwd_fp8", ctypes.byref(d), x8.ptr, P(w8), dqx, dqw, P(pc.bias if bias else None), y.ptr,
         P(part), ctypes.byref(nb), stream()))
     return int(nb.value)
-
-
-def conv_dgrad_in(pc: PackedConv, dy: Feat, dx: Feat, z: Feat, mr: torch.Tensor, act, work: torch.Tensor,
-                  accumulate=False) -> int:
-    """conv_dgrad of a reflect-padded 3x3 ResnetBlock conv (bf16) that also writes the
-    InstanceNorm-backward partials of dx for the IN with pre-norm input z, table mr and
-    activation act (irgan_conv_dgrad_in_stats) into ``work``.  Returns the partial rows
-    per image (pass as in_backward(nb=...)), or 0 when the kernel does not take the
-    layer -- then NOTHING ran."""
-    s = pc.spec
-    if not (pc.reflect and pc.dtype == BF16 and dx.dt == BF16 and s.stride == 1 and s.k == 3 and s.pad == 1):
-        return 0
-    assert dy.C == pc.cout_eff and dx.C == s.cin and (z.N, z.H, z.W, z.C) == (dx.N, dx.H, dx.W, dx.C)
-    H, W = dx.H, dx.W
-    (_, _, ay, c0y), (_, _, ax, c0x), buf = pc.dg[0]
-    d = _desc(N=dy.N, H=dy.H, W=dy.W, Cin=pc.cout_eff, ldx=dy.ld, xoff=dy.off, Cout=s.cin, KH=ay, KW=ax,
-              pad_mode=PAD_ZERO, act=0, dtype=pc.dtype, mask_act=0, ldm=0, moff=0, Ho=H, Wo=W, ldy=dx.ld,
-              yoff=dx.off, OH=H, OW=W, omy=1, ooy=0, omx=1, oox=0, sy=1, sx=1, c0y=c0y + 1, c0x=c0x + 1,
-              accumulate=int(accumulate), out_dtype=dx.dt)
-    nb = ctypes.c_int32(0)
-    fn = getattr(_lib.load(), "irgan_conv_dgrad_in_stats")
-    rc = [0]
-
-    def launch():
-        rc[0] = fn(ctypes.byref(d), dy.ptr, P(buf), 1, dx.ptr, z.ptr, z.ld, z.off, P(mr), act, P(work),
-                   ctypes.byref(nb), stream())
-    TIMER.wrap(conv_tag("dgrad", s, (H, W), dx.N), launch)
-    if rc[0] == IRGAN_EUNSUPPORTED:
-        return 0
-    if rc[0] != 0:
-        raise _lib.IrganError(f"irgan_conv_dgrad_in_stats failed with code {rc[0]}")
-    return nb.value
 
 
 def conv_dgrad_fp8(pc: PackedConv, wd8: torch.Tensor, dqw, dy8: Feat, dqx, dy: Feat, dx: Feat, accumulate=False):

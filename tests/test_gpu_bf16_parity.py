@@ -241,14 +241,12 @@ def test_bf16_res64_act_mask_tight(ops, cout, H, mode):
 
 
 @pytest.mark.parametrize("N,H,W", [(2, 32, 48), (1, 64, 64), (3, 48, 32), (2, 16, 64), (1, 37, 64)])
-def test_reflect_dgrad_ring_fold_tight(ops, N, H, W):
-    """irgan_conv_dgrad_reflect (ResnetBlock backward-data, ir:386-411): on 16-multiple
-    sides >= 32 the reflect-pad ring is folded into the conv_pp launch itself (ring rows in
-    the border patches' K loop, ring columns + corners as an epilogue GEMM), so every dx
-    pixel is rounded to bf16 ONCE: held to the plain bound (no twice-rounded band), for
-    plain / accumulating bf16 and fp32 outputs, non-square and multi-image shapes (every
-    corner / edge patch kind).  Sides that are not (16, 37) take interior + ring launch.
-    The fold is opt-in (ops.set_ring_fold): switched on for this test only."""
+def test_reflect_dgrad_ring_tight(ops, N, H, W):
+    """ResnetBlock backward-data (ir:386-411) through ops.conv_dgrad: the interior conv_pp launch
+    plus the reflect-pad ring (line GEMM folded into the interior's store pass on the bf16
+    line shapes, else the ring launch) against fp64, for plain / accumulating bf16 and fp32
+    outputs, non-square and multi-image shapes (every corner / edge patch kind).  The band
+    pixels are rounded twice (interior, then + ring): the bound allows the partial sum."""
     C = 256
     torch.manual_seed(12)
     x = q(torch.randn(N, C, H, W))
@@ -260,24 +258,14 @@ def test_reflect_dgrad_ring_fold_tight(ops, N, H, W):
     pc = ops.PackedConv(spec, w.permute(0, 2, 3, 1).contiguous().reshape(-1).to(DEV), None, ops.BF16)
     pc.pack()
     gyd = nhwc(gy)
-    for fold in (True, False):   # fold on, then the default interior + reflect_ring_kernel pair
-        old_fold = ops.set_ring_fold(fold)
-        try:
-            _ring_fold_cases(ops, pc, gyd, dx64, dxa, dxi, N, H, W, C, fold)
-        finally:
-            ops.set_ring_fold(old_fold)
-
-
-def _ring_fold_cases(ops, pc, gyd, dx64, dxa, dxi, N, H, W, C, fold):
-    folded = fold and H % 16 == 0 and W % 16 == 0 and H >= 32 and W >= 32
     for out_dt, r_out in ((torch.bfloat16, R_BF16), (torch.float32, 0.0)):
         dx = torch.zeros(N, H, W, C, device=DEV, dtype=out_dt)
         ops.conv_dgrad(pc, ops.Feat(gyd), ops.Feat(dx))
-        check(nchw64(dx), dx64, dxa, r_out, f"fold {out_dt}", partial=None if folded else dxi)
+        check(nchw64(dx), dx64, dxa, r_out, f"ring {out_dt}", partial=dxi)
     old = q(torch.randn(N, C, H, W))
     dxb = torch.zeros(N, H, W, C + 8, device=DEV, dtype=torch.bfloat16)
     dxb[..., 8:] = nhwc(old)
     ops.conv_dgrad(pc, ops.Feat(gyd), ops.Feat(dxb, 8, C), accumulate=True)
-    check(nchw64(dxb[..., 8:]), dx64 + old.double(), dxa + old.double().abs(), R_BF16, "fold accumulate",
-          partial=None if folded else dxi + old.double())
+    check(nchw64(dxb[..., 8:]), dx64 + old.double(), dxa + old.double().abs(), R_BF16, "ring accumulate",
+          partial=dxi + old.double())
     assert not dxb[..., :8].any()

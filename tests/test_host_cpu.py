@@ -23,6 +23,21 @@ def test_abi_exports_every_declared_symbol():
     assert ctypes.sizeof(irc._lib.ConvDesc) == 4 * len(irc._lib.ConvDesc._fields_)
 
 
+def test_abi_exports_exactly_the_header():
+    """libirgan.so's dynamic symbol table = include/irgan.h's IRGAN_API declarations (the
+    library is built with -fvisibility=hidden): no undeclared entry point is reachable.
+    The HIP compiler's per-module `__hip_cuid_*` markers are the only other symbols."""
+    import shutil
+    import subprocess
+    irc = pkg()
+    nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
+    out = subprocess.run([nm, "-D", "--defined-only", irc._lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    syms = {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+    syms = {s for s in syms if not s.startswith("__hip_cuid_")}
+    assert syms == {n for n, _, _ in irc._lib.PROTOS}, sorted(syms ^ {n for n, _, _ in irc._lib.PROTOS})
+
+
 def _dense(kind, n, p=0, transpose=False):
     irc = pkg()
     T = 8

@@ -1,6 +1,6 @@
-"""Resblock backward-data timing at B=16/32 (256 -> 256, 3x3 reflect, 64x64): interior +
-reflect_ring_kernel (default), the one-launch ring fold (ops.set_ring_fold), and the
-interior launch alone (ring skipped: the difference is the ring's cost)."""
+"""Resblock backward-data timing at B=16/32 (256 -> 256, 3x3 reflect, 64x64): the default
+(ring line GEMM + interior with the ring in its store pass) and the interior launch alone
+(ring skipped: the difference is the ring's cost)."""
 import importlib
 import sys
 
@@ -33,12 +33,9 @@ for N in (16, 32):
     dy = torch.randn(N, H, H, C, device=DEV).bfloat16()
     dx = torch.empty_like(dy)
     t = timeit(lambda: ops.conv_dgrad(pc, ops.Feat(dy), ops.Feat(dx)))
-    old = ops.set_ring_fold(True)
-    tf = timeit(lambda: ops.conv_dgrad(pc, ops.Feat(dy), ops.Feat(dx)))
-    ops.set_ring_fold(old)
     zspec = ops.ConvSpec(C, C, 3, 1, 1, ops.PAD_ZERO)   # same interior launch, no ring
     pz = ops.PackedConv(zspec, torch.randn(C * 9 * C, device=DEV) * 0.02, torch.zeros(C, device=DEV), ops.BF16)
     pz.pack()
     ti = timeit(lambda: ops.conv_dgrad(pz, ops.Feat(dy), ops.Feat(dx)))
-    print(f"N={N}: dgrad interior+ring {t:.1f} us, ring fold {tf:.1f} us, interior only {ti:.1f} us "
+    print(f"N={N}: dgrad interior+ring {t:.1f} us, interior only {ti:.1f} us "
           f"(ring ~{t - ti:.1f} us)", flush=True)
