@@ -37,16 +37,23 @@ def min_gflop_per_img(H, W):
     return MIN_GFLOP_PER_IMG_256 * (H * W) / (256 * 256)
 
 
+def pmc_file():
+    """The newest committed PMC summary (profiles/rNN_pmc_traffic.json, highest round)."""
+    import glob
+    fs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_traffic.json")))
+    return fs[-1] if fs else None
+
+
 def pmc_traffic(family):
     """HBM bytes per launch of the resblock conv `family` (fwd / dgrad / wgrad),
-    from the committed rocprofv3 --pmc passes of tools/gpu_traffic.sh (FETCH_SIZE
+    from the newest committed rocprofv3 --pmc passes of tools/gpu_traffic.sh (FETCH_SIZE
     doubled per the gfx950 correction, plus WRITE_SIZE).  PMC counters cannot be
     collected inside this process, so the measured figure is read, not recomputed."""
-    p = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
+    p = pmc_file()
     try:
         with open(p) as f:
             return json.load(f)[family]["hbm_bytes"]
-    except (OSError, KeyError, ValueError):
+    except (OSError, KeyError, ValueError, TypeError):
         return None
 
 
@@ -287,7 +294,7 @@ def main():
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4) if achieved else None, "traffic": traffic,
                          "traffic_unit": "HBM bytes per launch (rocprofv3 PMC: 2*FETCH_SIZE + WRITE_SIZE, "
-                                         "profiles/r02_pmc_traffic.json)",
+                                         f"{os.path.relpath(pmc_file(), ROOT) if pmc_file() else 'none'})",
                          "flop_per_launch": res_flop, "per_kernel": kern,
                          "kernel_timing": f"HIP events around each tagged launch on its stream, {args.kernel_steps} "
                                           "steps right after the timed region (same process, inputs and "

@@ -68,7 +68,8 @@ typedef struct irgan_conv_desc {
 } irgan_conv_desc;
 /* flags: IRGAN_CONV_DETERMINISTIC -- a split-K weight gradient (irgan_conv_wgrad_ws) reduces
  * its partials through the caller's workspace in a fixed order and never through fp32
- * atomics: it lowers its split count to what the workspace holds (torch's
+ * atomics: it lowers its split count to what the workspace holds (fp32 parity mode: one
+ * split, so each output element takes a single atomic add) (torch's
  * use_deterministic_algorithms analogue; bit-identical gradients run to run and under any
  * stream schedule).  Without it the atomics are kept where they are faster (high split
  * counts: up2 / down1-class layers at 256^2). */

@@ -628,6 +628,7 @@ int launch_wgrad(const irgan_conv_desc* d, const void* x, const void* dy, float*
     }
     const int BM = d->Cout > 64 ? 128 : 64;
     const int tiles = irgan_cdiv(d->Cout, BM) * irgan_cdiv(K, 64);
+    if (irgan_det(d)) splitk = 1;  // deterministic: one block per output element (its single atomic add)
     if (splitk <= 0) {  // aim at ~4 workgroups per CU over 256 CUs
         splitk = irgan_cdiv(1024, tiles);
         long maxs = (P + 4 * BKP - 1) / (4 * BKP);  // keep >= 4 K-tiles per split

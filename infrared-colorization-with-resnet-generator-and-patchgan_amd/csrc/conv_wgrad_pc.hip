@@ -53,6 +53,9 @@ IRGAN_HD int pc_t128(int r) { return ((r >> 1) & 1) | (((r >> 3) & 1) << 1); }
 IRGAN_HD int pc_t256(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
 
 constexpr int XPIECES = 9;               // 72 X span positions, 8 per piece
+#ifndef WGPC_LW
+#define WGPC_LW 4   // loader waves per block (8: twice the DMA issue slots, 1024 threads, <= 128 VGPRs)
+#endif
 #ifndef WGPC_STAGES
 #define WGPC_STAGES 4
 #endif
@@ -85,10 +88,11 @@ struct PC {
     static constexpr int APIECES = 64 * DYR / 1024; // dY tile pieces (16 of 4 rows / 8 of 8 rows)
     static constexpr int TP = APIECES + XPIECES;    // pieces per segment (25 / 17)
     static constexpr int STAGE = TP * 1024;
-    static constexpr int PPL = (TP + 3) / 4;        // max pieces per loader wave (7 / 5)
+    static constexpr int LW = WGPC_LW;              // loader waves
+    static constexpr int PPL = (TP + LW - 1) / LW;  // max pieces per loader wave (LW 4: 7 / 5)
     static constexpr int MI = BMC / 16 / (CW / 4);  // co fragments per compute wave
-    static constexpr int NT = (CW + 4) * 64;        // threads: CW compute + 4 loader waves
-    static_assert(TP % 4 == 1, "loader 0 takes PPL pieces, loaders 1-3 PPL - 1");
+    static constexpr int NT = (CW + LW) * 64;       // threads: CW compute + LW loader waves
+    static_assert(TP % LW == 1, "loader 0 takes PPL pieces, the others PPL - 1");
 };
 template <int BMC>
 IRGAN_HD int pc_dsw(int r) { return BMC == 128 ? pc_t256(r) : pc_t128(r); }  // dY row swizzle
@@ -144,8 +148,9 @@ __global__ __launch_bounds__((PC<BMC, CW>::NT), 1) void wgrad_pc_kernel(const ir
     if (loader) {
         // ------------------------------------------------------------------
         // loader wave l issues pieces j = l, l+4, ... (< TP) of every segment
+        constexpr int LW = Q::LW;
         const int l = wid - CW;
-        const int np = (TP - l + 3) / 4;  // PPL for l = 0, else PPL - 1
+        const int np = (TP - l + LW - 1) / LW;  // PPL for l = 0, else PPL - 1
         const bool reflect = d.pad_mode == IRGAN_PAD_REFLECT;
         // dY: buffer base at dy + yoff + co0; lane offset fixed per piece, the
         // segment's first pixel enters as the scalar soffset
@@ -158,7 +163,7 @@ __global__ __launch_bounds__((PC<BMC, CW>::NT), 1) void wgrad_pc_kernel(const ir
         uint32_t second = 0;  // PAIR: bit u set when piece u's lane row is in the segment's 2nd output row
 #pragma unroll
         for (int u = 0; u < PPL; ++u) {
-            const int j = l + 4 * u;
+            const int j = l + LW * u;
             voff[u] = IRGAN_OOB;
             xpos[u] = 0;
             xc16[u] = 0;
@@ -202,7 +207,7 @@ __global__ __launch_bounds__((PC<BMC, CW>::NT), 1) void wgrad_pc_kernel(const ir
 #pragma unroll
             for (int u = 0; u < PPL; ++u) {
                 if (u >= np) break;
-                const int j = l + 4 * u;
+                const int j = l + LW * u;
                 if (j < APIECES) {
                     const uint32_t vo = (PAIR && !second_ok && ((second >> u) & 1)) ? IRGAN_OOB : voff[u];
                     blds16(rs_dy, vo, dy_soff, base + j * 1024);

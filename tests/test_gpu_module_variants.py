@@ -192,7 +192,8 @@ def test_generator_dropout_eval_mode_is_deterministic_on_every_entry():
     P = O.seeded_params(O.g_param_shapes(use_dropout=True), 1, bias_std=0.02)
     model.netG.load_state_dict(P)
     x = (torch.rand(2, 1, 32, 32, generator=torch.Generator().manual_seed(5)) * 2 - 1).to(DEV)
-    ref = O.g_forward({k: v.clone() for k, v in P.items()}, x.cpu()).detach()
+    # eval: the Dropout layer is in the layout (conv_block.6) but multiplies by 1
+    ref = O.g_forward({k: v.clone() for k, v in P.items()}, x.cpu(), dropout_masks=[torch.ones(())] * 9).detach()
     model.eval()
     with torch.no_grad():
         a, b = model(x).cpu(), model(x).cpu()
