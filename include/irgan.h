@@ -103,6 +103,16 @@ IRGAN_API int irgan_conv_fwd_fp8(const irgan_conv_desc* d, const void* x, const 
                        const float* dqw, const float* bias, void* y, void* part, int32_t* nb,
                        irgan_stream_t s);
 
+/* Weight gradient of a 3x3 stride-1 conv on fp8 operands (BASELINE config 5: the ResnetBlock
+ * convs, ir:386-411): dw[co][ky][kx][ci] += dqx[0] * dqdy[0] * sum_p dy8[p][co] x8[p + tap][ci]
+ * with x8 / dy8 the OCP e4m3 copies of the conv's input and output gradient (d->dtype =
+ * IRGAN_FP8, NHWC, ld / off % 16 == 0) and dqx / dqdy their per-tensor dequantisation factors
+ * (device).  d is the FORWARD descriptor (pad 1: c0x == -1, zero or reflect).  Cout % 128,
+ * Cin % 64, Wo == 64 (then Ho even) or Wo % 128 == 0.  ws (ws_floats, nullable): the split-K
+ * slab as irgan_conv_wgrad_ws.  IRGAN_EUNSUPPORTED (nothing launched) for other layers. */
+IRGAN_API int irgan_conv_wgrad_fp8(const irgan_conv_desc* d, const void* x8, const void* dy8, const float* dqx,
+                         const float* dqdy, float* dw, float* ws, int64_t ws_floats, irgan_stream_t s);
+
 /* fp8 amax slots: each slot is IRGAN_FP8_AMAX_PARTS uint32 partial maxima (bits of
  * non-negative floats); a kernel's block b raises part b % IRGAN_FP8_AMAX_PARTS of
  * the slot it records into, irgan_fp8_scale takes the max over the parts. */

@@ -12,7 +12,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(ROOT, "include")
 LIB = os.path.join(HERE, "libirgan.so")
-SOURCES = ["conv.hip", "conv_glds.hip", "conv_halo.hip", "conv_pp.hip", "conv_res64.hip", "conv_wgrad_halo.hip", "conv_wgrad_pc.hip", "conv_wgrad_narrow.hip", "conv_ring.hip", "conv_c8.hip", "conv_rowspan.hip", "conv_dgrad_s2.hip", "fp8.hip", "infer.hip", "data.hip", "norm.hip", "resample.hip", "loss.hip"]
+SOURCES = ["conv.hip", "conv_glds.hip", "conv_halo.hip", "conv_pp.hip", "conv_res64.hip", "conv_wgrad_halo.hip", "conv_wgrad_pc.hip", "conv_wgrad_f8.hip", "conv_wgrad_narrow.hip", "conv_ring.hip", "conv_c8.hip", "conv_rowspan.hip", "conv_dgrad_s2.hip", "fp8.hip", "infer.hip", "data.hip", "norm.hip", "resample.hip", "loss.hip"]
 ARCH = os.environ.get("IRGAN_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", INCLUDE, "-I", CSRC,
          "-Wno-unused-result", "-fvisibility=hidden"]

@@ -350,6 +350,197 @@ __global__ __launch_bounds__((PC<BMC, CW>::NT), 1) void wgrad_pc_kernel(const ir
         }
 }
 
+// ---- Wide-n variant for Cin % 128 == 0 (the ResnetBlock convs, ir:386-411): block = (128 co,
+// 128 ci as TWO 64-channel planes of the X span, kernel row ty, the 3 tx taps), n = 384.  Per
+// 64-pixel segment a block does twice the MFMAs of wgrad_pc_kernel<128, 8> for 34 DMA pieces
+// instead of 25 and one barrier: fewer DMA issues, fragment reads (0.42 instead of 0.58 per
+// MFMA) and barriers per MFMA.  A compute wave holds 4 co x 6 n fragments (96 accumulator
+// VGPRs) and ONE operand set that it re-reads right after each fragment's last MFMA of the
+// k-step (b[j] after its 4 MFMAs, a[i] in the last column), so the 12-wave block stays within
+// 168 VGPRs; the other compute wave of the SIMD covers the reads' latency.  12 tiles x 21
+// splits = 252 blocks (wgrad_pc_kernel: 24 x 10 = 240).  Resblock shape incl. the reduce:
+// 93.8 -> 84.8 us (profiles/r04_w2_wgrad_ab.txt); the default wherever Cin % 128 == 0.
+constexpr int W2_AP = 16;                    // dY tile: 64 px x 128 co x 2 B
+constexpr int W2_XP = 2 * XPIECES;           // X span: 2 planes x 72 positions x 128 B
+constexpr int W2_TP = W2_AP + W2_XP;         // 34 pieces per segment
+constexpr int W2_STAGE = W2_TP * 1024;
+constexpr int W2_LW = 4, W2_CW = 8, W2_NT = (W2_CW + W2_LW) * 64;
+constexpr int W2_PPL = (W2_TP + W2_LW - 1) / W2_LW;  // 9 (loaders 0, 1) / 8 (loaders 2, 3)
+constexpr int W2_STAGES = 4;                 // 136 KiB
+
+// XCD-aware order for any grid size: XCD x (blocks b % 8 == x) takes a contiguous range of
+// logical tiles (xcd_tile needs nb % 8 == 0)
+IRGAN_HD int xcd_tile_any(int b, int nb) {
+    const int x = b & 7, k = b >> 3, per = nb >> 3, rem = nb & 7;
+    return x * per + (x < rem ? x : rem) + k;
+}
+
+__global__ __launch_bounds__(W2_NT, 1) void wgrad_w2_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
+                                                            const bf16_t* __restrict__ dy, float* __restrict__ dw,
+                                                            int segs_per_block, int nseg, int ntco, int nci2, int swz,
+                                                            float* __restrict__ slab) {
+    constexpr int DYR = 256, MI = 4, NJ = 6;
+    __shared__ __attribute__((aligned(1024))) char smem[W2_STAGES * W2_STAGE];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int tiles = ntco * nci2 * d.KH;
+    const int t = swz ? xcd_tile_any(blockIdx.x, gridDim.x) : blockIdx.x;
+    const int split = t / tiles;
+    int r = t - split * tiles;
+    const int ty = r % d.KH;
+    r /= d.KH;
+    const int cic = r % nci2, cot = r / nci2;
+    const int co0 = cot * 128, ci0 = cic * 128;
+    const int s_beg = split * segs_per_block;
+    const int s_end = min(nseg, s_beg + segs_per_block);
+    if (s_beg >= s_end) return;  // block-uniform
+    const int nk = s_end - s_beg;
+    const int segs_row = d.Wo / 64;
+
+    if (wid >= W2_CW) {
+        // ------------------------------------------------------------------ loaders
+        const int l = wid - W2_CW;
+        const int np = (W2_TP - l + W2_LW - 1) / W2_LW;  // PPL (loaders 0, 1) or PPL - 1
+        const bool reflect = d.pad_mode == IRGAN_PAD_REFLECT;
+        const i32x4 rs_dy = make_rsrc(dy + d.yoff + co0,
+                                      (uint32_t)(((long)d.N * d.Ho * d.Wo * d.ldy - d.yoff - co0) * 2));
+        const i32x4 rs_x = make_rsrc(x + d.xoff + ci0, (uint32_t)(((long)d.N * d.H * d.W * d.ldx - d.xoff - ci0) * 2));
+        uint32_t voff[W2_PPL];
+        int xpos[W2_PPL], xc16[W2_PPL];
+#pragma unroll
+        for (int u = 0; u < W2_PPL; ++u) {
+            const int j = l + W2_LW * u;
+            voff[u] = IRGAN_OOB;
+            xpos[u] = 0;
+            xc16[u] = 0;
+            if (j < W2_AP) {
+                const int pos = j * 4 + lane / 16, slot = lane % 16;
+                const int c16 = slot ^ (2 * pc_t256(pos));
+                voff[u] = (uint32_t)((pos * d.ldy + c16 * 8) * 2);
+            } else if (j < W2_TP) {
+                const int jx = j - W2_AP, plane = jx / XPIECES;
+                const int pos = (jx - plane * XPIECES) * 8 + (lane >> 3), slot = lane & 7;
+                xpos[u] = pos;
+                xc16[u] = ((slot ^ (2 * pc_t128(pos))) * 8 + plane * 64) * 2;  // byte offset: chunk + plane
+            }
+        }
+        auto issue = [&](int s, int stage) {
+            const int rowi = s / segs_row;
+            const int x0 = (s - rowi * segs_row) * 64;
+            const int n = rowi / d.Ho, oy = rowi - n * d.Ho;
+            int iy = oy + ty + d.c0y;
+            if (reflect) iy = reflect_idx(iy, d.H);
+            const bool row_ok = (unsigned)iy < (unsigned)d.H;
+            const uint32_t dy_soff = (uint32_t)((((long)n * d.Ho + oy) * d.Wo + x0) * d.ldy * 2);
+            const long xrow = ((long)n * d.H + iy) * d.W;
+            char* base = smem + stage * W2_STAGE;
+#pragma unroll
+            for (int u = 0; u < W2_PPL; ++u) {
+                if (u >= np) break;
+                const int j = l + W2_LW * u;
+                if (j < W2_AP) {
+                    blds16(rs_dy, voff[u], dy_soff, base + j * 1024);
+                } else {
+                    int ix = x0 + d.c0x + xpos[u];
+                    if (reflect) ix = reflect_idx(ix, d.W);
+                    const bool ok = row_ok & (xpos[u] < 66) & ((unsigned)ix < (unsigned)d.W);
+                    const uint32_t off = ok ? (uint32_t)((xrow + ix) * d.ldx * 2) + xc16[u] : IRGAN_OOB;
+                    blds16(rs_x, off, base + j * 1024);
+                }
+            }
+        };
+        for (int k = 0; k < W2_STAGES - 1; ++k)
+            if (k < nk) issue(s_beg + k, k);
+        wait_segs<W2_PPL, W2_STAGES - 2>(min(nk - 1, W2_STAGES - 2), np == W2_PPL);
+        lds_barrier();
+        for (int kt = 0; kt < nk; ++kt) {
+            if (kt + 1 < nk) wait_segs<W2_PPL, W2_STAGES - 3>(min(nk - kt - 2, W2_STAGES - 3), np == W2_PPL);
+            lds_barrier();
+            if (kt + W2_STAGES - 1 < nk) issue(s_beg + kt + W2_STAGES - 1, (kt + W2_STAGES - 1) % W2_STAGES);
+        }
+        return;
+    }
+
+    // ---------------------------------------------------------------------- compute
+    // wave (wm, wn): co fragments wm*4 + i, n fragments jj = 6 wn + j: tap jj >> 3, 16-channel
+    // ci group cg = jj & 7 (plane cg >> 2), two 32-pixel k-steps per segment
+    const int wn = wid & 3, wm = wid >> 2;
+    const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+    const int k_lo = 8 * g + q;
+    // fragment addresses as one per-lane base XOR a wave-uniform chunk term: the 16-B chunk
+    // index c16 = 2 * (16-channel group) + (p >> 1) enters the swizzle by XOR only, so the
+    // group's part is (32 * group) XORed into the base (bits 5..7, above `within`, below the row)
+    const int a_base = k_lo * DYR + (((p >> 1) ^ (2 * pc_t256(k_lo))) << 4) + (p & 1) * 8;
+    int xb[3][2];  // X span rows pos = k_lo + tx (+ 4 for the high half): plane 0, group 0
+#pragma unroll
+    for (int tx = 0; tx < 3; ++tx)
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            const int pos = k_lo + 4 * hh + tx;
+            xb[tx][hh] = W2_AP * 1024 + pos * 128 + (((p >> 1) ^ (2 * pc_t128(pos))) << 4) + (p & 1) * 8;
+        }
+    auto aoff = [&](int i) { return a_base ^ (32 * (wm * MI + i)); };
+    auto boff = [&](int j, int hh) {
+        const int jj = wn * NJ + j, tx = jj >> 3, cg = jj & 7;
+        return (xb[tx][hh] ^ (32 * (cg & 3))) + (cg >> 2) * XPIECES * 1024;
+    };
+    f32x4 acc[MI][NJ];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    uint4 a[MI], b[NJ];
+    // the MFMAs of the current k-step, each operand re-read from (stage, half h) after its last use
+    auto step = [&](int stage, int h) {
+        const char* S = smem + stage * W2_STAGE + h * 32 * DYR;
+        const char* X = smem + stage * W2_STAGE + h * 4096;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+#pragma unroll
+            for (int i = 0; i < MI; ++i) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a[i]),
+                                                                    __builtin_bit_cast(bf16x8_t, b[j]), acc[i][j], 0,
+                                                                    0, 0);
+                if (j == NJ - 1) a[i] = ld_tr_pair(S + aoff(i), S + aoff(i) + 4 * DYR);
+            }
+            b[j] = ld_tr_pair(X + boff(j, 0), X + boff(j, 1));
+        }
+    };
+    auto barrier = [] {
+        __builtin_amdgcn_sched_barrier(0);
+        lds_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    barrier();  // prologue barrier: segment 0 landed
+#pragma unroll
+    for (int i = 0; i < MI; ++i) a[i] = ld_tr_pair(smem + aoff(i), smem + aoff(i) + 4 * DYR);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) b[j] = ld_tr_pair(smem + boff(j, 0), smem + boff(j, 1));
+    for (int kt = 0; kt < nk; ++kt) {
+        step(kt % W2_STAGES, 1);        // segment kt, pixels 0-31 | read pixels 32-63
+        barrier();                      // barrier kt: segment kt+1 landed; segment kt-1 fully read
+        step((kt + 1) % W2_STAGES, 0);  // segment kt, pixels 32-63 | read segment kt+1, pixels 0-31
+    }                                   // (the last iteration's reads are unused)
+
+    // C[row = co][col = n]: co = co0 + (wm*4 + i)*16 + 4g + rr, n = jj*16 + (lane & 15)
+    const int K = d.KH * 3 * d.Cin;
+    float* const dst = slab ? slab + (long)split * d.Cout * K : nullptr;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const int co = co0 + (wm * MI + i) * 16 + g * 4 + rr;
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int jj = wn * NJ + j, tx = jj >> 3;
+                const int ci = ci0 + (jj & 7) * 16 + (lane & 15);
+                const long o = (long)co * K + (ty * 3 + tx) * d.Cin + ci;
+                if (dst) dst[o] = acc[i][j][rr];
+                else atomicAdd(dw + o, acc[i][j][rr]);
+            }
+        }
+}
+
 __global__ __launch_bounds__(256) void wgrad_pc_reduce(const float* __restrict__ slab, int splits, long n,
                                                         float* __restrict__ dw) {
     const long n4 = n / 4;
@@ -383,6 +574,31 @@ extern "C" int irgan_conv_wgrad_pc(const irgan_conv_desc* d, const void* x, cons
         return IRGAN_EUNSUPPORTED;
     const int cus = irgan_cu_count();
     static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
+    if (!pair && BMC == 128 && d->KW == 3 && d->Cin % 128 == 0 && splitk <= 0) {
+        const int ntco = d->Cout / 128, nci2 = d->Cin / 128;
+        const int tiles = ntco * nci2 * d->KH;
+        const int nseg = d->N * d->Ho * (d->Wo / 64);
+        int sk = cus / tiles;
+        if (sk < 1) sk = 1;
+        const int maxs = irgan_cdiv(nseg, 4);
+        if (sk > maxs) sk = maxs;
+        const long n = (long)d->Cout * d->KH * 3 * d->Cin;
+        if (irgan_det(d)) {
+            const long fit = ws ? ws_cap / n : 1;
+            if (sk > fit) sk = (int)(fit > 1 ? fit : 1);
+        }
+        const int spb = irgan_cdiv(nseg, sk);
+        sk = irgan_cdiv(nseg, spb);
+        float* slab = (ws && sk > 1 && (long)sk * n <= ws_cap) ? ws : nullptr;
+        wgrad_w2_kernel<<<tiles * sk, W2_NT, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)dy, dw, spb, nseg, ntco,
+                                                      nci2, swz, slab);
+        if (slab) {
+            const int blocks = (int)std::min<long>(irgan_cdiv(n / 4, 256), 2048);
+            wgrad_pc_reduce<<<blocks, 256, 0, st>>>(slab, sk, n, dw);
+        }
+        IRGAN_LAUNCH_CHECK();
+        return 0;
+    }
     const int ntco = d->Cout / BMC, nci = d->Cin / 64;
     const int tiles = ntco * nci * d->KH;
     const int nseg = pair ? d->N * ((d->Ho + 1) / 2) : d->N * d->Ho * (d->Wo / 64);

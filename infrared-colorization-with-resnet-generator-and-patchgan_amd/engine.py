@@ -565,28 +565,31 @@ class GeneratorEngine:
         # 9 ResnetBlocks  (ir:362-418, 485-490)
         # fp8: one e4m3 operand buffer, written by the producer of each conv input (the
         # IN passes, fused; h_0 from blur-down by a quantise launch) and read by the conv
-        x8 = Feat(g.get("x8", (B, H2, W2, c2), torch.float8_e4m3fn)) if self.fp8 else None
+        # (one buffer per conv input slot: the fp8 weight gradients of the backward read them)
+        x8s = [Feat(g.get(f"x8_{k}", (B, H2, W2, c2), torch.float8_e4m3fn)) for k in range(2 * len(self.res))] \
+            if self.fp8 else None
         A = self.f8a if self.fp8 else None
         if self.fp8:
-            A.quant(0, h, x8)
+            A.quant(0, h, x8s[0])
         nres = len(self.res)
         for b, (p1, p2) in enumerate(self.res):
             r1 = Feat(g.get(f"r1_{b}", (B, H2, W2, c2), T))
             t = Feat(g.get(f"t{b}", (B, H2, W2, c2), T))
             if self.fp8:
-                self.norms[f"r{b}_1"].conv_fwd8(g, f"r{b}_1", p1, *self._w8(4 * b), x8, A.dqp(2 * b), r1, t,
-                                                ACT_RELU, q8=A.spec(2 * b + 1, x8))
-                A.ensure(2 * b + 1, t, x8)
+                self.norms[f"r{b}_1"].conv_fwd8(g, f"r{b}_1", p1, *self._w8(4 * b), x8s[2 * b], A.dqp(2 * b), r1, t,
+                                                ACT_RELU, q8=A.spec(2 * b + 1, x8s[2 * b + 1]))
+                A.ensure(2 * b + 1, t, x8s[2 * b + 1])
             else:
                 self.norms[f"r{b}_1"].conv_fwd(g, f"r{b}_1", p1, self._res_in(g, f"xp1_{b}", h), r1, t, ACT_RELU)
             r2 = Feat(g.get(f"r2_{b}", (B, H2, W2, c2), T))
             hn = Feat(g.get(f"h{b + 1}", (B, H2, W2, c2), T))
             if self.fp8:
                 nxt = 2 * b + 2 if b + 1 < nres else None   # the next block's conv1 input
-                self.norms[f"r{b}_2"].conv_fwd8(g, f"r{b}_2", p2, *self._w8(4 * b + 2), x8, A.dqp(2 * b + 1), r2,
-                                                hn, ACT_NONE, res=h, q8=A.spec(nxt, x8) if nxt else None)
+                self.norms[f"r{b}_2"].conv_fwd8(g, f"r{b}_2", p2, *self._w8(4 * b + 2), x8s[2 * b + 1],
+                                                A.dqp(2 * b + 1), r2, hn, ACT_NONE, res=h,
+                                                q8=A.spec(nxt, x8s[nxt]) if nxt else None)
                 if nxt:
-                    A.ensure(nxt, hn, x8)
+                    A.ensure(nxt, hn, x8s[nxt])
             else:
                 t2 = t
                 if self.use_dropout and train:   # nn.Dropout(0.5) after the ReLU (ir:394-395)
@@ -596,7 +599,8 @@ class GeneratorEngine:
                                                res=h)
             h = hn
         if self.fp8:
-            self.f8a.update(0, 2 * self.n_blocks)   # next step's forward scales
+            self.f8a.snapshot(0, 2 * self.n_blocks)  # the scales x8s were made with (fp8 weight gradients)
+            self.f8a.update(0, 2 * self.n_blocks)    # next step's forward scales
         # up1 -> cat with x1 -> conv/IN/ReLU  (ir:554-558)
         # (odd sizes: the up-sampled map is 2*H2 x 2*W2 != H1 x W1 and is resized to the
         # skip's size, ir:555-556 -- folded into the UpsampleAA table, or a resize launch
@@ -708,6 +712,13 @@ class GeneratorEngine:
         dt_ = Feat(g.get("dtmp", (B, H2, W2, c2), T))
         nb2 = 2 * self.n_blocks
         dy8 = Feat(g.get("dy8", (B, H2, W2, c2), torch.float8_e4m3fn)) if self.fp8 else None
+
+        def wg8(pc, key, xslot, dslot, x, dy):
+            """ResnetBlock weight gradient on the fp8 copies (the forward's x8 of slot xslot with
+            the scale it was made with, dy8 of slot dslot); bf16 where the kernel does not take it."""
+            if not ops.conv_wgrad_fp8(pc.spec, Feat(g.d[f"x8_{xslot}"]), dy8, self.f8a.dqp_used(xslot),
+                                      self.f8a.dqp(dslot), S.krsc(key + ".weight", G)):
+                wg(pc, key, x, dy)
         k1, k2 = self.res_keys
         for b in reversed(range(self.n_blocks)):
             p1, p2 = self.res[b]
@@ -725,8 +736,8 @@ class GeneratorEngine:
                                       q8=A.spec(s2, dy8) if self.fp8 else None)
             dr = Feat(g.get("dtmp2", (B, H2, W2, c2), T))
             if self.fp8:
-                wg(p2, f"{key}{k2}", xin2, dt_)
                 A.ensure(s2, dt_, dy8)
+                wg8(p2, f"{key}{k2}", 2 * b + 1, s2, xin2, dt_)
                 ops.conv_dgrad_fp8(p2, *self._w8(4 * b + 3), dy8, A.dqp(s2), dt_, dr)
             else:
                 self._res_dgrad(g, p2, dt_, dr, False, padbuf)
@@ -736,8 +747,8 @@ class GeneratorEngine:
             self.norms[f"r{b}_1"].bwd(g, f"r{b}_1", dr, r1, ACT_RELU, dr, db=self._bgrad(f"{key}{k1}.bias"),
                                       q8=A.spec(s1, dy8) if self.fp8 else None)
             if self.fp8:
-                wg(p1, f"{key}{k1}", xin1, dr)
                 A.ensure(s1, dr, dy8)
+                wg8(p1, f"{key}{k1}", 2 * b, s1, xin1, dr)
                 ops.conv_dgrad_fp8(p1, *self._w8(4 * b + 1), dy8, A.dqp(s1), dr, dh, accumulate=True)
             else:
                 self._res_dgrad(g, p1, dr, dh, True, padbuf)

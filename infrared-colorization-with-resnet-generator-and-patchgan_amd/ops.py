@@ -942,6 +942,18 @@ class Fp8Acts:
     def dqp(self, slot):
         return Pi(self.dq, slot)
 
+    def snapshot(self, start=0, n=None):
+        """Keep the dequantisation factors slots [start, start+n) were just used with (before
+        update() moves them to the next step's): the weight gradients of the backward read
+        the forward's e4m3 copies with them."""
+        n = self.dq.numel() - start if n is None else n
+        if not hasattr(self, "dq_used"):
+            self.dq_used = torch.ones_like(self.dq)
+        self.dq_used[start:start + n].copy_(self.dq[start:start + n])
+
+    def dqp_used(self, slot):
+        return Pi(self.dq_used, slot)
+
     def update(self, start=0, n=None):
         fp8_scale(self.amax, self.q, self.dq, reset=True, start=start, n=n)
 
@@ -963,6 +975,30 @@ def conv_fwd_fp8(pc: PackedConv, w8: torch.Tensor, dqw, x8: Feat, dqx, y: Feat, 
         "irgan_conv_fwd_fp8", ctypes.byref(d), x8.ptr, P(w8), dqx, dqw, P(pc.bias if bias else None), y.ptr,
         P(part), ctypes.byref(nb), stream()))
     return int(nb.value)
+
+
+def conv_wgrad_fp8(spec: ConvSpec, x8: Feat, dy8: Feat, dqx, dqdy, dw: torch.Tensor) -> bool:
+    """dw (fp32 KRSC view, accumulated) += weight gradient of conv(x) given dy, on the fp8
+    copies x8 / dy8 with their dequantisation pointers (irgan_conv_wgrad_fp8).  False when
+    the kernel does not take the layer -- then NOTHING ran (the caller runs the bf16 conv_wgrad)."""
+    Ho, Wo = spec.out_hw(x8.H, x8.W)
+    assert (dy8.H, dy8.W, dy8.C) == (Ho, Wo, spec.cout) and x8.C == spec.cin and x8.dt == FP8 and dy8.dt == FP8
+    d = _desc(N=x8.N, H=x8.H, W=x8.W, Cin=spec.cin, ldx=x8.ld, xoff=x8.off, Ho=Ho, Wo=Wo, Cout=spec.cout, ldy=dy8.ld,
+              yoff=dy8.off, OH=Ho, OW=Wo, omy=1, ooy=0, omx=1, oox=0, KH=spec.k, KW=spec.k, sy=spec.stride,
+              sx=spec.stride, c0y=-spec.pad, c0x=-spec.pad, pad_mode=spec.mode, act=0, accumulate=1, dtype=FP8,
+              out_dtype=F32, mask_act=0, ldm=0, moff=0, flags=CONV_DETERMINISTIC if _DET[0] else 0)
+    ws = _wgrad_ws(dw.device)
+    rc = [0]
+
+    def launch():
+        rc[0] = _lib.load().irgan_conv_wgrad_fp8(ctypes.byref(d), x8.ptr, dy8.ptr, dqx, dqdy, P(dw), P(ws), ws.numel(),
+                                                 stream())
+    TIMER.wrap(conv_tag("wgrad8", spec, (x8.H, x8.W), x8.N), launch)
+    if rc[0] == IRGAN_EUNSUPPORTED:
+        return False
+    if rc[0] != 0:
+        raise _lib.IrganError(f"irgan_conv_wgrad_fp8 failed with code {rc[0]}")
+    return True
 
 
 def conv_dgrad_fp8(pc: PackedConv, wd8: torch.Tensor, dqw, dy8: Feat, dqx, dy: Feat, dx: Feat, accumulate=False):

@@ -190,7 +190,8 @@ class _Fp8ResConv(torch.autograd.Function):
     """The fp8 path's ResnetBlock conv (reflect pad 1, 3x3; GeneratorEngine(fp8=True)):
     forward on e4m3(x), e4m3(bf16(w)); backward-data on e4m3(dY) x e4m3(bf16(w)) over
     the padded interior, the reflect ring folded from the unquantised dY and bf16(w);
-    the weight / bias gradients on the unquantised x and dY.  Not a reference
+    the weight gradient on e4m3(x) x e4m3(dY) (irgan_conv_wgrad_fp8), the bias gradient
+    on the unquantised dY.  Not a reference
     function: the emulation the fp8 step is checked against (ir:390-411 otherwise)."""
 
     @staticmethod
@@ -202,19 +203,16 @@ class _Fp8ResConv(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         x, w, wb = ctx.saved_tensors
-        with torch.enable_grad():
-            xr = x.detach().requires_grad_(True)
-            wr = w.detach().requires_grad_(True)
-            y = F.conv2d(_rpad(xr, 1), wr)
-            dx_exact, dw = torch.autograd.grad(y, (xr, wr), gy)
+        gq = fp8_q(gy)
+        with torch.autocast("cpu", enabled=False):   # e4m3 operands: exact in fp32
+            dw = torch.nn.grad.conv2d_weight(_rpad(fp8_q(x).float(), 1), w.shape, gq.float()).to(w.dtype)
         H, W = x.shape[-2:]
         xp = torch.zeros(x.shape[0], x.shape[1], H + 2, W + 2, dtype=x.dtype)
-        g8 = torch.nn.grad.conv2d_input(xp.shape, fp8_q(wb), fp8_q(gy))
+        g8 = torch.nn.grad.conv2d_input(xp.shape, fp8_q(wb), gq)
         gb = torch.nn.grad.conv2d_input(xp.shape, wb, gy)
         xf = torch.zeros_like(x, requires_grad=True)
         with torch.enable_grad():
             ring = torch.autograd.grad(_rpad(xf, 1), xf, gb)[0] - gb[..., 1:-1, 1:-1]
-        del dx_exact
         return g8[..., 1:-1, 1:-1] + ring, dw, gy.sum(dim=(0, 2, 3))
 
 

@@ -213,6 +213,43 @@ def test_fp8_resblock_dgrad_tight(ops, H):
         check(nchw64(dx), ref, aref + old.double().abs(), R_BF16, f"fp8 dgrad acc={acc}", partial=interior)
 
 
+@pytest.mark.parametrize("N,H,W,cin,cout,mode", [(2, 64, 64, 256, 256, 1), (1, 8, 128, 128, 256, 1),
+                                                 (3, 64, 64, 64, 128, 0), (1, 4, 256, 64, 128, 1)])
+def test_fp8_wgrad_tight(ops, N, H, W, cin, cout, mode):
+    """irgan_conv_wgrad_fp8 (the ResnetBlock weight gradient on e4m3 operands, config 5):
+    against fp64 on the SAME e4m3 values times their dequantisation factors -- products of
+    e4m3 are exact in fp32, so only the fp32 accumulation order differs: |err| <= 2e-5 * the
+    sum of |terms| (+ 2^-20 |ref| for the scale product).  Two-row (64-wide) and one-row
+    (128 / 256-wide) segments, reflect and zero padding, several co / ci tiles, accumulate
+    into an existing dW."""
+    torch.manual_seed(3)
+    spec = ops.ConvSpec(cin, cout, 3, 1, 1, mode)
+    x = q(torch.randn(N, cin, H, W))
+    gy = q(torch.randn(N, cout, H, W) * 1e-3)
+    qx, qy = 2.0 ** 5, 2.0 ** 14
+    x8 = e4m3(x.permute(0, 2, 3, 1).float() * qx).contiguous().to(DEV)
+    gy8 = e4m3(gy.permute(0, 2, 3, 1).float() * qy).contiguous().to(DEV)
+    xq = x8.cpu().float().double().permute(0, 3, 1, 2) / qx
+    gq = gy8.cpu().float().double().permute(0, 3, 1, 2) / qy
+
+    def wgrad(xv, gv):
+        wt = torch.zeros(cout, cin, 3, 3, dtype=torch.float64, requires_grad=True)
+        ref_conv(xv, wt, None, 3, 1, 1, mode).backward(gv)
+        return wt.grad.permute(0, 2, 3, 1).contiguous()   # KRSC, as dW is stored
+
+    ref, aref = wgrad(xq, gq), wgrad(xq.abs(), gq.abs())
+    dqx = torch.tensor([1.0 / qx], device=DEV)
+    dqy = torch.tensor([1.0 / qy], device=DEV)
+    old = torch.randn(cout, 3, 3, cin) * 1e-3
+    dw = old.reshape(-1).clone().to(DEV)
+    assert ops.conv_wgrad_fp8(spec, ops.Feat(x8), ops.Feat(gy8), ops.Pi(dqx, 0), ops.Pi(dqy, 0), dw)
+    got = dw.cpu().double().reshape(cout, 3, 3, cin)
+    err = (got - (ref + old.double())).abs()
+    bound = R_ACC * aref + 2.0 ** -20 * ref.abs() + 2.0 ** -22 * old.double().abs() + 1e-30
+    ratio = (err / bound).max().item()
+    assert ratio <= 1.0, f"fp8 wgrad: worst |err|/bound = {ratio:.3g}"
+
+
 def _fp8_oracle(ir, rgb, lam, fp8=True):
     from oracle import step as O
     G = O.seeded_params(O.g_param_shapes(), 1, bias_std=0.02)

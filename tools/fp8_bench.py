@@ -1,5 +1,5 @@
-"""Kernel timing: resblock conv (256 -> 256, 3x3 reflect, 64x64) forward+stats and
-backward-data, bf16 vs fp8 operands, at the config-5 batch (32) and the bench batch."""
+"""Kernel timing: resblock conv (256 -> 256, 3x3 reflect, 64x64) forward+stats,
+backward-data and weight gradient, bf16 vs fp8 operands, at the config-5 batch (32) and the bench batch."""
 import importlib
 import sys
 
@@ -48,6 +48,10 @@ for N in (16, 32):
     t_dbf = timeit(lambda: ops.conv_dgrad(pc, ops.Feat(x), ops.Feat(dx)))
     t_df8 = timeit(lambda: ops.conv_dgrad_fp8(pc, fw.dst[1], ops.Pi(fw.dq, 1), ops.Feat(x8), ops.Pi(dq, 0),
                                               ops.Feat(x), ops.Feat(dx)))
+    dw = torch.zeros(C * 9 * C, device=DEV)
+    t_wbf = timeit(lambda: ops.conv_wgrad(spec, ops.Feat(x), ops.Feat(y), dw, ops.BF16))
+    t_wf8 = timeit(lambda: ops.conv_wgrad_fp8(spec, ops.Feat(x8), ops.Feat(x8), ops.Pi(dq, 0), ops.Pi(dq, 0), dw))
     print(f"N={N}: fwd+stats bf16 {t_bf:.1f} us ({flop / t_bf / 1e6:.0f} TF/s)  fp8 {t_f8:.1f} us "
-          f"({flop / t_f8 / 1e6:.0f} TF/s)  quant {t_q:.1f} us | dgrad bf16 {t_dbf:.1f} us  fp8 {t_df8:.1f} us",
+          f"({flop / t_f8 / 1e6:.0f} TF/s)  quant {t_q:.1f} us | dgrad bf16 {t_dbf:.1f} us  fp8 {t_df8:.1f} us | "
+          f"wgrad bf16 {t_wbf:.1f} us ({flop / t_wbf / 1e6:.0f} TF/s)  fp8 {t_wf8:.1f} us ({flop / t_wf8 / 1e6:.0f} TF/s)",
           flush=True)
