@@ -313,15 +313,23 @@ def main():
                    "rank_time_s": {"max": round(el, 4), "min": round(el_min, 4)},
                    "replicas_bit_identical": replicas_ok},
             "losses": {k: round(v, 5) for k, v in losses.items()},
-            **({"join_wait_ms": round(sum(a.elapsed_time(b) for a, b in irc.engine.JOIN_TIMES[-args.steps:]) /
-                                      max(1, len(irc.engine.JOIN_TIMES[-args.steps:])), 4)}
-               if irc.engine.JOIN_TIMES else {}),
+            **(step_phases(irc.engine.JOIN_TIMES[-args.steps:]) if irc.engine.JOIN_TIMES else {}),
         }
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(H, W, B, args.cpu_budget)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def step_phases(steps):
+    """IRGAN_JOIN_TIMING=1 diagnostics: the main stream's wait for the side stream's D step
+    (join_wait_ms) and each phase mark's median offset from the step start (ms)."""
+    import statistics
+    keys = [k for k in steps[0] if k != "start"]
+    off = {k: round(statistics.median(p["start"].elapsed_time(p[k]) for p in steps), 4) for k in keys}
+    wait = statistics.mean(p["terms"].elapsed_time(p["join"]) for p in steps)
+    return {"join_wait_ms": round(wait, 4), "step_phase_ms": off}
 
 
 if __name__ == "__main__":

@@ -528,6 +528,17 @@ __global__ __launch_bounds__(256) void weight_pack_batch_kernel(const irgan_pack
         }
         return;
     }
+    if (q.dtype == IRGAN_BF16 && Cp == Cr && Kp == taps * Cp && total % 8 == 0 && (uintptr_t)q.src % 16 == 0 &&
+        (uintptr_t)q.dst % 16 == 0) {
+        // unpadded forward pack: dst row = src row (taps x Cin contiguous) in bf16, 8 per thread
+        const float4* s4 = (const float4*)q.src;
+        uint4* d4 = (uint4*)q.dst;
+        for (long i = blockIdx.x * 256L + threadIdx.x; i < total / 8; i += (long)gridDim.x * 256) {
+            const float4 a = s4[2 * i], b = s4[2 * i + 1];
+            d4[i] = make_uint4(pk_bf16(a.x, a.y), pk_bf16(a.z, a.w), pk_bf16(b.x, b.y), pk_bf16(b.z, b.w));
+        }
+        return;
+    }
     for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
         const int row = (int)(idx / Kp), k = (int)(idx - (long)row * Kp);
         const int tap = k / Cp, c = k - tap * Cp;
@@ -707,7 +718,9 @@ extern "C" int irgan_weight_pack(const float* src, void* dst, int32_t dtype, int
 extern "C" int irgan_weight_pack_batch(const irgan_pack_desc* descs, int32_t n, irgan_stream_t st) {
     if (n <= 0) return 0;
     if (!descs || n > 65535) return IRGAN_EINVAL;
-    weight_pack_batch_kernel<<<dim3(128, n), 256, 0, (hipStream_t)st>>>(descs);
+    // 256 blocks per job: the largest (a 256 x 256 x 3 x 3 backward-data pack, 144 64 x 64 tiles;
+    // D model.8's, 512) in one or two rounds; a small job's spare blocks exit at once
+    weight_pack_batch_kernel<<<dim3(256, n), 256, 0, (hipStream_t)st>>>(descs);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }

@@ -1080,9 +1080,18 @@ class BucketedAllreduce:
         self.works, self.end = [], self.store.numel
 
 
-# IRGAN_JOIN_TIMING=1: (event, event) pairs around the main stream's wait for the side
-# stream's D step (tools: how much of the step is the D step on the critical path)
+# IRGAN_JOIN_TIMING=1: per step, timing events at the phase boundaries of both streams
+# (diagnostics: where the D step sits on the critical path).  Keys: start, gfwd (main: G
+# forward done), d0 / dend (side: the D step's first / last launch), terms (main: the G-step
+# terms done), join (main: after its wait for the side stream), end.
 JOIN_TIMES = [] if os.environ.get("IRGAN_JOIN_TIMING") else None
+
+
+def _mark(ph, key, stream):
+    if ph is not None:
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(stream)
+        ph[key] = e
 
 
 class GANStep:
@@ -1121,12 +1130,6 @@ class GANStep:
         self.gen.pack()
         self.dis.pack()
 
-    def _din(self, ir_t: Feat, img: torch.Tensor, out: Feat):
-        """cat([ir, img], 1) (ir:1639-1640) written straight into the NHWC D input."""
-        cin = self.cfg.input_nc
-        ops.axpby(Feat(ir_t.t, 0, cin), 1.0, Feat(out.t, 0, cin))
-        ops.axpby(Feat(img), 1.0, Feat(out.t, cin, img.shape[3]))
-
     def step(self, ir: torch.Tensor, rgb: torch.Tensor):
         """One train step on NCHW fp32 device tensors; returns the loss vector (device)."""
         cfg, b, T = self.cfg, self.bufs, self.tdt
@@ -1135,12 +1138,19 @@ class GANStep:
         self.losses.zero_()
         L = self.losses
         main = torch.cuda.current_stream() if self.side is not None else None
+        ph = {} if JOIN_TIMES is not None and main is not None else None
+        _mark(ph, "start", main)
         side_ctx = (lambda: torch.cuda.stream(self.side)) if main is not None else _nullcontext  # noqa: E731
         rgb_h = b.get("rgb_nhwc", (B, H, W, cout), torch.float32)
         ops.nchw_to_nhwc(rgb.contiguous(), Feat(rgb_h))
         # ---- VGG features of the real images (ir:1668) need nothing from G: side stream,
         # concurrent with the G forward
         vin = Feat(b.zeros("vin", (2 * B, H, W, max(8, cout)), T), 0, self.vgg.packs[0].cin_eff)
+        # D input [real; fake] as one 2B batch, cat([ir, img], 1) (ir:1639-1640) zero-padded to
+        # 8 channels (narrow-input conv path): the ir channels of both halves and the real
+        # images are written beside the G forward; the fake images once G has run
+        dpad = max(8, cin + cout)
+        din = Feat(b.zeros("din2", (2 * B, H, W, dpad), T), 0, self.dis.packs[0].cin_eff)
         vgg_side = main is not None and not os.environ.get("IRGAN_NO_VGG_OVERLAP")
         ev_in = None
         if vgg_side:
@@ -1151,9 +1161,13 @@ class GANStep:
             with side_ctx() if vgg_side else _nullcontext():
                 if ev_in is not None:
                     self.side.wait_event(ev_in)
+                for h in (0, B):
+                    ops.nchw_to_nhwc(ir.contiguous(), Feat(din.t[h:h + B], 0, cin))
+                ops.axpby(Feat(rgb_h), 1.0, Feat(din.t[:B], cin, cout))
                 ops.affine(Feat(rgb_h), self.vgg.scale, self.vgg.shift, vin.batch(B, B))
                 self.vgg.forward(vin, part=(B, B))
             if vgg_side:
+                _mark(ph, "vgg_real", self.side)
                 ev = torch.cuda.Event()
                 ev.record(self.side)
                 return ev
@@ -1168,11 +1182,7 @@ class GANStep:
         self.gen.training = True
         fake_d = self.gen.forward(ir, bufs=self.dbufs) if self.gen.use_dropout else None
         fake = self.gen.forward(ir)
-        ir_t = Feat(self.gen.bufs.d["ir"])
         # ---- D step on [real; fake] as one 2B batch (ir:1636-1651), on the side stream
-        dpad = max(8, cin + cout)   # D input zero-padded to 8 channels (narrow-input conv path)
-        din = Feat(b.zeros("din2", (2 * B, H, W, dpad), T), 0, self.dis.packs[0].cin_eff)
-        dinf = Feat(b.zeros("din1", (B, H, W, dpad), T), 0, self.dis.packs[0].cin_eff)
         dfake = b.get("dfake", (B, H, W, cout), torch.float32)
 
         def g_terms():
@@ -1200,6 +1210,7 @@ class GANStep:
         terms_first = main is not None
         ev_fwd = None
         if main is not None:
+            _mark(ph, "gfwd", main)
             ev_fwd = torch.cuda.Event()
             ev_fwd.record(main)                   # G output, the zeroed losses and D inputs
         if terms_first:
@@ -1207,9 +1218,9 @@ class GANStep:
         with side_ctx():
             if ev_fwd is not None:
                 self.side.wait_event(ev_fwd)
+                _mark(ph, "d0", self.side)
             self.D.zero_grad()
-            self._din(ir_t, rgb_h, din.batch(0, B))
-            self._din(ir_t, fake if fake_d is None else fake_d, din.batch(B, B))
+            ops.axpby(Feat(fake if fake_d is None else fake_d), 1.0, Feat(din.t[B:], cin, cout))
             pred = self.dis.forward(din, tag="d")
             dpred = b.get("dpred", tuple(pred.shape), torch.float32)
             ops.hinge(pred, pred[:B].numel(), 0, 1.0, dpred, L[0:1])
@@ -1220,26 +1231,28 @@ class GANStep:
             # that do not read D (L1, VGG, TV, SSIM)
             self.d_reduce.finish(self.D.adam_begin(cfg.lr_D * self.lr_scale, cfg.beta1, cfg.beta2))
             self.dis.pack()
-            self._din(ir_t, fake, dinf)
-            predg = self.dis.forward(dinf, tag="g")
+            # the G-step D pass reads cat([ir, fake]): the fake half of the D input (rewritten
+            # when the D step saw the other dropout draw)
+            if fake_d is not None:
+                ops.axpby(Feat(fake), 1.0, Feat(din.t[B:], cin, cout))
+            predg = self.dis.forward(din.batch(B, B), tag="g")
             dpg = b.get("dpredg", tuple(predg.shape), torch.float32)
             ops.hinge(predg, predg.numel(), 1, cfg.lambda_gan, dpg, L[1:2])
             dd = self.dis.backward(dpg, want_wgrad=False, want_dinput=True, tag="g")
+            _mark(ph, "dend", self.side)
         if not terms_first:
             g_terms()
         if main is not None:
-            jt = JOIN_TIMES is not None
-            if jt:   # diagnostics: how long the main stream waits here for the side stream's D step
-                ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                ea.record(main)
+            _mark(ph, "terms", main)
             main.wait_stream(self.side)           # the GAN term's d fake
-            if jt:
-                eb.record(main)
-                JOIN_TIMES.append((ea, eb))
+            _mark(ph, "join", main)
         ops.axpby(dd.sl(cin, cout), 1.0, Feat(dfake), 1.0)
         self.gen.backward(dfake, ready=self.g_reduce.ready)
         self.g_reduce.finish(self.G.adam_begin(cfg.lr_G * self.lr_scale, cfg.beta1, cfg.beta2))
         self.gen.pack()
+        if ph is not None:
+            _mark(ph, "end", main)
+            JOIN_TIMES.append(ph)
         return L
 
     @staticmethod
