@@ -196,21 +196,25 @@ enum { IRGAN_IN_PARTS = 256 };
  * written by irgan_conv_fwd_stats (the reduction half of irgan_in_stats). */
 IRGAN_API int irgan_in_finalize(const void* part, int32_t N, int32_t HW, int32_t C, int32_t nb, float* mr,
                       irgan_stream_t s);
-/* mr[n][c] = {mean, rstd}; work: IRGAN_IN_PARTS*N*C doubles of scratch. */
+/* mr[n][c] = {mean, rstd}; work: IRGAN_IN_PARTS*N*C doubles of scratch.  tickets: NULL, or
+ * N int32 counters that are zero before the call and zero again after it (per stream and
+ * buffer: no two launches in flight on one set) -- then the last block of each image sums
+ * that image's partials itself (fixed order) instead of a second, finalize launch. */
 IRGAN_API int irgan_in_stats(const void* x, int32_t dtype, int32_t N, int32_t HW, int32_t C,
-                   int32_t ld, int32_t off, double* work, float* mr, irgan_stream_t s);
+                   int32_t ld, int32_t off, double* work, int32_t* tickets, float* mr, irgan_stream_t s);
 /* y = act((x - mean) * rstd) [+ res];  optional xhat output ([P][C], dtype). */
 IRGAN_API int irgan_in_apply(const void* x, int32_t dtype, int32_t N, int32_t HW, int32_t C, int32_t ldx,
                    int32_t xoff, const float* mr, int32_t act, const void* res, int32_t ldr,
                    int32_t roff, void* y, int32_t ldy, int32_t yoff, void* xhat, irgan_stream_t s);
 /* Backward of y = act(IN(x)) [+ res] given the PRE-norm input x and its
  * (mean, rstd): xhat = (x - mean)*rstd, g = (dy [+ dy2]) * act'(xhat),
- * red[n][c] = {mean g, mean g*xhat}.  work: IRGAN_IN_PARTS*N*C doubles of scratch. */
+ * red[n][c] = {mean g, mean g*xhat}.  work: IRGAN_IN_PARTS*N*C doubles of scratch; tickets
+ * as irgan_in_stats. */
 IRGAN_API int irgan_in_bwd_reduce(const void* dy, int32_t dy_dtype, int32_t lddy, int32_t dyoff,
                         const void* dy2, int32_t dy2_dtype, int32_t lddy2, int32_t dy2off,
                         const void* x, int32_t x_dtype, int32_t ldx, int32_t xoff, int32_t act,
-                        int32_t N, int32_t HW, int32_t C, const float* mr, double* work, float* red,
-                        irgan_stream_t s);
+                        int32_t N, int32_t HW, int32_t C, const float* mr, double* work, int32_t* tickets,
+                        float* red, irgan_stream_t s);
 /* dx = rstd*(g - mean(g) - xhat*mean(g*xhat)); also db[c] += sum dx (fp32 bias
  * grad of the producing conv, caller zeroes) when db != NULL.  dx may alias dy. */
 IRGAN_API int irgan_in_bwd_apply(const void* dy, int32_t dy_dtype, int32_t lddy, int32_t dyoff,
@@ -285,6 +289,16 @@ IRGAN_API int irgan_reflect_dgrad_ring_ws(const irgan_conv_desc* d, const void* 
  * % 256 == 0 take the 256-channel conv tile. */
 IRGAN_API int irgan_conv_dgrad_reflect_line(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p, void* dx,
                                   float* ws, int64_t ws_floats, irgan_stream_t s);
+/* The fp8 path's ResnetBlock backward-data (config 5): the ring's line GEMM on the bf16 dy
+ * and bf16 flipped weights w (d: as irgan_conv_dgrad_reflect_line), then the interior on e4m3
+ * operands -- d8 = d with dtype IRGAN_FP8 and dy8's ld / offset, w8 the e4m3 flipped image,
+ * dqy / dqw their device dequantisation factors -- whose store pass folds the ring in: the
+ * same dx as irgan_conv_fwd_fp8 (interior) followed by irgan_reflect_dgrad_ring_ws.  dy
+ * channels % 128, dx channels % 256, dy8 ld / offset % 16; else IRGAN_EUNSUPPORTED. */
+IRGAN_API int irgan_conv_dgrad_reflect_line_fp8(const irgan_conv_desc* d, const void* dy, const void* w,
+                                      const irgan_conv_desc* d8, const void* dy8, const void* w8,
+                                      const float* dqy, const float* dqw, int32_t p, void* dx, float* ws,
+                                      int64_t ws_floats, irgan_stream_t s);
 /* Backward-data of a 4x4 stride-2 pad-1 conv (PatchGAN model.0 / .3 / .6, ir:600-612) in
  * ONE launch for all four output phases: d = the four per-phase descriptors (2x2 taps on
  * dy, omy = omx = 2, (ooy, oox) the phase, c0y / c0x in {-1, 0}; otherwise identical), w =

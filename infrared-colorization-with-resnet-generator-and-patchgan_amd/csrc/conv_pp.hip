@@ -144,6 +144,40 @@ extern "C" int irgan_conv_dgrad_reflect_line(const irgan_conv_desc* d, const voi
     return 0;
 }
 
+// The fp8 path's ResnetBlock backward-data (config 5): the ring's line GEMM on the bf16 dY and
+// bf16 flipped weights (d, dy, w: as irgan_conv_dgrad_reflect_line), then the interior on the
+// e4m3 operands (d8: d with dtype FP8 and dy8's ld / offset; dqy, dqw: their dequantisation
+// factors) whose store pass folds the ring in -- the interior launch + ring launch + fold of
+// before in one pass over dx, with the same terms and roundings.
+extern "C" int irgan_conv_dgrad_reflect_line_fp8(const irgan_conv_desc* d, const void* dy, const void* w,
+                                                 const irgan_conv_desc* d8, const void* dy8, const void* w8,
+                                                 const float* dqy, const float* dqw, int32_t p, void* dx, float* ws,
+                                                 int64_t ws_floats, irgan_stream_t s) {
+    if (!d || !dy || !w || !d8 || !dy8 || !w8 || !dqy || !dqw || !dx || !ws) return IRGAN_EINVAL;
+    if ((long)d->N * d->Ho * d->Wo <= 0 || d->Cout <= 0) return 0;
+    if (!ring_line_check(d, p, ws_floats) || d->dtype != IRGAN_BF16 || d->out_dtype != IRGAN_BF16 ||
+        d->act != IRGAN_ACT_NONE || d->sy != 1 || d->sx != 1 || d->Cin % 128 || d->Cout % 256 || d->mask_act ||
+        d8->dtype != IRGAN_FP8 || d8->out_dtype != IRGAN_BF16 || d8->ldx % 16 || d8->xoff % 16 || d8->N != d->N ||
+        d8->H != d->H || d8->W != d->W || d8->Cin != d->Cin || d8->Cout != d->Cout || d8->Ho != d->Ho ||
+        d8->Wo != d->Wo || d8->ldy != d->ldy || d8->yoff != d->yoff || d8->c0y != d->c0y || d8->c0x != d->c0x ||
+        d8->accumulate != d->accumulate || d8->KH != 3 || d8->KW != 3 || d8->act != IRGAN_ACT_NONE ||
+        (long)d->N * d->H * d->W * d8->ldx >= (1L << 30) || (long)d->Cout * 9 * d->Cin >= (1L << 30))
+        return IRGAN_EUNSUPPORTED;
+    hipStream_t st = (hipStream_t)s;
+    ring_line_gemm_launch(d, dy, w, ws, st);
+    static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
+    const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH), ntn = d->Cout / 256;
+    const int nb = d->N * tpy * tpx * ntn;
+    if (d->accumulate)
+        conv_pp_kernel<3, 3, 256, true, false, true><<<nb, 512, 0, st>>>(
+            *d8, (const bf16_t*)dy8, (const bf16_t*)w8, nullptr, dx, nullptr, ntn, tpx, tpy, swz, nullptr, dqy, dqw, ws);
+    else
+        conv_pp_kernel<3, 3, 256, false, false, true><<<nb, 512, 0, st>>>(
+            *d8, (const bf16_t*)dy8, (const bf16_t*)w8, nullptr, dx, nullptr, ntn, tpx, tpy, swz, nullptr, dqy, dqw, ws);
+    IRGAN_LAUNCH_CHECK();
+    return 0;
+}
+
 // Forward conv with the InstanceNorm statistics of its output fused into the
 // epilogue (replaces the separate irgan_in_stats pass over y; ir:154-165, 392, 417).
 // part: float2[N * nb * Cout] partials, nb (out) = 16x16 patches per image; reduce

@@ -367,6 +367,12 @@ constexpr int W2_STAGE = W2_TP * 1024;
 constexpr int W2_LW = 4, W2_CW = 8, W2_NT = (W2_CW + W2_LW) * 64;
 constexpr int W2_PPL = (W2_TP + W2_LW - 1) / W2_LW;  // 9 (loaders 0, 1) / 8 (loaders 2, 3)
 constexpr int W2_STAGES = 4;                 // 136 KiB
+// ablations for variant builds (tools/build_variant.sh -DW2_EXP=...): 1 no epilogue stores,
+// 2 no DMA after the prologue (the MFMAs run on stale stages), 4 no MFMAs (operand reads kept),
+// 8 fp32 atomics into dW instead of the split slabs + reduce
+#ifndef W2_EXP
+#define W2_EXP 0
+#endif
 
 // XCD-aware order for any grid size: XCD x (blocks b % 8 == x) takes a contiguous range of
 // logical tiles (xcd_tile needs nb % 8 == 0)
@@ -456,7 +462,8 @@ __global__ __launch_bounds__(W2_NT, 1) void wgrad_w2_kernel(const irgan_conv_des
         for (int kt = 0; kt < nk; ++kt) {
             if (kt + 1 < nk) wait_segs<W2_PPL, W2_STAGES - 3>(min(nk - kt - 2, W2_STAGES - 3), np == W2_PPL);
             lds_barrier();
-            if (kt + W2_STAGES - 1 < nk) issue(s_beg + kt + W2_STAGES - 1, (kt + W2_STAGES - 1) % W2_STAGES);
+            if (!(W2_EXP & 2) && kt + W2_STAGES - 1 < nk)
+                issue(s_beg + kt + W2_STAGES - 1, (kt + W2_STAGES - 1) % W2_STAGES);
         }
         return;
     }
@@ -498,9 +505,13 @@ __global__ __launch_bounds__(W2_NT, 1) void wgrad_w2_kernel(const irgan_conv_des
         for (int j = 0; j < NJ; ++j) {
 #pragma unroll
             for (int i = 0; i < MI; ++i) {
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a[i]),
-                                                                    __builtin_bit_cast(bf16x8_t, b[j]), acc[i][j], 0,
-                                                                    0, 0);
+                if constexpr (W2_EXP & 4) {   // operands consumed by a cheap dependency only
+                    acc[i][j][0] += __uint_as_float(a[i].x ^ b[j].y);
+                } else {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a[i]),
+                                                                        __builtin_bit_cast(bf16x8_t, b[j]), acc[i][j],
+                                                                        0, 0, 0);
+                }
                 if (j == NJ - 1) a[i] = ld_tr_pair(S + aoff(i), S + aoff(i) + 4 * DYR);
             }
             b[j] = ld_tr_pair(X + boff(j, 0), X + boff(j, 1));
@@ -535,6 +546,7 @@ __global__ __launch_bounds__(W2_NT, 1) void wgrad_w2_kernel(const irgan_conv_des
                 const int jj = wn * NJ + j, tx = jj >> 3;
                 const int ci = ci0 + (jj & 7) * 16 + (lane & 15);
                 const long o = (long)co * K + (ty * 3 + tx) * d.Cin + ci;
+                if ((W2_EXP & 1) && acc[i][j][rr] != 1234.5f) continue;
                 if (dst) dst[o] = acc[i][j][rr];
                 else atomicAdd(dw + o, acc[i][j][rr]);
             }
@@ -589,7 +601,7 @@ extern "C" int irgan_conv_wgrad_pc(const irgan_conv_desc* d, const void* x, cons
         }
         const int spb = irgan_cdiv(nseg, sk);
         sk = irgan_cdiv(nseg, spb);
-        float* slab = (ws && sk > 1 && (long)sk * n <= ws_cap) ? ws : nullptr;
+        float* slab = (!(W2_EXP & 8) && ws && sk > 1 && (long)sk * n <= ws_cap) ? ws : nullptr;
         wgrad_w2_kernel<<<tiles * sk, W2_NT, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)dy, dw, spb, nseg, ntco,
                                                       nci2, swz, slab);
         if (slab) {

@@ -211,6 +211,16 @@ def test_fp8_resblock_dgrad_tight(ops, H):
         ref = want + old.double()
         interior = g8[..., 1:-1, 1:-1] + old.double()
         check(nchw64(dx), ref, aref + old.double().abs(), R_BF16, f"fp8 dgrad acc={acc}", partial=interior)
+        # the ring folded into the fp8 interior's store pass (irgan_conv_dgrad_reflect_line_fp8,
+        # default) writes exactly the dx of the interior launch + ring launch + fold
+        dx2 = nhwc(old)
+        prev = ops.set_ring_epi(False)
+        try:
+            ops.conv_dgrad_fp8(pc, fw.dst[1], ops.Pi(fw.dq, 1), ops.Feat(gy8), ops.Pi(dqy, 0), ops.Feat(gyd),
+                               ops.Feat(dx2), accumulate=acc)
+        finally:
+            ops.set_ring_epi(prev)
+        assert torch.equal(dx.view(torch.int16), dx2.view(torch.int16)), f"fp8 ring epilogue acc={acc}"
 
 
 @pytest.mark.parametrize("N,H,W,cin,cout,mode", [(2, 64, 64, 256, 256, 1), (1, 8, 128, 128, 256, 1),
