@@ -277,50 +277,6 @@ IRGAN_HD void block_partials8(float* a0, float* a1, const Lay& L, bool on, int c
     __syncthreads();
 }
 
-// In-kernel finalize (irgan_in_stats / irgan_in_bwd_reduce with tickets): after writing its
-// partials a block takes a ticket of its image; the block that takes the last one sums that
-// image's partials (fp64, b = 0, 1, ... in order: deterministic) into out and resets the ticket,
-// so the finalize launch and its start-up go.  out: mr (MODE 0) or red (MODE 1).
-struct Fin {
-    int32_t* tickets;
-    float* out;
-};
-
-IRGAN_HD void finalize_row(const float2* part, int n, int nb, int C, int HW, int mode, float* out, int c) {
-    double s = 0.0, q = 0.0;
-    const float2* pp = part + (long)n * nb * C + c;
-#pragma unroll 8
-    for (int b = 0; b < nb; ++b) {
-        const float2 v = pp[(long)b * C];
-        s += v.x;
-        q += v.y;
-    }
-    const long i = (long)n * C + c;
-    const double mean = s / HW;
-    if (mode == 0) {
-        double var = q / HW - mean * mean;
-        if (var < 0) var = 0;
-        out[2 * i] = (float)mean;
-        out[2 * i + 1] = (float)(1.0 / sqrt(var + 1e-5));
-    } else {
-        out[2 * i] = (float)mean;
-        out[2 * i + 1] = (float)(q / HW);
-    }
-}
-
-// called by every thread of the block after its partials are stored
-IRGAN_HD void finalize_if_last(const Fin& fin, const float2* part, int n, int C, int HW, int mode) {
-    __shared__ int last_s;
-    __threadfence();  // this block's partials visible device-wide before its ticket
-    __syncthreads();
-    if (threadIdx.x == 0) last_s = atomicAdd(fin.tickets + n, 1) == (int)gridDim.x - 1;
-    __syncthreads();
-    if (!last_s) return;  // block-uniform
-    __threadfence();      // acquire: the other blocks' partials
-    for (int c = threadIdx.x; c < C; c += blockDim.x) finalize_row(part, n, gridDim.x, C, HW, mode, fin.out, c);
-    if (threadIdx.x == 0) fin.tickets[n] = 0;  // ready for the next launch on this buffer
-}
-
 // All-bf16 fast path of rows_kernel<MODE, 8> for MODE 0 (stats), 1 (backward
 // reduce) and 2 (backward apply without db), and MODE 4: the forward apply
 // y = act((x - mean) * rstd) [+ res] (res in the dy slot, nullable) -- apply_kernel's job
@@ -337,7 +293,7 @@ __global__ __launch_bounds__(TPB) void rows8_kernel(const bf16_t* x, int ldx, in
                                                     int dyoff, const bf16_t* dy2, int lddy2, int dy2off, int act,
                                                     const float* __restrict__ mr, const float* __restrict__ red,
                                                     bf16_t* dx, int lddx, int dxoff, int HW, int C, int rows_per_block,
-                                                    float2* __restrict__ part, Q8 q8 = Q8{}, Fin fin = Fin{}) {
+                                                    float2* __restrict__ part, Q8 q8 = Q8{}) {
     __shared__ float s0[TPB * 8], s1[TPB * 8];
     const float qs = F8 ? *q8.q : 1.f;
     float amx = 0.f;
@@ -444,9 +400,6 @@ __global__ __launch_bounds__(TPB) void rows8_kernel(const bf16_t* x, int ldx, in
         block_partials8(a0, a1, L, on, cb, c, C, n, s0, s1, part);
     }
     if constexpr (F8) fp8_block_amax(amx, q8.amax, blockIdx.y * gridDim.x + blockIdx.x);
-    if constexpr (MODE <= 1) {
-        if (fin.tickets) finalize_if_last(fin, part, n, C, HW, MODE);
-    }
 }
 
 // fp64 sum of the nb block partials of each (n, c).  Block (FC channels x FS
@@ -571,7 +524,7 @@ int blocks_per_image(long HW, int N, int RP, long rpt = 8) {
 template <int MODE>
 int launch_rows(Slice X, Slice DY, Slice DY2, int act, const float* mr, const float* red, void* dx, int dxdt, int lddx,
                 int dxoff, int N, int HW, int C, float2* part, float* db, bool vec, hipStream_t st, int* nb_out,
-                const Q8* q8 = nullptr, Fin fin = Fin{}, bool* finalized = nullptr) {
+                const Q8* q8 = nullptr) {
     const int VW = vec ? V : 1;
     int nb = blocks_per_image(HW, N, rp_of(C, VW), MODE == 2 ? 8 : 16);
     const int rows = irgan_cdiv(HW, nb);
@@ -588,12 +541,10 @@ int launch_rows(Slice X, Slice DY, Slice DY2, int act, const float* mr, const fl
                                                         red, (bf16_t*)dx, lddx, dxoff, HW, C, rows, part, *q8);
         else if (MODE == 0)
             rows8_kernel<0, 8><<<g, TPB, 0, st>>>(xp, X.ld, X.off, nullptr, 0, 0, nullptr, 0, 0, act, mr, red, nullptr,
-                                                  0, 0, HW, C, rows, part, Q8{}, fin);
+                                                  0, 0, HW, C, rows, part);
         else
             rows8_kernel<MODE, 4><<<g, TPB, 0, st>>>(xp, X.ld, X.off, gp, DY.ld, DY.off, hp, DY2.ld, DY2.off, act, mr,
-                                                     red, (bf16_t*)dx, lddx, dxoff, HW, C, rows, part, Q8{},
-                                                     MODE <= 1 ? fin : Fin{});
-        if (finalized) *finalized = MODE <= 1 && fin.tickets != nullptr;
+                                                     red, (bf16_t*)dx, lddx, dxoff, HW, C, rows, part);
         if (nb_out) *nb_out = nb;
         return 0;
     }
@@ -608,16 +559,14 @@ int launch_rows(Slice X, Slice DY, Slice DY2, int act, const float* mr, const fl
 }  // namespace
 
 extern "C" int irgan_in_stats(const void* x, int32_t dtype, int32_t N, int32_t HW, int32_t C, int32_t ld,
-                              int32_t off, double* work, int32_t* tickets, float* mr, irgan_stream_t s) {
+                              int32_t off, double* work, float* mr, irgan_stream_t s) {
     hipStream_t st = (hipStream_t)s;
     if ((long)N * HW * C <= 0) return 0;
     Slice X{x, dtype, ld, off}, Z{nullptr, 0, 0, 0};
     int nb = 1;
-    bool done = false;
     launch_rows<0>(X, Z, Z, 0, nullptr, nullptr, nullptr, 0, 0, 0, N, HW, C, (float2*)work, nullptr,
-                   vec_ok(C, {ld, off}), st, &nb, nullptr, Fin{tickets, mr}, &done);
-    if (!done)
-        finalize_kernel<<<dim3(irgan_cdiv(C, FC), N), 256, 0, st>>>((const float2*)work, mr, N, C, nb, HW, 0);
+                   vec_ok(C, {ld, off}), st, &nb);
+    finalize_kernel<<<dim3(irgan_cdiv(C, FC), N), 256, 0, st>>>((const float2*)work, mr, N, C, nb, HW, 0);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }
@@ -681,17 +630,14 @@ extern "C" int irgan_in_apply(const void* x, int32_t dtype, int32_t N, int32_t H
 extern "C" int irgan_in_bwd_reduce(const void* dy, int32_t dy_dtype, int32_t lddy, int32_t dyoff, const void* dy2,
                                    int32_t dy2_dtype, int32_t lddy2, int32_t dy2off, const void* x, int32_t x_dtype,
                                    int32_t ldx, int32_t xoff, int32_t act, int32_t N, int32_t HW, int32_t C,
-                                   const float* mr, double* work, int32_t* tickets, float* red, irgan_stream_t s) {
+                                   const float* mr, double* work, float* red, irgan_stream_t s) {
     hipStream_t st = (hipStream_t)s;
     if ((long)N * HW * C <= 0) return 0;
     const bool vec = vec_ok(C, {lddy, dyoff, ldx, xoff}) && (!dy2 || vec_ok(C, {lddy2, dy2off}));
     Slice X{x, x_dtype, ldx, xoff}, DY{dy, dy_dtype, lddy, dyoff}, DY2{dy2, dy2_dtype, lddy2, dy2off};
     int nb = 1;
-    bool done = false;
-    launch_rows<1>(X, DY, DY2, act, mr, nullptr, nullptr, 0, 0, 0, N, HW, C, (float2*)work, nullptr, vec, st, &nb,
-                   nullptr, Fin{tickets, red}, &done);
-    if (!done)
-        finalize_kernel<<<dim3(irgan_cdiv(C, FC), N), 256, 0, st>>>((const float2*)work, red, N, C, nb, HW, 1);
+    launch_rows<1>(X, DY, DY2, act, mr, nullptr, nullptr, 0, 0, 0, N, HW, C, (float2*)work, nullptr, vec, st, &nb);
+    finalize_kernel<<<dim3(irgan_cdiv(C, FC), N), 256, 0, st>>>((const float2*)work, red, N, C, nb, HW, 1);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }

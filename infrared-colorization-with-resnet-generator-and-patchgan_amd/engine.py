@@ -301,14 +301,8 @@ class INLayer:
         if nb:
             ops.in_finalize(x, work, nb, mr)
         else:
-            ops.in_stats(x, work, mr, tickets=self.tickets(bufs, N))
+            ops.in_stats(x, work, mr)
         ops.in_apply(x, mr, y, act=act, res=res, xhat=xhat, q8=q8)
-
-    @staticmethod
-    def tickets(bufs: Buffers, n):
-        """The reduce launches' finalize counters (ops.in_stats / in_backward): zeroed once,
-        left zero by every launch; one set per Buffers (its stream's launches are ordered)."""
-        return bufs.zeros("in_tickets", (max(4096, n),), torch.int32)
 
     def conv_fwd8(self, bufs: Buffers, name: str, pc, w8, dqw, x8: Feat, dqx, z: Feat, y: Feat, act,
                   res: Feat = None, q8=None):
@@ -336,7 +330,7 @@ class INLayer:
             ops.in_finalize(z, work, nb, mr)
         else:
             ops.conv_fwd(pc, x, z)
-            ops.in_stats(z, work, mr, tickets=self.tickets(bufs, z.N))
+            ops.in_stats(z, work, mr)
         return mr
 
     def resample_fwd(self, bufs: Buffers, name: str, pc, x: Feat, z: Feat, a_name: str, act, y: Feat, fused, plain):
@@ -357,7 +351,7 @@ class INLayer:
         red = bufs.flat("in_red", 2 * N * C)
         mr = bufs.d["mr_" + name]
         ops.in_backward(dy, z, act, mr, work, red, dx, db=db if INLayer.sum_bias_grad else None, dy2=dy2,
-                        q8=q8 if not INLayer.sum_bias_grad else None, tickets=self.tickets(bufs, N))
+                        q8=q8 if not INLayer.sum_bias_grad else None)
 
 class NoNorm(INLayer):
     """norm='none' (ir:162-163: ``lambda num_features: Identity()``): the layer is just its

@@ -176,37 +176,6 @@ def test_in_backward_bf16(ops, shape, act, dy2, inplace):
     assert HW > 0
 
 
-@pytest.mark.parametrize("shape", IN_SHAPES + [(32, 512, 31, 31)])
-def test_in_reduce_last_block_finalize(ops, shape):
-    """irgan_in_stats / irgan_in_bwd_reduce with tickets: the last block of each image sums
-    its image's partials (fp64, fixed order) instead of the finalize launch -- the same
-    (mean, rstd) and (mean g, mean g*xhat) as the two-launch form to fp32 rounding of an
-    fp64 sum in another order (1 ulp), bit-identical from call to call, tickets left zero."""
-    torch.manual_seed(4)
-    N, C, H, W = shape
-    z = q(torch.randn(shape) * 2 + 0.5)
-    zd = to_slice(z, 0, 0)
-    dy = q(torch.randn(shape))
-    dyd = to_slice(dy, 0, 0)
-    work = torch.empty(ops.IN_PARTS * N * C, dtype=torch.float64, device=DEV)
-    tickets = torch.zeros(4096, dtype=torch.int32, device=DEV)
-    outs = []
-    for t in (None, tickets, tickets):
-        mr = torch.empty(2 * N * C, device=DEV)
-        red = torch.empty(2 * N * C, device=DEV)
-        dx = torch.empty(N, H, W, C, device=DEV, dtype=torch.bfloat16)
-        ops.in_stats(ops.Feat(zd), work, mr, tickets=t)
-        mr0 = mr if not outs else outs[0][0]     # the same table into every backward
-        ops.in_backward(ops.Feat(dyd), ops.Feat(zd), 1, mr0, work, red, ops.Feat(dx), tickets=t)
-        torch.cuda.synchronize()
-        outs.append((mr, red, dx))
-        assert not tickets.any(), "tickets not reset"
-    for k in range(2):
-        torch.testing.assert_close(outs[1][k], outs[0][k], rtol=2.0 ** -22, atol=1e-30)
-        assert torch.equal(outs[1][k], outs[2][k])
-    assert torch.equal(outs[1][2], outs[2][2])
-
-
 # ---------------------------------------------------------------------------
 # resampling (sep_lds_kernel): the step's own shapes and slices at N = 1, and odd sizes
 # ---------------------------------------------------------------------------
