@@ -37,6 +37,12 @@ extern "C" {
 
 typedef void* irgan_stream_t;
 
+/* The source id this library was built from: a hash of csrc/*.hip, csrc/*.h and this header
+ * (computed by pkg/_build.py, baked in at compile time), NUL-terminated into buf[len].
+ * pkg/_lib.py refuses a library whose id differs from the tree it is loaded from.  No
+ * reference counterpart (build provenance of the drop-in library). */
+IRGAN_API int irgan_build_id(char* buf, int32_t len);
+
 enum { IRGAN_F32 = 0, IRGAN_BF16 = 1, IRGAN_FP8 = 2 };  /* FP8: OCP e4m3 (e4m3fn) */
 enum { IRGAN_PAD_ZERO = 0, IRGAN_PAD_REFLECT = 1 };
 /* forward activations (epilogues / IN apply) */
@@ -196,24 +202,21 @@ enum { IRGAN_IN_PARTS = 256 };
  * written by irgan_conv_fwd_stats (the reduction half of irgan_in_stats). */
 IRGAN_API int irgan_in_finalize(const void* part, int32_t N, int32_t HW, int32_t C, int32_t nb, float* mr,
                       irgan_stream_t s);
-/* mr[n][c] = {mean, rstd}; work: IRGAN_IN_PARTS*N*C doubles of scratch.  tickets: NULL, or
- * N int32 counters that are zero before the call and zero again after it (per stream and
- * buffer: no two launches in flight on one set) -- then the last block of each image sums
- * that image's partials itself (fixed order) instead of a second, finalize launch. */
+/* mr[n][c] = {mean, rstd}; work: IRGAN_IN_PARTS*N*C doubles of scratch (a reduce launch,
+ * then a fixed-order finalize launch). */
 IRGAN_API int irgan_in_stats(const void* x, int32_t dtype, int32_t N, int32_t HW, int32_t C,
-                   int32_t ld, int32_t off, double* work, int32_t* tickets, float* mr, irgan_stream_t s);
+                   int32_t ld, int32_t off, double* work, float* mr, irgan_stream_t s);
 /* y = act((x - mean) * rstd) [+ res];  optional xhat output ([P][C], dtype). */
 IRGAN_API int irgan_in_apply(const void* x, int32_t dtype, int32_t N, int32_t HW, int32_t C, int32_t ldx,
                    int32_t xoff, const float* mr, int32_t act, const void* res, int32_t ldr,
                    int32_t roff, void* y, int32_t ldy, int32_t yoff, void* xhat, irgan_stream_t s);
 /* Backward of y = act(IN(x)) [+ res] given the PRE-norm input x and its
  * (mean, rstd): xhat = (x - mean)*rstd, g = (dy [+ dy2]) * act'(xhat),
- * red[n][c] = {mean g, mean g*xhat}.  work: IRGAN_IN_PARTS*N*C doubles of scratch; tickets
- * as irgan_in_stats. */
+ * red[n][c] = {mean g, mean g*xhat}.  work: IRGAN_IN_PARTS*N*C doubles of scratch. */
 IRGAN_API int irgan_in_bwd_reduce(const void* dy, int32_t dy_dtype, int32_t lddy, int32_t dyoff,
                         const void* dy2, int32_t dy2_dtype, int32_t lddy2, int32_t dy2off,
                         const void* x, int32_t x_dtype, int32_t ldx, int32_t xoff, int32_t act,
-                        int32_t N, int32_t HW, int32_t C, const float* mr, double* work, int32_t* tickets,
+                        int32_t N, int32_t HW, int32_t C, const float* mr, double* work,
                         float* red, irgan_stream_t s);
 /* dx = rstd*(g - mean(g) - xhat*mean(g*xhat)); also db[c] += sum dx (fp32 bias
  * grad of the producing conv, caller zeroes) when db != NULL.  dx may alias dy. */

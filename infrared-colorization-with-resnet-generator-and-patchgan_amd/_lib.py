@@ -95,8 +95,27 @@ def load(path: str = LIB_PATH):
         fn = getattr(lib, name)  # AttributeError == symbol missing -> loud failure
         fn.restype = res
         fn.argtypes = args
+    got, want = build_id(lib), tree_id()
+    if got != want:
+        raise IrganError(f"{path} was built from sources {got}, but this tree is {want}: the library is "
+                         "stale -- rebuild it with __graft_entry__.build()")
     _lib = lib
     return lib
+
+
+def tree_id() -> str:
+    """Source id of the csrc/ + include/ tree next to this file (_build.source_id)."""
+    from . import _build
+    return _build.source_id()
+
+
+def build_id(lib=None) -> str:
+    """The source id compiled into a loaded library (irgan_build_id)."""
+    lib = lib if lib is not None else load()
+    buf = ctypes.create_string_buffer(64)
+    if lib.irgan_build_id(buf, len(buf)) != 0:
+        raise IrganError("irgan_build_id failed")
+    return buf.value.decode()
 
 
 def call(name, *args):

@@ -486,11 +486,9 @@ def _wgrad_ws(dev):
 # instance norm / reductions
 # ----------------------------------------------------------------------------
 
-def in_stats(x: Feat, work: torch.Tensor, mr: torch.Tensor, tickets: torch.Tensor = None):
-    """tickets: int32 counters, zero (>= x.N; kept per Buffers): the reduce launch finalizes
-    (irgan_in_stats' last-block sum) instead of a second launch."""
-    assert tickets is None or (tickets.dtype == torch.int32 and tickets.numel() >= x.N)
-    _lib.call("irgan_in_stats", x.ptr, x.dt, x.N, x.H * x.W, x.C, x.ld, x.off, P(work), P(tickets), P(mr), stream())
+def in_stats(x: Feat, work: torch.Tensor, mr: torch.Tensor):
+    """{mean, rstd} of x: partial-sum launch + fixed-order finalize launch."""
+    _lib.call("irgan_in_stats", x.ptr, x.dt, x.N, x.H * x.W, x.C, x.ld, x.off, P(work), P(mr), stream())
 
 
 def in_finalize(x: Feat, part: torch.Tensor, nb: int, mr: torch.Tensor):
@@ -514,17 +512,15 @@ def in_apply(x: Feat, mr, y: Feat, act=ACT_NONE, res: Feat = None, xhat: torch.T
         res.ld if res else 0, res.off if res else 0, y.ptr, y.ld, y.off, P(xhat), stream()))
 
 
-def in_bwd_parts(dy: Feat, x: Feat, act: int, mr, work, red, dx: Feat, db=None, dy2: Feat = None, q8=None,
-                 tickets=None):
+def in_bwd_parts(dy: Feat, x: Feat, act: int, mr, work, red, dx: Feat, db=None, dy2: Feat = None, q8=None):
     """(reduce, apply) launch closures of in_backward (also used for per-pass timing).
     q8 = (y8 Feat, q ptr, amax ptr): the apply also writes the fp8 copy of dx."""
     N, HW, C = x.N, x.H * x.W, x.C
     d2 = (dy2.ptr, dy2.dt, dy2.ld, dy2.off) if dy2 is not None else (None, 0, 0, 0)
-    assert tickets is None or (tickets.dtype == torch.int32 and tickets.numel() >= N)
 
     def reduce():
         _lib.call("irgan_in_bwd_reduce", dy.ptr, dy.dt, dy.ld, dy.off, *d2, x.ptr, x.dt, x.ld, x.off, act, N, HW, C,
-                  P(mr), P(work), P(tickets), P(red), stream())
+                  P(mr), P(work), P(red), stream())
 
     def apply():
         if q8 is not None:
@@ -538,10 +534,9 @@ def in_bwd_parts(dy: Feat, x: Feat, act: int, mr, work, red, dx: Feat, db=None, 
     return reduce, apply
 
 
-def in_backward(dy: Feat, x: Feat, act: int, mr, work, red, dx: Feat, db=None, dy2: Feat = None, q8=None,
-                tickets=None):
+def in_backward(dy: Feat, x: Feat, act: int, mr, work, red, dx: Feat, db=None, dy2: Feat = None, q8=None):
     """dx = backward of act(IN(x)) applied to (dy [+ dy2]); x = PRE-norm input."""
-    reduce, apply = in_bwd_parts(dy, x, act, mr, work, red, dx, db, dy2, q8, tickets)
+    reduce, apply = in_bwd_parts(dy, x, act, mr, work, red, dx, db, dy2, q8)
     _timed("in_bwd_reduce", x, reduce)
     _timed("in_bwd_apply", x, apply)
 

@@ -38,6 +38,24 @@ def test_abi_exports_exactly_the_header():
     assert syms == {n for n, _, _ in irc._lib.PROTOS}, sorted(syms ^ {n for n, _, _ in irc._lib.PROTOS})
 
 
+def test_library_build_id_matches_tree():
+    """libirgan.so carries the hash of the csrc/ + include/ sources it was compiled from
+    (irgan_build_id); it must be this tree's, or load() refuses it."""
+    irc = pkg()
+    lib = irc._lib.load()
+    assert irc._lib.build_id(lib) == irc._lib.tree_id()
+    assert len(irc._lib.tree_id()) == 16
+
+
+def test_stale_library_raises_on_load(monkeypatch):
+    irc = pkg()
+    irc._lib.load()
+    monkeypatch.setattr(irc._lib, "_lib", None)
+    monkeypatch.setattr(irc._lib, "tree_id", lambda: "0" * 16)
+    with pytest.raises(irc._lib.IrganError, match="stale"):
+        irc._lib.load()
+
+
 def _dense(kind, n, p=0, transpose=False):
     irc = pkg()
     T = 8

@@ -33,13 +33,17 @@ class _FakeLib:
         return self.fns.setdefault(name, _FakeFn())
 
 
-def test_stub_argtypes_match_header(monkeypatch):
+def _check_stub_argtypes(monkeypatch):
+    """Run the stub's declarations against a fake CDLL and compare every argtypes list with
+    include/irgan.h.  A raw ctypes call with the wrong arity does not fail, it crashes (the
+    round-4 GPU suite segfaulted on exactly that), so the GPU test runs this before any call."""
     lib = pkg()._lib
     protos = {n: a for n, _, a in lib.PROTOS}
     fake = _FakeLib()
-    monkeypatch.setattr(ctypes, "CDLL", lambda *a, **k: fake)
-    ns = {}
-    exec(compile(_stub_source(), "INTEGRATION.md", "exec"), ns)
+    with monkeypatch.context() as m:
+        m.setattr(ctypes, "CDLL", lambda *a, **k: fake)
+        ns = {}
+        exec(compile(_stub_source(), "INTEGRATION.md", "exec"), ns)
     assert [f for f, _ in ns["ConvDesc"]._fields_] == [f for f, _ in lib.ConvDesc._fields_]
     assert fake.fns, "stub declared no functions"
     for name, fn in fake.fns.items():
@@ -53,8 +57,13 @@ def test_stub_argtypes_match_header(monkeypatch):
                 assert g not in (ctypes.c_int32, ctypes.c_int, ctypes.c_float), name
 
 
+def test_stub_argtypes_match_header(monkeypatch):
+    _check_stub_argtypes(monkeypatch)
+
+
 @pytest.mark.gpu
-def test_stub_runs_on_gpu():
+def test_stub_runs_on_gpu(monkeypatch):
+    _check_stub_argtypes(monkeypatch)
     irc = pkg()
     irc._lib.load()
     src = _stub_source().replace(
