@@ -276,6 +276,9 @@ extern "C" int irgan_conv_wgrad_fp8(const irgan_conv_desc* d, const void* x8, co
         d->Ho != d->OH || d->Wo != d->OW || d->ldx % 16 || d->xoff % 16 || d->ldy % 16 || d->yoff % 16 ||
         (long)d->N * d->H * d->W * d->ldx >= (1L << 31) || (long)d->N * d->Ho * d->Wo * d->ldy >= (1L << 31))
         return IRGAN_EUNSUPPORTED;
+    // reflect_idx() mirrors one pixel past each edge: only the same-size pad-1 3x3 conv
+    if (d->pad_mode == IRGAN_PAD_REFLECT && (d->KH != 3 || d->c0y != -1 || d->H != d->Ho || d->W != d->Wo))
+        return IRGAN_EUNSUPPORTED;
     hipStream_t st = (hipStream_t)s;
     const int cus = irgan_cu_count();
     static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
