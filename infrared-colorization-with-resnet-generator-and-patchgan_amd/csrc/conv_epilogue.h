@@ -20,6 +20,20 @@ IRGAN_HD float conv_act(float v, int act) {
 
 IRGAN_HD float mask_mul(float mv, int mask_act) { return mv > 0.f ? 1.f : (mask_act == 2 ? 0.2f : 0.f); }
 
+// Two packed bf16 values times the ReLU mask of two packed bf16 mask values, on the rounded
+// bits: a value is kept where its mask is > 0 (bits 0x0001..0x7f80), else it becomes the
+// zero of its sign (v * 0.f; Inf / NaN * 0 -> NaN), exactly pk_bf16(v * mask_mul(m, 1)).
+IRGAN_HD uint32_t relu_mask_pk(uint32_t v, uint32_t m) {
+    uint32_t out = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const uint32_t vb = (v >> (16 * h)) & 0xffffu, mb = (m >> (16 * h)) & 0xffffu;
+        const uint32_t r = (mb - 1u) < 0x7f80u ? vb : ((vb & 0x7f80u) == 0x7f80u ? 0x7fc0u : (vb & 0x8000u));
+        out |= r << (16 * h);
+    }
+    return out;
+}
+
 // 8 consecutive output channels co..co+7 of pixel pix: mask, accumulate, store
 // (vec: 16-byte aligned full run; else per-channel with the Cout bound)
 IRGAN_HD void conv_store8(const irgan_conv_desc& d, float (&v)[8], long pix, int co, bool vec, bool out_f32,

@@ -415,13 +415,29 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
     // read latency is paid once per row instead of once per 2-byte element.
     // (a template flag, so the plain-store kernels keep their register allocation)
     const bool acc_vec = ACC && !out_f32 && d.ldy % 4 == 0 && d.yoff % 4 == 0;
+    // ReLU backward mask on a plain bf16 store (the VGG backward-data chain): applied in the
+    // store pass on the rounded values with 16-byte coalesced mask loads issued together
+    // (x * {0, 1} commutes with the bf16 rounding: bit-identical to masking before it);
+    // otherwise (LReLU 0.2, accumulate, fp32 out) in registers, one 8-byte load per fragment
+    // row issued for all NJ fragments before any is used
+    const bool late_mask = mask && d.mask_act == 1 && !ACC && !out_f32 && !STATS && !rg && d.ldm % 8 == 0 &&
+                           d.moff % 8 == 0 && d.ldy % 8 == 0 && d.yoff % 8 == 0;
+    const bool mask_vec = mask && d.ldm % 4 == 0 && d.moff % 4 == 0;
     auto emit = [&](auto actc) {
         constexpr int A = decltype(actc)::value;
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
             const int m = (prow + i) * 16 + (lane & 15);
             const long pix = pix_of(m);
-            uint2 old[NJ];
+            uint2 old[NJ], mk[NJ];
+            if (mask_vec && !late_mask && pix >= 0) {
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                    const int co = n0 + cl0 + j * 16;
+                    mk[j] = co + 4 <= d.Cout ? *(const uint2*)((const bf16_t*)mask + pix * d.ldm + d.moff + co)
+                                             : make_uint2(0u, 0u);
+                }
+            }
             if (acc_vec && pix >= 0) {
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) {
@@ -444,11 +460,18 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
 #pragma unroll
                 for (int r = 0; r < 4; ++r) v[r] = conv_act(v[r], A);
                 const bool full = co + 4 <= d.Cout;
-                if (pix >= 0 && mask) {
-                    const bf16_t* mp = (const bf16_t*)mask + pix * d.ldm + d.moff + co;
+                if (pix >= 0 && mask && !late_mask) {
+                    if (mask_vec && full) {
+                        v[0] *= mask_mul(__uint_as_float(mk[j].x << 16), d.mask_act);
+                        v[1] *= mask_mul(__uint_as_float(mk[j].x & 0xffff0000u), d.mask_act);
+                        v[2] *= mask_mul(__uint_as_float(mk[j].y << 16), d.mask_act);
+                        v[3] *= mask_mul(__uint_as_float(mk[j].y & 0xffff0000u), d.mask_act);
+                    } else {
+                        const bf16_t* mp = (const bf16_t*)mask + pix * d.ldm + d.moff + co;
 #pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        if (full || co + r < d.Cout) v[r] *= mask_mul(bf2f(mp[r]), d.mask_act);
+                        for (int r = 0; r < 4; ++r)
+                            if (full || co + r < d.Cout) v[r] *= mask_mul(bf2f(mp[r]), d.mask_act);
+                    }
                 }
                 if (out_f32) {
                     if (pix < 0) continue;
@@ -555,6 +578,28 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
     const int c8 = (tid % LPP) * 8, co8 = n0 + c8;
     if (co8 >= d.Cout) return;
     const bool vec = co8 + 8 <= d.Cout && d.ldy % 8 == 0 && d.yoff % 8 == 0;
+    if (late_mask && vec) {
+        constexpr int NIT = (256 + PPASS - 1) / PPASS;  // pixel rows per thread
+        uint4 mk[NIT];
+#pragma unroll
+        for (int q = 0; q < NIT; ++q) {  // every mask load in flight before the first store
+            const int m = tid / LPP + q * PPASS;
+            const long pix = m < 256 ? pix_of(m) : -1;
+            mk[q] = pix >= 0 ? *(const uint4*)((const bf16_t*)mask + pix * d.ldm + d.moff + co8)
+                             : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int q = 0; q < NIT; ++q) {
+            const int m = tid / LPP + q * PPASS;
+            const long pix = m < 256 ? pix_of(m) : -1;
+            if (pix < 0) continue;
+            const uint4 o = *(const uint4*)(smem + m * RSB + c8 * 2);
+            *(uint4*)((bf16_t*)y + pix * d.ldy + d.yoff + co8) = make_uint4(
+                relu_mask_pk(o.x, mk[q].x), relu_mask_pk(o.y, mk[q].y), relu_mask_pk(o.z, mk[q].z),
+                relu_mask_pk(o.w, mk[q].w));
+        }
+        return;
+    }
     for (int m = tid / LPP; m < 256; m += PPASS) {
         const long pix = pix_of(m);
         if (pix < 0) continue;

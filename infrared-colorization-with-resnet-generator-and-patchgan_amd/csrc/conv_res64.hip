@@ -155,9 +155,31 @@ __global__ __launch_bounds__(512, 1) void conv_res64_kernel(const irgan_conv_des
             wait_vm_dyn(__builtin_amdgcn_readfirstlane(younger));
         }
         lds_barrier();  // every wave's pieces of this patch's halo (and the weights) landed
+        // this patch's epilogue operands (backward mask, accumulate's old values) are loaded
+        // now, ahead of the next halo and the K loop, so their latency hides under the MFMAs
+        // (loaded at the epilogue they stalled every patch: VGG conv1_2 backward-data 130 us
+        // against its forward's 81)
+        const int pxi = p % tpx, pyi = (p / tpx) % tpy, img = p / (tpx * tpy);
+        uint2 old[MI][NJ], mk[MI][NJ];
+        long pixs[MI];
+        bool oks[MI];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+            const int oy = pyi * PH + prow + i, ox = pxi * PW + (lane & 15);
+            oks[i] = oy < d.Ho && ox < d.Wo;
+            pixs[i] = oks[i] ? ((long)img * d.OH + oy * d.omy + d.ooy) * d.OW + ox * d.omx + d.oox : 0;
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int co = n0 + cl0 + j * 16;
+                old[i][j] = mk[i][j] = make_uint2(0u, 0u);
+                if (ACC && oks[i]) old[i][j] = *(const uint2*)(y + pixs[i] * d.ldy + d.yoff + co);
+                if (vmask && oks[i]) mk[i][j] = *(const uint2*)(mask + pixs[i] * d.ldm + d.moff + co);
+            }
+        }
         // ONEB: every wave has also finished patch it-1 (K loop and stores), so its halo buffer
         // takes patch it+1's halo now
-        if (ONEB && it > 0 && p + qs < P) issue_halo(p + qs, buf ^ 1);
+        const bool halo_next = ONEB && it > 0 && p + qs < P;
+        if (halo_next) issue_halo(p + qs, buf ^ 1);
         if constexpr (STATS) {
             // patch it-1's partials: its 8 wave rows are complete (written before this barrier)
             if (it > 0 && lane < 8) {
@@ -205,8 +227,9 @@ __global__ __launch_bounds__(512, 1) void conv_res64_kernel(const irgan_conv_des
         // here -- a wave that finishes its MFMAs stores while the others still multiply
         if (!ONEB) lds_barrier();
 
-        // ---- epilogue from the accumulators
-        const int pxi = p % tpx, pyi = (p / tpx) % tpy, img = p / (tpx * tpy);
+        // ---- epilogue from the accumulators (the prefetched operands are older than the
+        // halo pieces issued after them: only those may stay in flight)
+        if (ACC || vmask) wait_vm_dyn(__builtin_amdgcn_readfirstlane(halo_next ? nh : 0));
         float st[2 * NJ * 4];  // STATS: (sum, sum of squares) of channel (j, r) at [2 (4j + r) + {0, 1}]
 #pragma unroll
         for (int k = 0; k < 2 * NJ * 4; ++k) st[k] = 0.f;
@@ -214,17 +237,8 @@ __global__ __launch_bounds__(512, 1) void conv_res64_kernel(const irgan_conv_des
             constexpr int A = decltype(actc)::value;
 #pragma unroll
             for (int i = 0; i < MI; ++i) {
-                const int oy = pyi * PH + prow + i, ox = pxi * PW + (lane & 15);
-                const bool ok = oy < d.Ho && ox < d.Wo;
-                const long pix = ok ? ((long)img * d.OH + oy * d.omy + d.ooy) * d.OW + ox * d.omx + d.oox : 0;
-                uint2 old[NJ], mk[NJ];
-#pragma unroll
-                for (int j = 0; j < NJ; ++j) {
-                    const int co = n0 + cl0 + j * 16;
-                    old[j] = mk[j] = make_uint2(0u, 0u);
-                    if (ACC && ok) old[j] = *(const uint2*)(y + pix * d.ldy + d.yoff + co);
-                    if (vmask && ok) mk[j] = *(const uint2*)(mask + pix * d.ldm + d.moff + co);
-                }
+                const bool ok = oks[i];
+                const long pix = pixs[i];
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) {
                     const int co = n0 + cl0 + j * 16;
@@ -234,11 +248,11 @@ __global__ __launch_bounds__(512, 1) void conv_res64_kernel(const irgan_conv_des
                     for (int r = 0; r < 4; ++r) {
                         v[r] = conv_act(acc[i][j][r] + bb[r], A);
                         if (vmask) {
-                            const uint32_t mw = r < 2 ? mk[j].x : mk[j].y;
+                            const uint32_t mw = r < 2 ? mk[i][j].x : mk[i][j].y;
                             v[r] *= mask_mul(__uint_as_float((r & 1) ? (mw & 0xffff0000u) : (mw << 16)), d.mask_act);
                         }
                         if (ACC) {
-                            const uint32_t ow = r < 2 ? old[j].x : old[j].y;
+                            const uint32_t ow = r < 2 ? old[i][j].x : old[i][j].y;
                             v[r] += __uint_as_float((r & 1) ? (ow & 0xffff0000u) : (ow << 16));
                         }
                     }
@@ -325,15 +339,13 @@ void launch(const irgan_conv_desc* d, const void* x, const void* w, const float*
             float2* part, hipStream_t st) {
     const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH), ntn = d->Cout / 64;
     const int grid = grid_for(ntn, d->N * tpx * tpy * ntn);
-    static const int xg = getenv("IRGAN_RES64_NO_XCDG") ? 0 : 1;
-    const int xcdg = xg && ntn > 1 && grid % (8 * ntn) == 0;
-    static const bool oneb = !getenv("IRGAN_RES64_TWOB");
+    const int xcdg = ntn > 1 && grid % (8 * ntn) == 0;
 #define R64(ACCV, STV, OB)                                                                                          \
     conv_res64_kernel<ACCV, STV, OB><<<grid, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias,             \
                                                            (bf16_t*)y, (const bf16_t*)mask, ntn, tpx, tpy, part, xcdg)
     if (part) R64(false, true, false);
-    else if (d->accumulate) { if (oneb) R64(true, false, true); else R64(true, false, false); }
-    else { if (oneb) R64(false, false, true); else R64(false, false, false); }
+    else if (d->accumulate) R64(true, false, true);
+    else R64(false, false, true);
 #undef R64
 }
 

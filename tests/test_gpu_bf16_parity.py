@@ -240,6 +240,46 @@ def test_bf16_res64_act_mask_tight(ops, cout, H, mode):
         check(nchw64(y), y64 * mm, ya, R_BF16, f"mask {mact}")
 
 
+@pytest.mark.parametrize("cin,cout,H", [(128, 128, 40), (256, 256, 24), (128, 64, 33), (256, 128, 16)])
+def test_bf16_pp_mask_tight(ops, cin, cout, H):
+    """conv_pp (Cin > 64) with a backward mask (the VGG backward-data chain, ir:664, and D's
+    LeakyReLU masks): the ReLU mask is applied in the store pass on the rounded values, the
+    LeakyReLU mask and accumulate in registers.  Mask slices with an offset and exact / signed
+    zeros in the mask; the ReLU-masked output must also equal the unmasked output with the
+    masked-off elements zeroed, bit for bit."""
+    torch.manual_seed(11)
+    N = 2
+    spec = ops.ConvSpec(cin, cout, 3, 1, 1, 0)
+    x = q(torch.randn(N, cin, H, H))
+    w = q(torch.randn(cout, cin, 3, 3) * (1.0 / (cin * 9) ** 0.5))
+    m = q(torch.randn(N, cout, H, H))
+    m[:, :, ::3] = 0.0
+    m[:, :, 1::5] = -0.0
+    pc = ops.PackedConv(spec, w.permute(0, 2, 3, 1).contiguous().reshape(-1).to(DEV), None, ops.BF16)
+    pc.pack()
+    y64 = ref_conv(x.double(), w.double(), None, 3, 1, 1, 0)
+    ya = ref_conv(x.abs().double(), w.abs().double(), None, 3, 1, 1, 0)
+    md = torch.zeros(N, H, H, cout + 16, device=DEV, dtype=torch.bfloat16)
+    md[..., 8:8 + cout] = nhwc(m)
+    xd = nhwc(x)
+    plain = torch.zeros(N, H, H, cout, device=DEV, dtype=torch.bfloat16)
+    ops.conv_fwd(pc, ops.Feat(xd), ops.Feat(plain), bias=False)
+    for mact, slope in ((1, 0.0), (2, 0.2)):
+        y = torch.zeros(N, H, H, cout, device=DEV, dtype=torch.bfloat16)
+        ops.conv_fwd(pc, ops.Feat(xd), ops.Feat(y), bias=False, mask=ops.Feat(md, 8, cout), mask_act=mact)
+        mm = torch.where(m > 0, 1.0, slope).double()
+        check(nchw64(y), y64 * mm, ya, R_BF16, f"mask {mact}")
+        if mact == 1:
+            keep = (md[..., 8:8 + cout].float() > 0)
+            assert torch.equal(y.view(torch.int16), torch.where(keep, plain, plain * 0).view(torch.int16))
+        # accumulate onto a prior gradient (the register path for both masks)
+        base = q(torch.randn(N, cout, H, H))
+        ya2 = nhwc(base)
+        ops.conv_fwd(pc, ops.Feat(xd), ops.Feat(ya2), bias=False, accumulate=True, mask=ops.Feat(md, 8, cout),
+                     mask_act=mact)
+        check(nchw64(ya2), y64 * mm + base.double(), ya + base.abs().double(), R_BF16, f"acc mask {mact}")
+
+
 @pytest.mark.parametrize("N,H,W", [(2, 32, 48), (1, 64, 64), (3, 48, 32), (2, 16, 64), (1, 37, 64)])
 def test_reflect_dgrad_ring_tight(ops, N, H, W):
     """ResnetBlock backward-data (ir:386-411) through ops.conv_dgrad: the interior conv_pp launch
