@@ -28,6 +28,24 @@ ALG = {"fwd": 2 * 16 * 64 * 64 * 256 * 2 + 256 * 256 * 9 * 2,
        "wgrad": 2 * 16 * 64 * 64 * 256 * 2 + 256 * 256 * 9 * 4}
 
 
+def kernel_name(k):
+    """'void (anonymous namespace)::conv_pp_kernel<3, 3, 256, ...>(irgan_conv_desc, ...)' ->
+    'conv_pp_kernel<3, 3, 256, ...>' (the template arguments name the variant)."""
+    k = k.replace("(anonymous namespace)::", "")
+    if k.startswith("void "):
+        k = k[5:]
+    depth, end = 0, len(k)
+    for i, ch in enumerate(k):
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == "(" and depth == 0:
+            end = i
+            break
+    return k[:end][:120]
+
+
 def per_kernel(d, counter):
     vals = collections.defaultdict(list)
     p = os.path.join(d, "run_counter_collection.csv")
@@ -45,7 +63,7 @@ def fam_mean(vals):
         vs = vs[1:] or vs   # drop the cold first dispatch
         tot += sum(vs) / len(vs)
         n = max(n, len(vs))
-        names.append(k.split("(")[0][:90])
+        names.append(kernel_name(k))
     return tot, n, names
 
 
