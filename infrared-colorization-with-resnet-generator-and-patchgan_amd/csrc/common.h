@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include "irgan.h"
 
 typedef uint16_t bf16_t;
@@ -143,3 +144,9 @@ static inline void* irgan_symbol(const void* sym, void** cache) {
     return p;
 }
 static inline bool irgan_det(const irgan_conv_desc* d) { return (d->flags & IRGAN_CONV_DETERMINISTIC) != 0; }
+// XCD-aware tile order (xcd_tile) for every launcher: on unless IRGAN_NO_XCD_SWZ is set (the
+// one A/B switch kept for it: the L2 locality it buys is layer-dependent)
+static inline int irgan_xcd_swz() {
+    static const int v = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
+    return v;
+}

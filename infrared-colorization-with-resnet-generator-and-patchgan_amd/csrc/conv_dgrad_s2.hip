@@ -234,7 +234,7 @@ extern "C" int irgan_conv_dgrad_s2(const irgan_conv_desc* d, const void* dy, con
     }
     // every dx pixel (2i + py, 2j + px) must come from dy position i (< H) of its phase
     if ((a.OH + 1) / 2 > a.H || (a.OW + 1) / 2 > a.W) return IRGAN_EUNSUPPORTED;
-    static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
+    const int swz = irgan_xcd_swz();
     const int tpy = irgan_cdiv((a.OH + 1) / 2, S2P), tpx = irgan_cdiv((a.OW + 1) / 2, S2P);
     hipStream_t st = (hipStream_t)s;
     const bool one = a.Cin == 64;  // one chunk: a single halo buffer (BN 16: two blocks per CU)

@@ -164,7 +164,7 @@ extern "C" int irgan_conv_fwd_glds_split(const irgan_conv_desc* d, const void* x
     static void* zero_cache[IRGAN_MAX_DEVICES];  // the zero page's address per device
     const bf16_t* zero = (const bf16_t*)irgan_symbol(HIP_SYMBOL(g_irgan_zero_page), zero_cache);
     if (!zero) return IRGAN_EUNSUPPORTED;
-    static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
+    const int swz = irgan_xcd_swz();
     if (ksplit < 1) ksplit = 1;
     if (d->Cout > 64) {
         const int ntn = irgan_cdiv(d->Cout, 128);
@@ -380,7 +380,7 @@ extern "C" int irgan_conv_wgrad_glds(const irgan_conv_desc* d, const void* x, co
         if (splitk > maxs) splitk = (int)maxs;
         if (splitk < 1) splitk = 1;
     }
-    static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
+    const int swz = irgan_xcd_swz();
     // prefer a split count that makes the grid a multiple of 8 (XCD remap)
     if (swz && splitk > 1 && (tiles * splitk) % 8) {
         for (int s2 = splitk; s2 >= 1 && s2 >= splitk - 7; --s2)

@@ -318,7 +318,7 @@ extern "C" int irgan_conv_fwd_halo(const irgan_conv_desc* d, const void* x, cons
     static void* zero_cache[IRGAN_MAX_DEVICES];  // the zero page's address per device
     const bf16_t* zero = (const bf16_t*)irgan_symbol(HIP_SYMBOL(g_halo_zero_page), zero_cache);
     if (!zero) return IRGAN_EUNSUPPORTED;
-    static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
+    const int swz = irgan_xcd_swz();
     static const bool narrow = !getenv("IRGAN_NO_NARROW");
     if (narrow && d->Cout <= 8) {
         // one 64-channel chunk: the row-span GEMM (conv_rowspan.hip: outc, VGG conv1_1 dgrad)

@@ -11,37 +11,18 @@ void launch(const irgan_conv_desc* d, const void* x, const void* w, const float*
 
 namespace {
 
-// single-halo-buffer policy for BN-64 tiles (A/B knobs: IRGAN_NO_PP_ONE,
-// IRGAN_PP_ONE_MAXCH = the most input channel chunks that take it; default: all)
-bool use_one(int cin) {
-    static int mx = -1;
-    if (mx < 0) {
-        mx = getenv("IRGAN_NO_PP_ONE") ? 0 : 1 << 20;
-        if (const char* e = getenv("IRGAN_PP_ONE_MAXCH")) mx = atoi(e);
-    }
-    return cin / 64 <= mx;
-}
-
-// Cout % 128 (not % 256) layers with at most this many input chunks run as BN-64
-// single-halo tiles (IRGAN_PP_SPLIT128, default: all): two blocks per CU beat one
-// BN-128 block on every such layer of the step (down1 / up1 / VGG conv2,
-// profiles/r02_s5_pp_one_ab.txt)
-bool split128(int cin) {
-    static int mx = -1;
-    if (mx < 0) {
-        mx = 1 << 20;
-        if (const char* e = getenv("IRGAN_PP_SPLIT128")) mx = atoi(e);
-    }
-    return cin / 64 <= mx;
-}
+// BN-64 tiles take the single-halo buffer (two blocks per CU), and Cout % 128 (not % 256)
+// layers run as BN-64 single-halo tiles: two blocks per CU beat one BN-128 block on every
+// such layer of the step (down1 / up1 / VGG conv2, profiles/r02_s5_pp_one_ab.txt)
+constexpr bool use_one(int) { return true; }
+constexpr bool split128(int) { return true; }
 
 // Output-channel tile for a Cout % 256 == 0 layer: 256 unless that leaves most CUs idle
 // (the PatchGAN 4x4 layers at 32x32: D model.8 backward-data at B = 16 is 64 BN-256 blocks
 // for 256 CUs) -- then 128 or the 64-channel single-halo tile (two blocks per CU)
 int narrow_bn(const irgan_conv_desc* d) {
-    static const bool off = getenv("IRGAN_NO_PP_NARROW_BN") != nullptr;
     const long patches = (long)d->N * irgan_cdiv(d->Ho, PH) * irgan_cdiv(d->Wo, PW);
-    if (off || patches * (d->Cout / 256) >= 160) return 256;
+    if (patches * (d->Cout / 256) >= 160) return 256;
     return patches * (d->Cout / 128) >= 160 ? 128 : 64;
 }
 
@@ -80,11 +61,7 @@ extern "C" int irgan_conv_fwd_pp(const irgan_conv_desc* d, const void* x, const 
         d->ldx % 8 || d->xoff % 8 || (long)d->N * d->H * d->W * d->ldx >= (1L << 30) ||
         (long)d->Cout * d->KH * d->KW * d->Cin >= (1L << 30))
         return IRGAN_EUNSUPPORTED;
-    static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
-    static const bool pp128 = !getenv("IRGAN_NO_PP128");
-    // measured (profiles/r01_s7_pp_ab.txt): up2 dgrad (Cout 192) 539 -> 351 us, Cout-64 layers +6 %
-    static const bool pp192 = !getenv("IRGAN_NO_PP192");
-    static const bool pp64 = !getenv("IRGAN_NO_PP64");
+    const int swz = irgan_xcd_swz();
     if (irgan_res64::ok(d) && (!mask || (d->ldm % 4 == 0 && d->moff % 4 == 0))) {  // one input chunk: resident weights
         irgan_res64::launch(d, x, w, bias, y, mask, nullptr, st);
         IRGAN_LAUNCH_CHECK();
@@ -95,16 +72,9 @@ extern "C" int irgan_conv_fwd_pp(const irgan_conv_desc* d, const void* x, const 
         if (k33) launch_pp<3, 3, 256>(d, x, w, bias, y, mask, st, swz);
         else launch_pp<4, 4, 256>(d, x, w, bias, y, mask, st, swz);
     } else if (nbn == 128 || (nbn == 0 && d->Cout % 128 == 0 && !split128(d->Cin))) {
-        if (!pp128) return IRGAN_EUNSUPPORTED;
         if (k33) launch_pp<3, 3, 128>(d, x, w, bias, y, mask, st, swz);
         else launch_pp<4, 4, 128>(d, x, w, bias, y, mask, st, swz);
-    } else if (d->Cout == 192 && getenv("IRGAN_PP_NOSPLIT192")) {  // up2_conv backward-data (dx = [up | skip] = 128 + 64 channels)
-        // (default: three BN-64 single-halo tiles, 350 -> 323 us)
-        if (!pp192) return IRGAN_EUNSUPPORTED;
-        if (k33) launch_pp<3, 3, 192>(d, x, w, bias, y, mask, st, swz);
-        else launch_pp<4, 4, 192>(d, x, w, bias, y, mask, st, swz);
-    } else {
-        if (!pp64) return IRGAN_EUNSUPPORTED;
+    } else {  // BN-64 single-halo tiles (up2_conv's Cout-192 backward-data: three of them, 350 -> 323 us)
         if (k33) launch_pp<3, 3, 64>(d, x, w, bias, y, mask, st, swz);
         else launch_pp<4, 4, 64>(d, x, w, bias, y, mask, st, swz);
     }
@@ -124,14 +94,13 @@ extern "C" int irgan_conv_dgrad_reflect_line(const irgan_conv_desc* d, const voi
                                              void* dx, float* ws, int64_t ws_floats, irgan_stream_t s) {
     if (!d || !dy || !w || !dx || !ws) return IRGAN_EINVAL;
     if ((long)d->N * d->Ho * d->Wo <= 0 || d->Cout <= 0) return 0;
-    static const bool off = getenv("IRGAN_NO_RING_EPI") != nullptr;
-    if (off || !ring_line_check(d, p, ws_floats) || d->out_dtype != IRGAN_BF16 || d->act != IRGAN_ACT_NONE ||
+    if (!ring_line_check(d, p, ws_floats) || d->out_dtype != IRGAN_BF16 || d->act != IRGAN_ACT_NONE ||
         d->sy != 1 || d->sx != 1 || d->Cin % 64 || d->Cout % 256 || narrow_bn(d) != 256 || irgan_res64::ok(d) ||
         (long)d->N * d->H * d->W * d->ldx >= (1L << 30) || (long)d->Cout * 9 * d->Cin >= (1L << 30))
         return IRGAN_EUNSUPPORTED;
     hipStream_t st = (hipStream_t)s;
     ring_line_gemm_launch(d, dy, w, ws, st);
-    static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
+    const int swz = irgan_xcd_swz();
     const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH), ntn = d->Cout / 256;
     const int nb = d->N * tpy * tpx * ntn;
     if (d->accumulate)
@@ -165,7 +134,7 @@ extern "C" int irgan_conv_dgrad_reflect_line_fp8(const irgan_conv_desc* d, const
         return IRGAN_EUNSUPPORTED;
     hipStream_t st = (hipStream_t)s;
     ring_line_gemm_launch(d, dy, w, ws, st);
-    static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
+    const int swz = irgan_xcd_swz();
     const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH), ntn = d->Cout / 256;
     const int nb = d->N * tpy * tpx * ntn;
     if (d->accumulate)
@@ -193,12 +162,12 @@ extern "C" int irgan_conv_fwd_stats(const irgan_conv_desc* d, const void* x, con
         d->xoff % 8 ||
         d->ldy % 8 || d->yoff % 8 || d->Ho != d->OH || d->Wo != d->OW || d->omy != 1 || d->omx != 1 || d->ooy ||
         d->oox || (long)d->N * d->H * d->W * d->ldx >= (1L << 30) ||
-        (long)d->Cout * d->KH * d->KW * d->Cin >= (1L << 30) || getenv("IRGAN_NO_FUSED_STATS"))
+        (long)d->Cout * d->KH * d->KW * d->Cin >= (1L << 30))
         return IRGAN_EUNSUPPORTED;
     const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH);
     if (tpx * tpy > IRGAN_IN_PARTS) return IRGAN_EUNSUPPORTED;
     if ((long)d->N * d->Ho * d->Wo <= 0) return IRGAN_EUNSUPPORTED;
-    static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
+    const int swz = irgan_xcd_swz();
     const int bn = d->Cout % 256 == 0 ? narrow_bn(d)
                                       : (d->Cout % 128 == 0 && !split128(d->Cin) ? 128 : 64);  // as irgan_conv_fwd_pp
     const int ntn = d->Cout / bn;
@@ -247,7 +216,7 @@ extern "C" int irgan_conv_fwd_fp8(const irgan_conv_desc* d, const void* x, const
         return IRGAN_EUNSUPPORTED;
     const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH);
     if (part && tpx * tpy > IRGAN_IN_PARTS) return IRGAN_EUNSUPPORTED;
-    static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
+    const int swz = irgan_xcd_swz();
     const int bn = d->Cout % 256 == 0 ? 256 : (d->Cout % 128 == 0 ? 128 : 64);
     const int ntn = d->Cout / bn;
     const int blocks = d->N * tpy * tpx * ntn;

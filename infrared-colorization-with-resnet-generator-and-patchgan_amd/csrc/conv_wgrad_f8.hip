@@ -281,7 +281,7 @@ extern "C" int irgan_conv_wgrad_fp8(const irgan_conv_desc* d, const void* x8, co
         return IRGAN_EUNSUPPORTED;
     hipStream_t st = (hipStream_t)s;
     const int cus = irgan_cu_count();
-    static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
+    const int swz = irgan_xcd_swz();
     const int ntco = d->Cout / 128, nci = d->Cin / 64;
     const int tiles = ntco * nci * d->KH;
     const int nseg = d->N * d->Ho * d->Wo / 128;

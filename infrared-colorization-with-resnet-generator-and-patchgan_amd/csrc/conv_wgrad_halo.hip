@@ -313,15 +313,9 @@ extern "C" int irgan_conv_wgrad_halo(const irgan_conv_desc* d, const void* x, co
     static void* zero_cache[IRGAN_MAX_DEVICES];  // the zero page's address per device
     const bf16_t* zero = (const bf16_t*)irgan_symbol(HIP_SYMBOL(g_wgh_zero_page), zero_cache);
     if (!zero) return IRGAN_EUNSUPPORTED;
-    static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
+    const int swz = irgan_xcd_swz();
     const int s2 = d->sx == 2;
-    static const bool wide = getenv("IRGAN_WGH_256") != nullptr;
-    static const int var = getenv("IRGAN_WGH_VAR") ? atoi(getenv("IRGAN_WGH_VAR")) : 0;
-    if (wide && d->Cout % 256 == 0 && d->KW == 3 && !s2) {
-        launch_t<256, 3, 1, 4, 2>(d, x, dy, dw, splitk, st, zero, swz, ws, ws_cap);
-    } else if (var == 22 && d->Cout % 128 == 0 && d->KW == 3 && !s2) {  // A/B: 4 waves, 64 x 96 wave tiles
-        launch_t<128, 3, 1, 2, 2>(d, x, dy, dw, splitk, st, zero, swz, ws, ws_cap);
-    } else if (var != 24 && d->Cout % 128 == 0 && d->KW == 3 && !s2) {
+    if (d->Cout % 128 == 0 && d->KW == 3 && !s2) {
         // 4 waves of 128 x 48 wave tiles (each A fragment read feeds 3 MFMAs, each B 8):
         // resblock wgrad 124 -> 114 us vs 8 waves of 64 x 48 (profiles/r01_s9_wgrad_ab.txt)
         launch_t<128, 3, 1, 1, 4>(d, x, dy, dw, splitk, st, zero, swz, ws, ws_cap);

@@ -575,17 +575,15 @@ __global__ __launch_bounds__(256) void wgrad_pc_reduce(const float* __restrict__
 extern "C" int irgan_conv_wgrad_pc(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, int splitk,
                                    float* ws, long ws_cap, hipStream_t st) {
     if ((long)d->N * d->Ho * d->Wo <= 0) return 0;
-    static const bool no64 = getenv("IRGAN_NO_WGRAD_PC64") != nullptr;
-    static const bool nopair = getenv("IRGAN_NO_WGRAD_PC_PAIR") != nullptr;
     const int BMC = d->Cout % 128 == 0 ? 128 : 64;
-    const bool pair = d->KW == 4 && d->KH == 4 && d->Wo <= 32 && BMC == 128 && !nopair;
-    if (getenv("IRGAN_NO_WGRAD_PC") || d->dtype != IRGAN_BF16 || (d->KW != 3 && !pair) || d->sx != 1 || d->sy != 1 ||
-        d->Cout % BMC || (BMC == 64 && no64) || d->Cin % 64 || (d->Wo % 64 && !pair) || d->ldx % 8 || d->xoff % 8 ||
+    const bool pair = d->KW == 4 && d->KH == 4 && d->Wo <= 32 && BMC == 128;
+    if (d->dtype != IRGAN_BF16 || (d->KW != 3 && !pair) || d->sx != 1 || d->sy != 1 ||
+        d->Cout % BMC || d->Cin % 64 || (d->Wo % 64 && !pair) || d->ldx % 8 || d->xoff % 8 ||
         d->ldy % 8 || d->yoff % 8 || (long)d->N * d->H * d->W * d->ldx * 2 >= (1L << 31) ||
         (long)d->N * d->Ho * d->Wo * d->ldy * 2 >= (1L << 31))
         return IRGAN_EUNSUPPORTED;
     const int cus = irgan_cu_count();
-    static const int swz = getenv("IRGAN_NO_XCD_SWZ") ? 0 : 1;
+    const int swz = irgan_xcd_swz();
     if (!pair && BMC == 128 && d->KW == 3 && d->Cin % 128 == 0 && splitk <= 0) {
         const int ntco = d->Cout / 128, nci2 = d->Cin / 128;
         const int tiles = ntco * nci2 * d->KH;
@@ -632,14 +630,12 @@ extern "C" int irgan_conv_wgrad_pc(const irgan_conv_desc* d, const void* x, cons
     splitk = irgan_cdiv(nseg, spb);
     const long n = (long)d->Cout * d->KH * d->KW * d->Cin;
     float* slab = (ws && splitk > 1 && n % 4 == 0 && (long)splitk * n <= ws_cap) ? ws : nullptr;
-    static const int cw = getenv("IRGAN_WGPC_CW4") ? 4 : 8;
 #define WPC(B, C, ...)                                                                                          \
     wgrad_pc_kernel<B, C, ##__VA_ARGS__><<<tiles * splitk, PC<B, C>::NT, 0, st>>>(                             \
         *d, (const bf16_t*)x, (const bf16_t*)dy, dw, spb, nseg, ntco, nci, swz, slab)
     if (pair) WPC(128, 8, 4, true);
     else if (BMC == 64) WPC(64, 4);   // 4 co fragments x 3 per compute wave (8 waves would hold 2 x 3)
-    else if (cw == 8) WPC(128, 8);
-    else WPC(128, 4);
+    else WPC(128, 8);
 #undef WPC
     if (slab) {
         const int blocks = (int)std::min<long>(irgan_cdiv(n / 4, 256), 2048);

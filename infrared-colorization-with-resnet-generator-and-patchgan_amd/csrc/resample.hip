@@ -205,26 +205,15 @@ __global__ __launch_bounds__(NT) void sep_lds_kernel(const void* __restrict__ in
 }
 
 // Threads per block of sep_lds_kernel and the LDS row cap (floats) that sizes its channel
-// group: 512 threads with CB <= 8192 / Win (A/B knob IRGAN_SEP_NT=1024: CB <= 16384 / Win,
-// 256: a quarter).  Half-size groups double the blocks and let two resident blocks per CU
-// overlap one's load with the other's taps: the six resample launches of a step sum
-// 659 -> 576 us standalone and the step goes 1191 -> 1204 img/s (same box, 3 reps each).
-int sep_nt() {
-    static int v = -1;
-    if (v < 0) v = getenv("IRGAN_SEP_NT") ? atoi(getenv("IRGAN_SEP_NT")) : 512;
-    if (v != 256 && v != 1024) v = 512;
-    return v;
-}
+// group: 512 threads with CB <= 8192 / Win.  Half-size groups (against 1024 threads) double
+// the blocks and let two resident blocks per CU overlap one's load with the other's taps: the
+// six resample launches of a step sum 659 -> 576 us standalone and the step goes 1191 -> 1204
+// img/s (same box, 3 reps each; profiles/r03_resample_nt_sweep.txt).
+constexpr int sep_nt() { return 512; }
 
-// XCD-aware row order for sep_lds_kernel, on by default (A/B knob IRGAN_SEP_SWZ=0): each
-// XCD takes a contiguous range of output rows, so the input rows their vertical taps share
-// stay in that XCD's L2
-
-int sep_swz() {
-    static int v = -1;
-    if (v < 0) v = getenv("IRGAN_SEP_SWZ") ? atoi(getenv("IRGAN_SEP_SWZ")) : 1;
-    return v;
-}
+// XCD-aware row order for sep_lds_kernel: each XCD takes a contiguous range of output rows,
+// so the input rows their vertical taps share stay in that XCD's L2 (IRGAN_NO_XCD_SWZ)
+int sep_swz() { return irgan_xcd_swz(); }
 
 // Reflect-pad backward, border part.  The backward-data result g over the
 // padded domain (H+2p) x (W+2p) has its interior in dx already; its RING comes
