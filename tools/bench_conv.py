@@ -20,6 +20,8 @@ CASES = [  # name, cin, cout, k, s, p, mode, H
     ("vgg33_256-256@64", 256, 256, 3, 1, 1, 0, 64),
     ("D2_128-256s2@64", 128, 256, 4, 2, 1, 0, 64),
     ("D3_256-512s1@32", 256, 512, 4, 1, 1, 0, 32),
+    ("D1_64-128s2@128", 64, 128, 4, 2, 1, 0, 128),
+    ("Dhead_512-1@31", 512, 1, 4, 1, 1, 0, 31),
 ]
 def t(fn, it=20):
     fn(); torch.cuda.synchronize()
@@ -33,8 +35,10 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--case", default=None, help="substring filter on case names")
 ap.add_argument("--which", default="fwd,dgrad,wgrad")
 ap.add_argument("--iters", type=int, default=20)
+ap.add_argument("--batch", type=int, default=16)
 ap.add_argument("--splitk", default="0", help="comma list of wgrad split-K values (0 = the kernel's choice)")
 args = ap.parse_args()
+B = args.batch
 res = {}
 for name, cin, cout, k, s, p, mode, H in CASES:
     if args.case and args.case not in name:
@@ -45,7 +49,7 @@ for name, cin, cout, k, s, p, mode, H in CASES:
     x = torch.randn(B, H, H, cin, device=DEV).bfloat16()
     Ho, Wo = spec.out_hw(H, H)
     y = torch.empty(B, Ho, Wo, cout, device=DEV, dtype=torch.bfloat16)
-    dy = torch.randn(B, Ho, Wo, cout, device=DEV).bfloat16()
+    dy = torch.randn(B, Ho, Wo, pc.cout_eff, device=DEV).bfloat16()   # narrow dY: 8-padded
     dx = torch.empty(B, H, H, cin, device=DEV, dtype=torch.bfloat16)
     pad = torch.empty(B * (H + 2 * p) ** 2 * cin, device=DEV)
     dw = torch.zeros(cout * k * k * cin, device=DEV)
@@ -55,12 +59,15 @@ for name, cin, cout, k, s, p, mode, H in CASES:
            "fwdr": lambda: ops.conv_fwd(pc, ops.Feat(x), ops.Feat(y), act=ops.ACT_RELU),
            "fwds": lambda: ops.conv_fwd_stats(pc, ops.Feat(x), ops.Feat(y), part),
            "dgrad": lambda: ops.conv_dgrad(pc, ops.Feat(dy), ops.Feat(dx), pad_buf=pad),
-           "wgrad": lambda: ops.conv_wgrad(spec, ops.Feat(x), ops.Feat(dy), dw, ops.BF16)}
+           # backward-data with the ReLU mask of the layer below (the VGG chain)
+           "dgradm": lambda: ops.conv_dgrad(pc, ops.Feat(dy), ops.Feat(dx), mask=ops.Feat(x), mask_act=1),
+           "wgrad": lambda: ops.conv_wgrad(spec, ops.Feat(x), ops.Feat(dy, 0, cout), dw, ops.BF16)}
     res[name] = {}
     for k2 in args.which.split(","):
         if k2 == "wgrad":
             for sk in (int(s) for s in args.splitk.split(",")):  # noqa: B007
-                v = t(lambda: ops.conv_wgrad(spec, ops.Feat(x), ops.Feat(dy), dw, ops.BF16, splitk=sk), args.iters)
+                v = t(lambda: ops.conv_wgrad(spec, ops.Feat(x), ops.Feat(dy, 0, cout), dw, ops.BF16, splitk=sk),
+                      args.iters)
                 res[name][k2 if sk == 0 else f"wgrad@{sk}"] = (round(v, 4), round(flop / v / 1e9, 1))
             continue
         v = t(fns[k2], args.iters)
