@@ -581,7 +581,8 @@ int launch_fwd(const irgan_conv_desc* d, const void* x, const void* w, const flo
             if (rc != IRGAN_EUNSUPPORTED) return rc;
         }
         static const bool use_pp = !getenv("IRGAN_NO_PP");
-        if (fast && use_pp && d->sy == 1 && d->sx == 1 && taps >= 2 && d->Cout % 64 == 0) {
+        if (fast && use_pp && ((d->sy == 1 && d->sx == 1) || (d->sy == 2 && d->sx == 2 && d->KH == 4 && d->KW == 4)) &&
+            taps >= 2 && d->Cout % 64 == 0) {
             const int rc = irgan_conv_fwd_pp(d, x, w, bias, y, mask, st);
             if (rc != IRGAN_EUNSUPPORTED) return rc;
         }

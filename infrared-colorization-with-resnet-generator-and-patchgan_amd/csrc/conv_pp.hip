@@ -26,7 +26,7 @@ int narrow_bn(const irgan_conv_desc* d) {
     return patches * (d->Cout / 128) >= 160 ? 128 : 64;
 }
 
-template <int KH, int KW, int BN>
+template <int KH, int KW, int BN, bool S2D = false>
 void launch_pp(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y, const void* mask,
                hipStream_t st, int swz) {
     const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH);
@@ -35,20 +35,20 @@ void launch_pp(const irgan_conv_desc* d, const void* x, const void* w, const flo
     if constexpr (BN == 64) {
         if (use_one(d->Cin)) {  // single halo buffer: two blocks per CU
             if (d->accumulate)
-                conv_pp_kernel<KH, KW, BN, true, false, false, true><<<nb, 512, 0, st>>>(
+                conv_pp_kernel<KH, KW, BN, true, false, false, true, S2D><<<nb, 512, 0, st>>>(
                     *d, (const bf16_t*)x, (const bf16_t*)w, bias, y, mask, ntn, tpx, tpy, swz);
             else
-                conv_pp_kernel<KH, KW, BN, false, false, false, true><<<nb, 512, 0, st>>>(
+                conv_pp_kernel<KH, KW, BN, false, false, false, true, S2D><<<nb, 512, 0, st>>>(
                     *d, (const bf16_t*)x, (const bf16_t*)w, bias, y, mask, ntn, tpx, tpy, swz);
             return;
         }
     }
     if (d->accumulate)
-        conv_pp_kernel<KH, KW, BN, true><<<nb, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, y, mask, ntn,
-                                                             tpx, tpy, swz);
+        conv_pp_kernel<KH, KW, BN, true, false, false, false, S2D><<<nb, 512, 0, st>>>(
+            *d, (const bf16_t*)x, (const bf16_t*)w, bias, y, mask, ntn, tpx, tpy, swz);
     else
-        conv_pp_kernel<KH, KW, BN, false><<<nb, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, y, mask, ntn,
-                                                              tpx, tpy, swz);
+        conv_pp_kernel<KH, KW, BN, false, false, false, false, S2D><<<nb, 512, 0, st>>>(
+            *d, (const bf16_t*)x, (const bf16_t*)w, bias, y, mask, ntn, tpx, tpy, swz);
 }
 
 }  // namespace
@@ -57,8 +57,9 @@ extern "C" int irgan_conv_fwd_pp(const irgan_conv_desc* d, const void* x, const 
                                  const void* mask, hipStream_t st) {
     if ((long)d->N * d->Ho * d->Wo <= 0 || d->Cout <= 0) return 0;
     const bool k33 = d->KH == 3 && d->KW == 3, k44 = d->KH == 4 && d->KW == 4;
-    if (d->dtype != IRGAN_BF16 || d->act == IRGAN_ACT_TANH || d->sy != 1 || d->sx != 1 || d->Cin % 64 || !(k33 || k44) || d->Cout % 64 ||
-        d->ldx % 8 || d->xoff % 8 || (long)d->N * d->H * d->W * d->ldx >= (1L << 30) ||
+    const bool s2d = k44 && d->sy == 2 && d->sx == 2;  // 4x4 stride 2 as a space-to-depth 2x2 conv
+    if (d->dtype != IRGAN_BF16 || d->act == IRGAN_ACT_TANH || ((d->sy != 1 || d->sx != 1) && !s2d) || d->Cin % 64 ||
+        !(k33 || k44) || d->Cout % 64 || d->ldx % 8 || d->xoff % 8 || (long)d->N * d->H * d->W * d->ldx >= (1L << 30) ||
         (long)d->Cout * d->KH * d->KW * d->Cin >= (1L << 30))
         return IRGAN_EUNSUPPORTED;
     const int swz = irgan_xcd_swz();
@@ -68,7 +69,12 @@ extern "C" int irgan_conv_fwd_pp(const irgan_conv_desc* d, const void* x, const 
         return 0;
     }
     const int nbn = d->Cout % 256 == 0 ? narrow_bn(d) : 0;
-    if (nbn == 256) {
+    if (s2d) {
+        if (nbn == 256) launch_pp<2, 2, 256, true>(d, x, w, bias, y, mask, st, swz);
+        else if (nbn == 128 || (nbn == 0 && d->Cout % 128 == 0 && !split128(d->Cin)))
+            launch_pp<2, 2, 128, true>(d, x, w, bias, y, mask, st, swz);
+        else launch_pp<2, 2, 64, true>(d, x, w, bias, y, mask, st, swz);
+    } else if (nbn == 256) {
         if (k33) launch_pp<3, 3, 256>(d, x, w, bias, y, mask, st, swz);
         else launch_pp<4, 4, 256>(d, x, w, bias, y, mask, st, swz);
     } else if (nbn == 128 || (nbn == 0 && d->Cout % 128 == 0 && !split128(d->Cin))) {
@@ -157,8 +163,9 @@ extern "C" int irgan_conv_fwd_stats(const irgan_conv_desc* d, const void* x, con
                                     void* part, int32_t* nb, irgan_stream_t s) {
     if (!d || !x || !w || !y || !part || !nb) return IRGAN_EINVAL;
     const bool k33 = d->KH == 3 && d->KW == 3, k44 = d->KH == 4 && d->KW == 4;
+    const bool s2d = k44 && d->sy == 2 && d->sx == 2;  // as irgan_conv_fwd_pp
     if (d->dtype != IRGAN_BF16 || d->out_dtype != IRGAN_BF16 || d->accumulate || d->act != IRGAN_ACT_NONE ||
-        d->sy != 1 || d->sx != 1 || d->Cin % 64 || !(k33 || k44) || d->Cout % 64 || d->Cout == 192 || d->ldx % 8 ||
+        ((d->sy != 1 || d->sx != 1) && !s2d) || d->Cin % 64 || !(k33 || k44) || d->Cout % 64 || d->Cout == 192 || d->ldx % 8 ||
         d->xoff % 8 ||
         d->ldy % 8 || d->yoff % 8 || d->Ho != d->OH || d->Wo != d->OW || d->omy != 1 || d->omx != 1 || d->ooy ||
         d->oox || (long)d->N * d->H * d->W * d->ldx >= (1L << 30) ||
@@ -179,11 +186,15 @@ extern "C" int irgan_conv_fwd_stats(const irgan_conv_desc* d, const void* x, con
         *nb = tpx * tpy;
         return 0;
     }
-#define PPS(KHV, BNV, ONEV)                                                                                        \
-    conv_pp_kernel<KHV, KHV, BNV, false, true, false, ONEV><<<blocks, 512, 0, st>>>(                                 \
+#define PPS(KHV, BNV, ONEV, ...)                                                                                   \
+    conv_pp_kernel<KHV, KHV, BNV, false, true, false, ONEV, ##__VA_ARGS__><<<blocks, 512, 0, st>>>(                  \
         *d, (const bf16_t*)x, (const bf16_t*)w, bias, y, nullptr, ntn, tpx, tpy, swz, (float2*)part)
     const bool one = bn == 64 && use_one(d->Cin);
-    if (k33) {
+    if (s2d) {
+        if (bn == 256) PPS(2, 256, false, true);
+        else if (bn == 128) PPS(2, 128, false, true);
+        else PPS(2, 64, true, true);
+    } else if (k33) {
         if (bn == 256) PPS(3, 256, false);
         else if (bn == 128) PPS(3, 128, false);
         else { if (one) PPS(3, 64, true); else PPS(3, 64, false); }

@@ -147,7 +147,15 @@ IRGAN_HD void ring_line_add(const irgan_conv_desc& d, const float* __restrict__ 
 // tiles, profiles/r02_s5_pp_one_ab.txt).  With more than one channel chunk the next chunk's halo cannot be
 // prefetched: after the last window that reads chunk c (4k+3 of its last tap) every
 // wave issues its pieces of chunk c+1, retires them and meets at one extra barrier.
-template <int KH, int KW, int BN, bool ACC, bool STATS = false, bool F8 = false, bool ONE = false>
+// S2D: a 4x4 stride-2 convolution (the PatchGAN's model.2 / model.5, ir:607-615) run as the
+// 2x2 stride-1 convolution it is over the space-to-depth input x''[u][v][(p, q, c)] =
+// x[2u + p + c0y][2v + q + c0x][c]: KH = KW = 2 here, the descriptor keeps the layer's own
+// 4x4 / stride-2 geometry.  x'' is never stored: a chunk of x'' (64 channels of one phase
+// (p, q)) is a halo DMA that gathers every other pixel of x, and the weight tile of K-step
+// (tap (a, b), chunk) is read from the layer's plain 4x4 pack at tap (2a + p, 2b + q) -- the
+// halo reuse of the stride-1 kernel (each input pixel loaded once per output patch instead of
+// once per tap) for the layers the generic implicit GEMM ran at 0.2 of peak.
+template <int KH, int KW, int BN, bool ACC, bool STATS = false, bool F8 = false, bool ONE = false, bool S2D = false>
 __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
                                                          const bf16_t* __restrict__ w, const float* __restrict__ bias,
                                                          void* __restrict__ y, const void* __restrict__ mask,
@@ -167,7 +175,8 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
     // sub-steps per K-step: bf16 2 (32 channels each); fp8 splits the pixel fragments,
     // MS per sub-step (4 sub-steps at MI = 8 keep the operand registers at the bf16 48)
     constexpr int HS = F8 && MI >= 8 ? 4 : 2, MS = F8 ? MI / HS : MI;
-    static_assert(HP <= HPMAX && HP > 40 && TAPS >= 2, "halo pieces per wave are 5 or 6");
+    static_assert(HP <= HPMAX && HP > 32 && TAPS >= 2, "halo pieces per wave are 4 to 6");
+    static_assert(!S2D || (KH == 2 && KW == 2 && !F8), "space-to-depth: the 2x2 form of a 4x4 stride-2 conv");
     __shared__ __attribute__((aligned(1024))) char smem[LDS];
     char* const sH = smem;
     char* const sB = smem + (ONE ? 1 : 2) * HBYTES;
@@ -185,9 +194,10 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
     const int pyi = t % tpy;
     const int img = t / tpy;
     const int py0 = pyi * PH, px0 = pxi * PW, n0 = nt * BN;
-    const int nh = (HP - wid + 7) >> 3;  // halo pieces this wave loads: wid, wid+8, ... (5 or 6)
-    const int Kw = TAPS * d.Cin;
-    const int nchunk = d.Cin / CHN;
+    const int nh = (HP - wid + 7) >> 3;  // halo pieces this wave loads: wid, wid+8, ... (4 to 6)
+    const int Kw = (S2D ? 16 : TAPS) * d.Cin;      // weight row stride (S2D: the 4x4 pack)
+    const int cpp = d.Cin / CHN;                   // S2D: chunks per phase
+    const int nchunk = (S2D ? 4 : 1) * d.Cin / CHN;
     const int sub = lane >> 3;
     const int chunk = (lane & 7) ^ sub;  // source chunk for this lane's LDS slot (row & 7 == sub)
     const bool reflect = d.pad_mode == IRGAN_PAD_REFLECT;
@@ -198,10 +208,14 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
     // byte offset of this lane's row of halo piece (u*8 + wid) (computed at issue
     // time, once per chunk: keeping six offsets live costs registers the MFMA
     // tile needs)
-    auto halo_off = [&](int u, int lsub) -> uint32_t {
+    auto halo_off = [&](int u, int lsub, int ph) -> uint32_t {
         const int h = (u * 8 + wid) * 8 + lsub;
         const int hy = h / HWd, hx = h - hy * HWd;
         int iy = py0 + hy + d.c0y, ix = px0 + hx + d.c0x;
+        if constexpr (S2D) {  // x''[py0 + hy][px0 + hx] of phase (p, q) = ph
+            iy = 2 * (py0 + hy) + (ph >> 1) + d.c0y;
+            ix = 2 * (px0 + hx) + (ph & 1) + d.c0x;
+        }
         if (reflect) {
             iy = reflect_idx(iy, d.H);
             ix = reflect_idx(ix, d.W);
@@ -215,15 +229,20 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
     const uint32_t b_off = (uint32_t)((n0 + wid * WU * 8 + sub) * Kw * ESZ + chunk * 16);  // piece u (8 rows): + u*8*Kw*ESZ
     auto issue_halo = [&](int c) {
         char* dst = sH + (ONE ? 0 : (c & 1) * HBYTES);
-        const i32x4 rs = make_rsrc(xb + c * 128, xbytes - c * 128);
+        const int cc = S2D ? c % cpp : c, ph = S2D ? c / cpp : 0;
+        const i32x4 rs = make_rsrc(xb + cc * 128, xbytes - cc * 128);
         int lsub = sub;
         asm volatile("" : "+v"(lsub));  // recompute the offsets here instead of hoisting them out of the loop
 #pragma unroll
         for (int u = 0; u < 6; ++u)
-            if (u < nh) blds16(rs, halo_off(u, lsub), dst + (u * 8 + wid) * 1024);
+            if (u < nh) blds16(rs, halo_off(u, lsub, ph), dst + (u * 8 + wid) * 1024);
     };
     auto issue_w = [&](int c, int tp, int stage) {
-        const int kcol = tp * d.Cin + c * CHN;
+        int kcol = tp * d.Cin + c * CHN;
+        if constexpr (S2D) {  // tap (a, b) of phase (p, q): the 4x4 tap (2a + p, 2b + q)
+            const int ph = c / cpp;
+            kcol = ((2 * (tp >> 1) + (ph >> 1)) * 4 + 2 * (tp & 1) + (ph & 1)) * d.Cin + (c % cpp) * CHN;
+        }
         const i32x4 rs = make_rsrc(wb + kcol * ESZ, wbytes - kcol * ESZ);
         char* dst = sB + stage * BBYTES + wid * WU * 1024;
 #pragma unroll
@@ -240,7 +259,8 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
     auto retire = [&](bool halo_now) {
         if (!halo_now) wait_vmcnt<0>();
         else if (nh == 6) wait_vmcnt<6>();
-        else wait_vmcnt<5>();
+        else if (nh == 5) wait_vmcnt<5>();
+        else wait_vmcnt<4>();
     };
 
     f32x4 acc[MI][NJ];

@@ -323,12 +323,12 @@ def conv_fwd_stats(pc: PackedConv, x: Feat, y: Feat, part: torch.Tensor) -> int:
     layer has no fused kernel -- then NOTHING ran and the caller does conv_fwd +
     in_stats."""
     s = pc.spec
-    if pc.dtype != BF16 or y.dt != BF16 or s.cout % 64 or s.cout == 192 or s.stride != 1:
+    if pc.dtype != BF16 or y.dt != BF16 or s.cout % 64 or s.cout == 192 or (s.stride != 1 and s.k != 4):
         return 0
     Ho, Wo = s.out_hw(x.H, x.W)
     assert (y.H, y.W, y.C) == (Ho, Wo, s.cout) and x.C == pc.cin_eff and y.N == x.N, "conv_fwd shape mismatch"
     d = _desc(N=x.N, H=x.H, W=x.W, Cin=pc.cin_eff, ldx=x.ld, xoff=x.off, Ho=Ho, Wo=Wo, Cout=s.cout, ldy=y.ld,
-              yoff=y.off, OH=Ho, OW=Wo, omy=1, ooy=0, omx=1, oox=0, KH=s.k, KW=s.k, sy=1, sx=1,
+              yoff=y.off, OH=Ho, OW=Wo, omy=1, ooy=0, omx=1, oox=0, KH=s.k, KW=s.k, sy=s.stride, sx=s.stride,
               c0y=-s.pad, c0x=-s.pad, pad_mode=s.mode, act=ACT_NONE, accumulate=0, dtype=pc.dtype,
               out_dtype=y.dt, mask_act=0, ldm=0, moff=0)
     nb = ctypes.c_int32(0)

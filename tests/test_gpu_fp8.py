@@ -260,6 +260,9 @@ def test_fp8_wgrad_tight(ops, N, H, W, cin, cout, mode):
     assert ratio <= 1.0, f"fp8 wgrad: worst |err|/bound = {ratio:.3g}"
 
 
+FP8_DW_REL = 0.25   # accepted rel-L2 of an fp8-step ResnetBlock dW against the unquantised one
+
+
 def _fp8_oracle(ir, rgb, lam, fp8=True):
     from oracle import step as O
     G = O.seeded_params(O.g_param_shapes(), 1, bias_std=0.02)
@@ -319,6 +322,19 @@ def test_fp8_step_vs_fp8_oracle(size):
             e = float((got - gr.double()).norm() / den)
             e_ac = float((oac[tag][k].double() - gr.double()).norm() / den)
             assert np.isfinite(e) and e <= 1.5 * e_ac + 0.02, (tag, k, e, e_ac)
+    # the accepted error of the e4m3 step against the UNQUANTISED reference gradient (the
+    # reference's fp32 autograd, o_nofp8): the ResnetBlock weight gradients (ir:386-411), whose
+    # fp8 kernels take e4m3 x (forward scales) and e4m3 dY (delayed-scaled), stay within
+    # FP8_DW_REL of it (rel-L2 per tensor; measured values printed, DESIGN.md "fp8")
+    worst = 0.0
+    for k, gr in o_nofp8["gradG"].items():
+        if "resblocks" not in k or not k.endswith(".weight"):
+            continue
+        den = gr.double().norm().clamp_min(1e-30)
+        e = float((tr.netG.store.oihw(k, tr.netG.store.grad).cpu().double() - gr.double()).norm() / den)
+        worst = max(worst, e)
+        assert np.isfinite(e) and e <= FP8_DW_REL, (k, e)
+    print(f"fp8 ResnetBlock dW vs the unquantised reference: worst rel-L2 {worst:.4f}")
 
 
 def test_fp8_step_config5_b32_finite():
