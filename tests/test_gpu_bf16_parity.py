@@ -66,8 +66,8 @@ EXTRA_CASES = [
     (64, 64, 3, 1, 1, 1, 37),
     (192, 64, 3, 1, 1, 1, 21),
     (64, 192, 3, 1, 1, 0, 50),
-    # the PatchGAN head (conv_head.hip: Cout 1 forward / one-channel-dY backward-data / weight
-    # gradient): n_layers = 2's 256-channel head and a multi-strip 512-channel one
+    # the PatchGAN head (Cout 1 forward / one-channel-dY backward-data / weight gradient):
+    # n_layers = 2's 256-channel head and a larger 512-channel one
     (256, 1, 4, 1, 1, 0, 21),
     (512, 1, 4, 1, 1, 0, 40),
 ]
