@@ -32,12 +32,6 @@ extern "C" int irgan_conv_wgrad_pc(const irgan_conv_desc* d, const void* x, cons
                                    float* ws, long ws_cap, hipStream_t st);
 extern "C" int irgan_conv_wgrad_narrow(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, float* ws,
                                        long ws_cap, hipStream_t st);
-extern "C" int irgan_conv_fwd_head(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
-                                   const void* mask, hipStream_t st);
-extern "C" int irgan_conv_dgrad_head(const irgan_conv_desc* d, const void* dy, const void* w, const float* bias,
-                                     void* dx, const void* mask, hipStream_t st);
-extern "C" int irgan_conv_wgrad_head(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, float* ws,
-                                     long ws_cap, hipStream_t st);
 extern "C" int irgan_conv_wgrad_glds(const irgan_conv_desc* d, const void* x, const void* dy, float* dw, int splitk,
                                      hipStream_t st, float* ws, long ws_cap);
 
@@ -575,11 +569,6 @@ int launch_fwd(const irgan_conv_desc* d, const void* x, const void* w, const flo
         const bool narrow = (d->Cin == 8 || d->Cin == 16 || d->Cin == 32) && d->ldx % 8 == 0 && d->xoff % 8 == 0;
         static const bool use_halo = !getenv("IRGAN_NO_HALO");
         const int taps = d->KH * d->KW;
-        {   // PatchGAN head (Cout 1, 4x4 s1) and its backward-data: conv_head.hip
-            int rc = irgan_conv_fwd_head(d, x, w, bias, y, mask, st);
-            if (rc == IRGAN_EUNSUPPORTED) rc = irgan_conv_dgrad_head(d, x, w, bias, y, mask, st);
-            if (rc != IRGAN_EUNSUPPORTED) return rc;
-        }
         static const bool use_pp = !getenv("IRGAN_NO_PP");
         if (fast && use_pp && ((d->sy == 1 && d->sx == 1) || (d->sy == 2 && d->sx == 2 && d->KH == 4 && d->KW == 4)) &&
             taps >= 2 && d->Cout % 64 == 0) {
@@ -628,10 +617,6 @@ int launch_wgrad(const irgan_conv_desc* d, const void* x, const void* dy, float*
     const bool fa = (d->Cout % EPC == 0) && (d->ldy % EPC == 0) && (d->yoff % EPC == 0);
     const bool fb = (d->Cin % 64 == 0) && (d->ldx % EPC == 0) && (d->xoff % EPC == 0);
     if constexpr (sizeof(T) == 2) {
-        {   // PatchGAN head (Cout 1, 4x4 s1): conv_head.hip
-            const int rc = irgan_conv_wgrad_head(d, x, dy, dw, ws, ws_cap, st);
-            if (rc != IRGAN_EUNSUPPORTED) return rc;
-        }
         {   // 8-channel inputs (G inc, D model.0): conv_wgrad_narrow.hip
             const int rc = irgan_conv_wgrad_narrow(d, x, dy, dw, ws, ws_cap, st);
             if (rc != IRGAN_EUNSUPPORTED) return rc;

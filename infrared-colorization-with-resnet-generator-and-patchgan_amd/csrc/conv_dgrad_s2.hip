@@ -197,6 +197,9 @@ __global__ __launch_bounds__(512, ONEC ? 2 : 1) void dgrad_s2_kernel(const irgan
 
 }  // namespace
 
+extern "C" int irgan_conv_dgrad_s2_pp(const irgan_conv_desc* dd, const void* dy, const void* const* w, void* dx,
+                                      const void* mask, hipStream_t st);
+
 // d: the FOUR phase descriptors ops.conv_dgrad builds for a stride-2 layer (in pc.dg order),
 // w: their four packed phase images.  Shapes (else IRGAN_EUNSUPPORTED, nothing launched):
 // bf16 operands, every phase 2x2 taps with c0y, c0x in {-1, 0}, stride 1 on dy, output pixel
@@ -234,6 +237,10 @@ extern "C" int irgan_conv_dgrad_s2(const irgan_conv_desc* d, const void* dy, con
     }
     // every dx pixel (2i + py, 2j + px) must come from dy position i (< H) of its phase
     if ((a.OH + 1) / 2 > a.H || (a.OW + 1) / 2 > a.W) return IRGAN_EUNSUPPORTED;
+    {   // 64-channel dx: the four phases as 2x2 convs on conv_pp (conv_pp.hip)
+        const int rc = irgan_conv_dgrad_s2_pp(d, dy, w, dx, mask, (hipStream_t)s);
+        if (rc != IRGAN_EUNSUPPORTED) return rc;
+    }
     const int swz = irgan_xcd_swz();
     const int tpy = irgan_cdiv((a.OH + 1) / 2, S2P), tpx = irgan_cdiv((a.OW + 1) / 2, S2P);
     hipStream_t st = (hipStream_t)s;

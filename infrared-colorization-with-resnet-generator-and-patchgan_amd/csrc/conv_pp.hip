@@ -153,6 +153,48 @@ extern "C" int irgan_conv_dgrad_reflect_line_fp8(const irgan_conv_desc* d, const
     return 0;
 }
 
+// The four-phase backward-data of a 4x4 stride-2 layer (irgan_conv_dgrad_s2's descriptors and
+// phase images) as ONE conv_pp launch of 2x2 stride-1 phase convs (PH4): dx channels % 64, dY
+// channels % 64, every phase the same Ho x Wo (even dx sides).  IRGAN_EUNSUPPORTED otherwise
+// (the caller then runs dgrad_s2_kernel).
+extern "C" int irgan_conv_dgrad_s2_pp(const irgan_conv_desc* dd, const void* dy, const void* const* w, void* dx,
+                                      const void* mask, hipStream_t st) {
+    const irgan_conv_desc& a = dd[0];
+    if (a.Cout % 64 || a.Cin % 64 || a.OH % 2 || a.OW % 2 || a.ldy % 8 || a.yoff % 8 ||
+        (mask && (a.ldm % 4 || a.moff % 4)) || (long)a.N * a.H * a.W * a.ldx >= (1L << 30) ||
+        (long)a.Cout * 4 * a.Cin >= (1L << 30))
+        return IRGAN_EUNSUPPORTED;
+    PhaseTab tab;
+    for (int k = 0; k < 4; ++k) {
+        const irgan_conv_desc& e = dd[k];
+        if (e.Ho != a.OH / 2 || e.Wo != a.OW / 2) return IRGAN_EUNSUPPORTED;
+        const int p = e.ooy * 2 + e.oox;
+        tab.w[p] = (const bf16_t*)w[k];
+        tab.c0y[p] = e.c0y;
+        tab.c0x[p] = e.c0x;
+        tab.ooy[p] = e.ooy;
+        tab.oox[p] = e.oox;
+    }
+    irgan_conv_desc d = a;  // the per-phase fields come from tab
+    d.Ho = a.OH / 2;
+    d.Wo = a.OW / 2;
+    const int swz = irgan_xcd_swz();
+    const int tpx = irgan_cdiv(d.Wo, PW), tpy = irgan_cdiv(d.Ho, PH);
+    const int bn = d.Cout % 256 == 0 ? narrow_bn(&d) : 64;
+    const int ntn = d.Cout / bn;
+    const int nb = d.N * tpy * tpx * 4 * ntn;
+#define PH4L(BNV, ACCV, ONEV)                                                                                     \
+    conv_pp_kernel<2, 2, BNV, ACCV, false, false, ONEV, false, true><<<nb, 512, 0, st>>>(                           \
+        d, (const bf16_t*)dy, (const bf16_t*)w[0], nullptr, dx, mask, ntn, tpx, tpy, swz, nullptr, nullptr, nullptr, \
+        nullptr, tab)
+    if (bn == 256) { if (d.accumulate) PH4L(256, true, false); else PH4L(256, false, false); }
+    else if (bn == 128) { if (d.accumulate) PH4L(128, true, false); else PH4L(128, false, false); }
+    else { if (d.accumulate) PH4L(64, true, true); else PH4L(64, false, true); }
+#undef PH4L
+    IRGAN_LAUNCH_CHECK();
+    return 0;
+}
+
 // Forward conv with the InstanceNorm statistics of its output fused into the
 // epilogue (replaces the separate irgan_in_stats pass over y; ir:154-165, 392, 417).
 // part: float2[N * nb * Cout] partials, nb (out) = 16x16 patches per image; reduce

@@ -155,7 +155,19 @@ IRGAN_HD void ring_line_add(const irgan_conv_desc& d, const float* __restrict__ 
 // (tap (a, b), chunk) is read from the layer's plain 4x4 pack at tap (2a + p, 2b + q) -- the
 // halo reuse of the stride-1 kernel (each input pixel loaded once per output patch instead of
 // once per tap) for the layers the generic implicit GEMM ran at 0.2 of peak.
-template <int KH, int KW, int BN, bool ACC, bool STATS = false, bool F8 = false, bool ONE = false, bool S2D = false>
+//
+// PH4: the four output phases of a stride-2 backward-data (4x4 stride 2: each phase a 2x2
+// stride-1 conv of dY onto every other dx pixel) in ONE launch: block = (channel tile, phase,
+// patch); the phase picks its taps' origin (c0y, c0x), its output pixel phase (ooy, oox) and
+// its packed weight image from `tab`; d carries the rest (omy = omx = 2, the per-phase Ho / Wo).
+struct PhaseTab {
+    const bf16_t* w[4];
+    int c0y[4], c0x[4], ooy[4], oox[4];
+};
+IRGAN_HD int pick4(const int (&a)[4], int i) { return i == 0 ? a[0] : (i == 1 ? a[1] : (i == 2 ? a[2] : a[3])); }
+
+template <int KH, int KW, int BN, bool ACC, bool STATS = false, bool F8 = false, bool ONE = false, bool S2D = false,
+          bool PH4 = false>
 __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
                                                          const bf16_t* __restrict__ w, const float* __restrict__ bias,
                                                          void* __restrict__ y, const void* __restrict__ mask,
@@ -163,10 +175,11 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
                                                          float2* __restrict__ part = nullptr,
                                                          const float* __restrict__ dqx = nullptr,
                                                          const float* __restrict__ dqw = nullptr,
-                                                         const float* __restrict__ rg = nullptr) {
+                                                         const float* __restrict__ rg = nullptr,
+                                                         const PhaseTab tab = PhaseTab{}) {
     constexpr int ESZ = F8 ? 1 : 2, CHN = 128 / ESZ;  // operand bytes, channels per 128-byte chunk
     const char* const xb = (const char*)x;
-    const char* const wb = (const char*)w;
+    const char* wb = (const char*)w;
     constexpr int TAPS = KH * KW, HWd = PW + KW - 1, HROWS = (PH + KH - 1) * HWd, HP = (HROWS + 7) / 8;
     constexpr int BBYTES = PP<BN>::BBYTES, NJ = PP<BN>::NJ, WU = PP<BN>::WU, RSB = PP<BN>::RSB;
     constexpr int LDS = ONE ? HBYTES + 2 * BBYTES : PP<BN>::LDS;
@@ -177,6 +190,7 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
     constexpr int HS = F8 && MI >= 8 ? 4 : 2, MS = F8 ? MI / HS : MI;
     static_assert(HP <= HPMAX && HP > 32 && TAPS >= 2, "halo pieces per wave are 4 to 6");
     static_assert(!S2D || (KH == 2 && KW == 2 && !F8), "space-to-depth: the 2x2 form of a 4x4 stride-2 conv");
+    static_assert(!PH4 || (!S2D && !F8 && !STATS), "four-phase backward-data: plain bf16");
     __shared__ __attribute__((aligned(1024))) char smem[LDS];
     char* const sH = smem;
     char* const sB = smem + (ONE ? 1 : 2) * HBYTES;
@@ -189,6 +203,16 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
     int t = xcd_tile(blockIdx.x, gridDim.x, swz);
     const int nt = t % ntn;
     t /= ntn;
+    int c0y = d.c0y, c0x = d.c0x, ooy = d.ooy, oox = d.oox;
+    if constexpr (PH4) {  // the phases of one patch are adjacent blocks: their dY halos share L2
+        const int ph = t & 3;
+        t >>= 2;
+        c0y = pick4(tab.c0y, ph);
+        c0x = pick4(tab.c0x, ph);
+        ooy = pick4(tab.ooy, ph);
+        oox = pick4(tab.oox, ph);
+        wb = (const char*)(ph == 0 ? tab.w[0] : (ph == 1 ? tab.w[1] : (ph == 2 ? tab.w[2] : tab.w[3])));
+    }
     const int pxi = t % tpx;
     t /= tpx;
     const int pyi = t % tpy;
@@ -211,10 +235,10 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
     auto halo_off = [&](int u, int lsub, int ph) -> uint32_t {
         const int h = (u * 8 + wid) * 8 + lsub;
         const int hy = h / HWd, hx = h - hy * HWd;
-        int iy = py0 + hy + d.c0y, ix = px0 + hx + d.c0x;
+        int iy = py0 + hy + c0y, ix = px0 + hx + c0x;
         if constexpr (S2D) {  // x''[py0 + hy][px0 + hx] of phase (p, q) = ph
-            iy = 2 * (py0 + hy) + (ph >> 1) + d.c0y;
-            ix = 2 * (px0 + hx) + (ph & 1) + d.c0x;
+            iy = 2 * (py0 + hy) + (ph >> 1) + c0y;
+            ix = 2 * (px0 + hx) + (ph & 1) + c0x;
         }
         if (reflect) {
             iy = reflect_idx(iy, d.H);
@@ -422,7 +446,7 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
     auto pix_of = [&](int m) -> long {
         const int oy = py0 + (m >> 4), ox = px0 + (m & 15);
         if (oy >= d.Ho || ox >= d.Wo) return -1;
-        return ((long)img * d.OH + oy * d.omy + d.ooy) * d.OW + ox * d.omx + d.oox;
+        return ((long)img * d.OH + oy * d.omy + ooy) * d.OW + ox * d.omx + oox;
     };
     // Each lane owns (pixel, 4 consecutive channels) per fragment: mask and
     // accumulate are applied right here on those 4 channels (8-byte loads).

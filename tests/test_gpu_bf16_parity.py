@@ -66,8 +66,8 @@ EXTRA_CASES = [
     (64, 64, 3, 1, 1, 1, 37),
     (192, 64, 3, 1, 1, 1, 21),
     (64, 192, 3, 1, 1, 0, 50),
-    # the PatchGAN head (conv_head.hip: Cout 1 forward / one-channel-dY backward-data / weight
-    # gradient): n_layers = 2's 256-channel head and a multi-strip 512-channel one
+    # the PatchGAN head (Cout 1 forward / one-channel-dY backward-data / weight gradient):
+    # n_layers = 2's 256-channel head and a larger 512-channel one
     (256, 1, 4, 1, 1, 0, 21),
     (512, 1, 4, 1, 1, 0, 40),
 ]
@@ -282,6 +282,33 @@ def test_bf16_pp_mask_tight(ops, cin, cout, H):
         ops.conv_fwd(pc, ops.Feat(xd), ops.Feat(ya2), bias=False, accumulate=True, mask=ops.Feat(md, 8, cout),
                      mask_act=mact)
         check(nchw64(ya2), y64 * mm + base.double(), ya + base.abs().double(), R_BF16, f"acc mask {mact}")
+
+
+@pytest.mark.parametrize("cin,cout,H", [(64, 128, 32), (128, 256, 18), (64, 128, 17)])
+def test_bf16_s2_dgrad_mask_tight(ops, cin, cout, H):
+    """Backward-data of the PatchGAN's 4x4 stride-2 layers (ir:607-615) with the LeakyReLU mask
+    of the layer below (D model.2's dgrad folds model.0's LReLU): the four phase convs in one
+    conv_pp launch (even dx sides) or dgrad_s2_kernel (odd), plain and accumulating."""
+    torch.manual_seed(5)
+    N = 2
+    spec = ops.ConvSpec(cin, cout, 4, 2, 1, 0)
+    x = q(torch.randn(N, cin, H, H))
+    w = q(torch.randn(cout, cin, 4, 4) * (1.0 / (cin * 16) ** 0.5))
+    Ho = spec.out_hw(H, H)[0]
+    gy = q(torch.randn(N, cout, Ho, Ho))
+    m = q(torch.randn(N, cin, H, H))
+    _, dx64, _, _ = references(x, w, None, gy, 4, 2, 1, 0)
+    _, dxa, _, _ = references(x.abs(), w.abs(), None, gy.abs(), 4, 2, 1, 0)
+    pc = ops.PackedConv(spec, w.permute(0, 2, 3, 1).contiguous().reshape(-1).to(DEV), None, ops.BF16)
+    pc.pack()
+    mm = torch.where(m > 0, 1.0, 0.2).double()
+    dx = torch.zeros(N, H, H, cin, device=DEV, dtype=torch.bfloat16)
+    ops.conv_dgrad(pc, ops.Feat(nhwc(gy)), ops.Feat(dx), mask=ops.Feat(nhwc(m)), mask_act=2)
+    check(nchw64(dx), dx64 * mm, dxa, R_BF16, "s2 dgrad mask")
+    base = q(torch.randn(N, cin, H, H))
+    dxb = nhwc(base)
+    ops.conv_dgrad(pc, ops.Feat(nhwc(gy)), ops.Feat(dxb), accumulate=True)
+    check(nchw64(dxb), dx64 + base.double(), dxa + base.abs().double(), R_BF16, "s2 dgrad acc")
 
 
 @pytest.mark.parametrize("N,H,W", [(2, 32, 48), (1, 64, 64), (3, 48, 32), (2, 16, 64), (1, 37, 64)])
