@@ -63,6 +63,9 @@
 #define PP_EXP 0  // A/B timing experiments only (tools/build_variant.sh); 0 = the real kernel
 #endif
 // bits: 1 no MFMA, 2 no weight DMA in the loop, 4 no fragment reads, 8 no barriers in the loop, 16 no epilogue
+#ifndef PP_ACC_BATCH
+#define PP_ACC_BATCH 1  // accumulate: old values loaded for half the fragment rows at once (0: row by row)
+#endif
 #define PPX(b) ((PP_EXP & (b)) != 0)
 
 namespace {
@@ -108,15 +111,15 @@ typedef int v8i_t __attribute__((ext_vector_type(8)));
 IRGAN_HD v8i_t cat8(i32x4 a, i32x4 b) { return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7); }
 
 // rg (irgan_conv_dgrad_reflect_line): the line-form reflect ring of a ResnetBlock backward-data
-// (conv_ring.hip: g[n][line][pos][c], lines top / bottom / left / right) folded onto the stored
-// bf16 dx in the store pass -- ring_line_fold_kernel's terms, order and roundings, so dx is
+// (conv_ring.hip: g[n][line][pos][c], lines top / bottom / left / right) folded onto the staged
+// bf16 dx before the store pass -- ring_line_fold_kernel's terms, order and roundings, so dx is
 // bit-identical to the interior launch + fold launch
-IRGAN_HD void ring_line_add(const irgan_conv_desc& d, const float* __restrict__ g, int n, int y, int x, int c,
-                            uint4& o) {
+// v = the ring terms of dx pixel (y, x) (a border-band pixel: row 1 / H-2 or column 1 / W-2),
+// channels c .. c+7, summed in ring_line_fold_kernel's order
+IRGAN_HD void ring_line_sum(const irgan_conv_desc& d, const float* __restrict__ g, int n, int y, int x, int c,
+                            float (&v)[8]) {
     const int H = d.Ho, W = d.Wo;
     const bool row = y == 1 || y == H - 2;
-    if (!row && x != 1 && x != W - 2) return;
-    float v[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = 0.f;
     auto add = [&](int line, int pos) {
@@ -133,6 +136,9 @@ IRGAN_HD void ring_line_add(const irgan_conv_desc& d, const float* __restrict__ 
     } else {
         add(x == 1 ? 2 : 3, y + 1);
     }
+}
+// o (8 bf16 of dx, the interior's rounded values) += its ring terms, one more rounding
+IRGAN_HD void ring_line_apply(const float (&v)[8], uint4& o) {
     const uint32_t wd[4] = {o.x, o.y, o.z, o.w};
     uint32_t o4[4];
 #pragma unroll
@@ -467,27 +473,43 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
     const bool late_mask = mask && d.mask_act == 1 && !ACC && !out_f32 && !STATS && !rg && d.ldm % 8 == 0 &&
                            d.moff % 8 == 0 && d.ldy % 8 == 0 && d.yoff % 8 == 0;
     const bool mask_vec = mask && d.ldm % 4 == 0 && d.moff % 4 == 0;
+    // accumulate: the old values of half the fragment rows are loaded before the first of them
+    // is combined (two exposed latencies per launch instead of one per row; all rows at once
+    // would hold 64 more VGPRs next to the accumulators and spill)
+    constexpr int OB = ACC && PP_ACC_BATCH ? (MI >= 2 ? MI / 2 : 1) : 1;  // rows per old-value batch
+    uint2 olda[OB][NJ];
+    auto load_old = [&](int i0) {
+        if constexpr (ACC) {
+            if (acc_vec) {
+#pragma unroll
+                for (int ii = 0; ii < OB; ++ii) {
+                    const long pix = pix_of((prow + i0 + ii) * 16 + (lane & 15));
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j) {
+                        const int co = n0 + cl0 + j * 16;
+                        olda[ii][j] = (pix >= 0 && co + 4 <= d.Cout)
+                                          ? *(const uint2*)((const bf16_t*)y + pix * d.ldy + d.yoff + co)
+                                          : make_uint2(0u, 0u);
+                    }
+                }
+            }
+        }
+    };
     auto emit = [&](auto actc) {
         constexpr int A = decltype(actc)::value;
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
+            if (ACC && i % OB == 0) load_old(i);
             const int m = (prow + i) * 16 + (lane & 15);
             const long pix = pix_of(m);
-            uint2 old[NJ], mk[NJ];
+            uint2 mk[NJ];
+            uint2(&old)[NJ] = olda[ACC ? i % OB : 0];
             if (mask_vec && !late_mask && pix >= 0) {
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) {
                     const int co = n0 + cl0 + j * 16;
                     mk[j] = co + 4 <= d.Cout ? *(const uint2*)((const bf16_t*)mask + pix * d.ldm + d.moff + co)
                                              : make_uint2(0u, 0u);
-                }
-            }
-            if (acc_vec && pix >= 0) {
-#pragma unroll
-                for (int j = 0; j < NJ; ++j) {
-                    const int co = n0 + cl0 + j * 16;
-                    old[j] = co + 4 <= d.Cout ? *(const uint2*)((const bf16_t*)y + pix * d.ldy + d.yoff + co)
-                                              : make_uint2(0u, 0u);
                 }
             }
 #pragma unroll
@@ -550,6 +572,34 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
             }
         }
     };
+    // rg: the patch's border-band pixels (rows 1 / H-2, columns 1 / W-2 of the image: at most
+    // two rows and two columns of the patch, 4 lines x 16 positions x LPP 8-channel slots) get
+    // their ring terms in a pass over the staged tile between the staging and the store pass.
+    // Every slot's line loads are issued here, before the staging, so their latency hides
+    // under it -- added in the store pass they stalled a border pixel's wave once per pixel row.
+    constexpr int RSL = 4 * 16 * PP<BN>::LPP / 512;  // ring slots per thread
+    float rv[RSL][8];
+    int rm[RSL];
+    if (rg) {
+        constexpr int LPPr = PP<BN>::LPP;
+        const int H = d.Ho, W = d.Wo;
+        const int rr1 = 1 - py0, rr2 = H - 2 - py0, cc1 = 1 - px0, cc2 = W - 2 - px0;
+        auto in16 = [](int a) { return (unsigned)a < 16u; };
+        const bool r1 = in16(rr1), r2 = in16(rr2), c1 = in16(cc1), c2 = in16(cc2);
+#pragma unroll
+        for (int k = 0; k < RSL; ++k) {
+            const int sl = tid + 512 * k;
+            const int line = sl / (16 * LPPr), pos = (sl / LPPr) % 16, ch = sl % LPPr;
+            int pr = -1, pc = -1;
+            if (line == 0 && r1) { pr = rr1; pc = pos; }
+            else if (line == 1 && r2) { pr = rr2; pc = pos; }
+            else if (line == 2 && c1 && !(r1 && pos == rr1) && !(r2 && pos == rr2)) { pr = pos; pc = cc1; }
+            else if (line == 3 && c2 && !(r1 && pos == rr1) && !(r2 && pos == rr2)) { pr = pos; pc = cc2; }
+            const int y = py0 + pr, x = px0 + pc;
+            rm[k] = (pr >= 0 && y < H && x < W && n0 + ch * 8 < d.Cout) ? pr * 16 + pc : -1;
+            if (rm[k] >= 0) ring_line_sum(d, rg, img, y, x, n0 + ch * 8, rv[k]);
+        }
+    }
     switch (d.act) {
         case IRGAN_ACT_RELU: emit(std::integral_constant<int, IRGAN_ACT_RELU>()); break;
         case IRGAN_ACT_LRELU: emit(std::integral_constant<int, IRGAN_ACT_LRELU>()); break;
@@ -557,6 +607,18 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
     }
     if (out_f32) return;
     __syncthreads();
+    if (rg) {  // the ring terms onto the staged pixels (each (pixel, slot) owned by one thread)
+#pragma unroll
+        for (int k = 0; k < RSL; ++k) {
+            if (rm[k] < 0) continue;
+            const int ch = (tid + 512 * k) % PP<BN>::LPP;
+            uint4* sp = (uint4*)(smem + rm[k] * RSB + ch * 16);
+            uint4 o = *sp;
+            ring_line_apply(rv[k], o);
+            *sp = o;
+        }
+        __syncthreads();
+    }
     constexpr int LPP = PP<BN>::LPP;
     constexpr int PPASS = PP<BN>::PPASS;
     if constexpr (STATS) {
@@ -650,9 +712,7 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
         bf16_t* yp = (bf16_t*)y + pix * d.ldy + d.yoff + co8;
         const char* sp = smem + m * RSB + c8 * 2;
         if (vec) {
-            uint4 o = *(const uint4*)sp;
-            if (rg) ring_line_add(d, rg, img, py0 + (m >> 4), px0 + (m & 15), co8, o);  // block-uniform test
-            *(uint4*)yp = o;
+            *(uint4*)yp = *(const uint4*)sp;
         } else {
             for (int q = 0; q < 8 && co8 + q < d.Cout; ++q) yp[q] = ((const bf16_t*)sp)[q];
         }

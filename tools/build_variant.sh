@@ -1,15 +1,16 @@
-# Build an A/B variant of libirgan.so with extra -D flags on ONE source file.
-# usage: bash tools/build_variant.sh <name> <source.hip> "-DFLAG=1 ..."
-#   -> infrared-...amd/build/libirgan_<name>.so (load with IRGAN_LIB=<path>)
+# Build an A/B variant of libirgan.so with extra -D flags on every source (tools/gpu_libab.sh,
+# tools/gpu_kvar.sh): objects under build/var_<name> (not shipped), the library at
+# variants/libirgan_<name>.so (shipped with the tree; load it with IRGAN_LIB=<path>).  The
+# variant has the default build's source id (same sources), so _lib.load() accepts it.
+# usage: bash tools/build_variant.sh <name> "-DFLAG=1 ..."
 set -e
 P=infrared-colorization-with-resnet-generator-and-patchgan_amd
-B=$P/build
-SRC=$2
-OBJ=$B/var_$1_$(basename $SRC .hip).o
-/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I include -I $P/csrc -Wno-unused-result $3 -c $P/csrc/$SRC -o $OBJ
-OBJS=""
-for s in $(python3 -c "import sys; sys.path.insert(0, '$P'); import _build; print(' '.join(x[:-4] for x in _build.SOURCES))"); do
-  if [ "$s.hip" = "$SRC" ]; then OBJS="$OBJS $OBJ"; else OBJS="$OBJS $B/$s.o"; fi
-done
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $B/libirgan_$1.so $OBJS
-echo $B/libirgan_$1.so
+mkdir -p $P/variants
+python3 - "$1" "$2" <<'PY'
+import sys
+sys.path.insert(0, "infrared-colorization-with-resnet-generator-and-patchgan_amd")
+import _build
+name, flags = sys.argv[1], sys.argv[2].split()
+lib = _build.build(extra_flags=flags, lib=f"{_build.HERE}/variants/libirgan_{name}.so", objdir=f"{_build.OBJDIR}/var_{name}")
+print(lib)
+PY

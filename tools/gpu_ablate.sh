@@ -5,7 +5,7 @@
 export TMPDIR=/tmp
 O=gpurun_out/${1:-ablate}
 mkdir -p $O
-B=infrared-colorization-with-resnet-generator-and-patchgan_amd/build
+B=infrared-colorization-with-resnet-generator-and-patchgan_amd/variants
 for v in default pp1 pp2 pp4 pp8 pp16; do
   L=""; [ $v != default ] && L=$B/libirgan_$v.so
   IRGAN_LIB=$L timeout -k 10 120 python tools/bench_conv.py --case res3x3 --which fwds,dgrad --iters 50 > $O/pp_$v.txt 2>&1 || { echo "$v failed"; break; }

@@ -4,7 +4,7 @@ export TMPDIR=/tmp
 O=gpurun_out/$1; shift
 MB=$1; shift
 mkdir -p $O
-B=infrared-colorization-with-resnet-generator-and-patchgan_amd/build
+B=infrared-colorization-with-resnet-generator-and-patchgan_amd/variants
 for v in default "$@"; do
   L=""; [ $v != default ] && L=$B/libirgan_$v.so
   IRGAN_LIB=$L timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $O/p_$v -o run --output-format csv -- python tools/bench_conv.py $MB > $O/mb_$v.txt 2>&1 || { echo "variant $v failed"; tail -3 $O/mb_$v.txt; exit 1; }

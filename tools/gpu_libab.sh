@@ -6,7 +6,7 @@ O=gpurun_out/$1; shift
 MB=$1; shift
 T=$1; shift
 mkdir -p $O
-B=infrared-colorization-with-resnet-generator-and-patchgan_amd/build
+B=infrared-colorization-with-resnet-generator-and-patchgan_amd/variants
 for v in default "$@"; do
   L=""; [ $v != default ] && L=$B/libirgan_$v.so
   IRGAN_LIB=$L timeout -k 10 120 python tools/bench_conv.py $MB > $O/mb_$v.txt 2>&1 || { echo "microbench $v failed"; echo ALLDONE; exit 0; }
