@@ -295,59 +295,48 @@ IRGAN_HD int rv_tap(int line, int k) {  // dgrad-conv tap ty*3 + tx of along-lin
     return line == 0 ? 6 + k : (line == 1 ? k : (line == 2 ? 3 * k + 2 : 3 * k));
 }
 
-// WREG: weight fragments straight into registers (default); else staged through LDS
-// (A/B knob IRGAN_RING_WLDS=1: 3 x 64 rows of Cin, 96 KiB, one barrier)
-template <bool WREG>
-__global__ __launch_bounds__(256, 1) void ring_line_gemm_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ dy,
-                                                                const bf16_t* __restrict__ w, float* __restrict__ gbuf,
-                                                                int ipb) {
-    constexpr int WB = WREG ? 0 : 3 * 64 * 512;
-    __shared__ __attribute__((aligned(16))) char smem[WB + RV_ROWS * 512];
-    char* const sW = smem;       // !WREG: [3 taps][64 co] rows of Cin bf16
-    char* const sL = smem + WB;  // [RV_ROWS positions] rows of Cin bf16
+// 512 threads: waves kh = 0 / 1 (wave >> 2) take the dy channel steps cs < ncs / 2 / the rest
+// (the K loop halved: one wave per SIMD ran a 3 x 8-step chain with each step's LDS reads
+// exposed), then half 1's accumulators are added onto half 0's through LDS in a fixed order
+constexpr int RV_NT = 512, RV_CSH = RV_CIN / 64;  // threads; channel steps per half (max)
+__global__ __launch_bounds__(RV_NT, 1) void ring_line_gemm_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ dy,
+                                                                 const bf16_t* __restrict__ w, float* __restrict__ gbuf,
+                                                                 int ipb) {
+    __shared__ __attribute__((aligned(16))) char smem[RV_ROWS * 512 + 4 * 64 * 5 * 16];
+    char* const sL = smem;                                   // [RV_ROWS positions] rows of Cin bf16
+    f32x4* const sP = (f32x4*)(smem + RV_ROWS * 512);        // half 1's accumulators [wave][f][lane]
     const int nct = d.Cout / 64;
     const int line = blockIdx.x / nct, ct = blockIdx.x - line * nct;
     const int n0 = blockIdx.y * ipb, n1 = min(d.N, n0 + ipb);
     const int H = d.Ho, W = d.Wo, L = line < 2 ? W : H;
     const int tid = threadIdx.x, lane = tid & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wv = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);
+    const int kh = __builtin_amdgcn_readfirstlane(tid >> 8);
     const int g = lane >> 4, l16 = lane & 15;
     const int Kw = (9 * d.Cin + 63) / 64 * 64;
     const int c32 = d.Cin / 8;  // 16-byte chunks per row
     const int ncs = d.Cin / 32;
+    const int cs0 = kh * ((ncs + 1) / 2), cs1 = kh ? ncs : (ncs + 1) / 2;  // this half's channel steps
 
     // this wave's weight fragments straight into registers (16 channels x 32 dy channels per
     // (tap k, channel step cs)): w[ct*64 + wv*16 + l16][rv_tap(line, k) * Cin + 32 cs + 8 g ..],
-    // all 24 loads in flight at once -- no LDS staging, no barrier before the first MFMA
-    uint4 af[3][WREG ? RV_CIN / 32 : 1];
-    if constexpr (WREG) {
+    // all loads in flight at once -- no LDS staging, no barrier before the first MFMA
+    uint4 af[3][RV_CSH];
+    {
         const bf16_t* wr = w + (long)(ct * 64 + wv * 16 + l16) * Kw + g * 8;
 #pragma unroll
         for (int k = 0; k < 3; ++k)
 #pragma unroll
-            for (int cs = 0; cs < RV_CIN / 32; ++cs)
-                af[k][cs] = cs < ncs ? *(const uint4*)(wr + rv_tap(line, k) * d.Cin + cs * 32) : make_uint4(0u, 0u, 0u, 0u);
-    } else {  // row (k * 64 + co), chunk c  <-  w[ct*64 + co][rv_tap(line, k) * Cin + 8c]
-        constexpr int PER = 3 * 64 * 32 / 256;
-        uint4 v[PER];
-#pragma unroll
-        for (int u = 0; u < PER; ++u) {
-            const int e = u * 256 + tid, row = e >> 5, c = e & 31, k = row >> 6, co = row & 63;
-            v[u] = c < c32 ? *(const uint4*)(w + (long)(ct * 64 + co) * Kw + rv_tap(line, k) * d.Cin + c * 8)
-                           : make_uint4(0u, 0u, 0u, 0u);
-        }
-#pragma unroll
-        for (int u = 0; u < PER; ++u) {
-            const int e = u * 256 + tid;
-            *(uint4*)(sW + rv_off(e >> 5, e & 31)) = v[u];
-        }
+            for (int c = 0; c < RV_CSH; ++c)
+                af[k][c] = cs0 + c < cs1 ? *(const uint4*)(wr + rv_tap(line, k) * d.Cin + (cs0 + c) * 32)
+                                         : make_uint4(0u, 0u, 0u, 0u);
     }
     // the dy line of image n: position p = dy coordinate + 2 along the line
-    constexpr int LPER = (RV_ROWS * 32 + 255) / 256;
+    constexpr int LPER = (RV_ROWS * 32 + RV_NT - 1) / RV_NT;
     auto load_line = [&](int n, uint4 (&v)[LPER]) {
 #pragma unroll
         for (int u = 0; u < LPER; ++u) {
-            const int e = u * 256 + tid, q = (e >> 5) - 2, c = e & 31;
+            const int e = u * RV_NT + tid, q = (e >> 5) - 2, c = e & 31;
             v[u] = make_uint4(0u, 0u, 0u, 0u);
             if (e < RV_ROWS * 32 && q >= 0 && q < L && c < c32) {
                 const int y = line == 0 ? 0 : (line == 1 ? H - 1 : q);
@@ -365,7 +354,7 @@ __global__ __launch_bounds__(256, 1) void ring_line_gemm_kernel(const irgan_conv
         __syncthreads();  // the previous image's GEMM is done with sL
 #pragma unroll
         for (int u = 0; u < LPER; ++u) {
-            const int e = u * 256 + tid;
+            const int e = u * RV_NT + tid;
             if (e < RV_ROWS * 32) *(uint4*)(sL + rv_off(e >> 5, e & 31)) = lv[u];
         }
         __syncthreads();
@@ -376,11 +365,10 @@ __global__ __launch_bounds__(256, 1) void ring_line_gemm_kernel(const irgan_conv
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
 #pragma unroll
-            for (int cs = 0; cs < RV_CIN / 32; ++cs) {
-                if (cs >= ncs) break;
-                uint4 a;
-                if constexpr (WREG) a = af[k][cs];
-                else a = *(const uint4*)(sW + rv_off(k * 64 + wv * 16 + l16, cs * 4 + g));
+            for (int c = 0; c < RV_CSH; ++c) {
+                const int cs = cs0 + c;
+                if (cs >= cs1) break;
+                const uint4 a = af[k][c];
                 uint4 b[5];
 #pragma unroll
                 for (int f = 0; f < 5; ++f)
@@ -391,12 +379,23 @@ __global__ __launch_bounds__(256, 1) void ring_line_gemm_kernel(const irgan_conv
                                                                      __builtin_bit_cast(bf16x8_t, b[f]), acc[f], 0, 0, 0);
             }
         }
-            // g[n][line][u + 1][co]: lane = position 16 f + l16 + ub, rows 4g + r = channels
-        float* gl = gbuf + ((long)n * 4 + line) * RV_ROWS * d.Cout;
+        // half 1 hands its sums to half 0 (one add per element, fixed order)
+        if (kh == 1) {
 #pragma unroll
-        for (int f = 0; f < 5; ++f) {
-            const int pos = 16 * f + l16 + ub + 1;
-            if (pos < RV_ROWS) *(float4*)(gl + (long)pos * d.Cout + co) = make_float4(acc[f][0], acc[f][1], acc[f][2], acc[f][3]);
+            for (int f = 0; f < 5; ++f) sP[(wv * 5 + f) * 64 + lane] = acc[f];
+        }
+        __syncthreads();
+        if (kh == 0) {
+            // g[n][line][u + 1][co]: lane = position 16 f + l16 + ub, rows 4g + r = channels
+            float* gl = gbuf + ((long)n * 4 + line) * RV_ROWS * d.Cout;
+#pragma unroll
+            for (int f = 0; f < 5; ++f) {
+                const f32x4 o = sP[(wv * 5 + f) * 64 + lane];
+                const int pos = 16 * f + l16 + ub + 1;
+                if (pos < RV_ROWS)
+                    *(float4*)(gl + (long)pos * d.Cout + co) =
+                        make_float4(acc[f][0] + o[0], acc[f][1] + o[1], acc[f][2] + o[2], acc[f][3] + o[3]);
+            }
         }
     }
 }
@@ -480,7 +479,7 @@ bool ring_line_check(const irgan_conv_desc* d, int p, long ws_floats) { return r
 void ring_line_gemm_launch(const irgan_conv_desc* d, const void* dy, const void* w, float* ws, hipStream_t st) {
     // one image per workgroup row (2 / 4 images per workgroup measured slower: the launch
     // is latency-bound, profiles/r03_ring_gemm_wreg_ab.txt)
-    ring_line_gemm_kernel<true><<<dim3(4 * (d->Cout / 64), d->N), 256, 0, st>>>(*d, (const bf16_t*)dy,
+    ring_line_gemm_kernel<<<dim3(4 * (d->Cout / 64), d->N), RV_NT, 0, st>>>(*d, (const bf16_t*)dy,
                                                                               (const bf16_t*)w, ws, 1);
 }
 
@@ -517,7 +516,7 @@ extern "C" int irgan_reflect_dgrad_ring_ws(const irgan_conv_desc* d, const void*
     if (groups > d->N) groups = d->N;
     const int ipb = irgan_cdiv(d->N, groups);
     groups = irgan_cdiv(d->N, ipb);
-    ring_line_gemm_kernel<true><<<dim3(tiles, groups), 256, 0, st>>>(*d, (const bf16_t*)dy, (const bf16_t*)w, ws, ipb);
+    ring_line_gemm_kernel<<<dim3(tiles, groups), RV_NT, 0, st>>>(*d, (const bf16_t*)dy, (const bf16_t*)w, ws, ipb);
     const long threads = (long)d->N * (2 * d->Wo + 2 * (d->Ho - 2)) * (d->Cout / 8);
     ring_line_fold_kernel<<<(unsigned)irgan_cdiv(threads, 256), 256, 0, st>>>(*d, ws, dx);
     IRGAN_LAUNCH_CHECK();
