@@ -288,6 +288,13 @@ IRGAN_HD void block_partials8(float* a0, float* a1, const Lay& L, bool on, int c
 // batch, unconverted, before using any; tail rows of the last batch re-load a
 // valid row and are masked.  dx may alias dy (no __restrict__ on either): a
 // thread stores only rows it has already loaded.
+// ROWS8_DB (default 1): two register batches in flight (U rows each); 0: one batch at a time
+// with twice the rows (the round-4 schedule, for A/B builds)
+#ifndef ROWS8_DB
+#define ROWS8_DB 1
+#endif
+constexpr int R8U_RED = ROWS8_DB ? 2 : 4, R8U_STATS = ROWS8_DB ? 4 : 8, R8U_APPLY = ROWS8_DB ? 4 : 8,
+              R8U_APPLY_RES = ROWS8_DB ? 2 : 4;
 template <int MODE, int U, bool F8 = false>
 __global__ __launch_bounds__(TPB) void rows8_kernel(const bf16_t* x, int ldx, int xoff, const bf16_t* dy, int lddy,
                                                     int dyoff, const bf16_t* dy2, int lddy2, int dy2off, int act,
@@ -326,37 +333,41 @@ __global__ __launch_bounds__(TPB) void rows8_kernel(const bf16_t* x, int ldx, in
             }
         }
         if (on) {
-#pragma unroll 1
-            for (int r = r0 + L.rl; r < r1; r += U * L.RP) {
-                uint4 xr[U], gr[U], hr[U];
+            // two register batches: batch b + 1's loads are issued before batch b is used, so a
+            // wave keeps a batch in flight while it computes (one batch at a time held the
+            // passes at 2.9-4.8 TB/s, the waves idle between their batches)
+            uint4 xr[2][U], gr[2][U], hr[2][U];
+            auto load = [&](int b, int r) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const long p = pb + min(r + u * L.RP, r1 - 1);
-                    xr[u] = *(const uint4*)(x + p * ldx + xoff + c);
-                    if (MODE != 0 && (MODE != 4 || dy)) gr[u] = *(const uint4*)(dy + p * lddy + dyoff + c);
+                    xr[b][u] = *(const uint4*)(x + p * ldx + xoff + c);
+                    if (MODE != 0 && (MODE != 4 || dy)) gr[b][u] = *(const uint4*)(dy + p * lddy + dyoff + c);
                 }
                 if (MODE != 0 && dy2) {
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
                         const long p = pb + min(r + u * L.RP, r1 - 1);
-                        hr[u] = *(const uint4*)(dy2 + p * lddy2 + dy2off + c);
+                        hr[b][u] = *(const uint4*)(dy2 + p * lddy2 + dy2off + c);
                     }
                 }
+            };
+            auto process = [&](int b, int r) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     if (r + u * L.RP >= r1) break;
                     float xv[8];
-                    bf8f(xr[u], xv);
+                    bf8f(xr[b][u], xv);
                     if (MODE == 0) {
 #pragma unroll
                         for (int k = 0; k < 8; ++k) { a0[k] += xv[k]; a1[k] += xv[k] * xv[k]; }
                         continue;
                     }
                     float gv[8];
-                    if (MODE != 4 || dy) bf8f(gr[u], gv);
+                    if (MODE != 4 || dy) bf8f(gr[b][u], gv);
                     if (dy2) {
                         float hv[8];
-                        bf8f(hr[u], hv);
+                        bf8f(hr[b][u], hv);
 #pragma unroll
                         for (int k = 0; k < 8; ++k) gv[k] += hv[k];
                     }
@@ -394,7 +405,26 @@ __global__ __launch_bounds__(TPB) void rows8_kernel(const bf16_t* x, int ldx, in
                         }
                     }
                 }
+            };
+            const int step = U * L.RP;
+            int r = r0 + L.rl;
+#if ROWS8_DB
+            if (r < r1) load(0, r);
+#pragma unroll 1
+            for (; r < r1; r += 2 * step) {
+                if (r + step < r1) load(1, r + step);
+                process(0, r);
+                if (r + step >= r1) break;
+                if (r + 2 * step < r1) load(0, r + 2 * step);
+                process(1, r + step);
             }
+#else
+#pragma unroll 1
+            for (; r < r1; r += step) {
+                load(0, r);
+                process(0, r);
+            }
+#endif
         }
         if (MODE == 2 || MODE == 4) continue;  // uniform across the block
         block_partials8(a0, a1, L, on, cb, c, C, n, s0, s1, part);
@@ -537,13 +567,13 @@ int launch_rows(Slice X, Slice DY, Slice DY2, int act, const float* mr, const fl
     if ((fast || q8) && vec && bf && MODE <= 2) {
         const bf16_t *xp = (const bf16_t*)X.p, *gp = (const bf16_t*)DY.p, *hp = (const bf16_t*)DY2.p;
         if (MODE == 2 && q8)
-            rows8_kernel<2, 4, true><<<g, TPB, 0, st>>>(xp, X.ld, X.off, gp, DY.ld, DY.off, hp, DY2.ld, DY2.off, act, mr,
+            rows8_kernel<2, R8U_RED, true><<<g, TPB, 0, st>>>(xp, X.ld, X.off, gp, DY.ld, DY.off, hp, DY2.ld, DY2.off, act, mr,
                                                         red, (bf16_t*)dx, lddx, dxoff, HW, C, rows, part, *q8);
         else if (MODE == 0)
-            rows8_kernel<0, 8><<<g, TPB, 0, st>>>(xp, X.ld, X.off, nullptr, 0, 0, nullptr, 0, 0, act, mr, red, nullptr,
+            rows8_kernel<0, R8U_STATS><<<g, TPB, 0, st>>>(xp, X.ld, X.off, nullptr, 0, 0, nullptr, 0, 0, act, mr, red, nullptr,
                                                   0, 0, HW, C, rows, part);
         else
-            rows8_kernel<MODE, 4><<<g, TPB, 0, st>>>(xp, X.ld, X.off, gp, DY.ld, DY.off, hp, DY2.ld, DY2.off, act, mr,
+            rows8_kernel<MODE, R8U_RED><<<g, TPB, 0, st>>>(xp, X.ld, X.off, gp, DY.ld, DY.off, hp, DY2.ld, DY2.off, act, mr,
                                                      red, (bf16_t*)dx, lddx, dxoff, HW, C, rows, part);
         if (nb_out) *nb_out = nb;
         return 0;
@@ -594,13 +624,13 @@ bool apply_rows(const void* x, int ldx, int xoff, int N, int HW, int C, const fl
     dim3 g(nb, N);
     const bf16_t *xp = (const bf16_t*)x, *rp = (const bf16_t*)res;
     if (q8)
-        rows8_kernel<4, 4, true><<<g, TPB, 0, st>>>(xp, ldx, xoff, rp, ldr, roff, nullptr, 0, 0, act, mr, nullptr,
+        rows8_kernel<4, R8U_APPLY_RES, true><<<g, TPB, 0, st>>>(xp, ldx, xoff, rp, ldr, roff, nullptr, 0, 0, act, mr, nullptr,
                                                     (bf16_t*)y, ldy, yoff, HW, C, rows, nullptr, *q8);
     else if (res)
-        rows8_kernel<4, 4><<<g, TPB, 0, st>>>(xp, ldx, xoff, rp, ldr, roff, nullptr, 0, 0, act, mr, nullptr,
+        rows8_kernel<4, R8U_APPLY_RES><<<g, TPB, 0, st>>>(xp, ldx, xoff, rp, ldr, roff, nullptr, 0, 0, act, mr, nullptr,
                                               (bf16_t*)y, ldy, yoff, HW, C, rows, nullptr);
     else
-        rows8_kernel<4, 8><<<g, TPB, 0, st>>>(xp, ldx, xoff, nullptr, 0, 0, nullptr, 0, 0, act, mr, nullptr,
+        rows8_kernel<4, R8U_APPLY><<<g, TPB, 0, st>>>(xp, ldx, xoff, nullptr, 0, 0, nullptr, 0, 0, act, mr, nullptr,
                                               (bf16_t*)y, ldy, yoff, HW, C, rows, nullptr);
     return true;
 }
