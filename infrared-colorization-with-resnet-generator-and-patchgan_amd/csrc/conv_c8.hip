@@ -241,9 +241,9 @@ struct C8R {
     static constexpr int KR = TAPS * CR, KP = (KR + 31) / 32 * 32, NCH = (KP + 63) / 64;
     static constexpr int WS = KP * 2 + 16;           // weight row stride (bytes)
     static constexpr int TS = 144;                   // tile row stride: 64 K (or 64 co) bf16 + 16 B
-    static constexpr int HBYTES = HPIX * 16;
     static constexpr int HPT = (HPIX + 255) / 256;
-    static constexpr int LDS = 64 * WS + HBYTES + 256 * TS;
+    static constexpr int HBYTES = HPT * 256 * 16;    // whole DMA pieces (the tail lanes land in the pad)
+    static constexpr int LDS = 64 * WS + HBYTES + 256 * TS + 64 * 4;  // + the bias
     static_assert(2 * LDS <= 160 * 1024, "two resident blocks per CU");
 };
 
@@ -258,6 +258,7 @@ __global__ __launch_bounds__(256, 2) void conv_c8r_kernel(const irgan_conv_desc 
     char* const sW = smem;
     char* const sH = smem + 64 * WS;
     char* const sT = sH + G::HBYTES;
+    float* const sBias = (float*)(sT + 256 * TS);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g = lane >> 4, c16 = lane & 15;
@@ -273,29 +274,31 @@ __global__ __launch_bounds__(256, 2) void conv_c8r_kernel(const irgan_conv_desc 
             *(bf16_t*)(sW + co * WS + k * 2) = v;
         }
     }
-    auto load_halo = [&](int p, uint4 (&hv)[G::HPT]) {
+    // The halo goes HBM -> LDS by DMA (buffer_load ... lds, out-of-range pixels as zeros), the
+    // output through unconditional raw buffer stores (out-of-range pixels dropped), so the loop
+    // issues exactly HPT DMA pieces and 8 stores per patch and waits by count: the next patch's
+    // halo lands while this patch's MFMAs, staging and stores run.  (Loaded through registers
+    // with predicated loads / stores, the compiler waited vmcnt(0) at the top of each patch and
+    // ahead of the epilogue, which serialised halo, compute and stores: inc forward 70 us for
+    // 150 MB.)
+    const i32x4 xrs = make_rsrc(x, (uint32_t)((long)d.N * d.H * d.W * d.ldx * 2));
+    const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)y, (short)0, (int)((long)d.N * d.OH * d.OW * d.ldy * 2), 0x00020000);
+    auto issue_halo = [&](int p) {
         const int pxi = p % tpx, r = p / tpx, pyi = r % tpy, img = r / tpy;
+        const int wid64 = wid * 64;
 #pragma unroll
         for (int u = 0; u < G::HPT; ++u) {
             const int h = u * 256 + tid;
-            hv[u] = make_uint4(0u, 0u, 0u, 0u);
-            if (h < HPIX) {
-                const int hy = h / HWd, hx = h - hy * HWd;
-                int iy = pyi * PH * S + hy + d.c0y, ix = pxi * PW * S + hx + d.c0x;
-                if (reflect) {
-                    iy = reflect_idx(iy, d.H);
-                    ix = reflect_idx(ix, d.W);
-                }
-                if ((unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W)
-                    hv[u] = *(const uint4*)(x + (((long)img * d.H + iy) * d.W + ix) * d.ldx + d.xoff);
+            const int hy = h / HWd, hx = h - hy * HWd;
+            int iy = pyi * PH * S + hy + d.c0y, ix = pxi * PW * S + hx + d.c0x;
+            if (reflect) {
+                iy = reflect_idx(iy, d.H);
+                ix = reflect_idx(ix, d.W);
             }
-        }
-    };
-    auto store_halo = [&](const uint4 (&hv)[G::HPT]) {
-#pragma unroll
-        for (int u = 0; u < G::HPT; ++u) {
-            const int h = u * 256 + tid;
-            if (h < HPIX) *(uint4*)(sH + h * 16) = hv[u];
+            const bool ok = h < HPIX && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+            const uint32_t off = ok ? (uint32_t)((((long)img * d.H + iy) * d.W + ix) * d.ldx + d.xoff) * 2 : IRGAN_OOB;
+            blds16(xrs, off, sH + (u * 256 + wid64) * 16);  // lane-linear: pixel h at sH + 16 h
         }
     };
     // im2col row of this thread's pixel (patch row pr, column pc) for K chunk kc: one 8-byte
@@ -328,23 +331,17 @@ __global__ __launch_bounds__(256, 2) void conv_c8r_kernel(const irgan_conv_desc 
         }
     };
 
-    float bv[4][4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int co = j * 16 + 4 * g + r;
-            bv[j][r] = (bias && co < d.Cout) ? bias[co] : 0.f;
-        }
-    uint4 hv[G::HPT];
+    // bias through LDS (read in the epilogue by ds_read: no global load for the waits to track)
+    if (tid < 64) sBias[tid] = (bias && tid < d.Cout) ? bias[tid] : 0.f;
     int p = blockIdx.x;
-    if (p < npatch) load_halo(p, hv);
+    if (p < npatch) issue_halo(p);
 #pragma unroll 1
-    for (; p < npatch; p += gridDim.x) {
-        store_halo(hv);
-        __syncthreads();  // halo p in LDS (and the previous patch's output tile stored)
+    for (int it = 0; p < npatch; p += gridDim.x, ++it) {
+        // halo p landed: its DMA pieces are older than the 8 stores of patch p - 1
+        if (it == 0) wait_vmcnt<0>();
+        else wait_vmcnt<8>();
+        __syncthreads();  // every wave's halo pieces (and the bias / weights) visible
         const int pn = p + gridDim.x;
-        if (pn < npatch) load_halo(pn, hv);  // in flight under this patch
         f32x4 acc[4][4];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -355,6 +352,8 @@ __global__ __launch_bounds__(256, 2) void conv_c8r_kernel(const irgan_conv_desc 
             if (kc) __syncthreads();  // the previous chunk's tile consumed
             build(kcc);
             __syncthreads();
+            // the last chunk's tile is built: the halo buffer takes the next patch's DMA
+            if (kc == G::NCH - 1 && pn < npatch) issue_halo(pn);
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
                 if (kc * 64 + s * 32 >= KP) break;
@@ -383,8 +382,10 @@ __global__ __launch_bounds__(256, 2) void conv_c8r_kernel(const irgan_conv_desc 
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 float v[4];
+                const float4 bb = *(const float4*)(sBias + j * 16 + 4 * g);
+                const float bj[4] = {bb.x, bb.y, bb.z, bb.w};
 #pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = conv_act(acc[i][j][r] + bv[j][r], d.act);
+                for (int r = 0; r < 4; ++r) v[r] = conv_act(acc[i][j][r] + bj[r], d.act);
                 uint2 o;
                 o.x = pk_bf16(v[0], v[1]);
                 o.y = pk_bf16(v[2], v[3]);
@@ -398,9 +399,11 @@ __global__ __launch_bounds__(256, 2) void conv_c8r_kernel(const irgan_conv_desc 
             for (int u = 0; u < 8; ++u) {
                 const int e = u * 256 + tid, px = e >> 3, ch = e & 7;
                 const int oy = pyi * PH + (px >> 4), ox = pxi * PW + (px & 15);
-                if (oy >= d.Ho || ox >= d.Wo) continue;
                 const long pix = ((long)img * d.OH + oy * d.omy + d.ooy) * d.OW + ox * d.omx + d.oox;
-                *(uint4*)(y + pix * d.ldy + d.yoff + ch * 8) = *(const uint4*)(sT + px * TS + ch * 16);
+                const int off = (oy < d.Ho && ox < d.Wo) ? (int)((pix * d.ldy + d.yoff + ch * 8) * 2) : (int)IRGAN_OOB;
+                const uint4 o = *(const uint4*)(sT + px * TS + ch * 16);
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, o), yr, off, 0, 0);
             }
         }
     }
