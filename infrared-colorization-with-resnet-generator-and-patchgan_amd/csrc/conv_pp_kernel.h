@@ -64,7 +64,8 @@
 #endif
 // bits: 1 no MFMA, 2 no weight DMA in the loop, 4 no fragment reads, 8 no barriers in the loop, 16 no epilogue
 #ifndef PP_ACC_BATCH
-#define PP_ACC_BATCH 1  // accumulate: old values loaded for half the fragment rows at once (0: row by row)
+#define PP_ACC_BATCH 0  // accumulate: 1 = old values loaded for half the fragment rows at once (measured:
+                        // 11 more VGPR spills in the BN-256 instance, step -0.3 %, profiles/r05_s5_ab.txt)
 #endif
 #define PPX(b) ((PP_EXP & (b)) != 0)
 

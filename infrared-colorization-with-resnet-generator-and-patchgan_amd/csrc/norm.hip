@@ -288,10 +288,12 @@ IRGAN_HD void block_partials8(float* a0, float* a1, const Lay& L, bool on, int c
 // batch, unconverted, before using any; tail rows of the last batch re-load a
 // valid row and are masked.  dx may alias dy (no __restrict__ on either): a
 // thread stores only rows it has already loaded.
-// ROWS8_DB (default 1): two register batches in flight (U rows each); 0: one batch at a time
-// with twice the rows (the round-4 schedule, for A/B builds)
+// ROWS8_DB = 1: two register batches in flight (U rows each, the next batch's loads issued
+// before the current one is used); 0 (default): one batch at a time with twice the rows.
+// Measured same box: no faster standalone (tools/norm_bench.py) and -0.5 % on the step
+// (profiles/r05_s5_nab.txt), so the round-4 schedule stays
 #ifndef ROWS8_DB
-#define ROWS8_DB 1
+#define ROWS8_DB 0
 #endif
 constexpr int R8U_RED = ROWS8_DB ? 2 : 4, R8U_STATS = ROWS8_DB ? 4 : 8, R8U_APPLY = ROWS8_DB ? 4 : 8,
               R8U_APPLY_RES = ROWS8_DB ? 2 : 4;
