@@ -40,13 +40,18 @@
 // fp8 (F8, irgan_conv_fwd_fp8): the same kernel on OCP e4m3 operands.  A K-step
 // is one tap x 128 channels (a 128-byte halo / weight row, so every DMA, LDS
 // image and barrier window is byte-for-byte the bf16 schedule); its MFMA is
-// mfma_scale_f32_16x16x128_f8f6f4 (unit block scales: 2x the bf16 rate), a
-// fragment is 32 bytes (chunks g and g+4 of the row for lane group g, the same
-// channels for both operands), and the sub-steps of a K-step split the wave's
-// pixel fragments instead of the channels (sub-step 0 also reads the weight
-// fragments, which stay in registers for the others); at 8 pixel fragments a
-// K-step has 4 sub-steps (8 barrier windows), so the operand registers stay at
-// the bf16 kernel's 48.  The per-tensor
+// mfma_scale_f32_32x32x64_f8f6f4 (unit block scales: 2x the bf16 rate).  The
+// wave tile is the bf16 one (MIW patch rows x NJ*16 channels) as 32 x 32
+// fragments: a weight fragment is 32 channels, a pixel fragment two patch rows
+// (lane bit 4 picks the row), each lane's 32 operand bytes are chunks
+// 4h + (lane >> 5) and + 2 of the 128-byte row in sub-step h (the same K bytes
+// for both operands).  So a sub-step is (MIW / 2) x (NJ / 2) MFMAs of 64 cycles
+// on 48 operand VGPRs -- the bf16 kernel's 512-cycle windows, 12 fragment reads
+// and registers at twice the FLOPs (the 16x16x128 form needed 4 sub-steps of
+// 256 cycles per K-step to stay in registers: twice the barriers per FLOP).
+// Accumulator (p, q) register 4*i4 + r is channel 32q + 8*i4 + 4*(lane >> 5) + r
+// of pixel 32p + (lane & 31); the epilogue sees it as the bf16 fragment
+// (i, j) = (2p + (i4 >> 1), 2q + (i4 & 1)) through m_of / cl_of.  The per-tensor
 // scales are undone in the epilogue: y = acc * (dqx[0] * dqw[0]) + bias.
 //
 // Preconditions (checked by irgan_conv_fwd_pp): bf16, sy = sx = 1, Cin % 64 == 0,
@@ -109,6 +114,7 @@ struct PP {
 };
 
 typedef int v8i_t __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 IRGAN_HD v8i_t cat8(i32x4 a, i32x4 b) { return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7); }
 
 // rg (irgan_conv_dgrad_reflect_line): the line-form reflect ring of a ResnetBlock backward-data
@@ -192,9 +198,10 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
     constexpr int LDS = ONE ? HBYTES + 2 * BBYTES : PP<BN>::LDS;
     static_assert(!ONE || (BN == 64 && 256 * RSB <= LDS && !F8), "single-halo variant: staging must fit");
     constexpr int MI = PP<BN>::MIW, RW = PP<BN>::RW;
-    // sub-steps per K-step: bf16 2 (32 channels each); fp8 splits the pixel fragments,
-    // MS per sub-step (4 sub-steps at MI = 8 keep the operand registers at the bf16 48)
-    constexpr int HS = F8 && MI >= 8 ? 4 : 2, MS = F8 ? MI / HS : MI;
+    // sub-steps per K-step: 2 (bf16: 32 channels each; fp8: 64)
+    constexpr int HS = 2;
+    constexpr int NP = F8 ? MI / 2 : 1, NQ = F8 ? NJ / 2 : 1;  // fp8 32 x 32 fragments per wave
+    static_assert(!F8 || (MI % 2 == 0 && NJ % 2 == 0), "fp8: 32 x 32 fragments");
     static_assert(HP <= HPMAX && HP > 32 && TAPS >= 2, "halo pieces per wave are 4 to 6");
     static_assert(!S2D || (KH == 2 && KW == 2 && !F8), "space-to-depth: the 2x2 form of a 4x4 stride-2 conv");
     static_assert(!PH4 || (!S2D && !F8 && !STATS), "four-phase backward-data: plain bf16");
@@ -294,13 +301,23 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
         else wait_vmcnt<4>();
     };
 
-    f32x4 acc[MI][NJ];
+    f32x4 acc[F8 ? 1 : MI][F8 ? 1 : NJ];
+    f32x16 acc32[NP][NQ];
+    if constexpr (F8) {
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+        for (int p = 0; p < NP; ++p)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    uint4 af[MI], bfr[NJ];
-    v8i_t af8[MS], bf8[NJ];  // fp8: 32-byte fragments (chunks g, g + 4)
+            for (int q = 0; q < NQ; ++q)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc32[p][q][r] = 0.f;
+    } else {
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    uint4 af[F8 ? 1 : MI], bfr[F8 ? 1 : NJ];
+    v8i_t pf8[NP], wf8[NQ];  // fp8: 32-byte fragments (chunks 4h + (lane >> 5), + 2)
     // prologue: W(0), halo(0), W(1); retire the first two
     issue_w(0, 0, 0);
     issue_halo(0);
@@ -313,17 +330,16 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
     // lane's row arow0 and lds_off's XOR term depends only on (arow0 + K) & 7,
     // so with the tap loop unrolled an A address is tsw[K & 7] + hb plus the
     // ds_read immediate K * 128: one VALU add per fragment read.
-    const int arow0 = prow * HWd + (lane & 15);  // halo row of fragment 0 at tap (0,0)
-    const int brow0 = cb + (lane & 15);          // weight row of fragment 0 (rows +16j share the XOR)
-    // bf16: sub-step h reads chunk (lane >> 4) + 4h; fp8: a fragment is chunks (lane >> 4) and
-    // (lane >> 4) + 4 (the same byte <-> channel map for both operands)
-    const int g0 = lane >> 4;
+    // halo row of fragment 0 at tap (0,0) (fp8: lane bit 4 = the second patch row of a fragment)
+    const int arow0 = (prow + (F8 ? (lane >> 4) & 1 : 0)) * HWd + (lane & 15);
+    const int brow0 = cb + (lane & (F8 ? 31 : 15));  // weight row of fragment 0 (rows +16j / +32q share the XOR)
+    // bf16: sub-step h reads chunk (lane >> 4) + 4h; fp8: chunks 4h + (lane >> 5) and + 2 (the
+    // same byte <-> channel map for both operands)
+    const int g0 = F8 ? lane >> 5 : lane >> 4;
     const int bb0 = lds_off(brow0, g0), bb1 = lds_off(brow0, 4 + g0);
-    int tsw[F8 ? 1 : 8];  // h = 1 / the second fp8 chunk flips chunk bit 2: tsw ^ 64 (v_xad_u32)
-    if constexpr (!F8) {
+    int tsw[8];  // h = 1 flips chunk bit 2 (tsw ^ 64), the second fp8 chunk bit 1 (^ 32)
 #pragma unroll
-        for (int k8 = 0; k8 < 8; ++k8) tsw[k8] = (g0 ^ ((arow0 + k8) & 7)) << 4;
-    }
+    for (int k8 = 0; k8 < 8; ++k8) tsw[k8] = (g0 ^ ((arow0 + k8) & 7)) << 4;
 #pragma unroll 1
     for (int c = 0; c < nchunk; ++c) {
         const int hb = arow0 * 128 + (ONE ? 0 : (c & 1) * HBYTES);
@@ -343,18 +359,15 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
                 int hbp = hb;
                 asm volatile("" : "+v"(hbp));  // per-phase base: the address adds stay here, not hoisted
                 if constexpr (F8) {
-                    if (h == 0) {
 #pragma unroll
-                        for (int j = 0; j < NJ; ++j)
-                            bf8[j] = cat8(*(const i32x4*)(B + bb0 + j * 2048), *(const i32x4*)(B + bb1 + j * 2048));
-                    }
+                    for (int q = 0; q < NQ; ++q)
+                        wf8[q] = cat8(*(const i32x4*)(B + bb + q * 4096), *(const i32x4*)(B + (bb ^ 32) + q * 4096));
 #pragma unroll
-                    for (int ii = 0; ii < MS; ++ii) {
-                        const int K = (h * MS + ii + ty) * HWd + tx;
-                        // the swizzle term from arow0 on the fly (fp8 has no registers to spare)
-                        const int sw = (g0 ^ ((arow0 + K) & 7)) << 4;
-                        af8[ii] = cat8(*(const i32x4*)(sH + (hbp + sw) + K * 128),
-                                       *(const i32x4*)(sH + (hbp + (sw ^ 64)) + K * 128));
+                    for (int p = 0; p < NP; ++p) {
+                        const int K = (2 * p + ty) * HWd + tx;
+                        const int sw = tsw[K & 7] ^ (h * 64);
+                        pf8[p] = cat8(*(const i32x4*)(sH + (hbp + sw) + K * 128),
+                                      *(const i32x4*)(sH + (hbp + (sw ^ 32)) + K * 128));
                     }
                 } else {
 #if !PPX(4)
@@ -391,17 +404,17 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
                 // ---- MFMA phase: C^T fragment (weights as A, pixels as B)
                 if constexpr (F8) {
 #pragma unroll
-                    for (int ii = 0; ii < MS; ++ii)
+                    for (int p = 0; p < NP; ++p)
 #pragma unroll
-                        for (int j = 0; j < NJ; ++j)
-                            acc[h * MS + ii][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
-                                bf8[j], af8[ii], acc[h * MS + ii][j], 0, 0, 0, 127, 0, 127);
+                        for (int q = 0; q < NQ; ++q)
+                            acc32[p][q] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+                                wf8[q], pf8[p], acc32[p][q], 0, 0, 0, 127, 0, 127);
                     // pin the scaled MFMAs inside this phase: hipcc otherwise sinks them past the
                     // barriers to the end of the chunk, keeping every tap's fragments live (spills)
 #pragma unroll
-                    for (int ii = 0; ii < MS; ++ii)
+                    for (int p = 0; p < NP; ++p)
 #pragma unroll
-                        for (int j = 0; j < NJ; ++j) asm volatile("" : "+v"(acc[h * MS + ii][j]));
+                        for (int q = 0; q < NQ; ++q) asm volatile("" : "+v"(acc32[p][q]));
                 } else {
 #pragma unroll
                     for (int i = 0; i < MI * !PPX(1); ++i)
@@ -425,28 +438,46 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) s += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+            for (int j = 0; j < NJ; ++j) s += F8 ? acc32[i >> 1][j >> 1][0] : acc[i][j][0] + acc[i][j][3];
         if (s == 123.f) *(float*)y = s;
         return;
     }
 #endif
 
-    // ---- epilogue.  Fragment (i, j): pixel m = (prow + i)*16 + (lane & 15),
-    // channels co = n0 + cb + j*16 + 4*(lane >> 4) + r, r = 0..3.
-    const int cl0 = cb + 4 * (lane >> 4);  // block-local channel of r = 0, j = 0
+    // ---- epilogue.  Fragment (i, j): pixel m = m_of(i), block-local channels cl_of(i, j) + r,
+    // r = 0..3 (bf16: m = (prow + i)*16 + (lane & 15), cl = cb + j*16 + 4*(lane >> 4); fp8: the
+    // 32 x 32 accumulator's quarter i4 = 2 (i & 1) + (j & 1) of fragment (i >> 1, j >> 1))
+    auto m_of = [&](int i) {
+        return F8 ? (prow + 2 * (i >> 1) + ((lane >> 4) & 1)) * 16 + (lane & 15) : (prow + i) * 16 + (lane & 15);
+    };
+    auto cl_of = [&](int i, int j) {
+        return F8 ? cb + 32 * (j >> 1) + 8 * (2 * (i & 1) + (j & 1)) + 4 * (lane >> 5) : cb + 4 * (lane >> 4) + j * 16;
+    };
+    auto accv = [&](int i, int j) -> f32x4 {
+        if constexpr (F8) {
+            const int o = 4 * (2 * (i & 1) + (j & 1));
+            const f32x16& t = acc32[i >> 1][j >> 1];
+            return f32x4{t[o], t[o + 1], t[o + 2], t[o + 3]};
+        } else {
+            return acc[i][j];
+        }
+    };
     const float osc = F8 ? *dqx * *dqw : 1.f;  // fp8: 1 / (x scale * w scale), powers of two
-    float4 b4[NJ];
+    constexpr int NB = F8 ? 2 : 1;  // bias quads per channel fragment (fp8: by i & 1)
+    float4 b4[NB][NJ];
+#pragma unroll
+    for (int ib = 0; ib < NB; ++ib)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-        const int co = n0 + cl0 + j * 16;
-        b4[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        const int co = n0 + cl_of(ib, j);
+        b4[ib][j] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (bias) {
             if (co + 3 < d.Cout) {
-                b4[j] = *(const float4*)(bias + co);
+                b4[ib][j] = *(const float4*)(bias + co);
             } else {
-                if (co < d.Cout) b4[j].x = bias[co];
-                if (co + 1 < d.Cout) b4[j].y = bias[co + 1];
-                if (co + 2 < d.Cout) b4[j].z = bias[co + 2];
+                if (co < d.Cout) b4[ib][j].x = bias[co];
+                if (co + 1 < d.Cout) b4[ib][j].y = bias[co + 1];
+                if (co + 2 < d.Cout) b4[ib][j].z = bias[co + 2];
             }
         }
     }
@@ -484,10 +515,10 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
             if (acc_vec) {
 #pragma unroll
                 for (int ii = 0; ii < OB; ++ii) {
-                    const long pix = pix_of((prow + i0 + ii) * 16 + (lane & 15));
+                    const long pix = pix_of(m_of(i0 + ii));
 #pragma unroll
                     for (int j = 0; j < NJ; ++j) {
-                        const int co = n0 + cl0 + j * 16;
+                        const int co = n0 + cl_of(i0 + ii, j);
                         olda[ii][j] = (pix >= 0 && co + 4 <= d.Cout)
                                           ? *(const uint2*)((const bf16_t*)y + pix * d.ldy + d.yoff + co)
                                           : make_uint2(0u, 0u);
@@ -501,28 +532,29 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
             if (ACC && i % OB == 0) load_old(i);
-            const int m = (prow + i) * 16 + (lane & 15);
+            const int m = m_of(i);
             const long pix = pix_of(m);
             uint2 mk[NJ];
             uint2(&old)[NJ] = olda[ACC ? i % OB : 0];
             if (mask_vec && !late_mask && pix >= 0) {
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) {
-                    const int co = n0 + cl0 + j * 16;
+                    const int co = n0 + cl_of(i, j);
                     mk[j] = co + 4 <= d.Cout ? *(const uint2*)((const bf16_t*)mask + pix * d.ldm + d.moff + co)
                                              : make_uint2(0u, 0u);
                 }
             }
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
-                const int cl = cl0 + j * 16, co = n0 + cl;
-                const float4 b = b4[j];
-                float v[4] = {acc[i][j][0] + b.x, acc[i][j][1] + b.y, acc[i][j][2] + b.z, acc[i][j][3] + b.w};
+                const int cl = cl_of(i, j), co = n0 + cl;
+                const float4 b = b4[F8 ? i & 1 : 0][j];
+                const f32x4 a = accv(i, j);
+                float v[4] = {a[0] + b.x, a[1] + b.y, a[2] + b.z, a[3] + b.w};
                 if constexpr (F8) {
-                    v[0] = acc[i][j][0] * osc + b.x;
-                    v[1] = acc[i][j][1] * osc + b.y;
-                    v[2] = acc[i][j][2] * osc + b.z;
-                    v[3] = acc[i][j][3] * osc + b.w;
+                    v[0] = a[0] * osc + b.x;
+                    v[1] = a[1] * osc + b.y;
+                    v[2] = a[2] * osc + b.z;
+                    v[3] = a[3] * osc + b.w;
                 }
 #pragma unroll
                 for (int r = 0; r < 4; ++r) v[r] = conv_act(v[r], A);
