@@ -189,7 +189,7 @@ def main():
 
     # dominant kernel for the live roofline: the resblock 3x3 conv (256->256 @ H/4)
     res_tags = [ops.conv_tag(k, ops.ConvSpec(256, 256, 3, 1, 1, ops.PAD_REFLECT), (H // 4, W // 4), B)
-                for k in (("fwd8", "dgrad8", "wgrad") if args.dtype == "fp8" else ("fwd", "dgrad", "wgrad"))]
+                for k in (("fwd8", "dgrad8", "wgrad8") if args.dtype == "fp8" else ("fwd", "dgrad", "wgrad"))]
     for _ in range(args.warmup):
         tr.step(ir, rgb)
     torch.cuda.synchronize()

@@ -37,7 +37,7 @@ extern "C" {
 
 typedef void* irgan_stream_t;
 
-/* The source id this library was built from: a hash of csrc/*.hip, csrc/*.h and this header
+/* The source id this library was built from: a hash of the csrc .hip / .h sources and this header
  * (computed by pkg/_build.py, baked in at compile time), NUL-terminated into buf[len].
  * pkg/_lib.py refuses a library whose id differs from the tree it is loaded from.  No
  * reference counterpart (build provenance of the drop-in library). */
@@ -329,6 +329,19 @@ IRGAN_API int irgan_sep_resample_in(const void* in, int32_t in_dtype, int32_t N,
                           void* out, int32_t out_dtype, int32_t Hout, int32_t Wout, int32_t ldo,
                           int32_t offo, const int32_t* ty, const float* wy, int32_t Ty,
                           const int32_t* tx, const float* wx, int32_t Tx, irgan_stream_t s);
+/* The fp8 path's producers of the down2 / up1_conv operands (config 5; ir:469-482, 554-558):
+ * irgan_sep_resample (mr == NULL) or irgan_sep_resample_in (mr != NULL) into a bf16 out (no
+ * accumulate) that also writes y8 = e4m3(clamp(bf16(out) * q[0], +-448)) (an NHWC slice, ld8 /
+ * off8) and raises max |bf16(out)| into the amax slot (IRGAN_FP8_AMAX_PARTS partials) -- the
+ * bytes irgan_fp8_quant makes from the stored out, with no pass reading it back.
+ * IRGAN_EUNSUPPORTED (nothing launched) unless the LDS form takes the shapes (8-channel-aligned
+ * slices, ld8 / off8 % 8, at most 8 taps per axis). */
+IRGAN_API int irgan_sep_resample_fp8(const void* in, int32_t in_dtype, int32_t N, int32_t Hin, int32_t Win,
+                           int32_t C, int32_t ldi, int32_t offi, const float* mr, int32_t act,
+                           void* out, int32_t out_dtype, int32_t Hout, int32_t Wout, int32_t ldo,
+                           int32_t offo, const int32_t* ty, const float* wy, int32_t Ty,
+                           const int32_t* tx, const float* wx, int32_t Tx, void* y8, int32_t ld8,
+                           int32_t off8, const float* q, uint32_t* amax, irgan_stream_t s);
 /* 2x2 max pool (VGG features) forward / backward (first max wins, as ATen). */
 IRGAN_API int irgan_maxpool_fwd(const void* x, int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t C,
                       void* y, irgan_stream_t s);

@@ -23,10 +23,10 @@ IRGAN_HD uint2 pack8_fp8(const float* v, float q) {
     return o;
 }
 
-// block max of m (every thread of a 256-thread block calls it) raised into
+// block max of m (every thread of a block of <= 1024 threads calls it) raised into
 // partial `part % IRGAN_FP8_AMAX_PARTS` of an amax slot
 __device__ inline void fp8_block_amax(float m, uint32_t* amax, int part) {
-    __shared__ float red_amax[4];
+    __shared__ float red_amax[16];
     for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
     if ((threadIdx.x & 63) == 0) red_amax[threadIdx.x >> 6] = m;
     __syncthreads();

@@ -6,6 +6,7 @@
 // Backward passes are gathers (each output element sums its contributors), so
 // they are deterministic and need no atomics.
 #include "common.h"
+#include "fp8_util.h"
 
 namespace {
 
@@ -113,8 +114,20 @@ __global__ __launch_bounds__(TPB) void sep_kernel(const void* __restrict__ in, i
 // the InstanceNorm apply + ReLU of down1 / down2 / up1_conv (ir:469-482, 557) fused into
 // the Downsample / UpsampleAA that consumes it, so the normalised tensor is never stored.
 // LTPB % G == 0, so a thread's channel group (and its 8 (mean, rstd) pairs) is fixed.
+//
+// Q8 (irgan_sep_resample_fp8): the stored bf16 output also as e4m3 bytes (o8: an NHWC slice,
+// e4m3(clamp(bf16(out) * q8[0], +-448))) with max |bf16(out)| raised into the amax slot --
+// the fp8 path's producers of the down2 / up1_conv operands (x1 from down1's Downsample, the
+// up-sampled bottleneck from UpsampleAA: the two halves of up1_conv's concat), so no separate
+// quantise pass reads them back.
+struct ResQ8 {
+    uint8_t* p;
+    int ld, off;
+    const float* q;
+    uint32_t* amax;
+};
 constexpr int LTPB = 1024;
-template <int TM, bool NORM = false, int NT = LTPB>
+template <int TM, bool NORM = false, int NT = LTPB, bool Q8 = false>
 __global__ __launch_bounds__(NT) void sep_lds_kernel(const void* __restrict__ in, int idt, int Hin, int Win,
                                                        int ldi, int offi, void* __restrict__ out, int odt, int Hout,
                                                        int Wout, int ldo, int offo, const int* __restrict__ ty,
@@ -122,7 +135,7 @@ __global__ __launch_bounds__(NT) void sep_lds_kernel(const void* __restrict__ in
                                                        const int* __restrict__ tx, const float* __restrict__ wx,
                                                        int Tx, int accumulate, int CB,
                                                        const float* __restrict__ mr = nullptr, int C = 0,
-                                                       int act = 0, int swz = 0) {
+                                                       int act = 0, int swz = 0, ResQ8 q8 = ResQ8{}) {
     extern __shared__ float4 sm4[];
     float* const sm = (float*)sm4;
     // XCD-aware row order: consecutive output rows (which share input rows through the
@@ -172,6 +185,8 @@ __global__ __launch_bounds__(NT) void sep_lds_kernel(const void* __restrict__ in
         d[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
     }
     __syncthreads();
+    const float qs = Q8 ? *q8.q : 1.f;
+    float amx = 0.f;
     for (int v = threadIdx.x; v < Wout * G; v += NT) {
         const int ox = v / G, g = v - ox * G;
         float wxv[TM];
@@ -200,8 +215,29 @@ __global__ __launch_bounds__(NT) void sep_lds_kernel(const void* __restrict__ in
 #pragma unroll
             for (int k = 0; k < 8; ++k) acc[k] += pv[k];
         }
-        stvec<8>(out, odt, o, acc);
+        if constexpr (Q8) {  // bf16 out (host-checked): quantise the stored values
+            uint4 u;
+            u.x = pk_bf16(acc[0], acc[1]);
+            u.y = pk_bf16(acc[2], acc[3]);
+            u.z = pk_bf16(acc[4], acc[5]);
+            u.w = pk_bf16(acc[6], acc[7]);
+            *(uint4*)((bf16_t*)out + o) = u;
+            const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
+            float vb[8];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                vb[2 * k] = __uint_as_float(wd[k] << 16);
+                vb[2 * k + 1] = __uint_as_float(wd[k] & 0xffff0000u);
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) amx = fmaxf(amx, fabsf(vb[k]));
+            const long o8 = (((long)n * Hout + oy) * Wout + ox) * q8.ld + q8.off + c0 + g * 8;
+            *(uint2*)(q8.p + o8) = pack8_fp8(vb, qs);
+        } else {
+            stvec<8>(out, odt, o, acc);
+        }
     }
+    if constexpr (Q8) fp8_block_amax(amx, q8.amax, blockIdx.y * gridDim.x + blockIdx.x);
 }
 
 // Threads per block of sep_lds_kernel and the LDS row cap (floats) that sizes its channel
@@ -593,6 +629,48 @@ extern "C" int irgan_sep_resample_in(const void* in, int32_t in_dtype, int32_t N
     if (nt == 256) { SEPT(256) } else if (nt == 512) { SEPT(512) } else { SEPT(1024) }
 #undef SEPT
 #undef SEPN
+    IRGAN_LAUNCH_CHECK();
+    return 0;
+}
+
+// irgan_sep_resample (mr == NULL) / irgan_sep_resample_in (mr: act(IN(in)) on load) into a
+// bf16 out, no accumulate, that also writes out's e4m3 copy y8 (ld8 / off8: an NHWC slice) with
+// the quantisation factor q[0] and raises max |bf16(out)| into the amax slot (the LDS form only:
+// IRGAN_EUNSUPPORTED otherwise, nothing launched)
+extern "C" int irgan_sep_resample_fp8(const void* in, int32_t in_dtype, int32_t N, int32_t Hin, int32_t Win,
+                                      int32_t C, int32_t ldi, int32_t offi, const float* mr, int32_t act, void* out,
+                                      int32_t out_dtype, int32_t Hout, int32_t Wout, int32_t ldo, int32_t offo,
+                                      const int32_t* ty, const float* wy, int32_t Ty, const int32_t* tx,
+                                      const float* wx, int32_t Tx, void* y8, int32_t ld8, int32_t off8,
+                                      const float* q, uint32_t* amax, irgan_stream_t s) {
+    if (!in || !out || !y8 || !q || !amax) return IRGAN_EINVAL;
+    const bool vec = (C % 8 == 0) && (ldi % 8 == 0) && (offi % 8 == 0) && (ldo % 8 == 0) && (offo % 8 == 0) &&
+                     ld8 % 8 == 0 && off8 % 8 == 0;
+    if ((long)N * Hout * Wout * C <= 0) return 0;
+    if (Ty < 1 || Tx < 1) return IRGAN_EINVAL;
+    const int TM = Ty > Tx ? Ty : Tx;
+    if (!vec || TM > 8 || out_dtype != IRGAN_BF16) return IRGAN_EUNSUPPORTED;
+    const int nt = sep_nt();
+    int CB = 0;
+    for (int cb = 128; cb >= 8 && !CB; cb >>= 1)
+        if (C % cb == 0 && (long)Win * cb <= 16384 * nt / 1024) CB = cb;
+    if (!CB) return IRGAN_EUNSUPPORTED;
+    dim3 g(N * Hout, C / CB);
+    const size_t sh = (size_t)Win * CB * 4;
+    hipStream_t st = (hipStream_t)s;
+    const ResQ8 q8{(uint8_t*)y8, ld8, off8, q, amax};
+#define SEPQ(T, NORMV)                                                                                            \
+    sep_lds_kernel<T, NORMV, 512, true><<<g, 512, sh, st>>>(in, in_dtype, Hin, Win, ldi, offi, out, out_dtype, Hout, \
+                                                            Wout, ldo, offo, ty, wy, Ty, tx, wx, Tx, 0, CB, mr, C,    \
+                                                            act, sep_swz(), q8)
+#define SEPT(NORMV)                  \
+    if (TM <= 2) SEPQ(2, NORMV);     \
+    else if (TM <= 4) SEPQ(4, NORMV); \
+    else if (TM <= 6) SEPQ(6, NORMV); \
+    else SEPQ(8, NORMV);
+    if (mr) { SEPT(true) } else { SEPT(false) }
+#undef SEPT
+#undef SEPQ
     IRGAN_LAUNCH_CHECK();
     return 0;
 }

@@ -320,11 +320,16 @@ class INLayer:
             ops.conv_fwd(pc, x, z)
         self.fwd(bufs, name, z, y, act, res=res, nb=nb)
 
-    def conv_stats(self, bufs: Buffers, name: str, pc, x: Feat, z: Feat):
+    def conv_stats(self, bufs: Buffers, name: str, pc, x: Feat, z: Feat, conv8=None):
         """z = conv(x) and z's {mean, rstd} table (returned, kept for bwd()) -- no apply:
-        the consumer normalises on load (ops.blur_down_in / ops.upsample_in)."""
+        the consumer normalises on load (ops.blur_down_in / ops.upsample_in).
+        conv8 = (w8, dqw, x8, dqx): the conv on fp8 operands (ops.conv_fwd_fp8)."""
         work = bufs.flat("in_work", ops.IN_PARTS * z.N * z.C, torch.float64)
         mr = bufs.get("mr_" + name, (z.N * z.C * 2,), torch.float32)
+        if conv8 is not None:
+            w8, dqw, x8, dqx = conv8
+            ops.in_finalize(z, work, ops.conv_fwd_fp8(pc, w8, dqw, x8, dqx, z, part=work), mr)
+            return mr
         nb = ops.conv_fwd_stats(pc, x, z, work) if INLayer.fused_stats else 0
         if nb:
             ops.in_finalize(z, work, nb, mr)
@@ -333,15 +338,19 @@ class INLayer:
             ops.in_stats(z, work, mr)
         return mr
 
-    def resample_fwd(self, bufs: Buffers, name: str, pc, x: Feat, z: Feat, a_name: str, act, y: Feat, fused, plain):
+    def resample_fwd(self, bufs: Buffers, name: str, pc, x: Feat, z: Feat, a_name: str, act, y: Feat, fused, plain,
+                     conv8=None, q8=None):
         """y = resample(act(IN(conv(x)))): the IN apply fused into the resample when
-        ``fused(z, mr, act, y)`` takes the shapes, else apply into bufs[a_name] + ``plain``."""
-        mr = self.conv_stats(bufs, name, pc, x, z)
-        if INLayer.fused_resample and fused(z, mr, act, y):
+        ``fused(z, mr, act, y)`` takes the shapes, else apply into bufs[a_name] + ``plain``.
+        conv8: the conv on fp8 operands (conv_stats); q8: also y's e4m3 copy (Fp8Acts.spec)."""
+        mr = self.conv_stats(bufs, name, pc, x, z, conv8=conv8)
+        if INLayer.fused_resample and (fused(z, mr, act, y, q8=q8) if q8 is not None else fused(z, mr, act, y)):
             return
         a = Feat(bufs.get(a_name, (z.N, z.H, z.W, z.C), z.t.dtype))
         ops.in_apply(z, mr, a, act=act)
         plain(a, y)
+        if q8 is not None:
+            ops.fp8_quant(y, *q8)
 
     def bwd(self, bufs: Buffers, name: str, dy: Feat, z: Feat, act, dx: Feat, db=None, dy2: Feat = None, q8=None):
         """z: the PRE-norm input kept from forward; act: the activation after IN.
@@ -380,7 +389,9 @@ class NoNorm(INLayer):
         ops.conv_fwd(pc, x, z, bias=pc.bias is not None)
         self.fwd(bufs, name, z, y, act, res=res)
 
-    def conv_stats(self, bufs, name, pc, x, z):
+    def conv_stats(self, bufs, name, pc, x, z, conv8=None):
+        if conv8 is not None:
+            raise NotImplementedError("the fp8 path runs with InstanceNorm (norm='instance')")
         ops.conv_fwd(pc, x, z, bias=pc.bias is not None)
         return self._ident(bufs, name, z.N, z.C)
 
@@ -424,10 +435,11 @@ class GeneratorEngine:
     def __init__(self, store: ParamStore, dtype=BF16, ngf=64, input_nc=1, output_nc=3, n_blocks=9,
                  no_antialias=False, no_antialias_up=False, fp8=False, norm="instance", padding_type="reflect",
                  use_dropout=False, dropout_seed=0):
-        """fp8: the ResnetBlock convs (forward and the backward-data interior) run on
-        OCP e4m3 operands (BASELINE config 5): per-tensor power-of-two scales, current
-        scaling for the re-packed weights, delayed scaling for the activations and
-        gradients they read; everything else (and every weight gradient) stays bf16.
+        """fp8: the ResnetBlock convs and, with the anti-aliased resamplers (the default),
+        down2 and up1_conv run on OCP e4m3 operands (BASELINE config 5: forward, backward-
+        data interior, weight gradient): per-tensor power-of-two scales, current scaling
+        for the re-packed weights, delayed scaling for the activations and gradients they
+        read; everything else stays bf16.
         norm / padding_type / use_dropout: the reference's constructor options (ir:154-165,
         375-411, 443-447); the ResnetBlock convs of padding 'replicate' read an explicitly
         padded copy of their input (ops.pad) and fold their input gradient back (ops.pad_fold)."""
@@ -464,13 +476,20 @@ class GeneratorEngine:
         self.outc = _pc(S, "outc.1", ConvSpec(c0, output_nc, 7, 1, 3, PAD_REFLECT), dtype)
         self.packs = [self.inc, self.down1, self.down2, self.up1, self.up2, self.outc] + \
             [p for pr in self.res for p in pr] + ([self.up1_up, self.up2_up] if no_antialias_up else [])
+        # fp8 on down2 / up1_conv too (ir:477-482, 557-558): their operands come from the
+        # fused resamplers (x1 from down1's Downsample, the up-sampled bottleneck)
+        self.fp8_ud = self.fp8 and not no_antialias and not no_antialias_up
         if self.fp8:
             # weight images 4b..4b+3: conv1 fwd, conv1 dgrad, conv2 fwd, conv2 dgrad of block b;
+            # 4n..4n+3: down2 fwd, down2 dgrad, up1_conv fwd, up1_conv dgrad.
             # activation slots: forward inputs 2b (conv1), 2b+1 (conv2); backward-data inputs
-            # 2n+2b (conv2's dY), 2n+2b+1 (conv1's dY)
+            # 2n+2b (conv2's dY), 2n+2b+1 (conv1's dY); 4n: up1_conv's concat [up(h) | x1] (x1
+            # is down2's input: one scale for both), 4n+1 / 4n+2: up1_conv's / down2's dY
+            ud = [self.down2.fwd, self.down2.dg[0][2], self.up1.fwd, self.up1.dg[0][2]] if self.fp8_ud else []
             self.f8w = ops.Fp8Weights([im for p1, p2 in self.res for im in (p1.fwd, p1.dg[0][2], p2.fwd,
-                                                                             p2.dg[0][2])], store.device)
-            self.f8a = ops.Fp8Acts(4 * n_blocks, store.device)
+                                                                             p2.dg[0][2])] + ud, store.device)
+            self.f8a = ops.Fp8Acts(4 * n_blocks + 3, store.device)
+            self.s_cat, self.s_dz3, self.s_dz2 = 4 * n_blocks, 4 * n_blocks + 1, 4 * n_blocks + 2
         n_in = 5 + 2 * n_blocks
         self.norms = {k: make_norm(norm) for k in ["inc", "down1", "down2", "up1", "up2"] +
                       [f"r{b}_{i}" for b in range(n_blocks) for i in (1, 2)]}
@@ -539,6 +558,10 @@ class GeneratorEngine:
         cat1 = g.get("cat1", (B, H1, W1, c2 + c1), T)     # [up1 out | x1]
         x0 = Feat(cat2, c1, c0)
         x1 = Feat(cat1, c2, c1)
+        A = self.f8a if self.fp8 else None
+        cat1_8 = Feat(g.get("cat1_8", (B, H1, W1, c2 + c1), torch.float8_e4m3fn)) if self.fp8_ud else None
+        x1_8 = cat1_8.sl(c2, c1) if self.fp8_ud else None
+        calib = self.fp8_ud and not A.seen[self.s_cat]   # first step: current scaling
         # inc: reflect-pad 3, conv7x7, IN, ReLU  (ir:458-463)
         z0 = Feat(g.get("z0", (B, H, W, c0), T))
         ops.conv_fwd(self.inc, ir_t, z0)
@@ -551,7 +574,9 @@ class GeneratorEngine:
         else:
             z1 = Feat(g.get("z1", (B, H, W, c1), T))
             self.norms["down1"].resample_fwd(g, "down1", self.down1, x0, z1, "a1", ACT_RELU, x1, ops.blur_down_in,
-                                             ops.blur_down)
+                                             ops.blur_down, q8=A.spec(self.s_cat, x1_8) if self.fp8_ud else None)
+            if calib:
+                A.quant(self.s_cat, x1, x1_8)   # down2's operand scaled from x1 alone on the first step
         # down2 (+ blur-down)  (ir:477-482)
         h = Feat(g.get("h0", (B, H2, W2, c2), T))
         if self.no_aa:
@@ -561,14 +586,14 @@ class GeneratorEngine:
         else:
             z2 = Feat(g.get("z2", (B, H1, W1, c2), T))
             self.norms["down2"].resample_fwd(g, "down2", self.down2, x1, z2, "a2", ACT_RELU, h, ops.blur_down_in,
-                                             ops.blur_down)
+                                             ops.blur_down, conv8=(*self._w8(4 * self.n_blocks), x1_8,
+                                                                   A.dqp(self.s_cat)) if self.fp8_ud else None)
         # 9 ResnetBlocks  (ir:362-418, 485-490)
         # fp8: one e4m3 operand buffer, written by the producer of each conv input (the
         # IN passes, fused; h_0 from blur-down by a quantise launch) and read by the conv
         # (one buffer per conv input slot: the fp8 weight gradients of the backward read them)
         x8s = [Feat(g.get(f"x8_{k}", (B, H2, W2, c2), torch.float8_e4m3fn)) for k in range(2 * len(self.res))] \
             if self.fp8 else None
-        A = self.f8a if self.fp8 else None
         if self.fp8:
             A.quant(0, h, x8s[0])
         nres = len(self.res)
@@ -609,7 +634,9 @@ class GeneratorEngine:
         if self.no_aa_up:
             self._convt(self.up1_up, h, y1, g, "ut1")
         else:
-            ops.upsample(h, y1)
+            ops.upsample(h, y1, q8=A.spec(self.s_cat, cat1_8.sl(0, c2)) if self.fp8_ud and not calib else None)
+        if calib:   # up1_conv's operand scaled from the whole concat on the first step
+            A.calibrate(self.s_cat, Feat(cat1), cat1_8)
         z3 = Feat(g.get("z3", (B, H1, W1, c1), T))
         # up2 -> cat with x0 -> conv/IN/ReLU  (ir:561-565)
         y2 = Feat(cat2, 0, c1)
@@ -619,7 +646,11 @@ class GeneratorEngine:
             self._convt(self.up2_up, a3, y2, g, "ut2")
         else:
             self.norms["up1"].resample_fwd(g, "up1", self.up1, Feat(cat1), z3, "a3", ACT_RELU, y2, ops.upsample_in,
-                                           ops.upsample)
+                                           ops.upsample, conv8=(*self._w8(4 * self.n_blocks + 2), cat1_8,
+                                                                A.dqp(self.s_cat)) if self.fp8_ud else None)
+        if self.fp8_ud:
+            A.snapshot(self.s_cat, 1)   # the scale cat1_8 was made with (the weight gradients)
+            A.update(self.s_cat, 1)
         z4 = Feat(g.get("z4", (B, H, W, c0), T))
         a4 = Feat(g.get("a4", (B, H, W, c0), T))
         self.norms["up2"].conv_fwd(g, "up2", self.up2, Feat(cat2), z4, a4, ACT_RELU)
@@ -695,10 +726,25 @@ class GeneratorEngine:
         else:
             ops.upsample_bwd(dy2, da3)
         # up1_conv
-        self.norms["up1"].bwd(g, "up1", da3, Feat(g.d["z3"]), ACT_RELU, da3, db=self._bgrad("up1_conv.0.bias"))
-        wg(self.up1, "up1_conv.0", cat1, da3)
+        A, nb4 = (self.f8a, 4 * self.n_blocks) if self.fp8 else (None, 0)
+        cat1_8 = Feat(g.d["cat1_8"]) if self.fp8_ud else None
+
+        def wg8(pc, key, x8, xslot, dy8, dslot, x, dy):
+            """weight gradient on the fp8 copies (x8 with the scale it was made with, dy8);
+            bf16 where the kernel does not take the layer"""
+            if not ops.conv_wgrad_fp8(pc.spec, x8, dy8, A.dqp_used(xslot), A.dqp(dslot), S.krsc(key + ".weight", G)):
+                wg(pc, key, x, dy)
+        da3_8 = Feat(g.get("dz3_8", (B, H1, W1, c1), torch.float8_e4m3fn)) if self.fp8_ud else None
+        self.norms["up1"].bwd(g, "up1", da3, Feat(g.d["z3"]), ACT_RELU, da3, db=self._bgrad("up1_conv.0.bias"),
+                              q8=A.spec(self.s_dz3, da3_8) if self.fp8_ud else None)
         dcat1 = Feat(g.get("dcat1", (B, H1, W1, c2 + c1), T))
-        ops.conv_dgrad(self.up1, da3, dcat1)
+        if self.fp8_ud:
+            A.ensure(self.s_dz3, da3, da3_8)
+            wg8(self.up1, "up1_conv.0", cat1_8, self.s_cat, da3_8, self.s_dz3, cat1, da3)
+            ops.conv_dgrad_fp8(self.up1, *self._w8(nb4 + 3), da3_8, A.dqp(self.s_dz3), da3, dcat1)
+        else:
+            wg(self.up1, "up1_conv.0", cat1, da3)
+            ops.conv_dgrad(self.up1, da3, dcat1)
         # up1_up
         h9 = Feat(g.d[f"h{self.n_blocks}"])
         dh = Feat(g.get("dh", (B, H2, W2, c2), T))
@@ -712,13 +758,6 @@ class GeneratorEngine:
         dt_ = Feat(g.get("dtmp", (B, H2, W2, c2), T))
         nb2 = 2 * self.n_blocks
         dy8 = Feat(g.get("dy8", (B, H2, W2, c2), torch.float8_e4m3fn)) if self.fp8 else None
-
-        def wg8(pc, key, xslot, dslot, x, dy):
-            """ResnetBlock weight gradient on the fp8 copies (the forward's x8 of slot xslot with
-            the scale it was made with, dy8 of slot dslot); bf16 where the kernel does not take it."""
-            if not ops.conv_wgrad_fp8(pc.spec, Feat(g.d[f"x8_{xslot}"]), dy8, self.f8a.dqp_used(xslot),
-                                      self.f8a.dqp(dslot), S.krsc(key + ".weight", G)):
-                wg(pc, key, x, dy)
         k1, k2 = self.res_keys
         for b in reversed(range(self.n_blocks)):
             p1, p2 = self.res[b]
@@ -730,14 +769,13 @@ class GeneratorEngine:
             t2 = Feat(g.d[f"td{b}"]) if drop else t
             xin1 = Feat(g.d[f"xp1_{b}"]) if self.padding_type == "replicate" else hb
             xin2 = Feat(g.d[f"xp2_{b}"]) if self.padding_type == "replicate" else t2
-            A = self.f8a if self.fp8 else None
             s2, s1 = nb2 + 2 * b, nb2 + 2 * b + 1
             self.norms[f"r{b}_2"].bwd(g, f"r{b}_2", dh, r2, ACT_NONE, dt_, db=self._bgrad(f"{key}{k2}.bias"),
                                       q8=A.spec(s2, dy8) if self.fp8 else None)
             dr = Feat(g.get("dtmp2", (B, H2, W2, c2), T))
             if self.fp8:
                 A.ensure(s2, dt_, dy8)
-                wg8(p2, f"{key}{k2}", 2 * b + 1, s2, xin2, dt_)
+                wg8(p2, f"{key}{k2}", Feat(g.d[f"x8_{2 * b + 1}"]), 2 * b + 1, dy8, s2, xin2, dt_)
                 ops.conv_dgrad_fp8(p2, *self._w8(4 * b + 3), dy8, A.dqp(s2), dt_, dr)
             else:
                 self._res_dgrad(g, p2, dt_, dr, False, padbuf)
@@ -748,7 +786,7 @@ class GeneratorEngine:
                                       q8=A.spec(s1, dy8) if self.fp8 else None)
             if self.fp8:
                 A.ensure(s1, dr, dy8)
-                wg8(p1, f"{key}{k1}", 2 * b, s1, xin1, dr)
+                wg8(p1, f"{key}{k1}", Feat(g.d[f"x8_{2 * b}"]), 2 * b, dy8, s1, xin1, dr)
                 ops.conv_dgrad_fp8(p1, *self._w8(4 * b + 1), dy8, A.dqp(s1), dr, dh, accumulate=True)
             else:
                 self._res_dgrad(g, p1, dr, dh, True, padbuf)
@@ -764,10 +802,18 @@ class GeneratorEngine:
         else:
             dz2 = Feat(g.get("da2", (B, H1, W1, c2), T))
             ops.blur_down_bwd(dh, dz2)
-            self.norms["down2"].bwd(g, "down2", dz2, z2, ACT_RELU, dz2, db=self._bgrad("down2.0.bias"))
-        wg(self.down2, "down2.0", x1, dz2)
+            dz2_8 = Feat(g.get("dz2_8", (B, H1, W1, c2), torch.float8_e4m3fn)) if self.fp8_ud else None
+            self.norms["down2"].bwd(g, "down2", dz2, z2, ACT_RELU, dz2, db=self._bgrad("down2.0.bias"),
+                                    q8=A.spec(self.s_dz2, dz2_8) if self.fp8_ud else None)
         dx1 = dcat1.sl(c2, c1)
-        ops.conv_dgrad(self.down2, dz2, dx1, accumulate=True)  # x1 feeds down2 and the up1 concat
+        if self.fp8_ud:
+            A.ensure(self.s_dz2, dz2, dz2_8)
+            wg8(self.down2, "down2.0", cat1_8.sl(c2, c1), self.s_cat, dz2_8, self.s_dz2, x1, dz2)
+            ops.conv_dgrad_fp8(self.down2, *self._w8(nb4 + 1), dz2_8, A.dqp(self.s_dz2), dz2, dx1, accumulate=True)
+            A.update(self.s_dz3, 2)   # next step's scales of the two dY slots
+        else:
+            wg(self.down2, "down2.0", x1, dz2)
+            ops.conv_dgrad(self.down2, dz2, dx1, accumulate=True)  # x1 feeds down2 and the up1 concat
         # down1 (+ blur-down)
         z1 = Feat(g.d["z1"])
         if self.no_aa:

@@ -683,13 +683,35 @@ def sep_resample_in(z: Feat, mr: torch.Tensor, act, y: Feat, ytab, xtab) -> bool
     return True
 
 
+def sep_resample_fp8(x: Feat, mr, act, y: Feat, ytab, xtab, q8) -> bool:
+    """sep_resample (mr None) / sep_resample_in (mr: act(IN(x)) on load) into bf16 y that
+    also writes y's e4m3 copy: q8 = (y8 Feat, q pointer, amax pointer) as Fp8Acts.spec()
+    gives it (irgan_sep_resample_fp8).  False when the kernel does not take the shapes --
+    then NOTHING ran."""
+    (ty, wy, ry, Ty), (tx, wx, rx, Tx) = ytab, xtab
+    y8, qp, ap = q8
+    assert (ry, rx) == (y.H, y.W) and x.C == y.C and x.N == y.N, "sep_resample_fp8 shape mismatch"
+    assert y8.dt == FP8 and (y8.N, y8.H, y8.W, y8.C) == (y.N, y.H, y.W, y.C)
+    rc = getattr(_lib.load(), "irgan_sep_resample_fp8")(
+        x.ptr, x.dt, x.N, x.H, x.W, x.C, x.ld, x.off, P(mr), act, y.ptr, y.dt, y.H, y.W, y.ld, y.off,
+        P(ty), P(wy), Ty, P(tx), P(wx), Tx, y8.ptr, y8.ld, y8.off, qp, ap, stream())
+    if rc == IRGAN_EUNSUPPORTED:
+        return False
+    if rc != 0:
+        raise _lib.IrganError(f"irgan_sep_resample_fp8 failed with code {rc}")
+    return True
+
+
 def blur_down(x: Feat, y: Feat):
     """Downsample (ir:269-310)."""
     sep_resample(x, y, resample_table(RS_DOWN, x.H), resample_table(RS_DOWN, x.W))
 
 
-def blur_down_in(z: Feat, mr: torch.Tensor, act, y: Feat) -> bool:
-    """Downsample of act(IN(z)) (ir:469-482) without storing the normalised tensor."""
+def blur_down_in(z: Feat, mr: torch.Tensor, act, y: Feat, q8=None) -> bool:
+    """Downsample of act(IN(z)) (ir:469-482) without storing the normalised tensor;
+    q8: also y's e4m3 copy (sep_resample_fp8)."""
+    if q8 is not None:
+        return sep_resample_fp8(z, mr, act, y, resample_table(RS_DOWN, z.H), resample_table(RS_DOWN, z.W), q8)
     return sep_resample_in(z, mr, act, y, resample_table(RS_DOWN, z.H), resample_table(RS_DOWN, z.W))
 
 
@@ -704,10 +726,17 @@ def _up_axis(n_in, n_out, transpose):
     return resize_table(n_in, n_out, after_up=True, transpose=transpose)   # odd-size fallback folded in
 
 
-def upsample(x: Feat, y: Feat):
+def upsample(x: Feat, y: Feat, q8=None):
     """UpsampleAA (ir:313-355); when y is not 2x (odd skip sizes) the reference's
-    bilinear resize to the skip's size (ir:555-556, 562-563) is folded into the map."""
-    sep_resample(x, y, _up_axis(x.H, y.H, False), _up_axis(x.W, y.W, False))
+    bilinear resize to the skip's size (ir:555-556, 562-563) is folded into the map.
+    q8: also y's e4m3 copy (sep_resample_fp8; the plain launch + fp8_quant if the LDS
+    form does not take the shapes)."""
+    yt, xt = _up_axis(x.H, y.H, False), _up_axis(x.W, y.W, False)
+    if q8 is not None and sep_resample_fp8(x, None, ACT_NONE, y, yt, xt, q8):
+        return
+    sep_resample(x, y, yt, xt)
+    if q8 is not None:
+        fp8_quant(y, *q8)
 
 
 def upsample_in(z: Feat, mr: torch.Tensor, act, y: Feat) -> bool:
@@ -940,6 +969,13 @@ class Fp8Acts:
         if not self.seen[slot]:
             self.quant(slot, x, y)
 
+    def calibrate(self, slot, x: Feat, y: Feat):
+        """Current scaling of slot from x alone, whatever was recorded before (the slot's
+        partial maxima are cleared first), then the quantisation of x into y."""
+        self.amax[slot * FP8_AMAX_PARTS:(slot + 1) * FP8_AMAX_PARTS].zero_()
+        self.seen[slot] = False
+        self.quant(slot, x, y)
+
     def dqp(self, slot):
         return Pi(self.dq, slot)
 
@@ -1003,11 +1039,25 @@ def conv_wgrad_fp8(spec: ConvSpec, x8: Feat, dy8: Feat, dqx, dqdy, dw: torch.Ten
 
 
 def conv_dgrad_fp8(pc: PackedConv, wd8: torch.Tensor, dqw, dy8: Feat, dqx, dy: Feat, dx: Feat, accumulate=False):
-    """Backward-data of a reflect-padded stride-1 3x3 layer: the interior on fp8
-    operands (dy8 = e4m3(dy), wd8 = e4m3 copy of the flipped image pc.dg[0]), the
-    padded ring from the bf16 dy by irgan_reflect_dgrad_ring (as conv_dgrad)."""
+    """Backward-data of a stride-1 3x3 layer on fp8 operands (dy8 = e4m3(dy), wd8 = e4m3
+    copy of the flipped image pc.dg[0]).  Reflect padding: the interior on fp8, the padded
+    ring from the bf16 dy by irgan_reflect_dgrad_ring (as conv_dgrad); zero padding (down2 /
+    up1_conv of config 5): the flipped conv alone (irgan_conv_fwd_fp8; dy unused)."""
     s = pc.spec
-    assert pc.reflect and s.stride == 1 and dy.dt == BF16 and dy8.dt == FP8 and dx.C == s.cin
+    assert s.stride == 1 and dy8.dt == FP8 and dx.C == s.cin
+    if not pc.reflect:
+        (py, _, ay, c0y), (px, _, ax, c0x), buf = pc.dg[0]
+        assert len(pc.dg) == 1 and (dy8.H, dy8.W, dy8.C) == (dx.H, dx.W, pc.cout_eff)
+        d8 = _desc(N=dy8.N, H=dy8.H, W=dy8.W, Cin=pc.cout_eff, ldx=dy8.ld, xoff=dy8.off, Ho=dx.H, Wo=dx.W,
+                   Cout=s.cin, ldy=dx.ld, yoff=dx.off, OH=dx.H, OW=dx.W, omy=1, ooy=py, omx=1, oox=px, KH=ay, KW=ax,
+                   sy=1, sx=1, c0y=c0y, c0x=c0x, pad_mode=PAD_ZERO, act=0, accumulate=int(accumulate), dtype=FP8,
+                   out_dtype=dx.dt, mask_act=0, ldm=0, moff=0)
+        nb = ctypes.c_int32(0)
+        TIMER.wrap(conv_tag("dgrad8", s, (dx.H, dx.W), dx.N), lambda: _lib.call(
+            "irgan_conv_fwd_fp8", ctypes.byref(d8), dy8.ptr, P(wd8), dqx, dqw, None, dx.ptr, None,
+            ctypes.byref(nb), stream()))
+        return
+    assert pc.reflect and dy.dt == BF16
     p = s.pad
     H, W = dx.H, dx.W
     (_, _, ay, c0y), (_, _, ax, c0x), buf = pc.dg[0]

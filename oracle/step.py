@@ -216,6 +216,29 @@ class _Fp8ResConv(torch.autograd.Function):
         return g8[..., 1:-1, 1:-1] + ring, dw, gy.sum(dim=(0, 2, 3))
 
 
+class _Fp8ZeroConv(torch.autograd.Function):
+    """The fp8 path's down2 / up1_conv (zero pad 1, 3x3; GeneratorEngine(fp8=True) with the
+    anti-aliased resamplers): forward on e4m3(x) x e4m3(bf16(w)), backward-data on e4m3(dY)
+    x e4m3(bf16(w)), the weight gradient on e4m3(x) x e4m3(dY), the bias gradient on the
+    unquantised dY.  Not a reference function: the emulation the fp8 step is checked against
+    (ir:477-482, 557-558 otherwise)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        wb = w.to(torch.bfloat16).to(w.dtype)
+        ctx.save_for_backward(x, w, wb)
+        return F.conv2d(fp8_q(x), fp8_q(wb), b, padding=1)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, wb = ctx.saved_tensors
+        gq = fp8_q(gy)
+        with torch.autocast("cpu", enabled=False):   # e4m3 operands: exact in fp32
+            dw = torch.nn.grad.conv2d_weight(fp8_q(x).float(), w.shape, gq.float(), padding=1).to(w.dtype)
+        dx = torch.nn.grad.conv2d_input(x.shape, fp8_q(wb), gq, padding=1)
+        return dx, dw, gy.sum(dim=(0, 2, 3))
+
+
 def _res_conv(h, w, b, padding_type):
     """[ReflectionPad2d(1) | ReplicationPad2d(1) | -] + Conv2d(3, padding 0 | 0 | 1) (ir:380-411)."""
     if padding_type == "reflect":
@@ -230,7 +253,8 @@ def _res_conv(h, w, b, padding_type):
 def g_forward(P, x, no_antialias=False, no_antialias_up=False, n_blocks=9, acts=None, fp8=False, norm="instance",
               padding_type="reflect", dropout_masks=None):
     """ResnetUNetGenerator.forward (ir:533-569); returns the tanh image.
-    fp8=True: the ResnetBlock convs as the fp8 path computes them (_Fp8ResConv).
+    fp8=True: the ResnetBlock convs as the fp8 path computes them (_Fp8ResConv), and with the
+    anti-aliased resamplers down2 / up1_conv too (_Fp8ZeroConv).
     norm 'none': Identity norm layers and no conv biases (ir:162-163, 450-455: absent
     keys read as None).  padding_type: the ResnetBlock padding (ir:380-411).
     dropout_masks: per block a tensor of keep / (1 - p) factors multiplied after the
@@ -250,7 +274,11 @@ def g_forward(P, x, no_antialias=False, no_antialias_up=False, n_blocks=9, acts=
     if not no_antialias:
         x1 = blur_down(x1, P["down1_down.filt"])
     rec("x1", x1)
-    x2 = F.relu(nrm(F.conv2d(x1, P["down2.0.weight"], bias("down2.0.bias"), stride=s, padding=1)))
+    fp8_ud = fp8 and not no_antialias and not no_antialias_up
+    if fp8_ud:
+        x2 = F.relu(nrm(_Fp8ZeroConv.apply(x1, P["down2.0.weight"], bias("down2.0.bias"))))
+    else:
+        x2 = F.relu(nrm(F.conv2d(x1, P["down2.0.weight"], bias("down2.0.bias"), stride=s, padding=1)))
     if not no_antialias:
         x2 = blur_down(x2, P["down2_down.filt"])
     h = rec("x2", x2)
@@ -274,8 +302,11 @@ def g_forward(P, x, no_antialias=False, no_antialias_up=False, n_blocks=9, acts=
         y = up_aa(h, P["up1_up.filt"])
     if y.shape[-2:] != x1.shape[-2:]:                          # ir:555-556
         y = F.interpolate(y, size=x1.shape[-2:], mode="bilinear", align_corners=True)
-    y = F.relu(nrm(F.conv2d(torch.cat([y, x1], 1), P["up1_conv.0.weight"],
-                            bias("up1_conv.0.bias"), padding=1)))
+    if fp8_ud:
+        y = F.relu(nrm(_Fp8ZeroConv.apply(torch.cat([y, x1], 1), P["up1_conv.0.weight"], bias("up1_conv.0.bias"))))
+    else:
+        y = F.relu(nrm(F.conv2d(torch.cat([y, x1], 1), P["up1_conv.0.weight"],
+                                bias("up1_conv.0.bias"), padding=1)))
     rec("u1", y)
     if no_antialias_up:
         y = F.conv_transpose2d(y, P["up2_up.weight"], bias("up2_up.bias"), stride=2,

@@ -3,15 +3,17 @@
 Quantisation (csrc/fp8.hip) is held bit-exact to torch's float8_e4m3fn
 conversion of clamp(x * q, +-448) (round to nearest even), its amax and the
 power-of-two scale rule exact.  The fp8 convolution (conv_pp's F8 instance,
-mfma_scale_f32_16x16x128_f8f6f4) is compared, like the bf16 kernels in
+mfma_scale_f32_32x32x64_f8f6f4) is compared, like the bf16 kernels in
 test_gpu_bf16_parity.py, with an fp64 reference computed on the SAME quantised
 operands (the e4m3 values times their dequantisation multipliers):
 
     |got - ref64| <= 2^-8 * |ref64| + 2e-5 * absref
 
 (bf16 output rounding + fp32 accumulation order), for the forward (plain,
-fused-IN-statistics, accumulate) and the resblock backward-data (fp8 interior +
-the bf16 reflect ring of the same dY).
+fused-IN-statistics, accumulate), the resblock backward-data (fp8 interior +
+the bf16 reflect ring of the same dY) and the zero-padded backward-data of down2 /
+up1_conv.  The resamplers that produce down2's / up1_conv's operands write the
+same fp8 bytes and amax as irgan_fp8_quant of the bf16 tensor they store.
 """
 import pytest
 import torch
@@ -107,6 +109,72 @@ def test_in_passes_emit_fp8_copy(ops):
     ops.in_backward(Fe(dy), Fe(z), ops.ACT_RELU, mr, work, red, Fe(dx2))
     assert torch.equal(dx, dx2)
     same(dx, y8, amax)
+
+
+def test_resamplers_emit_fp8_copy(ops):
+    """irgan_sep_resample_fp8: the Downsample of act(IN(z)) (down1 -> x1, into a channel slice
+    of the concat) and the UpsampleAA of h (into the other slice) store the same bf16 as
+    without the fp8 side output, and write the fp8 bytes / amax irgan_fp8_quant makes from it."""
+    torch.manual_seed(6)
+    Fe = ops.Feat
+    N, H, C1, C2 = 2, 20, 128, 256
+    z = torch.randn(N, 2 * H, 2 * H, C1).bfloat16().to(DEV)
+    mr = torch.empty(N * C1 * 2, device=DEV)
+    work = torch.empty(ops.IN_PARTS * N * C1, dtype=torch.float64, device=DEV)
+    ops.in_stats(Fe(z), work, mr)
+    h = torch.randn(N, H // 2, H // 2, C2).bfloat16().to(DEV)
+    qt = torch.tensor([32.0], device=DEV)
+    for kind in ("down_in", "up"):
+        cat = torch.zeros(N, H, H, C2 + C1, dtype=torch.bfloat16, device=DEV)
+        cat8 = torch.zeros(N, H, H, C2 + C1, dtype=torch.float8_e4m3fn, device=DEV)
+        ref = torch.zeros_like(cat)
+        amax = ops.amax_slots(1, DEV)
+        off, c = (C2, C1) if kind == "down_in" else (0, C2)
+        q8 = (Fe(cat8, off, c), ops.Pi(qt, 0), ops.amax_ptr(amax, 0))
+        if kind == "down_in":
+            assert ops.blur_down_in(Fe(z), mr, ops.ACT_RELU, Fe(cat, off, c), q8=q8)
+            assert ops.blur_down_in(Fe(z), mr, ops.ACT_RELU, Fe(ref, off, c))
+        else:
+            ops.upsample(Fe(h), Fe(cat, off, c), q8=q8)
+            ops.upsample(Fe(h), Fe(ref, off, c))
+        assert torch.equal(cat.view(torch.int16), ref.view(torch.int16)), kind
+        want8 = torch.zeros_like(cat8)
+        ra = ops.amax_slots(1, DEV)
+        ops.fp8_quant(Fe(ref, off, c), Fe(want8, off, c), ops.Pi(qt, 0), ops.amax_ptr(ra, 0))
+        assert torch.equal(cat8.view(torch.uint8), want8.view(torch.uint8)), kind
+        assert amax.max().item() == ra.max().item() > 0, kind
+
+
+@pytest.mark.parametrize("cin,cout,H,acc", [(384, 128, 24, False), (128, 256, 20, True)])
+def test_fp8_zero_pad_dgrad_tight(ops, cin, cout, H, acc):
+    """dx of a zero-padded 3x3 conv (up1_conv 384 -> 128, down2 128 -> 256 accumulating into
+    the concat's x1 slice) on e4m3 dY x the e4m3 flipped weights, against fp64 on the same
+    quantised operands."""
+    torch.manual_seed(7)
+    N = 2
+    spec = ops.ConvSpec(cin, cout, 3, 1, 1, 0)
+    w = q(torch.randn(cout, cin, 3, 3) * (1.0 / (cin * 9) ** 0.5))
+    pc, fw = _weights(ops, spec, w, torch.zeros(cout))
+    qd = fw.q[1].item()
+    gy = q(torch.randn(N, cout, H, H) * 1e-2)
+    qy = 2.0 ** 10
+    gyd = nhwc(gy)
+    gy8 = torch.empty(N, H, H, cout, dtype=torch.float8_e4m3fn, device=DEV)
+    ops.fp8_quant(ops.Feat(gyd), ops.Feat(gy8), ops.Pi(torch.tensor([qy], device=DEV), 0))
+    gyq = gy8.cpu().float().double().permute(0, 3, 1, 2) / qy
+    wq8 = (e4m3(w.permute(0, 2, 3, 1).float() * qd).float().double() / qd).permute(0, 3, 1, 2)
+
+    def dgrad(g, wt):
+        return torch.nn.grad.conv2d_input((N, cin, H, H), wt, g, padding=1)
+    want, aref = dgrad(gyq, wq8), dgrad(gyq.abs(), wq8.abs())
+    old = q(torch.randn(N, cin, H, H) * 1e-2) if acc else torch.zeros(N, cin, H, H)
+    dxb = torch.zeros(N, H, H, cin + 64, dtype=torch.bfloat16, device=DEV)   # a channel slice, as dcat1
+    dxb[..., 64:] = nhwc(old)
+    dqy = torch.tensor([1.0 / qy], device=DEV)
+    ops.conv_dgrad_fp8(pc, fw.dst[1], ops.Pi(fw.dq, 1), ops.Feat(gy8), ops.Pi(dqy, 0), ops.Feat(gyd),
+                       ops.Feat(dxb, 64, cin), accumulate=acc)
+    check(nchw64(dxb[..., 64:]), want + old.double(), aref + old.double().abs(), R_BF16, f"fp8 zero-pad dgrad")
+    assert not dxb[..., :64].any()
 
 
 def _weights(ops, spec, w, b):
@@ -224,7 +292,8 @@ def test_fp8_resblock_dgrad_tight(ops, H):
 
 
 @pytest.mark.parametrize("N,H,W,cin,cout,mode", [(2, 64, 64, 256, 256, 1), (1, 8, 128, 128, 256, 1),
-                                                 (3, 64, 64, 64, 128, 0), (1, 4, 256, 64, 128, 1)])
+                                                 (3, 64, 64, 64, 128, 0), (1, 4, 256, 64, 128, 1),
+                                                 (1, 6, 128, 384, 128, 0)])
 def test_fp8_wgrad_tight(ops, N, H, W, cin, cout, mode):
     """irgan_conv_wgrad_fp8 (the ResnetBlock weight gradient on e4m3 operands, config 5):
     against fp64 on the SAME e4m3 values times their dequantisation factors -- products of

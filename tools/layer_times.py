@@ -3,7 +3,7 @@ tagged conv / InstanceNorm launch on its stream, 3 steps after 3 warm-ups.  Conv
 the shape, so each line also gives TF/s against the 2.5 PF/s dense bf16 peak.  Event records
 add ~5-10 us bubbles per launch, so use this for attribution, not for the step time.
 
-    python tools/layer_times.py [--batch 16] [--size 256]
+    python tools/layer_times.py [--batch 16] [--size 256] [--dtype bf16|fp8]
 """
 import argparse
 import importlib
@@ -22,9 +22,10 @@ def main():
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
     a = ap.parse_args()
     cfg = irc.Config()
-    cfg.device, cfg.compute_dtype, cfg.batch_size, cfg.img_size = "cuda:0", "bf16", a.batch, a.size
+    cfg.device, cfg.compute_dtype, cfg.batch_size, cfg.img_size = "cuda:0", a.dtype, a.batch, a.size
     tr = irc.GANTrainer(cfg)
     tr.netG.store.load(irc.seeded_state(irc.g_param_shapes(), 0), strict=True)
     tr.netD.store.load(irc.seeded_state(irc.d_param_shapes(), 1), strict=True)
@@ -54,7 +55,8 @@ def main():
             if kind.startswith("dgrad"):   # tag carries dx size; the conv's output is the dY size
                 ho, wo = (h + s - 1) // s, (w + s - 1) // s
             flop = 2.0 * b * ho * wo * co * ci * k * k
-            tf = f"{flop / (ms * 1e-3) / 1e12:7.0f} TF/s ({flop / (ms * 1e-3) / 2.5e15:.2f})"
+            peak = 5e15 if kind.endswith("8") else 2.5e15   # fp8 tags: the dense e4m3 peak
+            tf = f"{flop / (ms * 1e-3) / 1e12:7.0f} TF/s ({flop / (ms * 1e-3) / peak:.2f})"
         rows.append((per_step * ms * 1e3, per_step, ms * 1e3, tag, tf))
     rows.sort(reverse=True)
     tot = sum(r[0] for r in rows)
