@@ -1212,6 +1212,15 @@ class GANStep:
                 ops.axpby(Feat(rgb_h), 1.0, Feat(din.t[:B], cin, cout))
                 ops.affine(Feat(rgb_h), self.vgg.scale, self.vgg.shift, vin.batch(B, B))
                 self.vgg.forward(vin, part=(B, B))
+                # the D step's real half (ir:1641-1643, 1647: netD(real) and its hinge term)
+                # needs nothing from G either: forward + weight gradient here, beside the G
+                # forward, so only the fake half stays between the G forward and the join
+                # (per-image InstanceNorm: the halves are independent; dW sums both)
+                self.D.zero_grad()
+                pr = self.dis.forward(din.batch(0, B), tag="dr")
+                dpr = b.get("dpred_r", tuple(pr.shape), torch.float32)
+                ops.hinge(pr, pr.numel(), 2, 1.0, dpr, L[0:1])
+                self.dis.backward(dpr, want_wgrad=True, want_dinput=False, tag="dr")
             if vgg_side:
                 _mark(ph, "vgg_real", self.side)
                 ev = torch.cuda.Event()
@@ -1228,7 +1237,7 @@ class GANStep:
         self.gen.training = True
         fake_d = self.gen.forward(ir, bufs=self.dbufs) if self.gen.use_dropout else None
         fake = self.gen.forward(ir)
-        # ---- D step on [real; fake] as one 2B batch (ir:1636-1651), on the side stream
+        # ---- D step (ir:1636-1651): the fake half, D Adam and the GAN-term pass on the side stream
         dfake = b.get("dfake", (B, H, W, cout), torch.float32)
 
         def g_terms():
@@ -1265,12 +1274,12 @@ class GANStep:
             if ev_fwd is not None:
                 self.side.wait_event(ev_fwd)
                 _mark(ph, "d0", self.side)
-            self.D.zero_grad()
+            # the fake half (ir:1639-1640, 1644-1647); the real half ran beside the G forward
             ops.axpby(Feat(fake if fake_d is None else fake_d), 1.0, Feat(din.t[B:], cin, cout))
-            pred = self.dis.forward(din, tag="d")
+            pred = self.dis.forward(din.batch(B, B), tag="df")
             dpred = b.get("dpred", tuple(pred.shape), torch.float32)
-            ops.hinge(pred, pred[:B].numel(), 0, 1.0, dpred, L[0:1])
-            self.dis.backward(dpred, want_wgrad=True, want_dinput=False, tag="d")
+            ops.hinge(pred, pred.numel(), 3, 1.0, dpred, L[0:1])
+            self.dis.backward(dpred, want_wgrad=True, want_dinput=False, tag="df")
             self.d_reduce.start()
             # D Adam, then the G-step GAN term through the updated D (ir:1651, 1659-1662),
             # still on the side stream: the main stream meanwhile runs the G-step terms
