@@ -250,12 +250,12 @@ def test_losses(ops):
     assert abs(loss[3].item() - ld.item()) < 1e-6
     assert relerr(gp.cpu(), pr.grad) < 1e-6
     # the D step's halves apart (modes 2 / 3, GANStep: real half beside the G forward): the
-    # same gradient bits and loss as mode 0 on [real; fake]
+    # same gradient bits as mode 0 on [real; fake], the loss to fp32 summation order
     gr, gf = torch.empty_like(pd[:50]), torch.empty_like(pd[50:])
     ops.hinge(pd[:50].contiguous(), 50, 2, 1.0, gr, loss[4:5])
     ops.hinge(pd[50:].contiguous(), 50, 3, 1.0, gf, loss[4:5])
     assert torch.equal(torch.cat([gr, gf]), gp)
-    assert abs(loss[4].item() - loss[3].item()) < 1e-12
+    assert abs(loss[4].item() - ld.item()) < 1e-6
 
 
 @pytest.mark.parametrize("count", [1 << 20, 1001])

@@ -85,11 +85,14 @@ def test_step_fp32_matches_reference_golden(variant):
         assert abs(d[k] - ref) <= 1e-4 * max(1.0, abs(ref)), (k, d[k], ref)
     fake = tr.netG.engine.bufs.d["fake"].permute(0, 3, 1, 2).cpu().numpy()
     assert np.max(np.abs(fake - fx["fake"])) <= 1e-4
-    pred = tr.netD.engine.bufs.d["de4"].permute(0, 3, 1, 2).cpu().numpy()
-    B = fx["ir"].shape[0]
+    # the D step's logits: real half (tag "dr", beside the G forward), fake half ("df")
+    De = tr.netD.engine
+    last = len(De.packs) - 1
+    pred_r = De.bufs.d[f"dre{last}"].permute(0, 3, 1, 2).cpu().numpy()
+    pred_f = De.bufs.d[f"dfe{last}"].permute(0, 3, 1, 2).cpu().numpy()
     scale = max(np.max(np.abs(fx["pred_real"])), 1e-6)
-    assert np.max(np.abs(pred[:B] - fx["pred_real"])) <= 1e-4 * max(1, scale)
-    assert np.max(np.abs(pred[B:] - fx["pred_fake"])) <= 1e-4 * max(1, scale)
+    assert np.max(np.abs(pred_r - fx["pred_real"])) <= 1e-4 * max(1, scale)
+    assert np.max(np.abs(pred_f - fx["pred_fake"])) <= 1e-4 * max(1, scale)
     pre_in = set(O.pre_in_bias_keys(list(tr.netG.store.shapes) + list(tr.netD.store.shapes)))
     digest_check(tr.netD.store, fx, "gD", pre_in, 5e-3, l2=True)
     digest_check(tr.netG.store, fx, "gG", pre_in, 5e-3, l2=True)
