@@ -1170,7 +1170,7 @@ class GANStep:
         # VGG, TV, SSIM); IRGAN_NO_D_OVERLAP=1 keeps everything on one stream
         self.side = None
         if G.device.type == "cuda" and not os.environ.get("IRGAN_NO_D_OVERLAP"):
-            self.side = torch.cuda.Stream(device=G.device, priority=-1 if os.environ.get("IRGAN_SIDE_PRIO") else 0)
+            self.side = torch.cuda.Stream(device=G.device)
         self.G.dev_adam = self.D.dev_adam = G.device.type == "cuda"
         self.vgg.pack()
         self.gen.pack()
@@ -1198,7 +1198,6 @@ class GANStep:
         dpad = max(8, cin + cout)
         din = Feat(b.zeros("din2", (2 * B, H, W, dpad), T), 0, self.dis.packs[0].cin_eff)
         vgg_side = main is not None and not os.environ.get("IRGAN_NO_VGG_OVERLAP")
-        d_split = not os.environ.get("IRGAN_NO_D_SPLIT")
         ev_in = None
         if vgg_side:
             ev_in = torch.cuda.Event()
@@ -1213,20 +1212,6 @@ class GANStep:
                 ops.axpby(Feat(rgb_h), 1.0, Feat(din.t[:B], cin, cout))
                 ops.affine(Feat(rgb_h), self.vgg.scale, self.vgg.shift, vin.batch(B, B))
                 self.vgg.forward(vin, part=(B, B))
-                if not d_split:
-                    return
-                # the D step's real half (ir:1641-1643, 1647: netD(real) and its hinge term)
-                # needs nothing from G either: forward + weight gradient here, beside the G
-                # forward, so only the fake half stays between the G forward and the join
-                # (per-image InstanceNorm: the halves are independent; dW sums both)
-                self.D.zero_grad()
-                pr = self.dis.forward(din.batch(0, B), tag="dr")
-                dpr = b.get("dpred_r", tuple(pr.shape), torch.float32)
-                ops.hinge(pr, pr.numel(), 2, 1.0, dpr, L[0:1])
-                self.dis.backward(dpr, want_wgrad=True, want_dinput=False, tag="dr")
-
-        def vgg_real_ev():
-            vgg_real()
             if vgg_side:
                 _mark(ph, "vgg_real", self.side)
                 ev = torch.cuda.Event()
@@ -1236,14 +1221,14 @@ class GANStep:
 
         # enqueued before the G forward's launches (after them measured neutral,
         # profiles/r03_vgg_after_gfwd_ab.txt)
-        ev_vgg = vgg_real_ev()
+        ev_vgg = vgg_real()
         # ---- G forward once: ir:1638 and ir:1657 compute the same image -- unless G has
         # dropout, whose two calls draw two masks: then the D step gets its own forward
         # (ir:1638-1639, under no_grad: its activations are never read back)
         self.gen.training = True
         fake_d = self.gen.forward(ir, bufs=self.dbufs) if self.gen.use_dropout else None
         fake = self.gen.forward(ir)
-        # ---- D step (ir:1636-1651): the fake half, D Adam and the GAN-term pass on the side stream
+        # ---- D step on [real; fake] as one 2B batch (ir:1636-1651), on the side stream
         dfake = b.get("dfake", (B, H, W, cout), torch.float32)
 
         def g_terms():
@@ -1280,19 +1265,14 @@ class GANStep:
             if ev_fwd is not None:
                 self.side.wait_event(ev_fwd)
                 _mark(ph, "d0", self.side)
-            # the fake half (ir:1639-1640, 1644-1647); the real half ran beside the G forward
+            # [real; fake] as one 2B batch.  (The real half apart, beside the G forward, measured
+            # -0.8 %: the G forward slowed by what it took off the join, profiles/r05_ab1_dsplit.txt)
+            self.D.zero_grad()
             ops.axpby(Feat(fake if fake_d is None else fake_d), 1.0, Feat(din.t[B:], cin, cout))
-            if d_split:
-                pred = self.dis.forward(din.batch(B, B), tag="df")
-                dpred = b.get("dpred", tuple(pred.shape), torch.float32)
-                ops.hinge(pred, pred.numel(), 3, 1.0, dpred, L[0:1])
-                self.dis.backward(dpred, want_wgrad=True, want_dinput=False, tag="df")
-            else:   # [real; fake] as one 2B batch
-                self.D.zero_grad()
-                pred = self.dis.forward(din, tag="d")
-                dpred = b.get("dpred2", tuple(pred.shape), torch.float32)
-                ops.hinge(pred, pred[:B].numel(), 0, 1.0, dpred, L[0:1])
-                self.dis.backward(dpred, want_wgrad=True, want_dinput=False, tag="d")
+            pred = self.dis.forward(din, tag="d")
+            dpred = b.get("dpred", tuple(pred.shape), torch.float32)
+            ops.hinge(pred, pred[:B].numel(), 0, 1.0, dpred, L[0:1])
+            self.dis.backward(dpred, want_wgrad=True, want_dinput=False, tag="d")
             self.d_reduce.start()
             # D Adam, then the G-step GAN term through the updated D (ir:1651, 1659-1662),
             # still on the side stream: the main stream meanwhile runs the G-step terms

@@ -85,11 +85,10 @@ def test_step_fp32_matches_reference_golden(variant):
         assert abs(d[k] - ref) <= 1e-4 * max(1.0, abs(ref)), (k, d[k], ref)
     fake = tr.netG.engine.bufs.d["fake"].permute(0, 3, 1, 2).cpu().numpy()
     assert np.max(np.abs(fake - fx["fake"])) <= 1e-4
-    # the D step's logits: real half (tag "dr", beside the G forward), fake half ("df")
-    De = tr.netD.engine
-    last = len(De.packs) - 1
-    pred_r = De.bufs.d[f"dre{last}"].permute(0, 3, 1, 2).cpu().numpy()
-    pred_f = De.bufs.d[f"dfe{last}"].permute(0, 3, 1, 2).cpu().numpy()
+    De = tr.netD.engine   # the D step's logits on [real; fake] (tag "d")
+    pred = De.bufs.d[f"de{len(De.packs) - 1}"].permute(0, 3, 1, 2).cpu().numpy()
+    B = fx["ir"].shape[0]
+    pred_r, pred_f = pred[:B], pred[B:]
     scale = max(np.max(np.abs(fx["pred_real"])), 1e-6)
     assert np.max(np.abs(pred_r - fx["pred_real"])) <= 1e-4 * max(1, scale)
     assert np.max(np.abs(pred_f - fx["pred_fake"])) <= 1e-4 * max(1, scale)
