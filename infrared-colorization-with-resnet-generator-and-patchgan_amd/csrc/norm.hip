@@ -295,8 +295,6 @@ IRGAN_HD void block_partials8(float* a0, float* a1, const Lay& L, bool on, int c
 #ifndef ROWS8_DB
 #define ROWS8_DB 0
 #endif
-constexpr int R8U_RED = ROWS8_DB ? 2 : 4, R8U_STATS = ROWS8_DB ? 4 : 8, R8U_APPLY = ROWS8_DB ? 4 : 8,
-              R8U_APPLY_RES = ROWS8_DB ? 2 : 4;
 template <int MODE, int U, bool F8 = false>
 __global__ __launch_bounds__(TPB) void rows8_kernel(const bf16_t* x, int ldx, int xoff, const bf16_t* dy, int lddy,
                                                     int dyoff, const bf16_t* dy2, int lddy2, int dy2off, int act,
@@ -434,6 +432,38 @@ __global__ __launch_bounds__(TPB) void rows8_kernel(const bf16_t* x, int ldx, in
     if constexpr (F8) fp8_block_amax(amx, q8.amax, blockIdx.y * gridDim.x + blockIdx.x);
 }
 
+// sweep overrides (tools/norm_sweep.sh) per pass key (0 stats, 1 backward reduce, 2 backward
+// apply, 4 forward apply, 5 forward apply + residual / fp8): IRGAN_IN_RPT_M<key> rows per
+// thread, IRGAN_IN_U_M<key> rows per load batch
+int pass_env(const char* what, int key, int dflt) {
+    char k[32];
+    snprintf(k, sizeof(k), "IRGAN_IN_%s_M%d", what, key);
+    const char* v = getenv(k);
+    return v && atoi(v) > 0 ? atoi(v) : dflt;
+}
+int pass_rpt(int key, int dflt) {
+    static int cache[6] = {0, 0, 0, 0, 0, 0};
+    if (!cache[key]) cache[key] = pass_env("RPT", key, dflt);
+    return cache[key];
+}
+int pass_u(int key) {
+    static int cache[6] = {-1, -1, -1, -1, -1, -1};
+    if (cache[key] < 0) cache[key] = pass_env("U", key, 0);
+    return cache[key];
+}
+
+// rows8_kernel with U = the thread's rows (one batch of loads, all in flight), from the
+// instances 2 / 4 / 8 / 16
+template <int MODE, bool F8 = false, typename... A>
+void rows8_go(int key, int rows_per_thread, dim3 g, hipStream_t st, A... args) {
+    const int force = pass_u(key);
+    const int u = force > 0 ? force : rows_per_thread;
+    if (u <= 2) rows8_kernel<MODE, 2, F8><<<g, TPB, 0, st>>>(args...);
+    else if (u <= 4) rows8_kernel<MODE, 4, F8><<<g, TPB, 0, st>>>(args...);
+    else if (u <= 8) rows8_kernel<MODE, 8, F8><<<g, TPB, 0, st>>>(args...);
+    else rows8_kernel<MODE, 16, F8><<<g, TPB, 0, st>>>(args...);
+}
+
 // fp64 sum of the nb block partials of each (n, c).  Block (FC channels x FS
 // partial lanes) per (image, channel group): a lane adds partials sub, sub + FS,
 // ... (at most nb / FS dependent loads: the launch is latency-bound, so the
@@ -558,9 +588,12 @@ int launch_rows(Slice X, Slice DY, Slice DY2, int act, const float* mr, const fl
                 int dxoff, int N, int HW, int C, float2* part, float* db, bool vec, hipStream_t st, int* nb_out,
                 const Q8* q8 = nullptr) {
     const int VW = vec ? V : 1;
-    int nb = blocks_per_image(HW, N, rp_of(C, VW), MODE == 2 ? 8 : 16);
+    const int rpt = pass_rpt(MODE, MODE == 2 ? 8 : 16);
+    const int RP = rp_of(C, VW);
+    int nb = blocks_per_image(HW, N, RP, rpt);
     const int rows = irgan_cdiv(HW, nb);
     nb = irgan_cdiv(HW, rows);
+    const int rpth = irgan_cdiv(rows, RP);
     dim3 g(nb, N);
     static const bool fast = !getenv("IRGAN_NO_ROWS8");
     const bool bf = X.dt == IRGAN_BF16 && (MODE == 0 || (DY.dt == IRGAN_BF16 && (!DY2.p || DY2.dt == IRGAN_BF16))) &&
@@ -569,14 +602,14 @@ int launch_rows(Slice X, Slice DY, Slice DY2, int act, const float* mr, const fl
     if ((fast || q8) && vec && bf && MODE <= 2) {
         const bf16_t *xp = (const bf16_t*)X.p, *gp = (const bf16_t*)DY.p, *hp = (const bf16_t*)DY2.p;
         if (MODE == 2 && q8)
-            rows8_kernel<2, R8U_RED, true><<<g, TPB, 0, st>>>(xp, X.ld, X.off, gp, DY.ld, DY.off, hp, DY2.ld, DY2.off, act, mr,
-                                                        red, (bf16_t*)dx, lddx, dxoff, HW, C, rows, part, *q8);
+            rows8_go<2, true>(2, rpth, g, st, xp, X.ld, X.off, gp, DY.ld, DY.off, hp, DY2.ld, DY2.off, act, mr, red,
+                              (bf16_t*)dx, lddx, dxoff, HW, C, rows, part, *q8);
         else if (MODE == 0)
-            rows8_kernel<0, R8U_STATS><<<g, TPB, 0, st>>>(xp, X.ld, X.off, nullptr, 0, 0, nullptr, 0, 0, act, mr, red, nullptr,
-                                                  0, 0, HW, C, rows, part);
+            rows8_go<0>(0, rpth, g, st, xp, X.ld, X.off, (const bf16_t*)nullptr, 0, 0, (const bf16_t*)nullptr, 0, 0, act, mr,
+                        red, (bf16_t*)nullptr, 0, 0, HW, C, rows, part, Q8{});
         else
-            rows8_kernel<MODE, R8U_RED><<<g, TPB, 0, st>>>(xp, X.ld, X.off, gp, DY.ld, DY.off, hp, DY2.ld, DY2.off, act, mr,
-                                                     red, (bf16_t*)dx, lddx, dxoff, HW, C, rows, part);
+            rows8_go<MODE>(MODE, rpth, g, st, xp, X.ld, X.off, gp, DY.ld, DY.off, hp, DY2.ld, DY2.off, act, mr, red,
+                           (bf16_t*)dx, lddx, dxoff, HW, C, rows, part, Q8{});
         if (nb_out) *nb_out = nb;
         return 0;
     }
@@ -620,20 +653,21 @@ bool apply_rows(const void* x, int ldx, int xoff, int N, int HW, int C, const fl
                 int ldr, int roff, void* y, int ldy, int yoff, hipStream_t st, const Q8* q8 = nullptr) {
     static const bool off = getenv("IRGAN_NO_APPLY_ROWS") != nullptr;
     if (off) return false;
-    int nb = blocks_per_image(HW, N, rp_of(C, 8), res ? 8 : 16);
+    const int key = res || q8 ? 5 : 4;  // 5: apply + residual, or with the fp8 copy
+    const int rpt = pass_rpt(key, key == 5 ? 8 : 16);
+    const int RP = rp_of(C, 8);
+    int nb = blocks_per_image(HW, N, RP, rpt);
     const int rows = irgan_cdiv(HW, nb);
     nb = irgan_cdiv(HW, rows);
+    const int rpth = irgan_cdiv(rows, RP);
     dim3 g(nb, N);
     const bf16_t *xp = (const bf16_t*)x, *rp = (const bf16_t*)res;
     if (q8)
-        rows8_kernel<4, R8U_APPLY_RES, true><<<g, TPB, 0, st>>>(xp, ldx, xoff, rp, ldr, roff, nullptr, 0, 0, act, mr, nullptr,
-                                                    (bf16_t*)y, ldy, yoff, HW, C, rows, nullptr, *q8);
-    else if (res)
-        rows8_kernel<4, R8U_APPLY_RES><<<g, TPB, 0, st>>>(xp, ldx, xoff, rp, ldr, roff, nullptr, 0, 0, act, mr, nullptr,
-                                              (bf16_t*)y, ldy, yoff, HW, C, rows, nullptr);
+        rows8_go<4, true>(key, rpth, g, st, xp, ldx, xoff, rp, ldr, roff, (const bf16_t*)nullptr, 0, 0, act, mr,
+                          (const float*)nullptr, (bf16_t*)y, ldy, yoff, HW, C, rows, (float2*)nullptr, *q8);
     else
-        rows8_kernel<4, R8U_APPLY><<<g, TPB, 0, st>>>(xp, ldx, xoff, nullptr, 0, 0, nullptr, 0, 0, act, mr, nullptr,
-                                              (bf16_t*)y, ldy, yoff, HW, C, rows, nullptr);
+        rows8_go<4>(key, rpth, g, st, xp, ldx, xoff, rp, ldr, roff, (const bf16_t*)nullptr, 0, 0, act, mr,
+                    (const float*)nullptr, (bf16_t*)y, ldy, yoff, HW, C, rows, (float2*)nullptr, Q8{});
     return true;
 }
 
