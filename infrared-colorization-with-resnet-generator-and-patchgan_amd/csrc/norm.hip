@@ -432,9 +432,13 @@ __global__ __launch_bounds__(TPB) void rows8_kernel(const bf16_t* x, int ldx, in
     if constexpr (F8) fp8_block_amax(amx, q8.amax, blockIdx.y * gridDim.x + blockIdx.x);
 }
 
-// sweep overrides (tools/norm_sweep.sh) per pass key (0 stats, 1 backward reduce, 2 backward
-// apply, 4 forward apply, 5 forward apply + residual / fp8): IRGAN_IN_RPT_M<key> rows per
-// thread, IRGAN_IN_U_M<key> rows per load batch
+// Rows per thread and rows per load batch (U) of each pass, by key: 0 stats, 1 backward
+// reduce, 2 backward apply, 4 forward apply, 5 forward apply + residual / with the fp8 copy.
+// Measured at the resblock shape, B = 16 (profiles/r05_nsw_norm_sweep.txt, tools/norm_sweep.sh
+// with IRGAN_IN_RPT_M<key> / IRGAN_IN_U_M<key>): forward apply 16.2 -> 14.4 us and backward
+// apply 17.9 -> 17.5 at 4 rows per thread in one batch; the reduce stays at 16 rows in batches
+// of 4 (one batch of 4: 20.7 us, 4x the partials), apply + residual at 8 rows in batches of 4
+constexpr int PASS_RPT[6] = {16, 16, 4, 0, 4, 8}, PASS_U[6] = {16, 4, 4, 0, 8, 4};  // U: the batch cap (larger maps: several batches)
 int pass_env(const char* what, int key, int dflt) {
     char k[32];
     snprintf(k, sizeof(k), "IRGAN_IN_%s_M%d", what, key);
@@ -447,17 +451,15 @@ int pass_rpt(int key, int dflt) {
     return cache[key];
 }
 int pass_u(int key) {
-    static int cache[6] = {-1, -1, -1, -1, -1, -1};
-    if (cache[key] < 0) cache[key] = pass_env("U", key, 0);
+    static int cache[6] = {0, 0, 0, 0, 0, 0};
+    if (!cache[key]) cache[key] = pass_env("U", key, PASS_U[key]);
     return cache[key];
 }
 
-// rows8_kernel with U = the thread's rows (one batch of loads, all in flight), from the
-// instances 2 / 4 / 8 / 16
+// rows8_kernel with U = min(the thread's rows, the pass's batch), from the instances 2 / 4 / 8 / 16
 template <int MODE, bool F8 = false, typename... A>
 void rows8_go(int key, int rows_per_thread, dim3 g, hipStream_t st, A... args) {
-    const int force = pass_u(key);
-    const int u = force > 0 ? force : rows_per_thread;
+    const int u = std::min(pass_u(key), rows_per_thread);
     if (u <= 2) rows8_kernel<MODE, 2, F8><<<g, TPB, 0, st>>>(args...);
     else if (u <= 4) rows8_kernel<MODE, 4, F8><<<g, TPB, 0, st>>>(args...);
     else if (u <= 8) rows8_kernel<MODE, 8, F8><<<g, TPB, 0, st>>>(args...);
@@ -588,7 +590,7 @@ int launch_rows(Slice X, Slice DY, Slice DY2, int act, const float* mr, const fl
                 int dxoff, int N, int HW, int C, float2* part, float* db, bool vec, hipStream_t st, int* nb_out,
                 const Q8* q8 = nullptr) {
     const int VW = vec ? V : 1;
-    const int rpt = pass_rpt(MODE, MODE == 2 ? 8 : 16);
+    const int rpt = pass_rpt(MODE, PASS_RPT[MODE]);
     const int RP = rp_of(C, VW);
     int nb = blocks_per_image(HW, N, RP, rpt);
     const int rows = irgan_cdiv(HW, nb);
@@ -654,7 +656,7 @@ bool apply_rows(const void* x, int ldx, int xoff, int N, int HW, int C, const fl
     static const bool off = getenv("IRGAN_NO_APPLY_ROWS") != nullptr;
     if (off) return false;
     const int key = res || q8 ? 5 : 4;  // 5: apply + residual, or with the fp8 copy
-    const int rpt = pass_rpt(key, key == 5 ? 8 : 16);
+    const int rpt = pass_rpt(key, PASS_RPT[key]);
     const int RP = rp_of(C, 8);
     int nb = blocks_per_image(HW, N, RP, rpt);
     const int rows = irgan_cdiv(HW, nb);
