@@ -68,10 +68,6 @@
 #define PP_EXP 0  // A/B timing experiments only (tools/build_variant.sh); 0 = the real kernel
 #endif
 // bits: 1 no MFMA, 2 no weight DMA in the loop, 4 no fragment reads, 8 no barriers in the loop, 16 no epilogue
-#ifndef PP_ACC_BATCH
-#define PP_ACC_BATCH 0  // accumulate: 1 = old values loaded for half the fragment rows at once (measured:
-                        // 11 more VGPR spills in the BN-256 instance, step -0.3 %, profiles/r05_s5_ab.txt)
-#endif
 #define PPX(b) ((PP_EXP & (b)) != 0)
 
 namespace {
@@ -432,6 +428,28 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
     }
     if (grp == 0) phase_barrier();  // match group 1's extra barrier
     __syncthreads();                // all operand reads done: LDS becomes the staging buffer
+    // bf16 accumulate (a dgrad into a tensor that holds another branch's gradient): the old
+    // tile is DMA'd straight into the staging layout (16-byte slots of RSB-byte pixel rows; the
+    // row's padding slot and pixels / channels outside the output are out-of-range loads) in
+    // one batch of ~17 loads per wave, so its latency is paid once per launch; the emit then
+    // adds each lane's 4 old channels from LDS and writes the sum back to the same slot.
+    // (Loaded in registers per fragment row the latency was exposed MI times.)
+    const bool out_f32 = d.out_dtype == IRGAN_F32;
+    const bool acc_lds = ACC && !out_f32 && d.ldy % 8 == 0 && d.yoff % 8 == 0 &&
+                         (long)d.N * d.OH * d.OW * d.ldy * 2 < (1L << 31);
+    if constexpr (ACC) {
+        if (acc_lds) {
+            constexpr int SPR = RSB / 16, SLOTS = 256 * SPR;  // slots per staged pixel row / tile
+            const i32x4 rs = make_rsrc(y, (uint32_t)((long)d.N * d.OH * d.OW * d.ldy * 2));
+            for (int k = wid; k * 64 < SLOTS; k += 8) {  // wave-uniform
+                const int e = k * 64 + lane, m = e / SPR, sl = e - m * SPR;
+                const int oy = py0 + (m >> 4), ox = px0 + (m & 15), co = n0 + sl * 8;
+                const bool ok = e < SLOTS && sl < BN / 8 && oy < d.Ho && ox < d.Wo && co + 8 <= d.Cout;
+                const long pix = ((long)img * d.OH + oy * d.omy + ooy) * d.OW + ox * d.omx + oox;
+                blds16(rs, ok ? (uint32_t)((pix * d.ldy + d.yoff + co) * 2) : IRGAN_OOB, smem + k * 1024);
+            }
+        }
+    }
 #if PPX(16)
     {
         float s = 0.f;
@@ -487,16 +505,9 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
         return ((long)img * d.OH + oy * d.omy + ooy) * d.OW + ox * d.omx + oox;
     };
     // Each lane owns (pixel, 4 consecutive channels) per fragment: mask and
-    // accumulate are applied right here on those 4 channels (8-byte loads).
+    // accumulate are applied right here on those 4 channels.
     // bf16 output: stage bf16 [256 px][256 ch] in LDS, then 16-byte row stores;
     // fp32 output: 16-byte stores straight from the registers.
-    const bool out_f32 = d.out_dtype == IRGAN_F32;
-    // bf16 accumulate (dgrad into a tensor that already holds another branch's
-    // gradient): the 4 old channels of a fragment are one 8-byte load, and a
-    // fragment row's NJ loads are all issued before the row is combined, so the
-    // read latency is paid once per row instead of once per 2-byte element.
-    // (a template flag, so the plain-store kernels keep their register allocation)
-    const bool acc_vec = ACC && !out_f32 && d.ldy % 4 == 0 && d.yoff % 4 == 0;
     // ReLU backward mask on a plain bf16 store (the VGG backward-data chain): applied in the
     // store pass on the rounded values with 16-byte coalesced mask loads issued together
     // (x * {0, 1} commutes with the bf16 rounding: bit-identical to masking before it);
@@ -505,37 +516,13 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
     const bool late_mask = mask && d.mask_act == 1 && !ACC && !out_f32 && !STATS && !rg && d.ldm % 8 == 0 &&
                            d.moff % 8 == 0 && d.ldy % 8 == 0 && d.yoff % 8 == 0;
     const bool mask_vec = mask && d.ldm % 4 == 0 && d.moff % 4 == 0;
-    // accumulate: the old values of half the fragment rows are loaded before the first of them
-    // is combined (two exposed latencies per launch instead of one per row; all rows at once
-    // would hold 64 more VGPRs next to the accumulators and spill)
-    constexpr int OB = ACC && PP_ACC_BATCH ? (MI >= 2 ? MI / 2 : 1) : 1;  // rows per old-value batch
-    uint2 olda[OB][NJ];
-    auto load_old = [&](int i0) {
-        if constexpr (ACC) {
-            if (acc_vec) {
-#pragma unroll
-                for (int ii = 0; ii < OB; ++ii) {
-                    const long pix = pix_of(m_of(i0 + ii));
-#pragma unroll
-                    for (int j = 0; j < NJ; ++j) {
-                        const int co = n0 + cl_of(i0 + ii, j);
-                        olda[ii][j] = (pix >= 0 && co + 4 <= d.Cout)
-                                          ? *(const uint2*)((const bf16_t*)y + pix * d.ldy + d.yoff + co)
-                                          : make_uint2(0u, 0u);
-                    }
-                }
-            }
-        }
-    };
     auto emit = [&](auto actc) {
         constexpr int A = decltype(actc)::value;
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
-            if (ACC && i % OB == 0) load_old(i);
             const int m = m_of(i);
             const long pix = pix_of(m);
             uint2 mk[NJ];
-            uint2(&old)[NJ] = olda[ACC ? i % OB : 0];
             if (mask_vec && !late_mask && pix >= 0) {
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) {
@@ -586,11 +573,12 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
                         for (int r = 0; r < 4 && co + r < d.Cout; ++r) yp[r] = ACC ? yp[r] + v[r] : v[r];
                     }
                 } else {
-                    if (acc_vec && pix >= 0 && full) {
-                        v[0] += bf2f((bf16_t)(old[j].x & 0xffffu));
-                        v[1] += bf2f((bf16_t)(old[j].x >> 16));
-                        v[2] += bf2f((bf16_t)(old[j].y & 0xffffu));
-                        v[3] += bf2f((bf16_t)(old[j].y >> 16));
+                    if (acc_lds && pix >= 0 && full) {
+                        const uint2 old = *(const uint2*)(smem + m * RSB + cl * 2);
+                        v[0] += bf2f((bf16_t)(old.x & 0xffffu));
+                        v[1] += bf2f((bf16_t)(old.x >> 16));
+                        v[2] += bf2f((bf16_t)(old.y & 0xffffu));
+                        v[3] += bf2f((bf16_t)(old.y >> 16));
                     } else if (ACC && pix >= 0) {
                         const bf16_t* yp = (const bf16_t*)y + pix * d.ldy + d.yoff + co;
 #pragma unroll
@@ -632,6 +620,10 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
             rm[k] = (pr >= 0 && y < H && x < W && n0 + ch * 8 < d.Cout) ? pr * 16 + pc : -1;
             if (rm[k] >= 0) ring_line_sum(d, rg, img, y, x, n0 + ch * 8, rv[k]);
         }
+    }
+    if (acc_lds) {  // the old tile landed (every wave's DMA) before any lane reads a slot
+        wait_vmcnt<0>();
+        __syncthreads();
     }
     switch (d.act) {
         case IRGAN_ACT_RELU: emit(std::integral_constant<int, IRGAN_ACT_RELU>()); break;
