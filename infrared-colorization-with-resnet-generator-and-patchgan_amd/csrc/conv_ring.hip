@@ -299,6 +299,10 @@ IRGAN_HD int rv_tap(int line, int k) {  // dgrad-conv tap ty*3 + tx of along-lin
 // (the K loop halved: one wave per SIMD ran a 3 x 8-step chain with each step's LDS reads
 // exposed), then half 1's accumulators are added onto half 0's through LDS in a fixed order
 constexpr int RV_NT = 512, RV_CSH = RV_CIN / 64;  // threads; channel steps per half (max)
+#ifndef RING_EXP
+#define RING_EXP 0  // ablation builds only (tools/build_variant.sh): 1 no weight loads, 2 no MFMA loop,
+                    // 4 no line loads, 8 no stores
+#endif
 __global__ __launch_bounds__(RV_NT, 1) void ring_line_gemm_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ dy,
                                                                  const bf16_t* __restrict__ w, float* __restrict__ gbuf,
                                                                  int ipb) {
@@ -328,8 +332,9 @@ __global__ __launch_bounds__(RV_NT, 1) void ring_line_gemm_kernel(const irgan_co
         for (int k = 0; k < 3; ++k)
 #pragma unroll
             for (int c = 0; c < RV_CSH; ++c)
-                af[k][c] = cs0 + c < cs1 ? *(const uint4*)(wr + rv_tap(line, k) * d.Cin + (cs0 + c) * 32)
-                                         : make_uint4(0u, 0u, 0u, 0u);
+                af[k][c] = cs0 + c < cs1 && !(RING_EXP & 1)
+                               ? *(const uint4*)(wr + rv_tap(line, k) * d.Cin + (cs0 + c) * 32)
+                               : make_uint4(0u, 0u, 0u, 0u);
     }
     // the dy line of image n: position p = dy coordinate + 2 along the line
     constexpr int LPER = (RV_ROWS * 32 + RV_NT - 1) / RV_NT;
@@ -338,7 +343,7 @@ __global__ __launch_bounds__(RV_NT, 1) void ring_line_gemm_kernel(const irgan_co
         for (int u = 0; u < LPER; ++u) {
             const int e = u * RV_NT + tid, q = (e >> 5) - 2, c = e & 31;
             v[u] = make_uint4(0u, 0u, 0u, 0u);
-            if (e < RV_ROWS * 32 && q >= 0 && q < L && c < c32) {
+            if (!(RING_EXP & 4) && e < RV_ROWS * 32 && q >= 0 && q < L && c < c32) {
                 const int y = line == 0 ? 0 : (line == 1 ? H - 1 : q);
                 const int x = line < 2 ? q : (line == 2 ? 0 : W - 1);
                 v[u] = *(const uint4*)(dy + ((long)(n * d.H + y) * d.W + x) * d.ldx + d.xoff + c * 8);
@@ -363,7 +368,7 @@ __global__ __launch_bounds__(RV_NT, 1) void ring_line_gemm_kernel(const irgan_co
 #pragma unroll
         for (int f = 0; f < 5; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
+        for (int k = 0; k < 3 * !(RING_EXP & 2); ++k) {
 #pragma unroll
             for (int c = 0; c < RV_CSH; ++c) {
                 const int cs = cs0 + c;
@@ -392,7 +397,7 @@ __global__ __launch_bounds__(RV_NT, 1) void ring_line_gemm_kernel(const irgan_co
             for (int f = 0; f < 5; ++f) {
                 const f32x4 o = sP[(wv * 5 + f) * 64 + lane];
                 const int pos = 16 * f + l16 + ub + 1;
-                if (pos < RV_ROWS)
+                if (pos < RV_ROWS && (!(RING_EXP & 8) || acc[f][0] == 1234.5f))
                     *(float4*)(gl + (long)pos * d.Cout + co) =
                         make_float4(acc[f][0] + o[0], acc[f][1] + o[1], acc[f][2] + o[2], acc[f][3] + o[3]);
             }
