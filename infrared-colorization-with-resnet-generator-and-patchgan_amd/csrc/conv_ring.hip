@@ -303,6 +303,10 @@ constexpr int RV_NT = 512, RV_CSH = RV_CIN / 64;  // threads; channel steps per 
 #define RING_EXP 0  // ablation builds only (tools/build_variant.sh): 1 no weight loads, 2 no MFMA loop,
                     // 4 no line loads, 8 no stores
 #endif
+// FULL (Cin == RV_CIN, the ResnetBlock): every half has exactly RV_CSH channel steps, so the K
+// loop is static and its LDS reads are scheduled ahead of the MFMAs (the dynamic trip count
+// exposed each step's reads: 3.8 of the launch's 10.3 us at B = 16, gpurun_out/r05_ringab)
+template <bool FULL>
 __global__ __launch_bounds__(RV_NT, 1) void ring_line_gemm_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ dy,
                                                                  const bf16_t* __restrict__ w, float* __restrict__ gbuf,
                                                                  int ipb) {
@@ -319,7 +323,7 @@ __global__ __launch_bounds__(RV_NT, 1) void ring_line_gemm_kernel(const irgan_co
     const int g = lane >> 4, l16 = lane & 15;
     const int Kw = (9 * d.Cin + 63) / 64 * 64;
     const int c32 = d.Cin / 8;  // 16-byte chunks per row
-    const int ncs = d.Cin / 32;
+    const int ncs = FULL ? RV_CIN / 32 : d.Cin / 32;
     const int cs0 = kh * ((ncs + 1) / 2), cs1 = kh ? ncs : (ncs + 1) / 2;  // this half's channel steps
 
     // this wave's weight fragments straight into registers (16 channels x 32 dy channels per
@@ -332,7 +336,7 @@ __global__ __launch_bounds__(RV_NT, 1) void ring_line_gemm_kernel(const irgan_co
         for (int k = 0; k < 3; ++k)
 #pragma unroll
             for (int c = 0; c < RV_CSH; ++c)
-                af[k][c] = cs0 + c < cs1 && !(RING_EXP & 1)
+                af[k][c] = (FULL || cs0 + c < cs1) && !(RING_EXP & 1)
                                ? *(const uint4*)(wr + rv_tap(line, k) * d.Cin + (cs0 + c) * 32)
                                : make_uint4(0u, 0u, 0u, 0u);
     }
@@ -372,7 +376,7 @@ __global__ __launch_bounds__(RV_NT, 1) void ring_line_gemm_kernel(const irgan_co
 #pragma unroll
             for (int c = 0; c < RV_CSH; ++c) {
                 const int cs = cs0 + c;
-                if (cs >= cs1) break;
+                if (!FULL && cs >= cs1) break;
                 const uint4 a = af[k][c];
                 uint4 b[5];
 #pragma unroll
@@ -484,8 +488,19 @@ bool ring_line_check(const irgan_conv_desc* d, int p, long ws_floats) { return r
 void ring_line_gemm_launch(const irgan_conv_desc* d, const void* dy, const void* w, float* ws, hipStream_t st) {
     // one image per workgroup row (2 / 4 images per workgroup measured slower: the launch
     // is latency-bound, profiles/r03_ring_gemm_wreg_ab.txt)
-    ring_line_gemm_kernel<<<dim3(4 * (d->Cout / 64), d->N), RV_NT, 0, st>>>(*d, (const bf16_t*)dy,
-                                                                              (const bf16_t*)w, ws, 1);
+    // one image per workgroup row while the grid fits the CUs (2 / 4 images per workgroup
+    // measured slower at B = 16: the launch is latency-bound, profiles/r03_ring_gemm_wreg_ab.txt);
+    // beyond that (B = 32: two rounds of one block per CU) the images of a row share its weight
+    // registers, the next image's line loaded under the current GEMM
+    const int per_img = 4 * (d->Cout / 64);
+    const int rows_fit = std::max(1, irgan_cu_count() / per_img);
+    const int ipb = irgan_cdiv(d->N, rows_fit), groups = irgan_cdiv(d->N, ipb);
+    if (d->Cin == RV_CIN)
+        ring_line_gemm_kernel<true><<<dim3(per_img, groups), RV_NT, 0, st>>>(*d, (const bf16_t*)dy, (const bf16_t*)w,
+                                                                             ws, ipb);
+    else
+        ring_line_gemm_kernel<false><<<dim3(per_img, groups), RV_NT, 0, st>>>(*d, (const bf16_t*)dy, (const bf16_t*)w,
+                                                                              ws, ipb);
 }
 
 extern "C" int irgan_reflect_dgrad_ring(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p, void* dx,
@@ -521,7 +536,10 @@ extern "C" int irgan_reflect_dgrad_ring_ws(const irgan_conv_desc* d, const void*
     if (groups > d->N) groups = d->N;
     const int ipb = irgan_cdiv(d->N, groups);
     groups = irgan_cdiv(d->N, ipb);
-    ring_line_gemm_kernel<<<dim3(tiles, groups), RV_NT, 0, st>>>(*d, (const bf16_t*)dy, (const bf16_t*)w, ws, ipb);
+    if (d->Cin == RV_CIN)
+        ring_line_gemm_kernel<true><<<dim3(tiles, groups), RV_NT, 0, st>>>(*d, (const bf16_t*)dy, (const bf16_t*)w, ws, ipb);
+    else
+        ring_line_gemm_kernel<false><<<dim3(tiles, groups), RV_NT, 0, st>>>(*d, (const bf16_t*)dy, (const bf16_t*)w, ws, ipb);
     const long threads = (long)d->N * (2 * d->Wo + 2 * (d->Ho - 2)) * (d->Cout / 8);
     ring_line_fold_kernel<<<(unsigned)irgan_cdiv(threads, 256), 256, 0, st>>>(*d, ws, dx);
     IRGAN_LAUNCH_CHECK();
