@@ -438,7 +438,7 @@ __global__ __launch_bounds__(TPB) void rows8_kernel(const bf16_t* x, int ldx, in
 // with IRGAN_IN_RPT_M<key> / IRGAN_IN_U_M<key>): forward apply 16.2 -> 14.4 us and backward
 // apply 17.9 -> 17.5 at 4 rows per thread in one batch; the reduce stays at 16 rows in batches
 // of 4 (one batch of 4: 20.7 us, 4x the partials), apply + residual at 8 rows in batches of 4
-constexpr int PASS_RPT[6] = {16, 16, 4, 0, 4, 8}, PASS_U[6] = {16, 4, 4, 0, 8, 4};  // U: the batch cap (larger maps: several batches)
+constexpr int PASS_RPT[6] = {16, 16, 4, 0, 4, 8}, PASS_U[6] = {16, 4, 4, 0, 4, 4};  // U: the batch cap (larger maps: several batches)
 int pass_env(const char* what, int key, int dflt) {
     char k[32];
     snprintf(k, sizeof(k), "IRGAN_IN_%s_M%d", what, key);
