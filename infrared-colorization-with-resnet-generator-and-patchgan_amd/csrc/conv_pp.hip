@@ -21,8 +21,6 @@ constexpr bool split128(int) { return true; }
 // (the PatchGAN 4x4 layers at 32x32: D model.8 backward-data at B = 16 is 64 BN-256 blocks
 // for 256 CUs) -- then 128 or the 64-channel single-halo tile (two blocks per CU)
 int narrow_bn(const irgan_conv_desc* d) {
-    static const int force = getenv("IRGAN_PP_BN") ? atoi(getenv("IRGAN_PP_BN")) : 0;  // A/B only
-    if (force == 64 || force == 128 || force == 256) return force;
     const long patches = (long)d->N * irgan_cdiv(d->Ho, PH) * irgan_cdiv(d->Wo, PW);
     if (patches * (d->Cout / 256) >= 160) return 256;
     return patches * (d->Cout / 128) >= 160 ? 128 : 64;
