@@ -61,6 +61,29 @@ def test_stub_argtypes_match_header(monkeypatch):
     _check_stub_argtypes(monkeypatch)
 
 
+def test_doc_binding_snippets_match_header():
+    """Every other INTEGRATION.md snippet that declares `lib.irgan_*.argtypes` (e.g. the fp8
+    resampler entry of section 4) declares the header's arity and int / pointer kinds."""
+    lib = pkg()._lib
+    protos = {n: a for n, _, a in lib.PROTOS}
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    blocks = [b for b in re.findall(r"```python\n(.*?)```", text, re.S)
+              if "class ConvDesc" not in b and re.search(r"lib\.irgan_\w+\.argtypes", b)]
+    assert blocks, "no binding snippet besides the stub"
+    for b in blocks:
+        fake = _FakeLib()
+        ns = {k: getattr(ctypes, k) for k in dir(ctypes) if k.startswith("c_")}
+        ns["lib"] = fake
+        exec(compile(b, "INTEGRATION.md", "exec"), ns)
+        for name, fn in fake.fns.items():
+            if fn.argtypes is None:
+                continue
+            want, got = protos[name], fn.argtypes
+            assert len(got) == len(want), (name, len(got), len(want))
+            for g, w in zip(got, want):
+                assert (g in (ctypes.c_int32, ctypes.c_int)) == (w in (ctypes.c_int32, ctypes.c_int)), name
+
+
 @pytest.mark.gpu
 def test_stub_runs_on_gpu(monkeypatch):
     _check_stub_argtypes(monkeypatch)
