@@ -109,12 +109,14 @@ def build(force: bool = False, verbose: bool = False, extra_flags=(), lib: str =
     with ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
         list(ex.map(compile_one, jobs))
     lsig = _sig([_read(_sig_path(o)) for o in objs])
-    if force or jobs or not _current(lib, lsig):
+    # the link signature also covers the library's own bytes, so a library copied over the
+    # linked one (another tree's build) is relinked rather than trusted
+    if force or jobs or not (os.path.exists(lib) and _current(lib, _sig([lsig, _read(lib)]))):
         if os.path.exists(_sig_path(lib)):
             os.remove(_sig_path(lib))
         run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib, *objs])
         with open(_sig_path(lib), "w") as f:
-            f.write(lsig)
+            f.write(_sig([lsig, _read(lib)]))
     return lib
 
 
