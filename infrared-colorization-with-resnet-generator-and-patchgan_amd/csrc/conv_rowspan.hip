@@ -197,8 +197,11 @@ void launch_rowspan(const irgan_conv_desc* d, const void* x, const void* w, cons
 // ty for the whole block (one A fragment feeds 4 MFMAs, one X fragment 2); both operands
 // are K-major in LDS ([q][n] and the [q][ci] ring) and are read with ds_read_b64_tr_b16
 // pairs (conv_wgrad_pc.hip's operand reads).  Per batch of 8 output rows every wave
-// builds its share of the 8 A tiles (64 q x 32 n bf16) from dY while the next 8 input
-// rows stream into the ring.  Block partials -> slab (ordered reduce) or fp32 atomics.
+// builds its share of the 8 A tiles (64 q x 32 n bf16; rows r and r + 4 share one 128-B
+// row image, n in its columns 32 (r >> 2) ..) from dY.  The ring holds two batches of
+// input rows: batch it + 1's 8 new rows and its dY rows are DMA'd when batch it's MFMAs
+// start (into the slots batch it - 1 released), so the HBM latency hides under them.
+// Block partials -> slab (ordered reduce) or fp32 atomics.
 typedef __attribute__((ext_vector_type(4))) short rs_s16x4;
 typedef __attribute__((address_space(3))) rs_s16x4 rs_lds_s4;
 IRGAN_HD uint4 rs_tr_pair(const char* lo, const char* hi) {
@@ -217,10 +220,12 @@ IRGAN_HD int rs_tr_off(int row, int col) { return row * 128 + (((col >> 3) ^ (2 
 
 template <int KH, int KW>
 struct RSW {
-    static constexpr int RR = RS_NR + KH - 1;
-    static constexpr int RING = (RR * RS_QP + 32) * 128;          // + 32 rows: K-step 1 of the last slot
-    static constexpr int AB = RS_NR * 64 * 128;                   // 8 A tiles [64 q][32 n, padded to 64] bf16
-    static constexpr int DB = RS_NR * RS_SEG * 16;                // the batch's dY rows (8 channels)
+    static constexpr int RR = RS_NR + KH - 1;                     // input rows one batch reads
+    static constexpr int RQ = RR + RS_NR;                         // ring slots: + the next batch's rows
+    static constexpr int RING = (RQ * RS_QP + 32) * 128;          // + 32 rows: K-step 1 of the last slot
+    static constexpr int AB = RS_NR / 2 * 64 * 128;               // 8 A tiles [64 q][32 n], two per row image
+    static constexpr int DBH = RS_NR * RS_SEG * 16;               // one batch's dY rows (8 channels)
+    static constexpr int DB = 2 * DBH;
     static constexpr int LDS = RING + AB + DB;
     static_assert(LDS <= 160 * 1024 && KH <= 8, "lds / one kernel row per wave");
 };
@@ -231,7 +236,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_rowspan_kernel(const irgan_conv_
                                                                float* __restrict__ slab, int nsx, int nrb,
                                                                int nchunk) {
     using L = RSW<KH, KW>;
-    constexpr int RR = L::RR;
+    constexpr int RR = L::RR, RQ = L::RQ;
     __shared__ __attribute__((aligned(1024))) char smem[L::LDS];
     char* const sR = smem;
     char* const sA = smem + L::RING;
@@ -251,13 +256,15 @@ __global__ __launch_bounds__(512, 1) void wgrad_rowspan_kernel(const irgan_conv_
     const int Cout = d.Cout;
     const bool reflect = d.pad_mode == IRGAN_PAD_REFLECT;
 
-    // the slack rows after the ring are read by K-step 1 of the last slot (times zeros of A):
-    // they must hold finite values
-    for (int e = tid; e < 32 * 8; e += 512) *(uint4*)(sR + (RR * RS_QP) * 128 + e * 16) = make_uint4(0u, 0u, 0u, 0u);
+    // K-step 1 of a slot reads the first rows of the next slot (the slack rows after the last
+    // one), times zeros of A: they must hold finite values, also while a prefetch is landing
+    // in them -- the slots the prologue does not load start as zeros
+    for (int e = tid; e < ((RQ - RR) * RS_QP + 32) * 8; e += 512)
+        *(uint4*)(sR + (RR * RS_QP) * 128 + e * 16) = make_uint4(0u, 0u, 0u, 0u);
     const i32x4 rs = make_rsrc(x, (uint32_t)((long)d.N * d.H * d.W * d.ldx * 2));
     const int sub = lane >> 3, cl = lane & 7;
     auto load_row = [&](int rel, int part) {
-        const int slot = rel % RR;
+        const int slot = rel % RQ;
         const int lrow = slot * RS_QP + part * 8 + sub;
         const int q = part * 8 + sub;
         int iy = R0 + d.c0y + rel, ix = x0 + q + d.c0x;
@@ -272,19 +279,20 @@ __global__ __launch_bounds__(512, 1) void wgrad_rowspan_kernel(const irgan_conv_
                : IRGAN_OOB;
         blds16(rs, off, sR + (slot * RS_QP + part * 8) * 128);
     };
-    // the batch's dY rows -> sD [8 rows][32 px][8 channels] (4 wave-instructions; out of
-    // range -> zeros)
+    // batch it's dY rows -> sD[it & 1] [8 rows][32 px][8 channels] (4 wave-instructions; out
+    // of range -> zeros)
     const i32x4 rsd = make_rsrc(dy, (uint32_t)((long)d.N * d.Ho * d.Wo * d.ldy * 2));
     auto load_dy = [&](int it) {
         if (wid < 4) {
             const int r = wid * 2 + (lane >> 5), j = lane & 31, oy = R0 + it * RS_NR + r, ox = x0 + j;
             const bool ok = oy < R1 && ox < d.Wo;
             const uint32_t off = ok ? (uint32_t)((((long)img * d.Ho + oy) * d.Wo + ox) * d.ldy + d.yoff) * 2 : IRGAN_OOB;
-            blds16(rsd, off, sD + wid * 1024);
+            blds16(rsd, off, sD + (it & 1) * L::DBH + wid * 1024);
         }
     };
     // A tiles of batch `it` (from sD): row r, q, 8 consecutive n -> one 16-byte LDS write
     auto build_a = [&](int it) {
+        const char* const sDi = sD + (it & 1) * L::DBH;
         for (int e = tid; e < RS_NR * 64 * 4; e += 512) {
             const int r = e >> 8, q = (e >> 2) & 63, n8 = (e & 3) * 8;
             float v[8];
@@ -292,14 +300,14 @@ __global__ __launch_bounds__(512, 1) void wgrad_rowspan_kernel(const irgan_conv_
             for (int k = 0; k < 8; ++k) {
                 const int n = n8 + k, tx = n / Cout, co = n - tx * Cout, j = q - tx;
                 const bool ok = n < KW * Cout && j >= 0 && j < RS_SEG;
-                v[k] = ok ? bf2f(*(const bf16_t*)(sD + (r * RS_SEG + j) * 16 + co * 2)) : 0.f;
+                v[k] = ok ? bf2f(*(const bf16_t*)(sDi + (r * RS_SEG + j) * 16 + co * 2)) : 0.f;
             }
             uint4 u;
             u.x = pk_bf16(v[0], v[1]);
             u.y = pk_bf16(v[2], v[3]);
             u.z = pk_bf16(v[4], v[5]);
             u.w = pk_bf16(v[6], v[7]);
-            *(uint4*)(sA + r * 8192 + rs_tr_off(q, n8)) = u;
+            *(uint4*)(sA + (r & 3) * 8192 + rs_tr_off(q, n8 + (r >> 2) * 32)) = u;
         }
     };
     for (int e = wid; e < RR * 5; e += 8) load_row(e / 5, e % 5);
@@ -325,17 +333,23 @@ __global__ __launch_bounds__(512, 1) void wgrad_rowspan_kernel(const irgan_conv_
 
 #pragma unroll 1
     for (int it = 0; R0 + it * RS_NR < R1; ++it) {
+        const bool nxt = R0 + (it + 1) * RS_NR < R1;
+        if (nxt && !RSX(4)) {  // batch it + 1: its 8 new input rows and its dY rows
+            for (int e = wid; e < RS_NR * 5; e += 8) load_row((it + 1) * RS_NR + KH - 1 + e / 5, e % 5);
+            load_dy(it + 1);
+        }
         if (ty < KH && !RSX(1)) {
 #pragma unroll 2
             for (int r = 0; r < RS_NR; ++r) {
-                const int slot = (it * RS_NR + r + ty) % RR;
-                const char* Ar = sA + r * 8192;
+                const int slot = (it * RS_NR + r + ty) % RQ;
+                const char* Ar = sA + (r & 3) * 8192;
+                const int ac = (r >> 2) * 32;
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     uint4 a[2], b[4];
 #pragma unroll
                     for (int i = 0; i < 2; ++i) {
-                        const int q0 = 32 * h + k_lo, col = 16 * i + 4 * p;
+                        const int q0 = 32 * h + k_lo, col = ac + 16 * i + 4 * p;
                         a[i] = rs_tr_pair(Ar + rs_tr_off(q0, col), Ar + rs_tr_off(q0 + 4, col));
                     }
 #pragma unroll
@@ -353,14 +367,9 @@ __global__ __launch_bounds__(512, 1) void wgrad_rowspan_kernel(const irgan_conv_
                 }
             }
         }
-        __syncthreads();  // ring rows of this batch and its A tiles consumed
-        if (R0 + (it + 1) * RS_NR < R1) {
-            if (!RSX(4)) {
-                for (int e = wid; e < RS_NR * 5; e += 8) load_row((it + 1) * RS_NR + KH - 1 + e / 5, e % 5);
-                load_dy(it + 1);
-                wait_vmcnt<0>();
-            }
-            __syncthreads();
+        if (nxt) wait_vmcnt<0>();
+        __syncthreads();  // this batch's A tiles consumed, the next batch's rows landed
+        if (nxt) {
             if (!RSX(2)) build_a(it + 1);
             __syncthreads();
         }
