@@ -220,6 +220,10 @@ IRGAN_HD int rs_tr_off(int row, int col) { return row * 128 + (((col >> 3) ^ (2 
 
 template <int KH, int KW>
 struct RSW {
+    // output pixels per row segment: 7x7 takes 26 so that its 32 input positions are ONE K-step
+    // (a 32-pixel segment needs 38: two K-steps, the second with 6 of 32 positions used)
+    static constexpr int SEG = KW == 7 ? 32 - (KW - 1) : RS_SEG;
+    static constexpr int HS = (SEG + KW - 1 + 31) / 32;           // K-steps per row
     static constexpr int RR = RS_NR + KH - 1;                     // input rows one batch reads
     static constexpr int RQ = RR + RS_NR;                         // ring slots: + the next batch's rows
     static constexpr int RING = (RQ * RS_QP + 32) * 128;          // + 32 rows: K-step 1 of the last slot
@@ -251,7 +255,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_rowspan_kernel(const irgan_conv_
     t /= nsx;
     const int rb = t % nrb;
     const int img = t / nrb;
-    const int x0 = sx * RS_SEG, R0 = rb * RS_RB;
+    const int x0 = sx * L::SEG, R0 = rb * RS_RB;
     const int R1 = min(d.Ho, R0 + RS_RB);
     const int Cout = d.Cout;
     const bool reflect = d.pad_mode == IRGAN_PAD_REFLECT;
@@ -272,7 +276,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_rowspan_kernel(const irgan_conv_
             iy = reflect_idx(iy, d.H);
             ix = reflect_idx(ix, d.W);
         }
-        const bool ok = q < RS_SEG + KW - 1 && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+        const bool ok = q < L::SEG + KW - 1 && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
         const int ck = cl ^ (2 * rs_t128(lrow));
         const uint32_t off =
             ok ? (uint32_t)((((img * d.H + iy) * d.W + ix) * d.ldx + d.xoff) * 2 + chunk * 128 + ck * 16)
@@ -293,13 +297,14 @@ __global__ __launch_bounds__(512, 1) void wgrad_rowspan_kernel(const irgan_conv_
     // A tiles of batch `it` (from sD): row r, q, 8 consecutive n -> one 16-byte LDS write
     auto build_a = [&](int it) {
         const char* const sDi = sD + (it & 1) * L::DBH;
-        for (int e = tid; e < RS_NR * 64 * 4; e += 512) {
-            const int r = e >> 8, q = (e >> 2) & 63, n8 = (e & 3) * 8;
+        constexpr int QB = 32 * L::HS;  // the A rows the K-steps read
+        for (int e = tid; e < RS_NR * QB * 4; e += 512) {
+            const int r = e / (QB * 4), q = (e >> 2) % QB, n8 = (e & 3) * 8;
             float v[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 const int n = n8 + k, tx = n / Cout, co = n - tx * Cout, j = q - tx;
-                const bool ok = n < KW * Cout && j >= 0 && j < RS_SEG;
+                const bool ok = n < KW * Cout && j >= 0 && j < L::SEG;
                 v[k] = ok ? bf2f(*(const bf16_t*)(sDi + (r * RS_SEG + j) * 16 + co * 2)) : 0.f;
             }
             uint4 u;
@@ -345,7 +350,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_rowspan_kernel(const irgan_conv_
                 const char* Ar = sA + (r & 3) * 8192;
                 const int ac = (r >> 2) * 32;
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
+                for (int h = 0; h < L::HS; ++h) {
                     uint4 a[2], b[4];
 #pragma unroll
                     for (int i = 0; i < 2; ++i) {
@@ -432,7 +437,8 @@ extern "C" int irgan_conv_wgrad_rowspan(const irgan_conv_desc* d, const void* x,
         d->ldy % 8 || d->yoff % 8 || (long)d->N * d->H * d->W * d->ldx * 2 >= (1L << 31) ||
         (long)d->N * d->Ho * d->Wo * d->ldy * 2 >= (1L << 31))
         return IRGAN_EUNSUPPORTED;
-    const int nsx = irgan_cdiv(d->Wo, RS_SEG), nrb = irgan_cdiv(d->Ho, RS_RB), nchunk = d->Cin / 64;
+    const int seg = d->KH == 7 ? RSW<7, 7>::SEG : RSW<4, 4>::SEG;
+    const int nsx = irgan_cdiv(d->Wo, seg), nrb = irgan_cdiv(d->Ho, RS_RB), nchunk = d->Cin / 64;
     const int ng = d->N * nsx * nrb;
     const long n = (long)d->Cout * d->KH * d->KW * d->Cin;
     const int per = 16, parts = irgan_cdiv(ng, per);
