@@ -352,12 +352,7 @@ __global__ __launch_bounds__(512, 2) void conv_wgrad_glds_kernel(const irgan_con
 __global__ __launch_bounds__(256) void glds_slab_reduce(const float* __restrict__ slab, int splits, long n,
                                                         float* __restrict__ dw) {
     for (long i = blockIdx.x * 256L + threadIdx.x; i < n / 4; i += (long)gridDim.x * 256) {
-        float4 a = ((const float4*)dw)[i];
-        for (int s = 0; s < splits; ++s) {
-            const float4 v = ((const float4*)(slab + (long)s * n))[i];
-            a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
-        }
-        ((float4*)dw)[i] = a;
+        slab_sum4(slab, splits, n, dw, i);
     }
 }
 

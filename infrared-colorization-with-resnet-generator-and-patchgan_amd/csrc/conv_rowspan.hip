@@ -409,7 +409,14 @@ __global__ __launch_bounds__(256) void wgrad_rowspan_reduce1(const float* __rest
     if (i >= n) return;
     const int b0 = blockIdx.y * per, b1 = min(nb, b0 + per);
     float a = 0.f;
-    for (int b = b0; b < b1; ++b) a += slab[(long)b * n + i];
+    for (int c0 = b0; c0 < b1; c0 += 8) {  // 8 loads in flight, added in order
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = c0 + k < b1 ? slab[(long)(c0 + k) * n + i] : 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (c0 + k < b1) a += v[k];
+    }
     tmp[(long)blockIdx.y * n + i] = a;
 }
 __global__ __launch_bounds__(256) void wgrad_rowspan_reduce2(const float* __restrict__ tmp, int parts, long n,

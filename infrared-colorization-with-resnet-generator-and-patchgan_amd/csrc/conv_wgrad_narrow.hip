@@ -247,7 +247,14 @@ __global__ __launch_bounds__(1024) void wgrad_narrow_reduce(const float* __restr
     const bool in = o < COT * npad;
     float s = 0.f;
     if (in)
-        for (int b = j; b < nb; b += 16) s += ws[(long)b * COT * npad + o];
+        for (int b0 = j; b0 < nb; b0 += 16 * 8) {  // 8 loads in flight, added in block order
+            float v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = b0 + 16 * k < nb ? ws[(long)(b0 + 16 * k) * COT * npad + o] : 0.f;
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (b0 + 16 * k < nb) s += v[k];
+        }
     red[j][ol] = s;
     __syncthreads();
     if (j != 0 || !in) return;
