@@ -326,15 +326,40 @@ __global__ __launch_bounds__(512, 1) void wgrad_rowspan_kernel(const irgan_conv_
     // high half, +32 for K-step 1), 4 consecutive columns from 4p
     const int g = lane >> 4, qq = (lane & 15) >> 2, p = lane & 3;
     const int k_lo = 8 * g + qq;
-    const int ty = wid;  // waves >= KH only build / load
-    f32x4 acc[2][4];
+    // Wave roles: wave w owns the kernel-row PAIR (2 pr, 2 pr + 1), pr = w % NPR, over the
+    // batch's rows [rh * RPW, rh * RPW + RPW), rh = w / NPR.  Output row r of kernel row ty
+    // reads input row r + ty, so the pair's second row at r is its first row at r + 1: the
+    // X fragments slide through registers and each step reads one A tile and ONE new X row
+    // for 16 MFMAs (one kernel row per wave read an A tile and an X row for 8).  The NRS
+    // waves of a pair sum their partials through LDS in a fixed order after the loop.
+    // (4x4, two K-steps per row: the window's registers would spill -- one kernel row per
+    // wave, the batch's rows split over two waves)
+    constexpr bool PAIRS = KH == 7;
+    constexpr int NPR = PAIRS ? (KH + 1) / 2 : KH, NRS = 8 / NPR, RPW = RS_NR / NRS, HS = L::HS;
+    static_assert(NPR * NRS == 8 && RS_NR % NRS == 0, "wave roles");
+    const int pr = wid % NPR, rh = wid / NPR, ty0 = PAIRS ? 2 * pr : pr;
+    const bool two = PAIRS && ty0 + 1 < KH;  // wave-uniform
+    f32x4 acc[2][2][4];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int u = 0; u < 2; ++u)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[u][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     int xo[4];  // X column byte terms of ci fragment j (swizzle applied per row below)
 #pragma unroll
     for (int j = 0; j < 4; ++j) xo[j] = (16 * j + 4 * p);
+    // the ci fragments of input row `rel` (relative to the block's first row), both K-steps
+    auto read_x = [&](int rel, uint4 (&b)[HS][4]) {
+        const int slot = rel % RQ;
+#pragma unroll
+        for (int h = 0; h < HS; ++h)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int row = slot * RS_QP + 32 * h + k_lo;
+                b[h][j] = rs_tr_pair(sR + rs_tr_off(row, xo[j]), sR + rs_tr_off(row + 4, xo[j]));
+            }
+    };
 
 #pragma unroll 1
     for (int it = 0; R0 + it * RS_NR < R1; ++it) {
@@ -343,33 +368,45 @@ __global__ __launch_bounds__(512, 1) void wgrad_rowspan_kernel(const irgan_conv_
             for (int e = wid; e < RS_NR * 5; e += 8) load_row((it + 1) * RS_NR + KH - 1 + e / 5, e % 5);
             load_dy(it + 1);
         }
-        if (ty < KH && !RSX(1)) {
-#pragma unroll 2
-            for (int r = 0; r < RS_NR; ++r) {
-                const int slot = (it * RS_NR + r + ty) % RQ;
+        if (!RSX(1)) {
+            uint4 xc[HS][4], xn[PAIRS ? HS : 1][4];
+#pragma unroll
+            for (int k = 0; k < RPW; ++k) {
+                const int r = rh * RPW + k;
+                if (k == 0 || !two) read_x(it * RS_NR + r + ty0, xc);
+                if constexpr (PAIRS)
+                    if (two) read_x(it * RS_NR + r + ty0 + 1, xn);
                 const char* Ar = sA + (r & 3) * 8192;
                 const int ac = (r >> 2) * 32;
 #pragma unroll
-                for (int h = 0; h < L::HS; ++h) {
-                    uint4 a[2], b[4];
+                for (int h = 0; h < HS; ++h) {
+                    uint4 a[2];
 #pragma unroll
                     for (int i = 0; i < 2; ++i) {
                         const int q0 = 32 * h + k_lo, col = ac + 16 * i + 4 * p;
                         a[i] = rs_tr_pair(Ar + rs_tr_off(q0, col), Ar + rs_tr_off(q0 + 4, col));
                     }
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int row = slot * RS_QP + 32 * h + k_lo;
-                        b[j] = rs_tr_pair(sR + rs_tr_off(row, xo[j]), sR + rs_tr_off(row + 4, xo[j]));
-                    }
-#pragma unroll
                     for (int i = 0; i < 2; ++i)
 #pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a[i]),
-                                                                                __builtin_bit_cast(bf16x8_t, b[j]),
-                                                                                acc[i][j], 0, 0, 0);
+                        for (int j = 0; j < 4; ++j) {
+                            acc[0][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                                __builtin_bit_cast(bf16x8_t, a[i]), __builtin_bit_cast(bf16x8_t, xc[h][j]), acc[0][i][j], 0,
+                                0, 0);
+                            if constexpr (PAIRS)
+                                if (two)
+                                    acc[1][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                                        __builtin_bit_cast(bf16x8_t, a[i]), __builtin_bit_cast(bf16x8_t, xn[h][j]),
+                                        acc[1][i][j], 0, 0, 0);
+                        }
                 }
+                if constexpr (PAIRS)
+                    if (two) {
+#pragma unroll
+                        for (int h = 0; h < HS; ++h)
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) xc[h][j] = xn[h][j];
+                    }
             }
         }
         if (nxt) wait_vmcnt<0>();
@@ -379,24 +416,54 @@ __global__ __launch_bounds__(512, 1) void wgrad_rowspan_kernel(const irgan_conv_
             __syncthreads();
         }
     }
-    if (ty >= KH) return;
+    // the pair's partials: waves rh > 0 park theirs in the (now idle) ring, wave rh = 0 adds
+    // them in rh order (deterministic)
+    f32x4* const part = (f32x4*)sR;  // [NPR][NRS - 1][16 tiles][64 lanes]
+    static_assert(NPR * (NRS - 1) * 16 * 64 * 16 <= L::RING, "partials fit in the ring");
+    if (rh > 0) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    part[((pr * (NRS - 1) + rh - 1) * 16 + u * 8 + i * 4 + j) * 64 + lane] = acc[u][i][j];
+    }
+    __syncthreads();
+    if (rh > 0) return;
+#pragma unroll
+    for (int q = 1; q < NRS; ++q)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const f32x4 v = part[((pr * (NRS - 1) + q - 1) * 16 + u * 8 + i * 4 + j) * 64 + lane];
+                    acc[u][i][j] += v;
+                }
     // C[row = n][col = ci]: n = 16i + 4g + rr, ci = 16j + (lane & 15)
     const int Kw = KH * KW * d.Cin;
     float* const dst = slab ? slab + (long)grp * Cout * Kw : nullptr;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int u = 0; u < 2; ++u) {
+        if (u == 1 && !two) break;
+        const int ty = ty0 + u;
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-            const int n = 16 * i + 4 * g + rr;
-            if (n >= KW * Cout) continue;
-            const int tx = n / Cout, co = n - tx * Cout;
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const long o = (long)co * Kw + (ty * KW + tx) * d.Cin + chunk * 64 + 16 * j + (lane & 15);
-                if (dst) dst[o] = acc[i][j][rr];
-                else atomicAdd(dw + o, acc[i][j][rr]);
+            for (int rr = 0; rr < 4; ++rr) {
+                const int n = 16 * i + 4 * g + rr;
+                if (n >= KW * Cout) continue;
+                const int tx = n / Cout, co = n - tx * Cout;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const long o = (long)co * Kw + (ty * KW + tx) * d.Cin + chunk * 64 + 16 * j + (lane & 15);
+                    if (dst) dst[o] = acc[u][i][j][rr];
+                    else atomicAdd(dw + o, acc[u][i][j][rr]);
+                }
             }
-        }
+    }
 }
 
 // Ordered two-level reduce of the nb group partials (n floats each; deterministic): level 1
