@@ -148,7 +148,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--size", type=int, default=256, help="square image side (default for --height/--width)")
+    ap.add_argument("--height", type=int, default=None, help="image height (BASELINE configs[3]: 512)")
+    ap.add_argument("--width", type=int, default=None, help="image width (BASELINE configs[3]: 640)")
     ap.add_argument("--batch", type=int, default=16, help="per-GPU batch")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp8"],
                     help="fp8: BASELINE configs[4] -- the ResnetBlock convs on e4m3 operands (use --batch 32)")
@@ -170,7 +172,8 @@ def main():
     irc = importlib.import_module(PKG)
     ops = irc.ops
 
-    H = W = args.size
+    H = args.height or args.size
+    W = args.width or args.size
     B = args.batch
     cfg = irc.Config()
     cfg.device = f"cuda:{local}"
@@ -283,11 +286,8 @@ def main():
             "ms_per_step_median": round(median_ms, 3), "img_per_s_median_step": round(B * world / median_ms * 1e3, 3),
             "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (U(-1,1) IR/RGB pairs, seeded; random-init weights)",
-            "config": {"workload": (f"GAN train step {H}x{W}, batch {B}/GPU, ResnetBlock convs on fp8 e4m3 "
-                                    f"operands (BASELINE configs[4])") if args.dtype == "fp8" else
-                                   (f"GAN train step {H}x{W}, batch {B}/GPU (BASELINE configs[1]"
-                                    f"{' / [2]' if world > 1 else ''})"), "global_batch": B * world,
-                       "img_size": H, "parallelism": f"dp{world}",
+            "config": {"workload": workload_label(H, W, B, args.dtype, world), "global_batch": B * world,
+                       "img_size": H, "height": H, "width": W, "parallelism": f"dp{world}",
                        "min_gflop_per_img": round(min_gflop_per_img(H, W), 2),
                        "step_tflops_per_gpu": round(step_tflops, 2),
                        "step_frac_of_bf16_peak": round(step_tflops / BF16_DENSE_PEAK_TFLOPS, 4)},
@@ -320,6 +320,23 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def workload_label(H, W, B, dtype, world):
+    """Names the workload from the actual (H, W, B, dtype); a BASELINE config is named only
+    when the per-GPU shape is exactly that config's (BASELINE.json configs: [1] 256^2 B=16
+    bf16 1 GPU, [2] the same at DP8, [3] 512x640 B=4/GPU, [4] 256^2 fp8 B=32/GPU)."""
+    base = f"GAN train step {H}x{W}, batch {B}/GPU, {dtype}"
+    if dtype == "fp8":
+        base += " (conv operands on e4m3 where the fp8 path covers the layer)"
+    tag = None
+    if (H, W, B, dtype) == (256, 256, 16, "bf16"):
+        tag = "BASELINE configs[2]" if world > 1 else "BASELINE configs[1]"
+    elif (H, W, B) == (512, 640, 4) and dtype != "fp8":
+        tag = "BASELINE configs[3] per-GPU shape"
+    elif (H, W, B, dtype) == (256, 256, 32, "fp8"):
+        tag = "BASELINE configs[4] per-GPU shape"
+    return f"{base} ({tag})" if tag else base
 
 
 def step_phases(steps):

@@ -375,9 +375,8 @@ IRGAN_API int irgan_act_bwd(const void* dy, int32_t dy_dtype, int32_t lddy, int3
 /* ---- losses (ir:1647-1679, 686-750) ; images NHWC fp32 (B,H,W,3) ---- */
 /* Hinge for D on a [real; fake] patch map (ir:1647-1649) and for G (ir:1662).
  * mode 0: loss = 0.5*(mean relu(1-p[:n]) + mean relu(1+p[n:])), grad written;
- * mode 1: loss = -mean p, grad = -scale/cnt; modes 2 / 3: one half of mode 0 on its own
- * n-element map (2: the real term 0.5*mean relu(1-p), 3: the fake term 0.5*mean relu(1+p)),
- * so the D step's real and fake halves can run apart.  loss accumulated into *loss (fp64). */
+ * mode 1: loss = -mean p, grad = -scale/cnt.  Other modes: IRGAN_EINVAL.
+ * loss accumulated into *loss (fp64). */
 IRGAN_API int irgan_hinge(const float* pred, int32_t n_half, int32_t mode, float scale, float* grad,
                 double* loss, irgan_stream_t s);
 /* Pixel / feature L1: loss += w*mean|a-b|; ga = w*sign(a-b)/cnt (dtype of ga). */

@@ -71,10 +71,12 @@ def _current(path, sig):
     return os.path.exists(path) and os.path.exists(_sig_path(path)) and _read(_sig_path(path)).decode() == sig
 
 
-def build(force: bool = False, verbose: bool = False, extra_flags=(), lib: str = LIB, objdir: str = OBJDIR) -> str:
+def build(force: bool = False, verbose: bool = False, extra_flags=(), lib: str = LIB, objdir: str = OBJDIR,
+          only=None) -> str:
     """Compile the sources whose inputs changed and link `lib`.  extra_flags (A/B variant
-    builds, tools/build_variant.sh) apply to every object and land in objdir's signatures,
-    so variant objects never stand in for the default build's."""
+    builds, tools/build_variant.sh) apply to every object -- or, with ``only`` (a list of
+    source names), to those alone, the others linked from the default objects -- and land
+    in the objects' signatures, so variant objects never stand in for the default build's."""
     hipcc = _hipcc()
     os.makedirs(objdir, exist_ok=True)
     sid = source_id()
@@ -82,8 +84,9 @@ def build(force: bool = False, verbose: bool = False, extra_flags=(), lib: str =
     jobs, objs = [], []
     for s in SOURCES:
         src = os.path.join(CSRC, s)
-        obj = os.path.join(objdir, s.replace(".hip", ".o"))
-        flags = list(FLAGS) + list(extra_flags)
+        var = only is None or s in only
+        obj = os.path.join(objdir if var else OBJDIR, s.replace(".hip", ".o"))
+        flags = list(FLAGS) + (list(extra_flags) if var else [])
         if s == "build_id.hip":
             flags.append(f'-DIRGAN_SOURCE_ID="{sid}"')
         sig = _sig([hipcc, *flags, _read(src), *hdr])

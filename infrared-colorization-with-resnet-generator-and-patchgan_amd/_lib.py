@@ -10,6 +10,7 @@ from __future__ import annotations
 import ctypes
 import os
 import re
+import warnings
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 HEADER = os.path.join(os.path.dirname(HERE), "include", "irgan.h")
@@ -21,15 +22,29 @@ PAD_ZERO, PAD_REFLECT = 0, 1
 ACT_NONE, ACT_RELU, ACT_LRELU, ACT_TANH = 0, 1, 2, 3
 
 
+class IrganError(RuntimeError):
+    pass
+
+
+def _header_text() -> str:
+    """include/irgan.h: the ctypes signatures are generated from it, so a deployment ships it
+    next to libirgan.so (the csrc/ sources are optional, see load())."""
+    try:
+        with open(HEADER) as f:
+            return f.read()
+    except OSError as e:
+        raise IrganError(f"{HEADER} is missing ({e}): the binding reads the ABI from the header") from None
+
+
 def header_enum(name: str) -> int:
-    return int(re.search(name + r"\s*=\s*(\d+)", open(HEADER).read()).group(1))
+    return int(re.search(name + r"\s*=\s*(\d+)", _header_text()).group(1))
 
 
 IN_PARTS = header_enum("IRGAN_IN_PARTS")
 
 
 def _desc_fields():
-    src = open(HEADER).read()
+    src = _header_text()
     body = re.search(r"typedef struct irgan_conv_desc \{(.*?)\} irgan_conv_desc;", src, re.S).group(1)
     names = []
     for line in body.splitlines():
@@ -65,7 +80,7 @@ def _ctype(decl: str):
 
 def parse_header():
     """[(name, restype, [argtypes])] for every prototype in irgan.h."""
-    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    src = re.sub(r"/\*.*?\*/", "", _header_text(), flags=re.S)
     out = []
     for m in re.finditer(r"\b(int)\s+(irgan_\w+)\s*\(([^)]*)\)\s*;", src):
         args = [a for a in (x.strip() for x in m.group(3).split(",")) if a and a != "void"]
@@ -75,10 +90,6 @@ def parse_header():
 
 PROTOS = parse_header()
 _lib = None
-
-
-class IrganError(RuntimeError):
-    pass
 
 
 def load(path: str = LIB_PATH):
@@ -96,17 +107,29 @@ def load(path: str = LIB_PATH):
         fn.restype = res
         fn.argtypes = args
     got, want = build_id(lib), tree_id()
-    if got != want:
+    if want is None:
+        # a deployment with the library, the Python files and the header but no csrc/:
+        # nothing to compare the compiled-in id with
+        warnings.warn(f"no kernel sources next to {path}: build id {got} not checked against a tree",
+                      RuntimeWarning)
+    elif got != want:
         raise IrganError(f"{path} was built from sources {got}, but this tree is {want}: the library is "
                          "stale -- rebuild it with __graft_entry__.build()")
     _lib = lib
     return lib
 
 
-def tree_id() -> str:
-    """Source id of the csrc/ + include/ tree next to this file (_build.source_id)."""
+def tree_id():
+    """Source id of the csrc/ + include/ tree next to this file (_build.source_id), or None
+    when the csrc/ directory is absent (a library-only deployment).  A tree that exists
+    but cannot be read raises IrganError."""
     from . import _build
-    return _build.source_id()
+    if not os.path.isdir(_build.CSRC):
+        return None
+    try:
+        return _build.source_id()
+    except OSError as e:
+        raise IrganError(f"cannot hash the kernel sources for the build-id check: {e}") from None
 
 
 def build_id(lib=None) -> str:

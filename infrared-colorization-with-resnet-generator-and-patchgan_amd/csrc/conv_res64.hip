@@ -40,6 +40,11 @@ IRGAN_HD void wait_vm_dyn(int n) {
         default: wait_vmcnt<31>(); break;
     }
 }
+// R64_EXP (ablation builds only, tools/build_variant.sh): bit 0 no MFMA, bit 1 no output
+// stores, bit 2 no halo DMA after the first two patches, bit 3 no fragment reads from LDS
+#ifndef R64_EXP
+#define R64_EXP 0
+#endif
 constexpr int R64_HP = 41;               // halo pieces: 18 x 18 rows of 128 B
 constexpr int R64_HB = R64_HP * 1024;
 constexpr int R64_WB = 9 * 64 * 128;
@@ -84,6 +89,7 @@ __global__ __launch_bounds__(512, 1) void conv_res64_kernel(const irgan_conv_des
     const i32x4 xr = make_rsrc(x, (uint32_t)((long)d.N * d.H * d.W * d.ldx * 2));
 
     auto issue_halo = [&](int p, int buf) {
+        if ((R64_EXP & 4) && p >= q0 + 2 * qs) return;
         const int pxi = p % tpx, pyi = (p / tpx) % tpy, img = p / (tpx * tpy);
         const int py0 = pyi * PH + d.c0y, px0 = pxi * PW + d.c0x;
         char* dst = sH + buf * R64_HB;
@@ -208,17 +214,18 @@ __global__ __launch_bounds__(512, 1) void conv_res64_kernel(const irgan_conv_des
             for (int h = 0; h < 2; ++h) {
                 uint4 af[MI], bfr[NJ];
 #pragma unroll
-                for (int j = 0; j < NJ; ++j) bfr[j] = *(const uint4*)(sW + tp * 8192 + (h ? bb1 : bb0) + j * 2048);
+                for (int j = 0; j < NJ; ++j)
+                    bfr[j] = (R64_EXP & 8) ? make_uint4(lane + j, tp, h, 1) : *(const uint4*)(sW + tp * 8192 + (h ? bb1 : bb0) + j * 2048);
 #pragma unroll
                 for (int i = 0; i < MI; ++i) {
                     const int K = (i + ty) * HWd + tx;
-                    af[i] = *(const uint4*)(sH + (hb + (tsw[K & 7] ^ (h * 64))) + K * 128);
+                    af[i] = (R64_EXP & 8) ? make_uint4(lane + i, K, h, 2) : *(const uint4*)(sH + (hb + (tsw[K & 7] ^ (h * 64))) + K * 128);
                 }
 #pragma unroll
                 for (int i = 0; i < MI; ++i)
 #pragma unroll
                     for (int j = 0; j < NJ; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, bfr[j]),
+                        if (!(R64_EXP & 1)) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, bfr[j]),
                                                                             __builtin_bit_cast(bf16x8_t, af[i]),
                                                                             acc[i][j], 0, 0, 0);
             }
@@ -259,7 +266,7 @@ __global__ __launch_bounds__(512, 1) void conv_res64_kernel(const irgan_conv_des
                     u32x2_t pk;
                     pk.x = pk_bf16(v[0], v[1]);
                     pk.y = pk_bf16(v[2], v[3]);
-                    const int off = ok ? (int)((pix * d.ldy + d.yoff + co) * 2) : (int)IRGAN_OOB;
+                    const int off = ok && !(R64_EXP & 2) ? (int)((pix * d.ldy + d.yoff + co) * 2) : (int)IRGAN_OOB;
                     __builtin_amdgcn_raw_buffer_store_b64(pk, yr, off, 0, 0);
                     if constexpr (STATS) {
                         if (ok) {

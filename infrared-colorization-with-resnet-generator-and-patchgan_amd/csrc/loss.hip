@@ -38,8 +38,8 @@ __global__ __launch_bounds__(TPB) void hinge_kernel(const float* __restrict__ pr
     const float inv = 1.f / (float)n;
     for (long i = blockIdx.x * (long)TPB + threadIdx.x; i < total; i += (long)gridDim.x * TPB) {
         const float p = pred[i];
-        if (mode != 1) {  // 0: [real; fake], 2: real only, 3: fake only
-            if (mode == 2 || (mode == 0 && i < n)) {
+        if (mode == 0) {  // [real; fake]
+            if (i < n) {
                 const float t = 1.f - p;
                 acc += t > 0.f ? t : 0.f;
                 grad[i] = t > 0.f ? -0.5f * inv * scale : 0.f;
@@ -53,7 +53,7 @@ __global__ __launch_bounds__(TPB) void hinge_kernel(const float* __restrict__ pr
             grad[i] = -scale * inv;
         }
     }
-    block_add(loss, mode != 1 ? 0.5f * acc * inv * scale : -acc * inv * scale);
+    block_add(loss, mode == 0 ? 0.5f * acc * inv * scale : -acc * inv * scale);
 }
 
 template <typename T>
@@ -413,7 +413,7 @@ int ssim_launch(const float* a, const float* b, int N, int H, int W, int C, floa
 
 extern "C" int irgan_hinge(const float* pred, int32_t n_half, int32_t mode, float scale, float* grad, double* loss,
                            irgan_stream_t s) {
-    if (mode < 0 || mode > 3) return IRGAN_EINVAL;
+    if (mode != 0 && mode != 1) return IRGAN_EINVAL;
     long total = mode == 0 ? 2L * n_half : n_half;
     hinge_kernel<<<nblocks_red(total), TPB, 0, (hipStream_t)s>>>(pred, n_half, mode, scale, grad, loss);
     IRGAN_LAUNCH_CHECK();

@@ -478,7 +478,8 @@ class GeneratorEngine:
             [p for pr in self.res for p in pr] + ([self.up1_up, self.up2_up] if no_antialias_up else [])
         # fp8 on down2 / up1_conv too (ir:477-482, 557-558): their operands come from the
         # fused resamplers (x1 from down1's Downsample, the up-sampled bottleneck)
-        self.fp8_ud = self.fp8 and not no_antialias and not no_antialias_up
+        # (their kernels take 128-channel K chunks: down2's Cin = 2*ngf must be a multiple of 128)
+        self.fp8_ud = self.fp8 and not no_antialias and not no_antialias_up and c1 % 128 == 0
         if self.fp8:
             # weight images 4b..4b+3: conv1 fwd, conv1 dgrad, conv2 fwd, conv2 dgrad of block b;
             # 4n..4n+3: down2 fwd, down2 dgrad, up1_conv fwd, up1_conv dgrad.
@@ -488,8 +489,9 @@ class GeneratorEngine:
             ud = [self.down2.fwd, self.down2.dg[0][2], self.up1.fwd, self.up1.dg[0][2]] if self.fp8_ud else []
             self.f8w = ops.Fp8Weights([im for p1, p2 in self.res for im in (p1.fwd, p1.dg[0][2], p2.fwd,
                                                                              p2.dg[0][2])] + ud, store.device)
-            self.f8a = ops.Fp8Acts(4 * n_blocks + 3, store.device)
+            self.f8a = ops.Fp8Acts(4 * n_blocks + 4, store.device)
             self.s_cat, self.s_dz3, self.s_dz2 = 4 * n_blocks, 4 * n_blocks + 1, 4 * n_blocks + 2
+            self.s_x1 = 4 * n_blocks + 3   # down2's own x1 copy on the calibration step
         n_in = 5 + 2 * n_blocks
         self.norms = {k: make_norm(norm) for k in ["inc", "down1", "down2", "up1", "up2"] +
                       [f"r{b}_{i}" for b in range(n_blocks) for i in (1, 2)]}
@@ -536,6 +538,21 @@ class GeneratorEngine:
         H2, W2 = (H1 - 1) // 2 + 1, (W1 - 1) // 2 + 1
         return H1, W1, H2, W2
 
+    def fp8_layers(self, B, H, W):
+        """(resblocks, down2 / up1_conv) on e4m3 for a (B, H, W) input: the fp8 conv fuses the
+        InstanceNorm partials of at most IN_PARTS 16x16 output tiles per image and addresses
+        fewer than 2^30 operand bytes (irgan_conv_fwd_fp8); a size beyond either runs that
+        group on the bf16 kernels for this call (no EUNSUPPORTED mid-step)."""
+        if not self.fp8:
+            return False, False
+        H1, W1, H2, W2 = self._dims(H, W)
+        c1, c2 = 2 * self.ngf, 4 * self.ngf
+
+        def ok(h, w, cin):
+            return -(-h // 16) * -(-w // 16) <= ops.IN_PARTS and B * h * w * cin < (1 << 30)
+        res = ok(H2, W2, c2)
+        return res, res and self.fp8_ud and ok(H1, W1, c2 + c1)
+
     def forward(self, ir_nchw: torch.Tensor, bufs: Buffers = None, training: bool = None) -> torch.Tensor:
         """ir (B, input_nc, H, W) fp32 in [-1,1] -> fake NHWC fp32 (B, H, W, 3).
         Activations land in ``bufs`` (default: the engine's own set).  ``training``
@@ -558,10 +575,17 @@ class GeneratorEngine:
         cat1 = g.get("cat1", (B, H1, W1, c2 + c1), T)     # [up1 out | x1]
         x0 = Feat(cat2, c1, c0)
         x1 = Feat(cat1, c2, c1)
-        A = self.f8a if self.fp8 else None
-        cat1_8 = Feat(g.get("cat1_8", (B, H1, W1, c2 + c1), torch.float8_e4m3fn)) if self.fp8_ud else None
-        x1_8 = cat1_8.sl(c2, c1) if self.fp8_ud else None
-        calib = self.fp8_ud and not A.seen[self.s_cat]   # first step: current scaling
+        f8, ud = self.fp8_layers(B, H, W)
+        g.state["fp8"] = (f8, ud)
+        A = self.f8a if f8 else None
+        cat1_8 = Feat(g.get("cat1_8", (B, H1, W1, c2 + c1), torch.float8_e4m3fn)) if ud else None
+        # first step (current scaling): down2 reads its own copy of x1, scaled from x1 alone,
+        # for its forward AND its weight gradient; up1_conv's concat is then scaled as a whole
+        calib = ud and not A.seen[self.s_cat]
+        g.state["fp8_calib"] = calib
+        x1_8 = Feat(g.get("x1_8c", (B, H1, W1, c1), torch.float8_e4m3fn)) if calib else \
+            (cat1_8.sl(c2, c1) if ud else None)
+        dq_x1 = (A.dqp(self.s_x1) if calib else A.dqp(self.s_cat)) if ud else None
         # inc: reflect-pad 3, conv7x7, IN, ReLU  (ir:458-463)
         z0 = Feat(g.get("z0", (B, H, W, c0), T))
         ops.conv_fwd(self.inc, ir_t, z0)
@@ -574,9 +598,9 @@ class GeneratorEngine:
         else:
             z1 = Feat(g.get("z1", (B, H, W, c1), T))
             self.norms["down1"].resample_fwd(g, "down1", self.down1, x0, z1, "a1", ACT_RELU, x1, ops.blur_down_in,
-                                             ops.blur_down, q8=A.spec(self.s_cat, x1_8) if self.fp8_ud else None)
+                                             ops.blur_down, q8=A.spec(self.s_cat, x1_8) if ud and not calib else None)
             if calib:
-                A.quant(self.s_cat, x1, x1_8)   # down2's operand scaled from x1 alone on the first step
+                A.calibrate(self.s_x1, x1, x1_8)   # down2's operand scaled from x1 alone on the first step
         # down2 (+ blur-down)  (ir:477-482)
         h = Feat(g.get("h0", (B, H2, W2, c2), T))
         if self.no_aa:
@@ -587,20 +611,20 @@ class GeneratorEngine:
             z2 = Feat(g.get("z2", (B, H1, W1, c2), T))
             self.norms["down2"].resample_fwd(g, "down2", self.down2, x1, z2, "a2", ACT_RELU, h, ops.blur_down_in,
                                              ops.blur_down, conv8=(*self._w8(4 * self.n_blocks), x1_8,
-                                                                   A.dqp(self.s_cat)) if self.fp8_ud else None)
+                                                                   dq_x1) if ud else None)
         # 9 ResnetBlocks  (ir:362-418, 485-490)
         # fp8: one e4m3 operand buffer, written by the producer of each conv input (the
         # IN passes, fused; h_0 from blur-down by a quantise launch) and read by the conv
         # (one buffer per conv input slot: the fp8 weight gradients of the backward read them)
         x8s = [Feat(g.get(f"x8_{k}", (B, H2, W2, c2), torch.float8_e4m3fn)) for k in range(2 * len(self.res))] \
-            if self.fp8 else None
-        if self.fp8:
+            if f8 else None
+        if f8:
             A.quant(0, h, x8s[0])
         nres = len(self.res)
         for b, (p1, p2) in enumerate(self.res):
             r1 = Feat(g.get(f"r1_{b}", (B, H2, W2, c2), T))
             t = Feat(g.get(f"t{b}", (B, H2, W2, c2), T))
-            if self.fp8:
+            if f8:
                 self.norms[f"r{b}_1"].conv_fwd8(g, f"r{b}_1", p1, *self._w8(4 * b), x8s[2 * b], A.dqp(2 * b), r1, t,
                                                 ACT_RELU, q8=A.spec(2 * b + 1, x8s[2 * b + 1]))
                 A.ensure(2 * b + 1, t, x8s[2 * b + 1])
@@ -608,7 +632,7 @@ class GeneratorEngine:
                 self.norms[f"r{b}_1"].conv_fwd(g, f"r{b}_1", p1, self._res_in(g, f"xp1_{b}", h), r1, t, ACT_RELU)
             r2 = Feat(g.get(f"r2_{b}", (B, H2, W2, c2), T))
             hn = Feat(g.get(f"h{b + 1}", (B, H2, W2, c2), T))
-            if self.fp8:
+            if f8:
                 nxt = 2 * b + 2 if b + 1 < nres else None   # the next block's conv1 input
                 self.norms[f"r{b}_2"].conv_fwd8(g, f"r{b}_2", p2, *self._w8(4 * b + 2), x8s[2 * b + 1],
                                                 A.dqp(2 * b + 1), r2, hn, ACT_NONE, res=h,
@@ -623,7 +647,7 @@ class GeneratorEngine:
                 self.norms[f"r{b}_2"].conv_fwd(g, f"r{b}_2", p2, self._res_in(g, f"xp2_{b}", t2), r2, hn, ACT_NONE,
                                                res=h)
             h = hn
-        if self.fp8:
+        if f8:
             self.f8a.snapshot(0, 2 * self.n_blocks)  # the scales x8s were made with (fp8 weight gradients)
             self.f8a.update(0, 2 * self.n_blocks)    # next step's forward scales
         # up1 -> cat with x1 -> conv/IN/ReLU  (ir:554-558)
@@ -634,7 +658,7 @@ class GeneratorEngine:
         if self.no_aa_up:
             self._convt(self.up1_up, h, y1, g, "ut1")
         else:
-            ops.upsample(h, y1, q8=A.spec(self.s_cat, cat1_8.sl(0, c2)) if self.fp8_ud and not calib else None)
+            ops.upsample(h, y1, q8=A.spec(self.s_cat, cat1_8.sl(0, c2)) if ud and not calib else None)
         if calib:   # up1_conv's operand scaled from the whole concat on the first step
             A.calibrate(self.s_cat, Feat(cat1), cat1_8)
         z3 = Feat(g.get("z3", (B, H1, W1, c1), T))
@@ -647,8 +671,8 @@ class GeneratorEngine:
         else:
             self.norms["up1"].resample_fwd(g, "up1", self.up1, Feat(cat1), z3, "a3", ACT_RELU, y2, ops.upsample_in,
                                            ops.upsample, conv8=(*self._w8(4 * self.n_blocks + 2), cat1_8,
-                                                                A.dqp(self.s_cat)) if self.fp8_ud else None)
-        if self.fp8_ud:
+                                                                A.dqp(self.s_cat)) if ud else None)
+        if ud:
             A.snapshot(self.s_cat, 1)   # the scale cat1_8 was made with (the weight gradients)
             A.update(self.s_cat, 1)
         z4 = Feat(g.get("z4", (B, H, W, c0), T))
@@ -726,21 +750,22 @@ class GeneratorEngine:
         else:
             ops.upsample_bwd(dy2, da3)
         # up1_conv
-        A, nb4 = (self.f8a, 4 * self.n_blocks) if self.fp8 else (None, 0)
-        cat1_8 = Feat(g.d["cat1_8"]) if self.fp8_ud else None
+        f8, ud = g.state.get("fp8", (False, False))
+        A, nb4 = (self.f8a, 4 * self.n_blocks) if f8 else (None, 0)
+        cat1_8 = Feat(g.d["cat1_8"]) if ud else None
 
-        def wg8(pc, key, x8, xslot, dy8, dslot, x, dy):
-            """weight gradient on the fp8 copies (x8 with the scale it was made with, dy8);
-            bf16 where the kernel does not take the layer"""
-            if not ops.conv_wgrad_fp8(pc.spec, x8, dy8, A.dqp_used(xslot), A.dqp(dslot), S.krsc(key + ".weight", G)):
+        def wg8(pc, key, x8, dqx, dy8, dslot, x, dy):
+            """weight gradient on the fp8 copies (x8 with the scale ``dqx`` it was made with,
+            dy8); bf16 where the kernel does not take the layer"""
+            if not ops.conv_wgrad_fp8(pc.spec, x8, dy8, dqx, A.dqp(dslot), S.krsc(key + ".weight", G)):
                 wg(pc, key, x, dy)
-        da3_8 = Feat(g.get("dz3_8", (B, H1, W1, c1), torch.float8_e4m3fn)) if self.fp8_ud else None
+        da3_8 = Feat(g.get("dz3_8", (B, H1, W1, c1), torch.float8_e4m3fn)) if ud else None
         self.norms["up1"].bwd(g, "up1", da3, Feat(g.d["z3"]), ACT_RELU, da3, db=self._bgrad("up1_conv.0.bias"),
-                              q8=A.spec(self.s_dz3, da3_8) if self.fp8_ud else None)
+                              q8=A.spec(self.s_dz3, da3_8) if ud else None)
         dcat1 = Feat(g.get("dcat1", (B, H1, W1, c2 + c1), T))
-        if self.fp8_ud:
+        if ud:
             A.ensure(self.s_dz3, da3, da3_8)
-            wg8(self.up1, "up1_conv.0", cat1_8, self.s_cat, da3_8, self.s_dz3, cat1, da3)
+            wg8(self.up1, "up1_conv.0", cat1_8, A.dqp_used(self.s_cat), da3_8, self.s_dz3, cat1, da3)
             ops.conv_dgrad_fp8(self.up1, *self._w8(nb4 + 3), da3_8, A.dqp(self.s_dz3), da3, dcat1)
         else:
             wg(self.up1, "up1_conv.0", cat1, da3)
@@ -757,7 +782,7 @@ class GeneratorEngine:
         # resblocks, reversed: dh holds d h_{b+1}; becomes d h_b in place
         dt_ = Feat(g.get("dtmp", (B, H2, W2, c2), T))
         nb2 = 2 * self.n_blocks
-        dy8 = Feat(g.get("dy8", (B, H2, W2, c2), torch.float8_e4m3fn)) if self.fp8 else None
+        dy8 = Feat(g.get("dy8", (B, H2, W2, c2), torch.float8_e4m3fn)) if f8 else None
         k1, k2 = self.res_keys
         for b in reversed(range(self.n_blocks)):
             p1, p2 = self.res[b]
@@ -771,11 +796,11 @@ class GeneratorEngine:
             xin2 = Feat(g.d[f"xp2_{b}"]) if self.padding_type == "replicate" else t2
             s2, s1 = nb2 + 2 * b, nb2 + 2 * b + 1
             self.norms[f"r{b}_2"].bwd(g, f"r{b}_2", dh, r2, ACT_NONE, dt_, db=self._bgrad(f"{key}{k2}.bias"),
-                                      q8=A.spec(s2, dy8) if self.fp8 else None)
+                                      q8=A.spec(s2, dy8) if f8 else None)
             dr = Feat(g.get("dtmp2", (B, H2, W2, c2), T))
-            if self.fp8:
+            if f8:
                 A.ensure(s2, dt_, dy8)
-                wg8(p2, f"{key}{k2}", Feat(g.d[f"x8_{2 * b + 1}"]), 2 * b + 1, dy8, s2, xin2, dt_)
+                wg8(p2, f"{key}{k2}", Feat(g.d[f"x8_{2 * b + 1}"]), A.dqp_used(2 * b + 1), dy8, s2, xin2, dt_)
                 ops.conv_dgrad_fp8(p2, *self._w8(4 * b + 3), dy8, A.dqp(s2), dt_, dr)
             else:
                 self._res_dgrad(g, p2, dt_, dr, False, padbuf)
@@ -783,16 +808,16 @@ class GeneratorEngine:
                 if drop:   # backward of the dropout: the same mask and scale on the gradient
                     ops.dropout(dr, dr, g.state["dropout_seed"] + 2 * b)
             self.norms[f"r{b}_1"].bwd(g, f"r{b}_1", dr, r1, ACT_RELU, dr, db=self._bgrad(f"{key}{k1}.bias"),
-                                      q8=A.spec(s1, dy8) if self.fp8 else None)
-            if self.fp8:
+                                      q8=A.spec(s1, dy8) if f8 else None)
+            if f8:
                 A.ensure(s1, dr, dy8)
-                wg8(p1, f"{key}{k1}", Feat(g.d[f"x8_{2 * b}"]), 2 * b, dy8, s1, xin1, dr)
+                wg8(p1, f"{key}{k1}", Feat(g.d[f"x8_{2 * b}"]), A.dqp_used(2 * b), dy8, s1, xin1, dr)
                 ops.conv_dgrad_fp8(p1, *self._w8(4 * b + 1), dy8, A.dqp(s1), dr, dh, accumulate=True)
             else:
                 self._res_dgrad(g, p1, dr, dh, True, padbuf)
                 wg(p1, f"{key}{k1}", xin1, dr)
             ready(f"{key}{k1}.weight")
-        if self.fp8:
+        if f8:
             self.f8a.update(nb2, nb2)   # next step's backward-data scales
         # down2 (+ blur-down)
         z2 = Feat(g.d["z2"])
@@ -802,13 +827,16 @@ class GeneratorEngine:
         else:
             dz2 = Feat(g.get("da2", (B, H1, W1, c2), T))
             ops.blur_down_bwd(dh, dz2)
-            dz2_8 = Feat(g.get("dz2_8", (B, H1, W1, c2), torch.float8_e4m3fn)) if self.fp8_ud else None
+            dz2_8 = Feat(g.get("dz2_8", (B, H1, W1, c2), torch.float8_e4m3fn)) if ud else None
             self.norms["down2"].bwd(g, "down2", dz2, z2, ACT_RELU, dz2, db=self._bgrad("down2.0.bias"),
-                                    q8=A.spec(self.s_dz2, dz2_8) if self.fp8_ud else None)
+                                    q8=A.spec(self.s_dz2, dz2_8) if ud else None)
         dx1 = dcat1.sl(c2, c1)
-        if self.fp8_ud:
+        if ud:
             A.ensure(self.s_dz2, dz2, dz2_8)
-            wg8(self.down2, "down2.0", cat1_8.sl(c2, c1), self.s_cat, dz2_8, self.s_dz2, x1, dz2)
+            if g.state.get("fp8_calib"):   # the calibration step's own x1 copy (as its forward read)
+                wg8(self.down2, "down2.0", Feat(g.d.pop("x1_8c")), A.dqp(self.s_x1), dz2_8, self.s_dz2, x1, dz2)
+            else:
+                wg8(self.down2, "down2.0", cat1_8.sl(c2, c1), A.dqp_used(self.s_cat), dz2_8, self.s_dz2, x1, dz2)
             ops.conv_dgrad_fp8(self.down2, *self._w8(nb4 + 1), dz2_8, A.dqp(self.s_dz2), dz2, dx1, accumulate=True)
             A.update(self.s_dz3, 2)   # next step's scales of the two dY slots
         else:

@@ -249,13 +249,9 @@ def test_losses(ops):
     ld.backward()
     assert abs(loss[3].item() - ld.item()) < 1e-6
     assert relerr(gp.cpu(), pr.grad) < 1e-6
-    # the D step's halves apart (modes 2 / 3, GANStep: real half beside the G forward): the
-    # same gradient bits as mode 0 on [real; fake], the loss to fp32 summation order
-    gr, gf = torch.empty_like(pd[:50]), torch.empty_like(pd[50:])
-    ops.hinge(pd[:50].contiguous(), 50, 2, 1.0, gr, loss[4:5])
-    ops.hinge(pd[50:].contiguous(), 50, 3, 1.0, gf, loss[4:5])
-    assert torch.equal(torch.cat([gr, gf]), gp)
-    assert abs(loss[4].item() - ld.item()) < 1e-6
+    # modes other than 0 / 1 are refused (the split D-step modes were removed)
+    with pytest.raises(Exception):
+        ops.hinge(pd[:50].contiguous(), 50, 2, 1.0, gp[:50], loss[4:5])
 
 
 @pytest.mark.parametrize("count", [1 << 20, 1001])

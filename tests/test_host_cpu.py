@@ -56,6 +56,18 @@ def test_stale_library_raises_on_load(monkeypatch):
         irc._lib.load()
 
 
+def test_library_only_deployment_skips_the_source_check(monkeypatch, tmp_path):
+    """A deployment with libirgan.so, the Python files and include/irgan.h but no csrc/
+    loads with a warning instead of failing on the missing sources."""
+    irc = pkg()
+    irc._lib.load()
+    monkeypatch.setattr(irc._lib, "_lib", None)
+    monkeypatch.setattr(irc._build, "CSRC", str(tmp_path / "no_csrc"))
+    assert irc._lib.tree_id() is None
+    with pytest.warns(RuntimeWarning, match="not checked"):
+        irc._lib.load()
+
+
 def _dense(kind, n, p=0, transpose=False):
     irc = pkg()
     T = 8

@@ -32,7 +32,7 @@ def t(fn, it=20):
     return a.elapsed_time(b) / it
 import argparse
 ap = argparse.ArgumentParser()
-ap.add_argument("--case", default=None, help="substring filter on case names")
+ap.add_argument("--case", default=None, help="comma list of substring filters on case names")
 ap.add_argument("--which", default="fwd,dgrad,wgrad")
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--batch", type=int, default=16)
@@ -41,7 +41,7 @@ args = ap.parse_args()
 B = args.batch
 res = {}
 for name, cin, cout, k, s, p, mode, H in CASES:
-    if args.case and args.case not in name:
+    if args.case and not any(c in name for c in args.case.split(",")):
         continue
     spec = ops.ConvSpec(cin, cout, k, s, p, mode)
     w = torch.randn(cout * k * k * cin, device=DEV) * 0.05
