@@ -343,6 +343,13 @@ IRGAN_API int irgan_sep_resample_fp8(const void* in, int32_t in_dtype, int32_t N
                            const int32_t* tx, const float* wx, int32_t Tx, void* y8, int32_t ld8,
                            int32_t off8, const float* q, uint32_t* amax, irgan_stream_t s);
 /* 2x2 max pool (VGG features) forward / backward (first max wins, as ATen). */
+/* VGG conv + ReLU + MaxPool2d(2) in one launch (ir:664: vgg16.features[:16] conv1_2 -> pool):
+ * y (NULL: not written) = act(conv(x) + bias) as irgan_conv_fwd, yp = its 2x2 max-pool, dense
+ * NHWC [N][Ho/2][Wo/2][Cout] bf16 -- bit-identical to irgan_conv_fwd + irgan_maxpool_fwd.
+ * IRGAN_EUNSUPPORTED (nothing launched) unless bf16 3x3 stride 1 with Cin == 64, even Ho, Wo,
+ * no accumulate / mask. */
+IRGAN_API int irgan_conv_fwd_pool(const irgan_conv_desc* d, const void* x, const void* w, const float* bias,
+                                  void* y, void* yp, irgan_stream_t s);
 IRGAN_API int irgan_maxpool_fwd(const void* x, int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t C,
                       void* y, irgan_stream_t s);
 IRGAN_API int irgan_maxpool_bwd(const void* x, const void* dy, int32_t dtype, int32_t N, int32_t H,

@@ -5,8 +5,8 @@
 // conv_res64.hip: the resident-weight persistent kernel for one input chunk (Cin == 64)
 namespace irgan_res64 {
 bool ok(const irgan_conv_desc* d);
-void launch(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y, const void* mask,
-            float2* part, hipStream_t st);
+int launch(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y, const void* mask,
+           float2* part, hipStream_t st, void* ypool = nullptr);
 }  // namespace irgan_res64
 
 namespace {
@@ -20,9 +20,27 @@ constexpr bool split128(int) { return true; }
 // Output-channel tile for a Cout % 256 == 0 layer: 256 unless that leaves most CUs idle
 // (the PatchGAN 4x4 layers at 32x32: D model.8 backward-data at B = 16 is 64 BN-256 blocks
 // for 256 CUs) -- then 128 or the 64-channel single-halo tile (two blocks per CU)
+//
+// Round 6: also when BN-256 blocks fill the CUs but end in a mostly empty last round -- the
+// 128 x 160 ResnetBlock maps of 512 x 640 at B = 4 (config 4) are 320 BN-256 blocks, two
+// rounds for 1.25 rounds of work.  Rounds are priced as measured at B = 16 / 32
+// (a round of BN-128 blocks, or of two BN-64 blocks per CU, takes 0.575
+// of a BN-256 round); BN-128 is taken when it is >= 10 % cheaper.  PP_BN_MODEL=0 builds the
+// round-5 rule alone (A/B variants).
+#ifndef PP_BN_MODEL
+#define PP_BN_MODEL 1
+#endif
 int narrow_bn(const irgan_conv_desc* d) {
     const long patches = (long)d->N * irgan_cdiv(d->Ho, PH) * irgan_cdiv(d->Wo, PW);
-    if (patches * (d->Cout / 256) >= 160) return 256;
+    if (patches * (d->Cout / 256) >= 160) {
+        if (PP_BN_MODEL) {
+            const long cus = irgan_cu_count();
+            const long r256 = irgan_cdiv(patches * (d->Cout / 256), cus);
+            const long r128 = irgan_cdiv(patches * (d->Cout / 128), cus);
+            if (r128 * 0.575 <= 0.9 * r256) return 128;
+        }
+        return 256;
+    }
     return patches * (d->Cout / 128) >= 160 ? 128 : 64;
 }
 
@@ -223,9 +241,8 @@ extern "C" int irgan_conv_fwd_stats(const irgan_conv_desc* d, const void* x, con
     const int blocks = d->N * tpy * tpx * ntn;
     hipStream_t st = (hipStream_t)s;
     if (irgan_res64::ok(d)) {
-        irgan_res64::launch(d, x, w, bias, y, nullptr, (float2*)part, st);
+        *nb = irgan_res64::launch(d, x, w, bias, y, nullptr, (float2*)part, st);
         IRGAN_LAUNCH_CHECK();
-        *nb = tpx * tpy;
         return 0;
     }
 #define PPS(KHV, BNV, ONEV, ...)                                                                                   \
@@ -248,6 +265,24 @@ extern "C" int irgan_conv_fwd_stats(const irgan_conv_desc* d, const void* x, con
 #undef PPS
     IRGAN_LAUNCH_CHECK();
     *nb = tpx * tpy;
+    return 0;
+}
+
+// Forward conv + activation + 2x2 max-pool in one launch (the VGG features[:16] conv1_2 ->
+// MaxPool2d(2), ir:664): y (may be NULL: the pooled map alone) gets the activated map, yp the
+// pooled one, dense [N][Ho / 2][Wo / 2][Cout] bf16 -- the bits of irgan_conv_fwd +
+// irgan_maxpool_fwd.  IRGAN_EUNSUPPORTED unless the layer takes the resident-weight kernel
+// (one 64-channel input chunk, 3x3 stride 1) with even Ho, Wo and a plain output.
+extern "C" int irgan_conv_fwd_pool(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
+                                   void* yp, irgan_stream_t s) {
+    if (!d || !x || !w || !yp) return IRGAN_EINVAL;
+    if ((long)d->N * d->Ho * d->Wo <= 0) return 0;
+    if (!irgan_res64::ok(d) || d->accumulate || d->mask_act || d->Ho % 2 || d->Wo % 2 || d->Ho != d->OH ||
+        d->Wo != d->OW || d->omy != 1 || d->omx != 1 || d->ooy || d->oox ||
+        (long)d->N * (d->Ho / 2) * (d->Wo / 2) * d->Cout * 2 >= (1L << 31))
+        return IRGAN_EUNSUPPORTED;
+    irgan_res64::launch(d, x, w, bias, y, nullptr, nullptr, (hipStream_t)s, yp);
+    IRGAN_LAUNCH_CHECK();
     return 0;
 }
 

@@ -50,17 +50,34 @@ constexpr int R64_HB = R64_HP * 1024;
 constexpr int R64_WB = 9 * 64 * 128;
 constexpr int R64_LDS = R64_WB + 2 * R64_HB + 8 * 64 * 8;
 
-// ONEB (no STATS): one barrier per patch -- the next-but-one halo is issued at the top of the
-// following iteration instead of after a second, post-K-loop barrier
-template <bool ACC, bool STATS, bool ONEB = false>
+// ONEB: one barrier per patch -- the next-but-one halo is issued at the top of the following
+// iteration instead of after a second, post-K-loop barrier.
+// RUN (round 6): the block walks a CONTIGUOUS run of `runk` patches (q0 .. q0 + runk - 1) instead
+// of every qs-th patch.  With STATS each lane then keeps its two reduce-scattered channel sums
+// (sum, sum of squares) in registers over the whole run; they are summed across the 8 waves
+// (stats rows in LDS) only where the run ends or crosses into the next image -- one partial
+// row per (image, run) instead of per patch -- so the per-patch stats rows and the post-K-loop
+// barrier are gone and STATS runs the ONEB schedule.  Runs align with the
+// images (runk divides the patches per image, or is a multiple of them): row = run index, or
+// the image when a run covers whole images.
+// POOL (round 6): the epilogue also writes the 2x2 max-pool of the activated output (VGG
+// conv1_2 -> pool, ir:664 features[:16]): a wave's two patch rows are one pooled row, the two
+// columns of a window sit in lanes px and px ^ 1.  y == nullptr: the pooled map alone (the
+// real images' half, whose pre-pool activations nothing reads).  Max of the fp32 values then
+// one bf16 rounding == max of the rounded values (rounding is monotone): the bits of
+// irgan_maxpool_fwd over the stored map.
+template <bool ACC, bool STATS, bool ONEB = false, bool RUN = false, bool POOL = false>
 __global__ __launch_bounds__(512, 1) void conv_res64_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
                                                            const bf16_t* __restrict__ w,
                                                            const float* __restrict__ bias, bf16_t* __restrict__ y,
                                                            const bf16_t* __restrict__ mask, int ntn, int tpx,
-                                                           int tpy, float2* __restrict__ part, int xcdg) {
+                                                           int tpy, float2* __restrict__ part, int xcdg, int runk,
+                                                           bf16_t* __restrict__ ypool) {
     constexpr int TAPS = 9, HWd = PW + 2, HROWS = (PH + 2) * HWd, MI = 2, NJ = 4, Kw = TAPS * 64;
     static_assert(HROWS <= R64_HP * 8 && R64_HP * 8 - HROWS < 8, "halo pieces");
-    static_assert(!(ONEB && STATS), "the stats rows need the post-loop barrier");
+    static_assert(!(ONEB && STATS && !RUN), "per-patch stats rows need the post-loop barrier");
+    static_assert(!RUN || ONEB, "runs use the one-barrier schedule");
+    static_assert(!POOL || (ONEB && !ACC && !STATS), "pooling: plain forward");
     __shared__ __attribute__((aligned(1024))) char smem[R64_LDS];
     char* const sW = smem;
     char* const sH = smem + R64_WB;
@@ -82,6 +99,10 @@ __global__ __launch_bounds__(512, 1) void conv_res64_kernel(const irgan_conv_des
         q0 = blockIdx.x / ntn;
     }
     const int P = d.N * tpy * tpx;
+    const int tpi = tpx * tpy;
+    const int pstep = RUN ? 1 : qs;                          // patch sequence q0, q0 + pstep, ...
+    const int pend = RUN ? min(P, (q0 + 1) * runk) : P;
+    if (RUN) q0 *= runk;                                     // run index -> its first patch
     const int n0 = nt * 64;
     const int nh = (R64_HP - wid + 7) >> 3;  // halo pieces of this wave: 6 (wave 0) or 5
     const int sub = lane >> 3;
@@ -122,8 +143,8 @@ __global__ __launch_bounds__(512, 1) void conv_res64_kernel(const irgan_conv_des
 #pragma unroll
         for (int u = 0; u < TAPS; ++u) blds16(wr, off, (uint32_t)(u * 128), sW + (u * 8 + wid) * 1024);
     }
-    if (q0 < P) issue_halo(q0, 0);
-    if (q0 + qs < P) issue_halo(q0 + qs, 1);
+    if (q0 < pend) issue_halo(q0, 0);
+    if (q0 + pstep < pend) issue_halo(q0 + pstep, 1);
 
     const int prow = wid * 2;
     const int g0 = lane >> 4;
@@ -142,12 +163,19 @@ __global__ __launch_bounds__(512, 1) void conv_res64_kernel(const irgan_conv_des
     // output through a raw buffer resource: exactly MI * NJ store instructions per wave and
     // patch (a pixel outside the image gets the out-of-range offset and is dropped), so the
     // counted vmcnt at the top of the loop knows how many of its ops are younger than a halo
+    const bool yfull = !POOL || y != nullptr;
     const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(
-        y, (short)0, (int)((long)d.N * d.OH * d.OW * d.ldy * 2), 0x00020000);
-    constexpr int NST = MI * NJ;
+        yfull ? y : ypool, (short)0, yfull ? (int)((long)d.N * d.OH * d.OW * d.ldy * 2) : 0, 0x00020000);
+    // pooled map: [N][Ho / 2][Wo / 2][Cout] bf16, dense
+    const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(
+        POOL ? ypool : y, (short)0, POOL ? (int)((long)d.N * (d.Ho / 2) * (d.Wo / 2) * d.Cout * 2) : 0, 0x00020000);
+    // stores per wave and patch (the counted vmcnt at the top of the loop)
+    const int NST = (yfull ? MI * NJ : 0) + (POOL ? NJ : 0);
     int it = 0;
+    int flushed = 0;          // RUN && STATS: the previous patch ended with a partial-row store
+    float2 racc = make_float2(0.f, 0.f);  // RUN && STATS: this lane's two sums over the run so far
 #pragma unroll 1
-    for (int p = q0; p < P; p += qs, ++it) {
+    for (int p = q0; p < pend; p += pstep, ++it) {
         const int buf = it & 1;
         // VMEM ops issued after this patch's halo, in issue order: (it >= 2) the stats
         // store of patch it-2 (made at the top of it-1), the stores of patch it-1, the halo
@@ -155,9 +183,10 @@ __global__ __launch_bounds__(512, 1) void conv_res64_kernel(const irgan_conv_des
         // (ONEB: halo it+1 was issued at the top of iteration it-1, so only patch it-1's stores
         // are younger from it == 1 on)
         {
-            const int nxt = p + qs < P ? nh : 0;
+            const int nxt = p + pstep < pend ? nh : 0;
             const int younger = it == 0 ? nxt
-                                        : (ONEB ? NST : (it == 1 ? NST + nxt : (STATS ? 1 : 0) + NST + nxt));
+                                        : (ONEB ? NST + flushed
+                                                : (it == 1 ? NST + nxt : (STATS ? 1 : 0) + NST + nxt));
             wait_vm_dyn(__builtin_amdgcn_readfirstlane(younger));
         }
         lds_barrier();  // every wave's pieces of this patch's halo (and the weights) landed
@@ -184,9 +213,9 @@ __global__ __launch_bounds__(512, 1) void conv_res64_kernel(const irgan_conv_des
         }
         // ONEB: every wave has also finished patch it-1 (K loop and stores), so its halo buffer
         // takes patch it+1's halo now
-        const bool halo_next = ONEB && it > 0 && p + qs < P;
-        if (halo_next) issue_halo(p + qs, buf ^ 1);
-        if constexpr (STATS) {
+        const bool halo_next = ONEB && it > 0 && p + pstep < pend;
+        if (halo_next) issue_halo(p + pstep, buf ^ 1);
+        if constexpr (STATS && !RUN) {
             // patch it-1's partials: its 8 wave rows are complete (written before this barrier)
             if (it > 0 && lane < 8) {
                 const int c = wid * 8 + lane;
@@ -240,6 +269,7 @@ __global__ __launch_bounds__(512, 1) void conv_res64_kernel(const irgan_conv_des
         float st[2 * NJ * 4];  // STATS: (sum, sum of squares) of channel (j, r) at [2 (4j + r) + {0, 1}]
 #pragma unroll
         for (int k = 0; k < 2 * NJ * 4; ++k) st[k] = 0.f;
+        float pmx[POOL ? NJ : 1][4];  // POOL: row prow's activated values, per (j, r)
         auto body = [&](auto actc) {
             constexpr int A = decltype(actc)::value;
 #pragma unroll
@@ -267,7 +297,29 @@ __global__ __launch_bounds__(512, 1) void conv_res64_kernel(const irgan_conv_des
                     pk.x = pk_bf16(v[0], v[1]);
                     pk.y = pk_bf16(v[2], v[3]);
                     const int off = ok && !(R64_EXP & 2) ? (int)((pix * d.ldy + d.yoff + co) * 2) : (int)IRGAN_OOB;
-                    __builtin_amdgcn_raw_buffer_store_b64(pk, yr, off, 0, 0);
+                    if (yfull) __builtin_amdgcn_raw_buffer_store_b64(pk, yr, off, 0, 0);
+                    if constexpr (POOL) {
+                        // rows prow, prow + 1 (i = 0, 1) then columns px, px ^ 1 (lane ^ 1)
+                        if (i == 0) {
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) pmx[j][r] = v[r];
+                        } else {
+                            float m[4];
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                m[r] = fmaxf(pmx[j][r], v[r]);
+                                m[r] = fmaxf(m[r], __shfl_xor(m[r], 1, 64));
+                            }
+                            u32x2_t pp;
+                            pp.x = pk_bf16(m[0], m[1]);
+                            pp.y = pk_bf16(m[2], m[3]);
+                            const int oy = pyi * PH + prow, ox = pxi * PW + (lane & 15);
+                            const bool pok = ((lane & 1) == 0) && oy + 1 < d.Ho && ox + 1 < d.Wo;
+                            const long ppix = ((long)img * (d.Ho / 2) + (oy >> 1)) * (d.Wo / 2) + (ox >> 1);
+                            __builtin_amdgcn_raw_buffer_store_b64(pp, pr, pok ? (int)((ppix * d.Cout + co) * 2)
+                                                                              : (int)IRGAN_OOB, 0, 0);
+                        }
+                    }
                     if constexpr (STATS) {
                         if (ok) {
                             const float q[4] = {__uint_as_float(pk.x << 16), __uint_as_float(pk.x & 0xffff0000u),
@@ -301,12 +353,39 @@ __global__ __launch_bounds__(512, 1) void conv_res64_kernel(const irgan_conv_des
                     st[k] = keep + __shfl_xor(send, m, 64);
                 }
             }
-            const int k = lane & 15;
-            sR[wid * 64 + (k >> 2) * 16 + cl0 + (k & 3)] = make_float2(st[0], st[1]);
+        }
+        const int sk = lane & 15;
+        float2* const srow = sR + wid * 64 + (sk >> 2) * 16 + cl0 + (sk & 3);
+        if constexpr (STATS && !RUN) *srow = make_float2(st[0], st[1]);
+        if constexpr (STATS && RUN) {
+            racc.x += st[0];
+            racc.y += st[1];
+            // the run ends, or the next patch is another image's: this (image, run)'s partial row
+            const int img_p = p / tpi;
+            flushed = 0;
+            if (p + pstep >= pend || (p + pstep) / tpi != img_p) {
+                *srow = racc;
+                lds_barrier();  // every wave's row of the run's sums
+                if (lane < 8) {
+                    const int c = wid * 8 + lane;
+                    float a = 0.f, b = 0.f;
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) {
+                        const float2 e = sR[r * 64 + c];
+                        a += e.x;
+                        b += e.y;
+                    }
+                    const long row = runk <= tpi ? (long)(p / runk) : (long)img_p;
+                    part[row * d.Cout + n0 + c] = make_float2(a, b);
+                }
+                lds_barrier();  // the rows were read before the next flush rewrites them
+                racc = make_float2(0.f, 0.f);
+                flushed = 1;
+            }
         }
         if (!ONEB && p + 2 * qs < P) issue_halo(p + 2 * qs, buf);
     }
-    if constexpr (STATS) {
+    if constexpr (STATS && !RUN) {
         lds_barrier();  // the last patch's stats rows
         if (lane < 8) {
             const int c = wid * 8 + lane;
@@ -341,19 +420,38 @@ static int grid_for(int ntn, int tiles) {
     return g < tiles ? (g > 0 ? g : ntn) : tiles;
 }
 
-// mask: NULL or the bf16 backward mask (8-byte aligned slices: checked by the caller)
-void launch(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y, const void* mask,
-            float2* part, hipStream_t st) {
+// The statistics variant's run length: the smallest k >= the patches one block must take for
+// the grid to fit the CUs, with k | P and (k | patches per image or patches per image | k)
+static int run_len(int P, int tpi, int ntn) {
+    const int cus = irgan_cu_count();
+    const int per = cus / ntn > 0 ? cus / ntn : 1;
+    for (int k = irgan_cdiv(P, per); k < P; ++k)
+        if (P % k == 0 && (tpi % k == 0 || k % tpi == 0)) return k;
+    return P;
+}
+
+// mask: NULL or the bf16 backward mask (8-byte aligned slices: checked by the caller).
+// Returns the InstanceNorm partial rows per image written into part (0 without part).
+int launch(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y, const void* mask,
+           float2* part, hipStream_t st, void* ypool) {
     const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH), ntn = d->Cout / 64;
-    const int grid = grid_for(ntn, d->N * tpx * tpy * ntn);
+    const int P = d->N * tpx * tpy, tpi = tpx * tpy;
+    static const bool per_patch = getenv("IRGAN_R64_PATCH_STATS") != nullptr;  // A/B: round-5 schedule
+    const int runk = part && !per_patch ? run_len(P, tpi, ntn) : 0;
+    const int grid = runk ? ntn * (P / runk) : grid_for(ntn, P * ntn);
     const int xcdg = ntn > 1 && grid % (8 * ntn) == 0;
-#define R64(ACCV, STV, OB)                                                                                          \
-    conv_res64_kernel<ACCV, STV, OB><<<grid, 512, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias,             \
-                                                           (bf16_t*)y, (const bf16_t*)mask, ntn, tpx, tpy, part, xcdg)
-    if (part) R64(false, true, false);
-    else if (d->accumulate) R64(true, false, true);
-    else R64(false, false, true);
+#define R64(ACCV, STV, OB, RN, ...)                                                                                 \
+    conv_res64_kernel<ACCV, STV, OB, RN, ##__VA_ARGS__><<<grid, 512, 0, st>>>(                                        \
+        *d, (const bf16_t*)x, (const bf16_t*)w, bias, (bf16_t*)y, (const bf16_t*)mask, ntn, tpx, tpy, part, xcdg,      \
+        runk, (bf16_t*)ypool)
+    if (ypool) R64(false, false, true, false, true);
+    else if (part && runk) R64(false, true, true, true);
+    else if (part) R64(false, true, false, false);
+    else if (d->accumulate) R64(true, false, true, false);
+    else R64(false, false, true, false);
 #undef R64
+    if (!part) return 0;
+    return runk ? (runk <= tpi ? tpi / runk : 1) : tpi;
 }
 
 }  // namespace irgan_res64

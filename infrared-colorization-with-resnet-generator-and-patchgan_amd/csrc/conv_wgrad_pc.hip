@@ -401,7 +401,7 @@ __global__ __launch_bounds__(W2_NT, 1) void wgrad_w2_kernel(const irgan_conv_des
     const int s_end = min(nseg, s_beg + segs_per_block);
     if (s_beg >= s_end) return;  // block-uniform
     const int nk = s_end - s_beg;
-    const int segs_row = d.Wo / 64;
+    const int segs_row = (d.Wo + 63) / 64;  // the last segment of a row may be partial (Wo % 64)
 
     if (wid >= W2_CW) {
         // ------------------------------------------------------------------ loaders
@@ -423,6 +423,7 @@ __global__ __launch_bounds__(W2_NT, 1) void wgrad_w2_kernel(const irgan_conv_des
                 const int pos = j * 4 + lane / 16, slot = lane % 16;
                 const int c16 = slot ^ (2 * pc_t256(pos));
                 voff[u] = (uint32_t)((pos * d.ldy + c16 * 8) * 2);
+                xpos[u] = pos;   // the dY pixel within the segment (a partial segment zero-fills past Wo)
             } else if (j < W2_TP) {
                 const int jx = j - W2_AP, plane = jx / XPIECES;
                 const int pos = (jx - plane * XPIECES) * 8 + (lane >> 3), slot = lane & 7;
@@ -445,7 +446,7 @@ __global__ __launch_bounds__(W2_NT, 1) void wgrad_w2_kernel(const irgan_conv_des
                 if (u >= np) break;
                 const int j = l + W2_LW * u;
                 if (j < W2_AP) {
-                    blds16(rs_dy, voff[u], dy_soff, base + j * 1024);
+                    blds16(rs_dy, x0 + xpos[u] < d.Wo ? voff[u] : IRGAN_OOB, dy_soff, base + j * 1024);
                 } else {
                     int ix = x0 + d.c0x + xpos[u];
                     if (reflect) ix = reflect_idx(ix, d.W);
@@ -572,17 +573,20 @@ extern "C" int irgan_conv_wgrad_pc(const irgan_conv_desc* d, const void* x, cons
     if ((long)d->N * d->Ho * d->Wo <= 0) return 0;
     const int BMC = d->Cout % 128 == 0 ? 128 : 64;
     const bool pair = d->KW == 4 && d->KH == 4 && d->Wo <= 32 && BMC == 128;
+    // the wide-n kernel takes any Wo: a row's last 64-pixel segment may be partial (its dY
+    // pieces past Wo zero-filled), e.g. the 128 x 160 ResnetBlock maps of 512 x 640 (config 4)
+    const bool w2 = !pair && BMC == 128 && d->KW == 3 && d->Cin % 128 == 0 && splitk <= 0;
     if (d->dtype != IRGAN_BF16 || (d->KW != 3 && !pair) || d->sx != 1 || d->sy != 1 ||
-        d->Cout % BMC || d->Cin % 64 || (d->Wo % 64 && !pair) || d->ldx % 8 || d->xoff % 8 ||
+        d->Cout % BMC || d->Cin % 64 || (d->Wo % 64 && !pair && !w2) || d->ldx % 8 || d->xoff % 8 ||
         d->ldy % 8 || d->yoff % 8 || (long)d->N * d->H * d->W * d->ldx * 2 >= (1L << 31) ||
         (long)d->N * d->Ho * d->Wo * d->ldy * 2 >= (1L << 31))
         return IRGAN_EUNSUPPORTED;
     const int cus = irgan_cu_count();
     const int swz = irgan_xcd_swz();
-    if (!pair && BMC == 128 && d->KW == 3 && d->Cin % 128 == 0 && splitk <= 0) {
+    if (w2) {
         const int ntco = d->Cout / 128, nci2 = d->Cin / 128;
         const int tiles = ntco * nci2 * d->KH;
-        const int nseg = d->N * d->Ho * (d->Wo / 64);
+        const int nseg = d->N * d->Ho * irgan_cdiv(d->Wo, 64);
         int sk = cus / tiles;
         if (sk < 1) sk = 1;
         const int maxs = irgan_cdiv(nseg, 4);

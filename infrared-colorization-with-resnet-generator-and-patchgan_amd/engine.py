@@ -907,9 +907,13 @@ class DiscriminatorEngine:
             x = y
         return x.t
 
-    def backward(self, dout: torch.Tensor, want_wgrad=True, want_dinput=False, tag="", bufs: Buffers = None):
+    def backward(self, dout: torch.Tensor, want_wgrad=True, want_dinput=False, tag="", bufs: Buffers = None,
+                 ready=None):
         """dout: dL/dlogits fp32 (same shape as forward output).  Weight grads
-        accumulate into store.grad; returns d input (fp32 NHWC) if asked."""
+        accumulate into store.grad; returns d input (fp32 NHWC) if asked.
+        ``ready(key)`` (as GeneratorEngine.backward): called once every gradient from layer
+        ``key``'s weight to the end of the flat buffer is final, so the caller's bucketed
+        all-reduce starts on the tail while the earlier layers' backward still runs."""
         g, T, S = bufs or self.bufs, self.tdt, self.store
         acts, pre = g.state[tag]
         G = S.grad
@@ -933,6 +937,8 @@ class DiscriminatorEngine:
                 if bias_sum is not None:
                     ops.channel_sum(bias_sum, S.krsc(key + ".bias", G))
                 ops.conv_wgrad(pc.spec, x, Feat(dy.t, dy.off, pc.spec.cout), S.krsc(key + ".weight", G), self.dtype)
+                if ready is not None:
+                    ready(key + ".weight")
             if i == 0:
                 if not want_dinput:
                     return None
@@ -945,7 +951,6 @@ class DiscriminatorEngine:
             else:
                 ops.conv_dgrad(pc, dy, dx)
             dy = dx
-        join()
         return None
 
 
@@ -972,22 +977,29 @@ class VGGEngine:
             self._pack_batch = ops.PackBatch(self.packs)
         self._pack_batch.run()
 
-    def forward(self, vin: Feat, bufs: Buffers = None, part=None) -> Feat:
+    def forward(self, vin: Feat, bufs: Buffers = None, part=None, keep=True) -> Feat:
         """relu3_3 features of vin.  part = (b0, nb): compute only images [b0, b0+nb)
         into the full-batch activation buffers (the step runs the real and the fake
-        half on different streams)."""
+        half on different streams).  keep=False: no backward will read these images'
+        activations (the real half), so a conv followed by MaxPool2d may write the pooled
+        map alone (ops.conv_fwd_pool)."""
         g, T = bufs or self.bufs, self.tdt
         x = vin
         acts = g.state["acts"] = [vin]
         sl = (lambda f: f) if part is None else (lambda f: f.batch(*part))  # noqa: E731
         for j, pc in enumerate(self.packs):
             y = Feat(g.get(f"v{j}", (x.N, x.H, x.W, pc.spec.cout), T))
-            ops.conv_fwd(pc, sl(x), sl(y), act=ACT_RELU)
+            pooled = j in (1, 3)
+            if pooled:   # conv -> ReLU -> MaxPool2d(2) (ir:664), fused where a kernel takes the layer
+                p = Feat(g.get(f"p{j}", (x.N, x.H // 2, x.W // 2, pc.spec.cout), T))
+                if not ops.conv_fwd_pool(pc, sl(x), sl(y) if keep else None, sl(p)):
+                    ops.conv_fwd(pc, sl(x), sl(y), act=ACT_RELU)
+                    ops.maxpool(sl(y), sl(p))
+            else:
+                ops.conv_fwd(pc, sl(x), sl(y), act=ACT_RELU)
             acts.append(y)
             x = y
-            if j in (1, 3):
-                p = Feat(g.get(f"p{j}", (x.N, x.H // 2, x.W // 2, x.C), T))
-                ops.maxpool(sl(x), sl(p))
+            if pooled:
                 acts.append(p)
                 x = p
         return x
@@ -1239,7 +1251,7 @@ class GANStep:
                     ops.nchw_to_nhwc(ir.contiguous(), Feat(din.t[h:h + B], 0, cin))
                 ops.axpby(Feat(rgb_h), 1.0, Feat(din.t[:B], cin, cout))
                 ops.affine(Feat(rgb_h), self.vgg.scale, self.vgg.shift, vin.batch(B, B))
-                self.vgg.forward(vin, part=(B, B))
+                self.vgg.forward(vin, part=(B, B), keep=False)   # no backward through the real half
             if vgg_side:
                 _mark(ph, "vgg_real", self.side)
                 ev = torch.cuda.Event()
@@ -1300,8 +1312,9 @@ class GANStep:
             pred = self.dis.forward(din, tag="d")
             dpred = b.get("dpred", tuple(pred.shape), torch.float32)
             ops.hinge(pred, pred[:B].numel(), 0, 1.0, dpred, L[0:1])
-            self.dis.backward(dpred, want_wgrad=True, want_dinput=False, tag="d")
-            self.d_reduce.start()
+            # D grads reduced tail-first under the D backward (8 MB buckets: model.8 + the head
+            # go out while model.5 / .2 / .0 still run), each bucket's Adam right behind it
+            self.dis.backward(dpred, want_wgrad=True, want_dinput=False, tag="d", ready=self.d_reduce.ready)
             # D Adam, then the G-step GAN term through the updated D (ir:1651, 1659-1662),
             # still on the side stream: the main stream meanwhile runs the G-step terms
             # that do not read D (L1, VGG, TV, SSIM)

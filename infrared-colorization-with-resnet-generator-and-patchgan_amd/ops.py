@@ -317,6 +317,31 @@ def conv_fwd(pc: PackedConv, x: Feat, y: Feat, act=ACT_NONE, bias=True, accumula
 IRGAN_EUNSUPPORTED = 1002   # include/irgan.h
 
 
+def conv_fwd_pool(pc: PackedConv, x: Feat, y, yp: Feat, act=ACT_RELU) -> bool:
+    """y = act(conv(x)) (y: a Feat, or None when only the pooled map is needed) and yp = its
+    2x2 max-pool, in one launch (irgan_conv_fwd_pool: the VGG conv1_2 -> MaxPool2d(2),
+    ir:664).  False when the layer has no fused kernel -- then NOTHING ran."""
+    s = pc.spec
+    Ho, Wo = s.out_hw(x.H, x.W)
+    if pc.dtype != BF16 or yp.dt != BF16 or yp.off or yp.ld != s.cout or Ho % 2 or Wo % 2:
+        return False
+    assert (yp.N, yp.H, yp.W, yp.C) == (x.N, Ho // 2, Wo // 2, s.cout) and x.C == pc.cin_eff
+    if y is not None:
+        assert (y.H, y.W, y.C, y.N, y.dt) == (Ho, Wo, s.cout, x.N, BF16)
+    d = _desc(N=x.N, H=x.H, W=x.W, Cin=pc.cin_eff, ldx=x.ld, xoff=x.off, Ho=Ho, Wo=Wo, Cout=s.cout,
+              ldy=y.ld if y is not None else s.cout, yoff=y.off if y is not None else 0, OH=Ho, OW=Wo, omy=1, ooy=0,
+              omx=1, oox=0, KH=s.k, KW=s.k, sy=s.stride, sx=s.stride, c0y=-s.pad, c0x=-s.pad, pad_mode=s.mode,
+              act=act, accumulate=0, dtype=pc.dtype, out_dtype=BF16, mask_act=0, ldm=0, moff=0)
+    fn = getattr(_lib.load(), "irgan_conv_fwd_pool")
+    rc = TIMER.wrap(conv_tag("fwdpool", s, (x.H, x.W), x.N), lambda: fn(
+        ctypes.byref(d), x.ptr, P(pc.fwd), P(pc.bias), y.ptr if y is not None else None, yp.ptr, stream()))
+    if rc == IRGAN_EUNSUPPORTED:
+        return False
+    if rc != 0:
+        raise _lib.IrganError(f"irgan_conv_fwd_pool failed with code {rc}")
+    return True
+
+
 def conv_fwd_stats(pc: PackedConv, x: Feat, y: Feat, part: torch.Tensor) -> int:
     """conv_fwd (no activation) that also writes y's InstanceNorm partials into
     ``part`` (irgan_conv_fwd_stats).  Returns the partials per image, or 0 when the

@@ -70,6 +70,11 @@ EXTRA_CASES = [
     # n_layers = 2's 256-channel head and a larger 512-channel one
     (256, 1, 4, 1, 1, 0, 21),
     (512, 1, 4, 1, 1, 0, 40),
+    # non-square maps (H, W): the ResnetBlock at 512 x 640's 128 x 160 (config 4, scaled down in
+    # H) and widths that are not a multiple of 64 -- the wide-n weight gradient's partial segments
+    (256, 256, 3, 1, 1, 1, 16, 160),
+    (128, 256, 3, 1, 1, 0, 12, 96),
+    (384, 128, 3, 1, 1, 0, 8, 40),
 ]
 
 
@@ -128,14 +133,15 @@ def ops():
 
 @pytest.mark.parametrize("case", CONV_CASES + EXTRA_CASES)
 def test_bf16_conv_family_tight(ops, case):
-    cin, cout, k, s, p, mode, H = case
+    cin, cout, k, s, p, mode, H = case[:7]
+    W = case[7] if len(case) > 7 else H
     torch.manual_seed(0)
     N = 2
-    x = q(torch.randn(N, cin, H, H))
+    x = q(torch.randn(N, cin, H, W))
     w = q(torch.randn(cout, cin, k, k) * (1.0 / (cin * k * k) ** 0.5))
     b = torch.randn(cout) * 0.1
     spec = ops.ConvSpec(cin, cout, k, s, p, mode)
-    Ho, Wo = spec.out_hw(H, H)
+    Ho, Wo = spec.out_hw(H, W)
     gy = q(torch.randn(N, cout, Ho, Wo))
     y64, dx64, dw64, dxi = references(x, w, b, gy, k, s, p, mode)
     ya, dxa, dwa, _ = references(x.abs(), w.abs(), b.abs(), gy.abs(), k, s, p, mode)
@@ -143,7 +149,7 @@ def test_bf16_conv_family_tight(ops, case):
     master = w.permute(0, 2, 3, 1).contiguous().reshape(-1).to(DEV)
     pc = ops.PackedConv(spec, master, b.to(DEV), ops.BF16)
     pc.pack()
-    xd = torch.zeros(N, H, H, pc.cin_eff, device=DEV, dtype=torch.bfloat16)
+    xd = torch.zeros(N, H, W, pc.cin_eff, device=DEV, dtype=torch.bfloat16)
     xd[..., :cin] = nhwc(x)
 
     # forward, bf16 output into a channel slice (ld = cout + 8, off 8) -- the step's layout
@@ -159,16 +165,16 @@ def test_bf16_conv_family_tight(ops, case):
     # backward-data: dY zero-padded to cout_eff channels
     gyd = torch.zeros(N, Ho, Wo, pc.cout_eff, device=DEV, dtype=torch.bfloat16)
     gyd[..., :cout] = nhwc(gy)
-    pad = torch.empty(N * (H + 2 * p) ** 2 * cin, device=DEV) if mode == 1 else None
+    pad = torch.empty(N * (H + 2 * p) * (W + 2 * p) * cin, device=DEV) if mode == 1 else None
     for out_dt, r_out in ((torch.float32, 0.0), (torch.bfloat16, R_BF16)):
-        dx = torch.zeros(N, H, H, cin, device=DEV, dtype=out_dt)
+        dx = torch.zeros(N, H, W, cin, device=DEV, dtype=out_dt)
         ops.conv_dgrad(pc, ops.Feat(gyd), ops.Feat(dx), pad_buf=pad)
         check(nchw64(dx), dx64, dxa, r_out, f"dgrad {out_dt}", partial=dxi)
     # backward-data accumulating onto another branch's gradient (bf16, the step's
     # resblock / down2 / down1 skip paths), into a channel slice when aligned
     sl = 8 if cin % 8 == 0 else 0
-    old = q(torch.randn(N, cin, H, H))
-    dxb = torch.zeros(N, H, H, cin + sl, device=DEV, dtype=torch.bfloat16)
+    old = q(torch.randn(N, cin, H, W))
+    dxb = torch.zeros(N, H, W, cin + sl, device=DEV, dtype=torch.bfloat16)
     dxb[..., sl:] = nhwc(old)
     ops.conv_dgrad(pc, ops.Feat(gyd), ops.Feat(dxb, sl, cin), accumulate=True, pad_buf=pad)
     check(nchw64(dxb[..., sl:]), dx64 + old.double(), dxa + old.double().abs(), R_BF16, "dgrad accumulate",
@@ -340,3 +346,36 @@ def test_reflect_dgrad_ring_tight(ops, N, H, W):
     check(nchw64(dxb[..., 8:]), dx64 + old.double(), dxa + old.double().abs(), R_BF16, "ring accumulate",
           partial=dxi + old.double())
     assert not dxb[..., :8].any()
+
+
+@pytest.mark.parametrize("N,H,W,cout,keep", [(2, 32, 48, 64, True), (2, 32, 48, 64, False), (3, 20, 36, 128, True),
+                                             (1, 256, 256, 64, False)])
+def test_conv_pool_fused_bit_identical(ops, N, H, W, cout, keep):
+    """irgan_conv_fwd_pool (the VGG conv1_2 -> ReLU -> MaxPool2d(2), ir:664, in one launch of the
+    resident-weight kernel) against irgan_conv_fwd + irgan_maxpool_fwd: the activated map (when
+    kept) and the pooled map bit-identical; ragged 16x16 patches (20 x 36), two co tiles, the
+    full 256 x 256 VGG map; an odd size is refused (nothing launched)."""
+    torch.manual_seed(2)
+    cin = 64
+    spec = ops.ConvSpec(cin, cout, 3, 1, 1, 0)
+    w = q(torch.randn(cout, cin, 3, 3) * (1.0 / (cin * 9) ** 0.5))
+    pc = ops.PackedConv(spec, w.permute(0, 2, 3, 1).contiguous().reshape(-1).to(DEV),
+                        (torch.randn(cout) * 0.1).to(DEV), ops.BF16)
+    pc.pack()
+    x = torch.randn(N, H, W, cin, device=DEV).bfloat16()
+    y_ref = torch.empty(N, H, W, cout, device=DEV, dtype=torch.bfloat16)
+    p_ref = torch.empty(N, H // 2, W // 2, cout, device=DEV, dtype=torch.bfloat16)
+    ops.conv_fwd(pc, ops.Feat(x), ops.Feat(y_ref), act=ops.ACT_RELU)
+    ops.maxpool(ops.Feat(y_ref), ops.Feat(p_ref))
+    y = torch.full_like(y_ref, 7.0)
+    p = torch.full_like(p_ref, 7.0)
+    assert ops.conv_fwd_pool(pc, ops.Feat(x), ops.Feat(y) if keep else None, ops.Feat(p))
+    torch.cuda.synchronize()
+    assert torch.equal(p.view(torch.int16), p_ref.view(torch.int16)), "pooled map"
+    if keep:
+        assert torch.equal(y.view(torch.int16), y_ref.view(torch.int16)), "activated map"
+    else:
+        assert bool((y == 7.0).all()), "y written although not kept"
+    xo = torch.randn(1, 21, 32, cin, device=DEV).bfloat16()
+    assert not ops.conv_fwd_pool(pc, ops.Feat(xo), None,
+                                 ops.Feat(torch.empty(1, 10, 16, cout, device=DEV, dtype=torch.bfloat16)))

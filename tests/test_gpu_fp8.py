@@ -329,7 +329,23 @@ def test_fp8_wgrad_tight(ops, N, H, W, cin, cout, mode):
     assert ratio <= 1.0, f"fp8 wgrad: worst |err|/bound = {ratio:.3g}"
 
 
-FP8_DW_RATIO, FP8_DW_ABS = 1.5, 0.05   # fp8-step ResnetBlock dW drift vs the fp8 restatement's
+# fp8 ResnetBlock dW against the unquantised reference (ir:386-411), absolute bounds per
+# resolution on the learnable pair: (max rel-L2, min cosine, |dW| / |dW_ref| range).  The fp8
+# restatement (oracle, fp32 arithmetic) measures 0.496 / 0.878 at 64x64 and 0.236 / 0.972 at
+# 256x256 (profiles/r06_fp8_drift.txt; the bf16-rounded weights alone: 0.10 / 0.045)
+FP8_DW_BOUND = {64: (0.65, 0.80, (0.75, 1.33)), 256: (0.35, 0.93, (0.85, 1.18))}
+
+
+def fp8_dw_check(got, ref, bound):
+    """(ok, rel-L2, cosine, norm ratio) of a weight gradient against its reference."""
+    d, r = got.double().flatten(), ref.double().flatten()
+    rn = float(r.norm())
+    e = float((d - r).norm()) / max(rn, 1e-300)
+    dn = float(d.norm())
+    c = float(d @ r) / max(dn * rn, 1e-300)
+    ratio = dn / max(rn, 1e-300)
+    emax, cmin, (lo, hi) = bound
+    return (e <= emax and c >= cmin and lo <= ratio <= hi), e, c, ratio
 
 
 def _fp8_oracle(ir, rgb, lam, fp8=True):
@@ -391,23 +407,55 @@ def test_fp8_step_vs_fp8_oracle(size):
             e = float((got - gr.double()).norm() / den)
             e_ac = float((oac[tag][k].double() - gr.double()).norm() / den)
             assert np.isfinite(e) and e <= 1.5 * e_ac + 0.02, (tag, k, e, e_ac)
-    # the e4m3 step against the UNQUANTISED reference gradient (the reference's fp32 autograd,
-    # o_nofp8): the ResnetBlock weight gradients (ir:386-411) drift from it by the e4m3
-    # rounding of the operands and of everything upstream (the loss terms are discontinuous:
-    # ReLU masks, L1 signs flip), measured 0.7 rel-L2 at the first block.  The accepted bound:
-    # no further than FP8_DW_RATIO x the drift of the fp8 restatement itself (o, the same
-    # quantisation in fp32 arithmetic) from that reference, + FP8_DW_ABS (values printed)
-    worst = 0.0
-    for k, gr in o_nofp8["gradG"].items():
+    # (the fp8 dW against the UNQUANTISED reference: test_fp8_resblock_dw_vs_unquantised)
+
+
+@pytest.mark.parametrize("size", [64, 256])
+def test_fp8_resblock_dw_vs_unquantised(size):
+    """The fp8 step's ResnetBlock weight gradients (ir:386-411) against the UNQUANTISED
+    reference gradient (the oracle's fp32 autograd of ir:1636-1681) at absolute bounds
+    (FP8_DW_BOUND: rel-L2, cosine and norm ratio), on a learnable pair
+    (tests/trajectory_data.py) at 64x64 and at config 5's resolution 256x256, B=2.
+
+    Why not the U(-1, 1) noise of test_fp8_step_vs_fp8_oracle: at random init on noise
+    images the gradient is a near-cancelling sum whose ReLU masks flip under any forward
+    perturbation -- rounding only the weights to bf16 moves it 0.17 rel-L2, e4m3 forward
+    operands 0.77-0.80 (the dY quantisation adds ~0.015; per-(n,c) / block scales or e5m2
+    for dY change nothing: tools/fp8_drift_diag.py, profiles/r06_fp8_drift.txt).  On a
+    learnable pair the same recipe is 0.24 at 256x256.  Negative controls: a zeroed, a
+    permuted, a half-scaled and a negated gradient must fail the same check."""
+    from conftest import load_golden
+    from oracle import step as O
+    from test_gpu_step import make_trainer
+    from trajectory_data import pair
+    fx = load_golden("s64")
+    tr, cfg = make_trainer(fx, "fp8")
+    lam = {k: getattr(cfg, k) for k in O.LAMBDAS}
+    g = torch.Generator().manual_seed(41)
+    ir, rgb = pair(g, 2, size)
+    tr.step(ir.to(DEV), rgb.to(DEV))
+    o = _fp8_oracle(ir, rgb, lam)
+    ref = _fp8_oracle(ir, rgb, lam, fp8=False)
+    bound = FP8_DW_BOUND[size]
+    gen = torch.Generator().manual_seed(5)
+    worst = (0.0, 1.0)
+    for k, gr in ref["gradG"].items():
         if "resblocks" not in k or not k.endswith(".weight"):
             continue
-        den = gr.double().norm().clamp_min(1e-30)
-        e = float((tr.netG.store.oihw(k, tr.netG.store.grad).cpu().double() - gr.double()).norm() / den)
-        e_o = float((o["gradG"][k].double() - gr.double()).norm() / den)
-        worst = max(worst, e / max(e_o, 1e-12))
-        print(f"fp8 dW {k}: vs unquantised {e:.4f}, fp8 oracle vs unquantised {e_o:.4f}")
-        assert np.isfinite(e) and e <= FP8_DW_RATIO * e_o + FP8_DW_ABS, (k, e, e_o)
-    print(f"fp8 ResnetBlock dW: worst drift ratio against the fp8 oracle's {worst:.3f}")
+        got = tr.netG.store.oihw(k, tr.netG.store.grad).cpu()
+        ok, e, c, ratio = fp8_dw_check(got, gr, bound)
+        _, e_o, c_o, _ = fp8_dw_check(o["gradG"][k], gr, bound)
+        print(f"fp8 dW {k}: rel-L2 {e:.4f} cos {c:.4f} |dW| ratio {ratio:.3f}  "
+              f"(fp8 restatement: {e_o:.4f} / {c_o:.4f})")
+        assert ok, (k, e, c, ratio, bound)
+        worst = (max(worst[0], e), min(worst[1], c))
+        # negative controls: each must fail the same check
+        flat = got.flatten()
+        for tag, bad in (("zero", torch.zeros_like(got)), ("permuted", flat[torch.randperm(flat.numel(), generator=gen)]),
+                         ("half", 0.5 * got), ("negated", -got)):
+            assert not fp8_dw_check(bad, gr, bound)[0], f"negative control {tag} passed for {k}"
+    print(f"fp8 ResnetBlock dW at {size}x{size}: worst rel-L2 {worst[0]:.4f}, min cosine {worst[1]:.4f} "
+          f"(bound {bound[0]} / {bound[1]})")
 
 
 def test_fp8_step_config5_b32_finite():

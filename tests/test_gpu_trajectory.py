@@ -5,13 +5,16 @@ The reference's only runtime correctness signal is the per-epoch validation L1
 (ir:1683-1694).  Single-step gradient comparisons at random init cannot hold the
 bf16 / fp8 paths tightly (a ReLU-mask flip per perturbed element: the fp32
 reference's own weight gradients move 0.17 rel-L2 when only its weights are
-rounded to bf16, tools/fp8_drift_diag.py), so this test trains: 200 steps at 64x64,
+rounded to bf16, tools/fp8_drift_diag.py), so this test trains: 400 steps at 64x64,
 B=4 on learnable synthetic pairs (tests/trajectory_data.py: IR = a smooth field,
 RGB = a fixed colour map of it) from one seeded init, in compute_dtype "fp32",
-"bf16" and "fp8", then scores held-out batches with validate_kaist.
+"bf16" and "fp8", scoring held-out batches with validate_kaist every 20 steps over
+the second half (a single val-L1 swings +-20 % between evaluations of one run: the
+GAN's oscillation; averaged over 10, two fp32 runs from inits 2^-9 apart agree to 2 %,
+profiles/r06_fp8_trajectory_oracle.txt).
 
-Pass: loss_G falls in all three (last-20 mean below 0.5x the first-20 mean); the
-bf16 and fp8 last-20 mean loss_G and the held-out val-L1 within TRAJ_BAND of fp32
+Pass: loss_G falls in all three (second-half mean below 0.5x the first-20 mean); the
+bf16 and fp8 second-half mean loss_G and averaged val-L1 within TRAJ_BAND of fp32
 mode's.  CPU counterpart (the oracle's fp32 and fp8 restatement on the same data):
 tools/fp8_trajectory_oracle.py, profiles/r06_fp8_trajectory_oracle.txt.
 """
@@ -23,8 +26,8 @@ from trajectory_data import learnable_pairs
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-STEPS, SIZE, BATCH = 200, 64, 4
-TRAJ_BAND = 0.10   # relative to fp32 mode: last-20 mean loss_G and val-L1
+STEPS, SIZE, BATCH, EVAL_EVERY = 400, 64, 4, 20
+TRAJ_BAND = 0.10   # relative to fp32 mode: second-half mean loss_G and averaged val-L1
 
 
 def _trainer(dtype):
@@ -47,26 +50,29 @@ def _trainer(dtype):
 def _train(dtype, train, val):
     irc = pkg()
     tr = _trainer(dtype)
-    lg = []
+    vbatches = [{"ir": ir, "rgb": rgb} for ir, rgb in val]
+    lg, vls = [], []
     for s in range(STEPS):
         ir, rgb = train[s % len(train)]
         lg.append(tr.losses(tr.step(ir.to(DEV), rgb.to(DEV)))["loss_G"])
-    vl = irc.validate_kaist(tr.model, [{"ir": ir, "rgb": rgb} for ir, rgb in val], DEV)
+        if s + 1 > STEPS // 2 and (s + 1) % EVAL_EVERY == 0:
+            vls.append(irc.validate_kaist(tr.model, vbatches, DEV))
     assert all(torch.isfinite(torch.tensor(lg))), dtype
-    return sum(lg[:20]) / 20, sum(lg[-20:]) / 20, vl
+    half = lg[STEPS // 2:]
+    return sum(lg[:20]) / 20, sum(half) / len(half), sum(vls) / len(vls)
 
 
 def test_loss_trajectory_fast_dtypes():
     train, val = learnable_pairs(SIZE, BATCH)
     res = {dt: _train(dt, train, val) for dt in ("fp32", "bf16", "fp8")}
     for dt, (first, last, vl) in res.items():
-        print(f"{dt}: loss_G first-20 {first:.4f} last-20 {last:.4f}  val-L1 {vl:.4f}")
+        print(f"{dt}: loss_G first-20 {first:.4f} second-half {last:.4f}  val-L1 (mean of 10) {vl:.4f}")
     for dt, (first, last, vl) in res.items():
         assert last < 0.5 * first, (dt, first, last)
     _, last32, vl32 = res["fp32"]
     for dt in ("bf16", "fp8"):
         _, last, vl = res[dt]
-        print(f"{dt} vs fp32: last-20 loss_G {last / last32 - 1:+.2%}, val-L1 {vl / vl32 - 1:+.2%} "
+        print(f"{dt} vs fp32: second-half loss_G {last / last32 - 1:+.2%}, val-L1 {vl / vl32 - 1:+.2%} "
               f"(band {TRAJ_BAND:.0%})")
         assert abs(last / last32 - 1) <= TRAJ_BAND, (dt, last, last32)
         assert abs(vl / vl32 - 1) <= TRAJ_BAND, (dt, vl, vl32)

@@ -22,6 +22,8 @@ CASES = [  # name, cin, cout, k, s, p, mode, H
     ("D3_256-512s1@32", 256, 512, 4, 1, 1, 0, 32),
     ("D1_64-128s2@128", 64, 128, 4, 2, 1, 0, 128),
     ("Dhead_512-1@31", 512, 1, 4, 1, 1, 0, 31),
+    # 512 x 640 at B = 4 (BASELINE configs[3]): the ResnetBlock maps are 128 x 160
+    ("res3x3_256@128x160b4", 256, 256, 3, 1, 1, 1, (128, 160, 4)),
 ]
 def t(fn, it=20):
     fn(); torch.cuda.synchronize()
@@ -43,18 +45,19 @@ res = {}
 for name, cin, cout, k, s, p, mode, H in CASES:
     if args.case and not any(c in name for c in args.case.split(",")):
         continue
+    H, Wd, B = H if isinstance(H, tuple) else (H, H, args.batch)
     spec = ops.ConvSpec(cin, cout, k, s, p, mode)
     w = torch.randn(cout * k * k * cin, device=DEV) * 0.05
     pc = ops.PackedConv(spec, w, torch.zeros(cout, device=DEV), ops.BF16); pc.pack()
-    x = torch.randn(B, H, H, cin, device=DEV).bfloat16()
-    Ho, Wo = spec.out_hw(H, H)
+    x = torch.randn(B, H, Wd, cin, device=DEV).bfloat16()
+    Ho, Wo = spec.out_hw(H, Wd)
     y = torch.empty(B, Ho, Wo, cout, device=DEV, dtype=torch.bfloat16)
     dy = torch.randn(B, Ho, Wo, pc.cout_eff, device=DEV).bfloat16()   # narrow dY: 8-padded
-    dx = torch.empty(B, H, H, cin, device=DEV, dtype=torch.bfloat16)
-    pad = torch.empty(B * (H + 2 * p) ** 2 * cin, device=DEV)
+    dx = torch.empty(B, H, Wd, cin, device=DEV, dtype=torch.bfloat16)
+    pad = torch.empty(B * (H + 2 * p) * (Wd + 2 * p) * cin, device=DEV)
     dw = torch.zeros(cout * k * k * cin, device=DEV)
     flop = 2.0 * B * Ho * Wo * cout * cin * k * k
-    part = torch.empty(B * 256 * cout * 2, device=DEV)
+    part = torch.empty(B * 512 * cout * 2, device=DEV)
     fns = {"fwd": lambda: ops.conv_fwd(pc, ops.Feat(x), ops.Feat(y)),
            "fwdr": lambda: ops.conv_fwd(pc, ops.Feat(x), ops.Feat(y), act=ops.ACT_RELU),
            "fwds": lambda: ops.conv_fwd_stats(pc, ops.Feat(x), ops.Feat(y), part),

@@ -126,15 +126,17 @@ def main():
     print(f"ResnetBlock dW rel-L2 vs the unquantised oracle step ({a.size}x{a.size}, B={a.batch}, {a.data} data)")
 
     def report(tag, o):
-        errs, coss = [], []
+        errs, coss, rats = [], [], []
         for k, gr in base["gradG"].items():
             if "resblocks" in k and k.endswith(".weight"):
                 d, r = o["gradG"][k].double().flatten(), gr.double().flatten()
                 errs.append(float((d - r).norm() / r.norm()))
                 coss.append(float(d @ r / (d.norm() * r.norm())))
+                rats.append(float(d.norm() / r.norm()))
         fe = (o["fake"] - base["fake"]).abs().mean().item()
         print(f"  {tag:24s} G out mean|d| {fe:.4f}   dW rel-L2 worst {max(errs):.3f} mean "
-              f"{sum(errs) / len(errs):.3f}   cosine min {min(coss):.3f}", flush=True)
+              f"{sum(errs) / len(errs):.3f}   cosine min {min(coss):.3f}   |dW| ratio "
+              f"{min(rats):.3f}-{max(rats):.3f}", flush=True)
 
     R0, Z0 = O._Fp8ResConv, O._Fp8ZeroConv
 
