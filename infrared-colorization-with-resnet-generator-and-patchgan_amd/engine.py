@@ -958,6 +958,9 @@ class DiscriminatorEngine:
 # VGG-16 features[:16] perceptual extractor  (ir:642-683), frozen
 # ----------------------------------------------------------------------------
 
+NO_POOL_FUSION = bool(os.environ.get("IRGAN_NO_POOL_FUSION"))   # A/B: separate conv and maxpool launches
+
+
 class VGGEngine:
     _pack_batch = None  # ops.PackBatch of self.packs, built on the first pack()
 
@@ -992,7 +995,7 @@ class VGGEngine:
             pooled = j in (1, 3)
             if pooled:   # conv -> ReLU -> MaxPool2d(2) (ir:664), fused where a kernel takes the layer
                 p = Feat(g.get(f"p{j}", (x.N, x.H // 2, x.W // 2, pc.spec.cout), T))
-                if not ops.conv_fwd_pool(pc, sl(x), sl(y) if keep else None, sl(p)):
+                if NO_POOL_FUSION or not ops.conv_fwd_pool(pc, sl(x), sl(y) if keep else None, sl(p)):
                     ops.conv_fwd(pc, sl(x), sl(y), act=ACT_RELU)
                     ops.maxpool(sl(y), sl(p))
             else:
