@@ -116,6 +116,25 @@ IRGAN_HD void wait_vmcnt() {
     static_assert(N >= 0 && N <= 63, "vmcnt");
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
+// v from lane (lane ^ M), M in {1, 2, 4, 8} -- within each 16-lane row, by DPP on the VALU
+// (no LDS round trip, unlike __shfl_xor's ds_bpermute): 1, 2 quad_perm; 8 row_ror:8; 4 as
+// row_half_mirror (i -> 7 - i) then quad_perm [3,2,1,0] (i -> i ^ 3)
+template <int M>
+IRGAN_HD float dpp_xor16(float v) {
+    int x = __float_as_int(v);
+    if constexpr (M == 1) {
+        x = __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false);
+    } else if constexpr (M == 2) {
+        x = __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false);
+    } else if constexpr (M == 4) {
+        x = __builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, false);
+        x = __builtin_amdgcn_update_dpp(0, x, 0x1B, 0xF, 0xF, false);
+    } else {
+        static_assert(M == 8, "dpp_xor16: M in {1, 2, 4, 8}");
+        x = __builtin_amdgcn_update_dpp(0, x, 0x128, 0xF, 0xF, false);
+    }
+    return __int_as_float(x);
+}
 IRGAN_HD void lds_barrier() { asm volatile("s_barrier" ::: "memory"); }
 
 // XCD-aware tile order.  Workgroups are dealt round-robin to the 8 XCDs

@@ -308,7 +308,7 @@ __global__ __launch_bounds__(512, 1) void conv_res64_kernel(const irgan_conv_des
 #pragma unroll
                             for (int r = 0; r < 4; ++r) {
                                 m[r] = fmaxf(pmx[j][r], v[r]);
-                                m[r] = fmaxf(m[r], __shfl_xor(m[r], 1, 64));
+                                m[r] = fmaxf(m[r], dpp_xor16<1>(m[r]));
                             }
                             u32x2_t pp;
                             pp.x = pk_bf16(m[0], m[1]);
@@ -341,18 +341,22 @@ __global__ __launch_bounds__(512, 1) void conv_res64_kernel(const irgan_conv_des
         }
         if constexpr (STATS) {
             // reduce-scatter over the 16 pixel lanes (lane & 15): 32 values -> 2 per lane;
-            // lane (g0, k) ends with channel (j, r) = (k >> 2, k & 3) of its lane group
-#pragma unroll
-            for (int lv = 0; lv < 4; ++lv) {
-                const int m = 8 >> lv, n = 32 >> lv;  // xor distance, values held
+            // lane (g0, k) ends with channel (j, r) = (k >> 2, k & 3) of its lane group.  The
+            // partner values move by DPP (dpp_xor16): no LDS round trips in the epilogue
+            auto level = [&](auto mc) {
+                constexpr int m = decltype(mc)::value, n = 4 * m;  // xor distance, values held
                 const bool hi = (lane & m) != 0;
 #pragma unroll
                 for (int k = 0; k < n / 2; ++k) {
                     const float keep = hi ? st[n / 2 + k] : st[k];
                     const float send = hi ? st[k] : st[n / 2 + k];
-                    st[k] = keep + __shfl_xor(send, m, 64);
+                    st[k] = keep + dpp_xor16<m>(send);
                 }
-            }
+            };
+            level(std::integral_constant<int, 8>());
+            level(std::integral_constant<int, 4>());
+            level(std::integral_constant<int, 2>());
+            level(std::integral_constant<int, 1>());
         }
         const int sk = lane & 15;
         float2* const srow = sR + wid * 64 + (sk >> 2) * 16 + cl0 + (sk & 3);

@@ -244,39 +244,71 @@ __global__ __launch_bounds__(TPB) void ssim_hrow_kernel(const float* __restrict_
     }
 }
 
-// vertical 11-tap pass over NM planar maps.  A thread owns one element (x*C + c)
-// of R consecutive rows: it loads the R + 10 input rows once into registers and
-// slides the window, so each input is read (R+10)/R times instead of 11 (the
-// pass was bound by those L2 re-reads).  blockIdx.y = n * ceil(H/R) + row block.
-template <int K, int NM, int R>
-__global__ __launch_bounds__(TPB) void ssim_v_kernel(const float* __restrict__ in, int H, int W, int C, WinK<K> win,
-                                                     float* __restrict__ out, long S) {
-    constexpr int HK = K / 2;
+// Round 6: the vertical pass fused with its elementwise consumer -- the five moment maps'
+// vertical sums feed the SSIM map and dL/d{mu1, e11, e12} (ssim_map_kernel's arithmetic) in
+// registers, and the three adjoint maps' sums feed the input gradient (ssim_grad_kernel's),
+// so neither the 5 nor the 3 vertically filtered maps are written and re-read (5 + 3 fp32
+// maps of N*H*W*C).  Per element the operations and their order are those of the unfused
+// pair: d3 and g bit-identical; the loss is the same sum in another block grouping.
+template <int K, int R, bool MAP>
+__global__ __launch_bounds__(TPB) void ssim_vfused_kernel(const float* __restrict__ in, int H, int W, int C,
+                                                          WinK<K> win, float w, float* __restrict__ d3,
+                                                          double* __restrict__ loss, const float* __restrict__ a,
+                                                          const float* __restrict__ b, float* __restrict__ g,
+                                                          long S) {
+    constexpr int HK = K / 2, NM = MAP ? 5 : 3;
     const int e = blockIdx.x * TPB + threadIdx.x;  // element within the row (x*C + c)
-    if (e >= W * C) return;
-    const int hb = (H + R - 1) / R;
-    const int n = blockIdx.y / hb, y0 = (blockIdx.y - n * hb) * R;
-    const long WC = (long)W * C;
-    const long base = (long)n * H * WC + e;
-    float v[NM][R + K - 1];
+    float lacc = 0.f;
+    if (e < W * C) {
+        const int hb = (H + R - 1) / R;
+        const int n = blockIdx.y / hb, y0 = (blockIdx.y - n * hb) * R;
+        const long WC = (long)W * C;
+        const long base = (long)n * H * WC + e;
+        float v[NM][R + K - 1];
 #pragma unroll
-    for (int r = 0; r < R + K - 1; ++r) {
-        const int yy = y0 + r - HK;
-        const bool ok = yy >= 0 && yy < H;
+        for (int r = 0; r < R + K - 1; ++r) {
+            const int yy = y0 + r - HK;
+            const bool ok = yy >= 0 && yy < H;
 #pragma unroll
-        for (int m = 0; m < NM; ++m) v[m][r] = ok ? in[m * S + base + yy * WC] : 0.f;
-    }
+            for (int m = 0; m < NM; ++m) v[m][r] = ok ? in[m * S + base + yy * WC] : 0.f;
+        }
+        const float C1 = 0.01f * 0.01f, C2 = 0.03f * 0.03f;
+        const float dLdS = -w / (float)S;
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        if (y0 + r >= H) break;
+        for (int r = 0; r < R; ++r) {
+            if (y0 + r >= H) break;
+            float mom[NM];
 #pragma unroll
-        for (int m = 0; m < NM; ++m) {
-            float acc = 0.f;
+            for (int m = 0; m < NM; ++m) {
+                float acc = 0.f;
 #pragma unroll
-            for (int k = 0; k < K; ++k) acc += win.g[k] * v[m][r + k];
-            out[m * S + base + (y0 + r) * WC] = acc;
+                for (int k = 0; k < K; ++k) acc += win.g[k] * v[m][r + k];
+                mom[m] = acc;
+            }
+            const long idx = base + (y0 + r) * WC;
+            if constexpr (MAP) {
+                const float mu1 = mom[0], mu2 = mom[1], e11 = mom[2], e22 = mom[3], e12 = mom[4];
+                const float m11 = mu1 * mu1, m22 = mu2 * mu2, m12 = mu1 * mu2;
+                const float s11 = e11 - m11, s22 = e22 - m22, s12 = e12 - m12;
+                const float A1 = 2.f * m12 + C1, A2 = 2.f * s12 + C2;
+                const float B1 = m11 + m22 + C1, B2 = s11 + s22 + C2;
+                const float den = B1 * B2;
+                const float Sv = (A1 * A2) / den;
+                lacc += 1.f - Sv;
+                const float dmu1 = (2.f * mu2 * (A2 - A1)) / den - Sv * 2.f * mu1 / B1 + Sv * 2.f * mu1 / B2;
+                const float de11 = -Sv / B2;
+                const float de12 = 2.f * A1 / den;
+                d3[idx] = dLdS * dmu1;
+                d3[S + idx] = dLdS * de11;
+                d3[2 * S + idx] = dLdS * de12;
+            } else {
+                const float p = (a[idx] + 1.f) * 0.5f, q = (b[idx] + 1.f) * 0.5f;
+                const float gp = mom[0] + 2.f * p * mom[1] + q * mom[2];
+                g[idx] += 0.5f * gp;  // d a'/d a = 1/2
+            }
         }
     }
+    if constexpr (MAP) block_add(loss, w * lacc / (float)S);
 }
 
 // horizontal 11-tap pass over NM planar maps
@@ -302,42 +334,6 @@ __global__ __launch_bounds__(TPB) void ssim_h_kernel(const float* __restrict__ i
         }
 #pragma unroll
         for (int m = 0; m < NM; ++m) out[m * S + idx] = acc[m];
-    }
-}
-
-// SSIM map, loss and dL/d{mu1, e11, e12} (ir:738-750)
-__global__ __launch_bounds__(TPB) void ssim_map_kernel(const float* __restrict__ mom, float w, float* __restrict__ d3,
-                                                       double* __restrict__ loss, long S) {
-    const float C1 = 0.01f * 0.01f, C2 = 0.03f * 0.03f;
-    const float dLdS = -w / (float)S;
-    float acc = 0.f;
-    for (long idx = blockIdx.x * (long)TPB + threadIdx.x; idx < S; idx += (long)gridDim.x * TPB) {
-        const float mu1 = mom[idx], mu2 = mom[S + idx], e11 = mom[2 * S + idx], e22 = mom[3 * S + idx],
-                    e12 = mom[4 * S + idx];
-        const float m11 = mu1 * mu1, m22 = mu2 * mu2, m12 = mu1 * mu2;
-        const float s11 = e11 - m11, s22 = e22 - m22, s12 = e12 - m12;
-        const float A1 = 2.f * m12 + C1, A2 = 2.f * s12 + C2;
-        const float B1 = m11 + m22 + C1, B2 = s11 + s22 + C2;
-        const float den = B1 * B2;
-        const float Sv = (A1 * A2) / den;
-        acc += 1.f - Sv;
-        // dS/dmu1 = (2 mu2 A2 - 2 mu2 A1)/den - S*2 mu1/B1 + S*2 mu1/B2
-        const float dmu1 = (2.f * mu2 * (A2 - A1)) / den - Sv * 2.f * mu1 / B1 + Sv * 2.f * mu1 / B2;
-        const float de11 = -Sv / B2;
-        const float de12 = 2.f * A1 / den;
-        d3[idx] = dLdS * dmu1;
-        d3[S + idx] = dLdS * de11;
-        d3[2 * S + idx] = dLdS * de12;
-    }
-    block_add(loss, w * acc / (float)S);
-}
-
-__global__ __launch_bounds__(TPB) void ssim_grad_kernel(const float* __restrict__ bd3, const float* __restrict__ a,
-                                                        const float* __restrict__ b, float* __restrict__ g, long S) {
-    for (long idx = blockIdx.x * (long)TPB + threadIdx.x; idx < S; idx += (long)gridDim.x * TPB) {
-        const float p = (a[idx] + 1.f) * 0.5f, q = (b[idx] + 1.f) * 0.5f;
-        const float gp = bd3[idx] + 2.f * p * bd3[S + idx] + q * bd3[2 * S + idx];
-        g[idx] += 0.5f * gp;  // d a'/d a = 1/2
     }
 }
 
@@ -387,7 +383,6 @@ int ssim_launch(const float* a, const float* b, int N, int H, int W, int C, floa
     const WinK<K> win = gauss_win<K>();
     float* w0 = work;          // 5 maps
     float* w1 = work + 5 * S;  // 5 maps
-    const int nb = nblocks(S);
     constexpr int VR = 8;  // rows per thread in the vertical passes
     const dim3 gx(irgan_cdiv(W, TPB), N * H), ge(irgan_cdiv((long)W * C, TPB), N * irgan_cdiv(H, VR));
     const size_t row5 = (size_t)W * C * 2 * sizeof(float), row3 = (size_t)W * C * 3 * sizeof(float);
@@ -396,15 +391,15 @@ int ssim_launch(const float* a, const float* b, int N, int H, int W, int C, floa
     } else {
         ssim_h5_kernel<K><<<gx, TPB, 0, st>>>(a, b, W, C, win, w0, S);
     }
-    ssim_v_kernel<K, 5, VR><<<ge, TPB, 0, st>>>(w0, H, W, C, win, w1, S);
-    ssim_map_kernel<<<nblocks_red(S), TPB, 0, st>>>(w1, w, w0, loss, S);
+    // vertical pass + SSIM map + its gradient maps (into w1's first 3 maps)
+    ssim_vfused_kernel<K, VR, true><<<ge, TPB, 0, st>>>(w0, H, W, C, win, w, w1, loss, nullptr, nullptr, nullptr, S);
     if (row3 <= 64 * 1024) {
-        ssim_hrow_kernel<K, 3, 3, false><<<N * H, TPB, row3, st>>>(nullptr, nullptr, w0, W, C, win, w1, S);
+        ssim_hrow_kernel<K, 3, 3, false><<<N * H, TPB, row3, st>>>(nullptr, nullptr, w1, W, C, win, w0, S);
     } else {
-        ssim_h_kernel<K, 3><<<gx, TPB, 0, st>>>(w0, W, C, win, w1, S);
+        ssim_h_kernel<K, 3><<<gx, TPB, 0, st>>>(w1, W, C, win, w0, S);
     }
-    ssim_v_kernel<K, 3, VR><<<ge, TPB, 0, st>>>(w1, H, W, C, win, w0, S);
-    ssim_grad_kernel<<<nb, TPB, 0, st>>>(w0, a, b, g, S);
+    // vertical pass of the adjoint + the input gradient
+    ssim_vfused_kernel<K, VR, false><<<ge, TPB, 0, st>>>(w0, H, W, C, win, w, nullptr, nullptr, a, b, g, S);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }
