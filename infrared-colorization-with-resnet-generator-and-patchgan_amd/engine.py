@@ -908,28 +908,13 @@ class DiscriminatorEngine:
         return x.t
 
     def backward(self, dout: torch.Tensor, want_wgrad=True, want_dinput=False, tag="", bufs: Buffers = None,
-                 ready=None, wgrad_stream=None):
+                 ready=None):
         """dout: dL/dlogits fp32 (same shape as forward output).  Weight grads
         accumulate into store.grad; returns d input (fp32 NHWC) if asked.
         ``ready(key)`` (as GeneratorEngine.backward): called once every gradient from layer
         ``key``'s weight to the end of the flat buffer is final, so the caller's bucketed
-        all-reduce starts on the tail while the earlier layers' backward still runs.
-        ``wgrad_stream``: the weight and bias gradients run there, each behind an event on the
-        calling stream's backward-data chain (their operands, the layer input and its dY, are
-        not written again in this call), so the chain does not wait for them; the caller
-        joins that stream before reading store.grad (GANStep: the D step's weight gradients
-        on the main stream, idle while the side stream's D chain finishes)."""
+        all-reduce starts on the tail while the earlier layers' backward still runs."""
         g, T, S = bufs or self.bufs, self.tdt, self.store
-
-        def wgrad_side(fn):
-            if wgrad_stream is None:
-                fn()
-                return
-            ev = torch.cuda.Event()
-            ev.record()
-            wgrad_stream.wait_event(ev)
-            with torch.cuda.stream(wgrad_stream):
-                fn()
         acts, pre = g.state[tag]
         G = S.grad
         n = len(self.packs)
@@ -949,14 +934,11 @@ class DiscriminatorEngine:
             elif want_wgrad:  # layer 0: LReLU mask already folded into dy by the layer-1 dgrad
                 bias_sum = dy
             if want_wgrad:
-                def wgrad(bias_sum=bias_sum, pc=pc, key=key, x=x, dy=dy):
-                    if bias_sum is not None:
-                        ops.channel_sum(bias_sum, S.krsc(key + ".bias", G))
-                    ops.conv_wgrad(pc.spec, x, Feat(dy.t, dy.off, pc.spec.cout), S.krsc(key + ".weight", G),
-                                   self.dtype)
-                    if ready is not None:
-                        ready(key + ".weight")
-                wgrad_side(wgrad)
+                if bias_sum is not None:
+                    ops.channel_sum(bias_sum, S.krsc(key + ".bias", G))
+                ops.conv_wgrad(pc.spec, x, Feat(dy.t, dy.off, pc.spec.cout), S.krsc(key + ".weight", G), self.dtype)
+                if ready is not None:
+                    ready(key + ".weight")
             if i == 0:
                 if not want_dinput:
                     return None
@@ -1192,9 +1174,6 @@ class BucketedAllreduce:
 # forward done), d0 / dend (side: the D step's first / last launch), terms (main: the G-step
 # terms done), join (main: after its wait for the side stream), end.
 JOIN_TIMES = [] if os.environ.get("IRGAN_JOIN_TIMING") else None
-# the D step's weight gradients on the main stream beside the side stream's D backward-data
-# chain (IRGAN_D_WGRAD_SIDE=1: all of the D step on the side stream, the round-5 schedule)
-D_WGRAD_MAIN = not os.environ.get("IRGAN_D_WGRAD_SIDE")
 
 
 def _mark(ph, key, stream):
@@ -1338,12 +1317,9 @@ class GANStep:
             ops.hinge(pred, pred[:B].numel(), 0, 1.0, dpred, L[0:1])
             # D grads reduced tail-first under the D backward (8 MB buckets: model.8 + the head
             # go out while model.5 / .2 / .0 still run), each bucket's Adam right behind it
-            # the weight gradients on the main stream (D_WGRAD_MAIN): it has finished its G-step
-            # terms by then and would otherwise wait idle for this chain (profiles/r06_c trace)
-            self.dis.backward(dpred, want_wgrad=True, want_dinput=False, tag="d", ready=self.d_reduce.ready,
-                              wgrad_stream=main if D_WGRAD_MAIN and main is not None else None)
-            if D_WGRAD_MAIN and main is not None:
-                self.side.wait_stream(main)   # D Adam reads every weight gradient
+            # (the weight gradients on the main stream instead, beside this chain: -1.4 %, the main
+            # stream is still busy with the G-step terms then, profiles/r06_d_ab.txt)
+            self.dis.backward(dpred, want_wgrad=True, want_dinput=False, tag="d", ready=self.d_reduce.ready)
             # D Adam, then the G-step GAN term through the updated D (ir:1651, 1659-1662),
             # still on the side stream: the main stream meanwhile runs the G-step terms
             # that do not read D (L1, VGG, TV, SSIM)
