@@ -1,7 +1,7 @@
 # Round-6 pass e: full GPU suite, bench lines (B=16 bf16, B=32 bf16 / fp8), 64-channel family PMC
 export TMPDIR=/tmp
 O=gpurun_out/r06_e; mkdir -p $O
-timeout -k 10 1200 python -u -m pytest tests -m gpu -x -q -rP --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
+timeout -k 10 1200 python -u -m pytest tests -m gpu -q -rP --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc $(tail -1 $O/pytest_gpu.log)"
 [ $rc -ne 0 ] && { grep -E "FAILED|Error" $O/pytest_gpu.log | head; exit 1; }
 grep -E "fp8 ResnetBlock dW at|vs fp32:|loss_G first-20" $O/pytest_gpu.log | head
