@@ -240,6 +240,238 @@ __global__ __launch_bounds__(NT) void sep_lds_kernel(const void* __restrict__ in
     if constexpr (Q8) fp8_block_amax(amx, q8.amax, blockIdx.y * gridDim.x + blockIdx.x);
 }
 
+// Round 6: sep_lds_kernel's map with R output rows per block and the next row's vertical
+// taps in flight under the current row's horizontal pass.  sep_lds_kernel runs one output row
+// per block: load its <= TM input rows, barrier, horizontal taps, store, exit -- every block
+// exposes its loads' latency and the resamplers ran at 1.4-3.9 TB/s.  Here a block walks rows
+// oy0 .. oy0 + R - 1 of one image and channel group with two [Win][CB] fp32 row buffers:
+//   * the vertical-tap loads of row r + 1 are issued (raw 16-byte buffer loads, invalid
+//     items and zero-weight taps at the out-of-range offset) right after row r's vertical
+//     sums are written to LDS, and consumed at the top of the next row;
+//   * the horizontal tables live in LDS (loaded once per block), the output goes through raw
+//     buffer stores (an item past the row at the out-of-range offset), so a row issues a
+//     fixed number of VMEM ops and the wait for the prefetched taps is a counted vmcnt that
+//     leaves the previous row's stores in flight;
+//   * one barrier per row (a buffer is rewritten two rows later, after every thread passed
+//     the next row's barrier).
+// Same per-element arithmetic and tap order as sep_lds_kernel (bf16 in, bf16 out, no
+// accumulate; NORM / Q8 as there).  IPT / OPT: input / output items per thread (host-sized).
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+int sep_swz();
+
+template <int TM, bool NORM, bool Q8, int IPT, int OPT>
+__global__ __launch_bounds__(512) void sep_pipe_kernel(const bf16_t* __restrict__ in, int Hin, int Win, int ldi,
+                                                       int offi, bf16_t* __restrict__ out, int Hout, int Wout,
+                                                       int ldo, int offo, const int* __restrict__ ty,
+                                                       const float* __restrict__ wy, int Ty,
+                                                       const int* __restrict__ tx, const float* __restrict__ wx,
+                                                       int Tx, int CB, int R, const float* __restrict__ mr, int C,
+                                                       int act, int swz, ResQ8 q8) {
+    constexpr int NT = 512;
+    extern __shared__ float4 sm4[];
+    float* const sm = (float*)sm4;                       // [2][Win][CB] fp32 rows
+    const int G = CB >> 3;
+    const int WG = Win * G, OG = Wout * G;
+    float* const tw = sm + 2 * Win * CB;                 // [Wout][TM] horizontal weights
+    int* const ti = (int*)(tw + Wout * TM);              // [Wout][TM] horizontal taps (input column)
+    const int nrb = (Hout + R - 1) / R;
+    const int rbk = xcd_tile(blockIdx.x, gridDim.x, swz);
+    const int n = rbk / nrb, oy0 = (rbk - n * nrb) * R;
+    const int oy1 = min(Hout, oy0 + R);
+    const int c0 = blockIdx.y * CB;
+    const int tid = threadIdx.x;
+    for (int e = tid; e < Wout * TM; e += NT) {
+        const int ox = e / TM, j = e - ox * TM;
+        tw[e] = j < Tx ? wx[ox * Tx + j] : 0.f;
+        ti[e] = j < Tx ? tx[ox * Tx + j] : 0;
+    }
+    float nm[NORM ? 8 : 1], nr[NORM ? 8 : 1];
+    if constexpr (NORM) {
+        const float4* m4 = (const float4*)(mr + 2 * ((long)n * C + c0 + (tid % G) * 8));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float4 t = m4[k];
+            nm[2 * k] = -t.x * t.y; nr[2 * k] = t.y; nm[2 * k + 1] = -t.z * t.w; nr[2 * k + 1] = t.w;
+        }
+    }
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)in, (short)0, (int)((long)(n + 1) * Hin * Win * ldi * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(
+        out, (short)0, (int)((long)(n + 1) * Hout * Wout * ldo * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t qr = __builtin_amdgcn_make_buffer_rsrc(
+        Q8 ? (void*)q8.p : (void*)out, (short)0, Q8 ? (int)((long)(n + 1) * Hout * Wout * q8.ld) : 0, 0x00020000);
+    // this thread's input items (col, group) and their offsets within an input row
+    int icol[IPT], ig[IPT];
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+        const int v = tid + k * NT;
+        icol[k] = v < WG ? v / G : -1;
+        ig[k] = v - (v / G) * G;
+    }
+    uint4 pre[IPT][TM];   // raw bf16x8 of the next row's vertical taps
+    float wnext[TM];
+    auto issue = [&](int oy) {
+        int trow[TM];   // the row's taps (block-uniform: scalar loads, all issued before any use)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            wnext[i] = i < Ty ? wy[oy * Ty + i] : 0.f;
+            trow[i] = i < Ty ? ty[oy * Ty + i] : 0;
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const long rb = (long)(n * Hin + trow[i]) * Win;
+#pragma unroll
+            for (int k = 0; k < IPT; ++k) {
+                const bool ok = icol[k] >= 0 && wnext[i] != 0.f;
+                const uint32_t off = ok ? (uint32_t)(((rb + icol[k]) * ldi + offi + c0 + ig[k] * 8) * 2) : IRGAN_OOB;
+                pre[k][i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+            }
+        }
+    };
+    issue(oy0);
+    __syncthreads();  // the horizontal tables
+    const float qs = Q8 ? *q8.q : 1.f;
+    float amx = 0.f;
+    int buf = 0;
+#pragma unroll 1
+    for (int oy = oy0; oy < oy1; ++oy, buf ^= 1) {
+        float wcur[TM];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) wcur[i] = wnext[i];
+        // vertical taps of row oy (its loads were issued one row ago)
+        float* const row = sm + buf * Win * CB;
+#pragma unroll
+        for (int k = 0; k < IPT; ++k) {
+            if (icol[k] < 0) continue;
+            float acc[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                if (wcur[i] == 0.f) continue;
+                const uint32_t wd[4] = {pre[k][i].x, pre[k][i].y, pre[k][i].z, pre[k][i].w};
+                float xv[8];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    xv[2 * q] = __uint_as_float(wd[q] << 16);
+                    xv[2 * q + 1] = __uint_as_float(wd[q] & 0xffff0000u);
+                }
+                if constexpr (NORM) {
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) {
+                        const float h = fmaf(xv[q], nr[q], nm[q]);
+                        xv[q] = act == IRGAN_ACT_RELU ? fmaxf(h, 0.f) : (act == IRGAN_ACT_LRELU && h < 0.f ? 0.2f * h : h);
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < 8; ++q) acc[q] += wcur[i] * xv[q];
+            }
+            float4* d = (float4*)(row + (icol[k] * CB + ig[k] * 8));
+            d[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+            d[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+        }
+        if (oy + 1 < oy1) issue(oy + 1);
+        __syncthreads();  // row oy's vertical sums complete
+        // horizontal taps of row oy
+#pragma unroll
+        for (int k = 0; k < OPT; ++k) {
+            const int v = tid + k * NT;
+            const bool okv = v < OG;
+            const int ox = okv ? v / G : 0, g = v - (v / G) * G;
+            float acc[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+#pragma unroll
+            for (int j = 0; j < TM; ++j) {
+                const float w = tw[ox * TM + j];
+                if (w == 0.f) continue;
+                const float4* sp = (const float4*)(row + (ti[ox * TM + j] * CB + g * 8));
+                const float4 a = sp[0], b = sp[1];
+                acc[0] += w * a.x; acc[1] += w * a.y; acc[2] += w * a.z; acc[3] += w * a.w;
+                acc[4] += w * b.x; acc[5] += w * b.y; acc[6] += w * b.z; acc[7] += w * b.w;
+            }
+            u32x4_t u;
+            u.x = pk_bf16(acc[0], acc[1]);
+            u.y = pk_bf16(acc[2], acc[3]);
+            u.z = pk_bf16(acc[4], acc[5]);
+            u.w = pk_bf16(acc[6], acc[7]);
+            const long o = (((long)n * Hout + oy) * Wout + ox) * ldo + offo + c0 + g * 8;
+            __builtin_amdgcn_raw_buffer_store_b128(u, yr, okv ? (int)(o * 2) : (int)IRGAN_OOB, 0, 0);
+            if constexpr (Q8) {
+                const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
+                float vb[8];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    vb[2 * q] = __uint_as_float(wd[q] << 16);
+                    vb[2 * q + 1] = __uint_as_float(wd[q] & 0xffff0000u);
+                }
+                if (okv) {
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) amx = fmaxf(amx, fabsf(vb[q]));
+                }
+                const uint2 p8 = pack8_fp8(vb, qs);
+                const long o8 = (((long)n * Hout + oy) * Wout + ox) * q8.ld + q8.off + c0 + g * 8;
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, p8), qr, okv ? (int)o8 : (int)IRGAN_OOB,
+                                                      0, 0);
+            }
+        }
+    }
+    if constexpr (Q8) fp8_block_amax(amx, q8.amax, blockIdx.y * gridDim.x + blockIdx.x);
+}
+
+// the pipelined form for a (bf16 -> bf16, no accumulate) resample, or false (nothing launched)
+bool sep_pipe_launch(const void* in, int in_dtype, int N, int Hin, int Win, int C, int ldi, int offi, void* out,
+                     int out_dtype, int Hout, int Wout, int ldo, int offo, const int* ty, const float* wy, int Ty,
+                     const int* tx, const float* wx, int Tx, const float* mr, int act, const ResQ8* q8,
+                     hipStream_t st) {
+    static const bool off = getenv("IRGAN_SEP_ROWS1") != nullptr;   // A/B: sep_lds_kernel
+    if (off || in_dtype != IRGAN_BF16 || out_dtype != IRGAN_BF16) return false;
+    const int TM = Ty > Tx ? Ty : Tx;
+    if (TM > 8 || C % 8 || ldi % 8 || offi % 8 || ldo % 8 || offo % 8) return false;
+    if (q8 && (q8->ld % 8 || q8->off % 8)) return false;
+    int CB = 0;
+    for (int cb = 128; cb >= 8 && !CB; cb >>= 1)
+        if (C % cb == 0 && (long)Win * cb <= 8192) CB = cb;
+    if (!CB) return false;
+    const int G = CB / 8;
+    const long WG = (long)Win * G, OG = (long)Wout * G;
+    const int ipt = WG <= 512 ? 1 : (WG <= 1024 ? 2 : 0);
+    const int opt = OG <= 512 ? 1 : (OG <= 1024 ? 2 : (OG <= 2048 ? 4 : 0));
+    if (!ipt || !opt || 512 % G) return false;
+    if ((long)N * Hin * Win * ldi * 2 >= (1L << 31) || (long)N * Hout * Wout * ldo * 2 >= (1L << 31)) return false;
+    const int R = Hout >= 64 ? 8 : (Hout >= 16 ? 4 : 1);
+    const size_t sh = (size_t)2 * Win * CB * 4 + (size_t)Wout * 8 * 8;
+    if (sh > 80 * 1024) return false;
+    dim3 g(N * irgan_cdiv(Hout, R), C / CB);
+    const ResQ8 qq = q8 ? *q8 : ResQ8{};
+    const int swz = sep_swz();
+#define SPK(TMV, NORMV, Q8V, IP, OP)                                                                               \
+    sep_pipe_kernel<TMV, NORMV, Q8V, IP, OP><<<g, 512, sh, st>>>((const bf16_t*)in, Hin, Win, ldi, offi,          \
+                                                                 (bf16_t*)out, Hout, Wout, ldo, offo, ty, wy, Ty, \
+                                                                 tx, wx, Tx, CB, R, mr, C, act, swz, qq)
+#define SPO(TMV, NORMV, Q8V, IP)                              \
+    if (opt == 1) SPK(TMV, NORMV, Q8V, IP, 1);                \
+    else if (opt == 2) SPK(TMV, NORMV, Q8V, IP, 2);           \
+    else SPK(TMV, NORMV, Q8V, IP, 4);
+#define SPI(TMV, NORMV, Q8V)                                  \
+    if (ipt == 1) { SPO(TMV, NORMV, Q8V, 1) } else { SPO(TMV, NORMV, Q8V, 2) }
+#define SPT(NORMV, Q8V)                                       \
+    if (TM <= 2) { SPI(2, NORMV, Q8V) }                       \
+    else if (TM <= 4) { SPI(4, NORMV, Q8V) }                  \
+    else if (TM <= 6) { SPI(6, NORMV, Q8V) }                  \
+    else { SPI(8, NORMV, Q8V) }
+    if (mr && q8) { SPT(true, true) }
+    else if (mr) { SPT(true, false) }
+    else if (q8) { SPT(false, true) }
+    else { SPT(false, false) }
+#undef SPT
+#undef SPI
+#undef SPO
+#undef SPK
+    return true;
+}
+
 // Threads per block of sep_lds_kernel and the LDS row cap (floats) that sizes its channel
 // group: 512 threads with CB <= 8192 / Win.  Half-size groups (against 1024 threads) double
 // the blocks and let two resident blocks per CU overlap one's load with the other's taps: the
@@ -558,6 +790,12 @@ extern "C" int irgan_sep_resample(const void* in, int32_t in_dtype, int32_t N, i
     if (Ty < 1 || Tx < 1) return IRGAN_EINVAL;
     static const bool use_lds = !getenv("IRGAN_NO_SEP_LDS");
     const int TM = Ty > Tx ? Ty : Tx;
+    if (use_lds && !accumulate &&
+        sep_pipe_launch(in, in_dtype, N, Hin, Win, C, ldi, offi, out, out_dtype, Hout, Wout, ldo, offo, ty, wy, Ty, tx,
+                        wx, Tx, nullptr, 0, nullptr, (hipStream_t)s)) {
+        IRGAN_LAUNCH_CHECK();
+        return 0;
+    }
     if (vec && use_lds && TM <= 8) {
         // channel group: the widest of 128..8 dividing C whose fp32 row [Win][CB] fits the cap
         const int nt = sep_nt();
@@ -610,6 +848,11 @@ extern "C" int irgan_sep_resample_in(const void* in, int32_t in_dtype, int32_t N
     if (Ty < 1 || Tx < 1) return IRGAN_EINVAL;
     const int TM = Ty > Tx ? Ty : Tx;
     if (!vec || TM > 8 || getenv("IRGAN_NO_SEP_LDS") || getenv("IRGAN_NO_IN_RESAMPLE")) return IRGAN_EUNSUPPORTED;
+    if (sep_pipe_launch(in, in_dtype, N, Hin, Win, C, ldi, offi, out, out_dtype, Hout, Wout, ldo, offo, ty, wy, Ty, tx,
+                        wx, Tx, mr, act, nullptr, (hipStream_t)s)) {
+        IRGAN_LAUNCH_CHECK();
+        return 0;
+    }
     const int nt = sep_nt();
     int CB = 0;
     for (int cb = 128; cb >= 8 && !CB; cb >>= 1)
@@ -650,6 +893,12 @@ extern "C" int irgan_sep_resample_fp8(const void* in, int32_t in_dtype, int32_t 
     if (Ty < 1 || Tx < 1) return IRGAN_EINVAL;
     const int TM = Ty > Tx ? Ty : Tx;
     if (!vec || TM > 8 || out_dtype != IRGAN_BF16) return IRGAN_EUNSUPPORTED;
+    const ResQ8 q8{(uint8_t*)y8, ld8, off8, q, amax};
+    if (sep_pipe_launch(in, in_dtype, N, Hin, Win, C, ldi, offi, out, out_dtype, Hout, Wout, ldo, offo, ty, wy, Ty, tx,
+                        wx, Tx, mr, act, &q8, (hipStream_t)s)) {
+        IRGAN_LAUNCH_CHECK();
+        return 0;
+    }
     const int nt = sep_nt();
     int CB = 0;
     for (int cb = 128; cb >= 8 && !CB; cb >>= 1)
@@ -658,7 +907,6 @@ extern "C" int irgan_sep_resample_fp8(const void* in, int32_t in_dtype, int32_t 
     dim3 g(N * Hout, C / CB);
     const size_t sh = (size_t)Win * CB * 4;
     hipStream_t st = (hipStream_t)s;
-    const ResQ8 q8{(uint8_t*)y8, ld8, off8, q, amax};
 #define SEPQ(T, NORMV)                                                                                            \
     sep_lds_kernel<T, NORMV, 512, true><<<g, 512, sh, st>>>(in, in_dtype, Hin, Win, ldi, offi, out, out_dtype, Hout, \
                                                             Wout, ldo, offo, ty, wy, Ty, tx, wx, Tx, 0, CB, mr, C,    \
