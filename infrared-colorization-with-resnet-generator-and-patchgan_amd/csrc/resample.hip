@@ -275,11 +275,16 @@ __global__ __launch_bounds__(512) void sep_pipe_kernel(const bf16_t* __restrict_
     const int WG = Win * G, OG = Wout * G;
     float* const tw = sm + 2 * Win * CB;                 // [Wout][TM] horizontal weights
     int* const ti = (int*)(tw + Wout * TM);              // [Wout][TM] horizontal taps (input column)
-    const int nrb = (Hout + R - 1) / R;
-    const int rbk = xcd_tile(blockIdx.x, gridDim.x, swz);
+    // block -> (row block, channel group), groups fastest: the C / CB blocks that read the
+    // same input pixels (each a CB-channel slice of every pixel row) are consecutive logical
+    // tiles, i.e. (XCD-aware order) dispatched together on one XCD, so a 64 / 128-byte slice
+    // read pulls the whole pixel row into that L2 once for all of them
+    const int nrb = (Hout + R - 1) / R, ng = C / CB;
+    const int t = xcd_tile(blockIdx.x, gridDim.x, swz);
+    const int rbk = t / ng;
     const int n = rbk / nrb, oy0 = (rbk - n * nrb) * R;
     const int oy1 = min(Hout, oy0 + R);
-    const int c0 = blockIdx.y * CB;
+    const int c0 = (t - rbk * ng) * CB;
     const int tid = threadIdx.x;
     for (int e = tid; e < Wout * TM; e += NT) {
         const int ox = e / TM, j = e - ox * TM;
@@ -417,7 +422,7 @@ __global__ __launch_bounds__(512) void sep_pipe_kernel(const bf16_t* __restrict_
             }
         }
     }
-    if constexpr (Q8) fp8_block_amax(amx, q8.amax, blockIdx.y * gridDim.x + blockIdx.x);
+    if constexpr (Q8) fp8_block_amax(amx, q8.amax, blockIdx.x);
 }
 
 // the pipelined form for a (bf16 -> bf16, no accumulate) resample, or false (nothing launched)
@@ -443,7 +448,7 @@ bool sep_pipe_launch(const void* in, int in_dtype, int N, int Hin, int Win, int 
     const int R = Hout >= 64 ? 8 : (Hout >= 16 ? 4 : 1);
     const size_t sh = (size_t)2 * Win * CB * 4 + (size_t)Wout * 8 * 8;
     if (sh > 80 * 1024) return false;
-    dim3 g(N * irgan_cdiv(Hout, R), C / CB);
+    const dim3 g(N * irgan_cdiv(Hout, R) * (C / CB));
     const ResQ8 qq = q8 ? *q8 : ResQ8{};
     const int swz = sep_swz();
 #define SPK(TMV, NORMV, Q8V, IP, OP)                                                                               \
