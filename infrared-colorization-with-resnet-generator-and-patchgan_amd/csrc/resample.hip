@@ -266,14 +266,14 @@ __global__ __launch_bounds__(512) void sep_pipe_kernel(const bf16_t* __restrict_
                                                        int ldo, int offo, const int* __restrict__ ty,
                                                        const float* __restrict__ wy, int Ty,
                                                        const int* __restrict__ tx, const float* __restrict__ wx,
-                                                       int Tx, int CB, int R, const float* __restrict__ mr, int C,
-                                                       int act, int swz, ResQ8 q8) {
+                                                       int Tx, int CB, int CBP, int R, const float* __restrict__ mr,
+                                                       int C, int act, int swz, ResQ8 q8) {
     constexpr int NT = 512;
     extern __shared__ float4 sm4[];
-    float* const sm = (float*)sm4;                       // [2][Win][CB] fp32 rows
+    float* const sm = (float*)sm4;                       // [2][Win][CBP] fp32 rows (CBP >= CB: bank spread)
     const int G = CB >> 3;
     const int WG = Win * G, OG = Wout * G;
-    float* const tw = sm + 2 * Win * CB;                 // [Wout][TM] horizontal weights
+    float* const tw = sm + 2 * Win * CBP;                // [Wout][TM] horizontal weights
     int* const ti = (int*)(tw + Wout * TM);              // [Wout][TM] horizontal taps (input column)
     // block -> (row block, channel group), groups fastest: the C / CB blocks that read the
     // same input pixels (each a CB-channel slice of every pixel row) are consecutive logical
@@ -345,7 +345,7 @@ __global__ __launch_bounds__(512) void sep_pipe_kernel(const bf16_t* __restrict_
 #pragma unroll
         for (int i = 0; i < TM; ++i) wcur[i] = wnext[i];
         // vertical taps of row oy (its loads were issued one row ago)
-        float* const row = sm + buf * Win * CB;
+        float* const row = sm + buf * Win * CBP;
 #pragma unroll
         for (int k = 0; k < IPT; ++k) {
             if (icol[k] < 0) continue;
@@ -372,7 +372,7 @@ __global__ __launch_bounds__(512) void sep_pipe_kernel(const bf16_t* __restrict_
 #pragma unroll
                 for (int q = 0; q < 8; ++q) acc[q] += wcur[i] * xv[q];
             }
-            float4* d = (float4*)(row + (icol[k] * CB + ig[k] * 8));
+            float4* d = (float4*)(row + (icol[k] * CBP + ig[k] * 8));
             d[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
             d[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
         }
@@ -391,7 +391,7 @@ __global__ __launch_bounds__(512) void sep_pipe_kernel(const bf16_t* __restrict_
             for (int j = 0; j < TM; ++j) {
                 const float w = tw[ox * TM + j];
                 if (w == 0.f) continue;
-                const float4* sp = (const float4*)(row + (ti[ox * TM + j] * CB + g * 8));
+                const float4* sp = (const float4*)(row + (ti[ox * TM + j] * CBP + g * 8));
                 const float4 a = sp[0], b = sp[1];
                 acc[0] += w * a.x; acc[1] += w * a.y; acc[2] += w * a.z; acc[3] += w * a.w;
                 acc[4] += w * b.x; acc[5] += w * b.y; acc[6] += w * b.z; acc[7] += w * b.w;
@@ -446,7 +446,15 @@ bool sep_pipe_launch(const void* in, int in_dtype, int N, int Hin, int Win, int 
     if (!ipt || !opt || 512 % G) return false;
     if ((long)N * Hin * Win * ldi * 2 >= (1L << 31) || (long)N * Hout * Wout * ldo * 2 >= (1L << 31)) return false;
     const int R = Hout >= 64 ? 8 : (Hout >= 16 ? 4 : 1);
-    const size_t sh = (size_t)2 * Win * CB * 4 + (size_t)Wout * 8 * 8;
+    const int TMt = TM <= 2 ? 2 : (TM <= 4 ? 4 : (TM <= 6 ? 6 : 8));
+    // rows padded by 4 floats where two blocks per CU still fit: a stride-2 horizontal read
+    // (Downsample, the UpsampleAA adjoint) otherwise lands every 64-float step on one bank
+    int CBP = CB + 4;
+    size_t sh = (size_t)2 * Win * CBP * 4 + (size_t)Wout * TMt * 8;
+    if (sh > 80 * 1024) {
+        CBP = CB;
+        sh = (size_t)2 * Win * CBP * 4 + (size_t)Wout * TMt * 8;
+    }
     if (sh > 80 * 1024) return false;
     const dim3 g(N * irgan_cdiv(Hout, R) * (C / CB));
     const ResQ8 qq = q8 ? *q8 : ResQ8{};
@@ -454,7 +462,7 @@ bool sep_pipe_launch(const void* in, int in_dtype, int N, int Hin, int Win, int 
 #define SPK(TMV, NORMV, Q8V, IP, OP)                                                                               \
     sep_pipe_kernel<TMV, NORMV, Q8V, IP, OP><<<g, 512, sh, st>>>((const bf16_t*)in, Hin, Win, ldi, offi,          \
                                                                  (bf16_t*)out, Hout, Wout, ldo, offo, ty, wy, Ty, \
-                                                                 tx, wx, Tx, CB, R, mr, C, act, swz, qq)
+                                                                 tx, wx, Tx, CB, CBP, R, mr, C, act, swz, qq)
 #define SPO(TMV, NORMV, Q8V, IP)                              \
     if (opt == 1) SPK(TMV, NORMV, Q8V, IP, 1);                \
     else if (opt == 2) SPK(TMV, NORMV, Q8V, IP, 2);           \
