@@ -207,7 +207,7 @@ class _Fp8ResConv(torch.autograd.Function):
         with torch.autocast("cpu", enabled=False):   # e4m3 operands: exact in fp32
             dw = torch.nn.grad.conv2d_weight(_rpad(fp8_q(x).float(), 1), w.shape, gq.float()).to(w.dtype)
         H, W = x.shape[-2:]
-        xp = torch.zeros(x.shape[0], x.shape[1], H + 2, W + 2, dtype=x.dtype)
+        xp = torch.zeros(x.shape[0], x.shape[1], H + 2, W + 2, dtype=x.dtype, device=x.device)
         g8 = torch.nn.grad.conv2d_input(xp.shape, fp8_q(wb), gq)
         gb = torch.nn.grad.conv2d_input(xp.shape, wb, gy)
         xf = torch.zeros_like(x, requires_grad=True)
@@ -336,8 +336,8 @@ def d_forward(P, x, n_layers=3, norm="instance"):
 
 def vgg_features(V, x):
     """VGGPerceptual.forward (ir:677-683): [-1,1] -> ImageNet-normalised -> relu3_3."""
-    mean = torch.tensor(IMAGENET_MEAN, dtype=x.dtype).view(1, 3, 1, 1)
-    std = torch.tensor(IMAGENET_STD, dtype=x.dtype).view(1, 3, 1, 1)
+    mean = torch.tensor(IMAGENET_MEAN, dtype=x.dtype, device=x.device).view(1, 3, 1, 1)
+    std = torch.tensor(IMAGENET_STD, dtype=x.dtype, device=x.device).view(1, 3, 1, 1)
     h = ((x + 1.0) / 2.0 - mean) / std
     for i, _, _ in VGG_CONVS:
         h = F.relu(F.conv2d(h, V[f"{i}.weight"], V[f"{i}.bias"], padding=1))
@@ -362,7 +362,7 @@ def ssim_loss(a, b, window_size=11, size_average=True):
     """1 - mean SSIM with a window_size^2 Gaussian (sigma 1.5), zero pad window_size // 2,
     C1=1e-4, C2=9e-4 (ir:714-750); size_average=False: the per-image vector (ir:746-747)."""
     c = a.shape[1]
-    g = gaussian_window(window_size, 1.5, a.dtype)[:, None]
+    g = gaussian_window(window_size, 1.5, a.dtype).to(a.device)[:, None]
     w = (g @ g.t()).expand(c, 1, window_size, window_size).contiguous()
     p = window_size // 2
     blur = lambda t: F.conv2d(t, w, padding=p, groups=c)   # noqa: E731
