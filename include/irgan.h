@@ -218,10 +218,6 @@ IRGAN_API int irgan_in_bwd_reduce(const void* dy, int32_t dy_dtype, int32_t lddy
                         const void* x, int32_t x_dtype, int32_t ldx, int32_t xoff, int32_t act,
                         int32_t N, int32_t HW, int32_t C, const float* mr, double* work,
                         float* red, irgan_stream_t s);
-/* The finalize half of irgan_in_bwd_reduce over nb float2 (sum g, sum g*xhat) partials
- * per (n, c) ([N][nb][C]) written by irgan_conv_dgrad_reflect_line_inred. */
-IRGAN_API int irgan_in_bwd_finalize(const void* part, int32_t N, int32_t HW, int32_t C, int32_t nb, float* red,
-                          irgan_stream_t s);
 /* dx = rstd*(g - mean(g) - xhat*mean(g*xhat)); also db[c] += sum dx (fp32 bias
  * grad of the producing conv, caller zeroes) when db != NULL.  dx may alias dy. */
 IRGAN_API int irgan_in_bwd_apply(const void* dy, int32_t dy_dtype, int32_t lddy, int32_t dyoff,
@@ -296,18 +292,6 @@ IRGAN_API int irgan_reflect_dgrad_ring_ws(const irgan_conv_desc* d, const void* 
  * % 256 == 0 take the 256-channel conv tile. */
 IRGAN_API int irgan_conv_dgrad_reflect_line(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p, void* dx,
                                   float* ws, int64_t ws_floats, irgan_stream_t s);
-/* irgan_conv_dgrad_reflect_line (the same dx) whose store pass also writes the backward
- * partials of the InstanceNorm that dx feeds (ir:386-411: conv -> IN [-> ReLU]): z = that IN's
- * PRE-norm input ([N][Ho][Wo] x dx channels, ldz / zoff), mr its {mean, rstd}, act its
- * activation; part[N][nb][dx channels] float2 (sum g, sum g*xhat) as irgan_in_bwd_reduce's
- * reduce pass computes them from (dx, z), *nb = 16x16 output patches per image (<=
- * IRGAN_IN_PARTS).  Then irgan_in_bwd_finalize + irgan_in_bwd_apply.  IRGAN_EUNSUPPORTED
- * (nothing launched, *nb = 0) where irgan_conv_dgrad_reflect_line is, or when dx / z strides
- * or offsets are not multiples of 8. */
-IRGAN_API int irgan_conv_dgrad_reflect_line_inred(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p,
-                                        void* dx, float* ws, int64_t ws_floats, const void* z, int32_t ldz,
-                                        int32_t zoff, const float* mr, int32_t act, void* part, int32_t* nb,
-                                        irgan_stream_t s);
 /* The fp8 path's ResnetBlock backward-data (config 5): the ring's line GEMM on the bf16 dy
  * and bf16 flipped weights w (d: as irgan_conv_dgrad_reflect_line), then the interior on e4m3
  * operands -- d8 = d with dtype IRGAN_FP8 and dy8's ld / offset, w8 the e4m3 flipped image,

@@ -137,43 +137,6 @@ extern "C" int irgan_conv_dgrad_reflect_line(const irgan_conv_desc* d, const voi
     return 0;
 }
 
-// irgan_conv_dgrad_reflect_line whose store pass also writes the InstanceNorm backward
-// partials of dx for the IN in front of it (conv_pp_kernel BRED: z = that IN's pre-norm input,
-// mr its {mean, rstd}, act its activation; part: float2[N][nb][Cout], nb = 16x16 patches per
-// image) -- irgan_in_bwd_reduce's pass over (dx, z) becomes irgan_in_bwd_finalize.
-extern "C" int irgan_conv_dgrad_reflect_line_inred(const irgan_conv_desc* d, const void* dy, const void* w, int32_t p,
-                                                   void* dx, float* ws, int64_t ws_floats, const void* z, int32_t ldz,
-                                                   int32_t zoff, const float* mr, int32_t act, void* part, int32_t* nb,
-                                                   irgan_stream_t s) {
-    if (!d || !dy || !w || !dx || !ws || !z || !mr || !part || !nb) return IRGAN_EINVAL;
-    if (act != IRGAN_ACT_NONE && act != IRGAN_ACT_RELU && act != IRGAN_ACT_LRELU) return IRGAN_EINVAL;
-    *nb = 0;
-    if ((long)d->N * d->Ho * d->Wo <= 0 || d->Cout <= 0) return 0;
-    const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH), ntn = d->Cout / 256;
-    if (!ring_line_check(d, p, ws_floats) || d->out_dtype != IRGAN_BF16 || d->act != IRGAN_ACT_NONE ||
-        d->sy != 1 || d->sx != 1 || d->Cin % 64 || d->Cout % 256 || narrow_bn(d) != 256 || irgan_res64::ok(d) ||
-        (long)d->N * d->H * d->W * d->ldx >= (1L << 30) || (long)d->Cout * 9 * d->Cin >= (1L << 30) ||
-        d->OH != d->Ho || d->OW != d->Wo || d->ldy % 8 || d->yoff % 8 || ldz % 8 || zoff % 8 ||
-        tpx * tpy > IRGAN_IN_PARTS)
-        return IRGAN_EUNSUPPORTED;
-    hipStream_t st = (hipStream_t)s;
-    ring_line_gemm_launch(d, dy, w, ws, st);
-    const int swz = irgan_xcd_swz();
-    const int blocks = d->N * tpy * tpx * ntn;
-    const InRef inr{(const bf16_t*)z, ldz, zoff, mr, act};
-    if (d->accumulate)
-        conv_pp_kernel<3, 3, 256, true, false, false, false, false, false, true><<<blocks, 512, 0, st>>>(
-            *d, (const bf16_t*)dy, (const bf16_t*)w, nullptr, dx, nullptr, ntn, tpx, tpy, swz, (float2*)part, nullptr,
-            nullptr, ws, PhaseTab{}, inr);
-    else
-        conv_pp_kernel<3, 3, 256, false, false, false, false, false, false, true><<<blocks, 512, 0, st>>>(
-            *d, (const bf16_t*)dy, (const bf16_t*)w, nullptr, dx, nullptr, ntn, tpx, tpy, swz, (float2*)part, nullptr,
-            nullptr, ws, PhaseTab{}, inr);
-    IRGAN_LAUNCH_CHECK();
-    *nb = tpx * tpy;
-    return 0;
-}
-
 // The fp8 path's ResnetBlock backward-data (config 5): the ring's line GEMM on the bf16 dY and
 // bf16 flipped weights (d, dy, w: as irgan_conv_dgrad_reflect_line), then the interior on the
 // e4m3 operands (d8: d with dtype FP8 and dy8's ld / offset; dqy, dqw: their dequantisation

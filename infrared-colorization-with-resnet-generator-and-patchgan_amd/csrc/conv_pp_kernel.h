@@ -175,21 +175,8 @@ struct PhaseTab {
 };
 IRGAN_HD int pick4(const int (&a)[4], int i) { return i == 0 ? a[0] : (i == 1 ? a[1] : (i == 2 ? a[2] : a[3])); }
 
-// BRED (irgan_conv_dgrad_reflect_line_inred): the backward-data's output dx is the gradient
-// that a following InstanceNorm backward reduces (dy of act(IN(z)), ir:154-165): the store pass
-// also loads z (the IN's pre-norm input, same pixels and channels as dx) and writes the
-// per-(image, patch, channel) partials (sum g, sum g * xh), xh = (z - mean) * rstd,
-// g = dx * act'(xh) -- the terms of rows8_kernel<1> (norm.hip) on the same bf16 dx -- in the
-// layout finalize_kernel reduces, so the separate backward reduce pass over (dx, z) is gone.
-struct InRef {
-    const bf16_t* z;
-    int ldz, zoff;
-    const float* mr;  // {mean, rstd} per (image, channel)
-    int act;
-};
-
 template <int KH, int KW, int BN, bool ACC, bool STATS = false, bool F8 = false, bool ONE = false, bool S2D = false,
-          bool PH4 = false, bool BRED = false>
+          bool PH4 = false>
 __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
                                                          const bf16_t* __restrict__ w, const float* __restrict__ bias,
                                                          void* __restrict__ y, const void* __restrict__ mask,
@@ -198,7 +185,7 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
                                                          const float* __restrict__ dqx = nullptr,
                                                          const float* __restrict__ dqw = nullptr,
                                                          const float* __restrict__ rg = nullptr,
-                                                         const PhaseTab tab = PhaseTab{}, const InRef inr = InRef{}) {
+                                                         const PhaseTab tab = PhaseTab{}) {
     constexpr int ESZ = F8 ? 1 : 2, CHN = 128 / ESZ;  // operand bytes, channels per 128-byte chunk
     const char* const xb = (const char*)x;
     const char* wb = (const char*)w;
@@ -214,7 +201,6 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
     static_assert(HP <= HPMAX && HP > 32 && TAPS >= 2, "halo pieces per wave are 4 to 6");
     static_assert(!S2D || (KH == 2 && KW == 2 && !F8), "space-to-depth: the 2x2 form of a 4x4 stride-2 conv");
     static_assert(!PH4 || (!S2D && !F8 && !STATS), "four-phase backward-data: plain bf16");
-    static_assert(!BRED || (!STATS && !ONE && !S2D && !PH4 && BN == 256), "IN-reduce store pass: ResnetBlock dgrad");
     __shared__ __attribute__((aligned(1024))) char smem[LDS];
     char* const sH = smem;
     char* const sB = smem + (ONE ? 1 : 2) * HBYTES;
@@ -645,18 +631,6 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
         default: emit(std::integral_constant<int, IRGAN_ACT_NONE>()); break;
     }
     if (out_f32) return;
-    constexpr int LPP = PP<BN>::LPP;
-    constexpr int PPASS = PP<BN>::PPASS;
-    constexpr int NZ = BRED ? 256 / PPASS : 1;  // z rows per thread (BRED)
-    uint4 zr[NZ];
-    if constexpr (BRED) {  // every z load in flight before the barrier / ring pass / stores
-        const int c8 = (tid % LPP) * 8;
-#pragma unroll
-        for (int q = 0; q < NZ; ++q) {
-            const long pix = pix_of(tid / LPP + q * PPASS);
-            zr[q] = pix >= 0 ? *(const uint4*)(inr.z + pix * inr.ldz + inr.zoff + n0 + c8) : make_uint4(0u, 0u, 0u, 0u);
-        }
-    }
     __syncthreads();
     if (rg) {  // the ring terms onto the staged pixels (each (pixel, slot) owned by one thread)
 #pragma unroll
@@ -670,57 +644,29 @@ __global__ __launch_bounds__(512, ONE ? 2 : 1) void conv_pp_kernel(const irgan_c
         }
         __syncthreads();
     }
-    if constexpr (STATS || BRED) {
+    constexpr int LPP = PP<BN>::LPP;
+    constexpr int PPASS = PP<BN>::PPASS;
+    if constexpr (STATS) {
         // InstanceNorm statistics of the stored (bf16) outputs fused into the store
         // pass: per-channel (sum, sum of squares) over this block's valid pixels, one
         // float2 partial per (image, patch, channel) in the layout finalize_kernel
         // (norm.hip) reduces.  Host guarantees Cout % BN == 0, LPP * PPASS == 512.
-        // BRED: (sum g, sum g * xh) of the IN backward instead (InRef above).
-        static_assert(PP<BN>::LPP * PP<BN>::PPASS == 512, "all threads store");
+        static_assert(!STATS || PP<BN>::LPP * PP<BN>::PPASS == 512, "all threads store");
         const int c8 = (tid % LPP) * 8, co8 = n0 + c8;
-        float s1[8], s2[8], mean[8], rstd[8];
+        float s1[8], s2[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.f;
-        if constexpr (BRED) {
-            const float4* m4 = (const float4*)(inr.mr + 2 * ((long)img * d.Cout + co8));
+        for (int m = tid / LPP; m < 256; m += PPASS) {
+            const long pix = pix_of(m);
+            if (pix < 0) continue;
+            const uint4 v = *(const uint4*)(smem + m * RSB + c8 * 2);
+            *(uint4*)((bf16_t*)y + pix * d.ldy + d.yoff + co8) = v;
+            const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const float4 t = m4[k];
-                mean[2 * k] = t.x; rstd[2 * k] = t.y; mean[2 * k + 1] = t.z; rstd[2 * k + 1] = t.w;
-            }
-        }
-        if constexpr (BRED) {
-#pragma unroll
-            for (int q = 0; q < NZ; ++q) {
-                const long pix = pix_of(tid / LPP + q * PPASS);
-                if (pix < 0) continue;
-                const uint4 v = *(const uint4*)(smem + (tid / LPP + q * PPASS) * RSB + c8 * 2);
-                *(uint4*)((bf16_t*)y + pix * d.ldy + d.yoff + co8) = v;
-                const uint32_t wv[4] = {v.x, v.y, v.z, v.w}, zv[4] = {zr[q].x, zr[q].y, zr[q].z, zr[q].w};
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const float gv = __uint_as_float(k & 1 ? wv[k >> 1] & 0xffff0000u : wv[k >> 1] << 16);
-                    const float xv = __uint_as_float(k & 1 ? zv[k >> 1] & 0xffff0000u : zv[k >> 1] << 16);
-                    const float xh = (xv - mean[k]) * rstd[k];
-                    const float g = inr.act == IRGAN_ACT_RELU ? (xh > 0.f ? gv : 0.f)
-                                                              : (inr.act == IRGAN_ACT_LRELU ? (xh > 0.f ? gv : gv * 0.2f) : gv);
-                    s1[k] += g;
-                    s2[k] += g * xh;
-                }
-            }
-        } else {
-            for (int m = tid / LPP; m < 256; m += PPASS) {
-                const long pix = pix_of(m);
-                if (pix < 0) continue;
-                const uint4 v = *(const uint4*)(smem + m * RSB + c8 * 2);
-                *(uint4*)((bf16_t*)y + pix * d.ldy + d.yoff + co8) = v;
-                const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const float lo = __uint_as_float(wv[k] << 16), hi = __uint_as_float(wv[k] & 0xffff0000u);
-                    s1[2 * k] += lo; s2[2 * k] += lo * lo;
-                    s1[2 * k + 1] += hi; s2[2 * k + 1] += hi * hi;
-                }
+                const float lo = __uint_as_float(wv[k] << 16), hi = __uint_as_float(wv[k] & 0xffff0000u);
+                s1[2 * k] += lo; s2[2 * k] += lo * lo;
+                s1[2 * k + 1] += hi; s2[2 * k + 1] += hi * hi;
             }
         }
         __syncthreads();  // staging reads done: reuse LDS for the cross-row reduction

@@ -710,17 +710,6 @@ extern "C" int irgan_in_bwd_reduce(const void* dy, int32_t dy_dtype, int32_t ldd
     return 0;
 }
 
-// the backward reduce's finalize alone, over partials another pass wrote (float2[N][nb][C]:
-// irgan_conv_dgrad_reflect_line_inred): red = {mean g, mean g * xh} per (image, channel)
-extern "C" int irgan_in_bwd_finalize(const void* part, int32_t N, int32_t HW, int32_t C, int32_t nb, float* red,
-                                     irgan_stream_t s) {
-    if ((long)N * HW * C <= 0) return 0;
-    if (!part || !red || nb < 1 || nb > IRGAN_IN_PARTS) return IRGAN_EINVAL;
-    finalize_kernel<<<dim3(irgan_cdiv(C, FC), N), 256, 0, (hipStream_t)s>>>((const float2*)part, red, N, C, nb, HW, 1);
-    IRGAN_LAUNCH_CHECK();
-    return 0;
-}
-
 extern "C" int irgan_in_bwd_apply(const void* dy, int32_t dy_dtype, int32_t lddy, int32_t dyoff, const void* dy2,
                                   int32_t dy2_dtype, int32_t lddy2, int32_t dy2off, const void* x, int32_t x_dtype,
                                   int32_t ldx, int32_t xoff, int32_t act, int32_t N, int32_t HW, int32_t C,

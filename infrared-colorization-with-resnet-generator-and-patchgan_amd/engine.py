@@ -352,26 +352,15 @@ class INLayer:
         if q8 is not None:
             ops.fp8_quant(y, *q8)
 
-    def bwd(self, bufs: Buffers, name: str, dy: Feat, z: Feat, act, dx: Feat, db=None, dy2: Feat = None, q8=None,
-            part_nb=0):
+    def bwd(self, bufs: Buffers, name: str, dy: Feat, z: Feat, act, dx: Feat, db=None, dy2: Feat = None, q8=None):
         """z: the PRE-norm input kept from forward; act: the activation after IN.
-        q8: also write dx's fp8 copy (ops.in_backward).  part_nb: the backward partials of
-        (dy, z) are already in the work buffer (the dgrad that produced dy wrote them, see
-        inred())."""
+        q8: also write dx's fp8 copy (ops.in_backward)."""
         N, C = z.N, z.C
         work = bufs.flat("in_work", ops.IN_PARTS * N * C, torch.float64)
         red = bufs.flat("in_red", 2 * N * C)
         mr = bufs.d["mr_" + name]
         ops.in_backward(dy, z, act, mr, work, red, dx, db=db if INLayer.sum_bias_grad else None, dy2=dy2,
-                        q8=q8 if not INLayer.sum_bias_grad else None, part_nb=part_nb)
-
-    def inred(self, bufs: Buffers, name: str, z: Feat, act):
-        """ops.conv_dgrad(inred=...) operands for the dgrad whose dx this layer's bwd reduces
-        next: (z, mr, act, the work buffer bwd reads), or None where that fusion does not apply
-        (NoNorm, or the bias-gradient reduction that the apply pass does with the partials)."""
-        if type(self) is not INLayer or INLayer.sum_bias_grad or z.dt != BF16:
-            return None
-        return (z, bufs.d["mr_" + name], act, bufs.flat("in_work", ops.IN_PARTS * z.N * z.C, torch.float64))
+                        q8=q8 if not INLayer.sum_bias_grad else None)
 
 class NoNorm(INLayer):
     """norm='none' (ir:162-163: ``lambda num_features: Identity()``): the layer is just its
@@ -406,7 +395,7 @@ class NoNorm(INLayer):
         ops.conv_fwd(pc, x, z, bias=pc.bias is not None)
         return self._ident(bufs, name, z.N, z.C)
 
-    def bwd(self, bufs, name, dy, z, act, dx, db=None, dy2=None, q8=None, part_nb=0):
+    def bwd(self, bufs, name, dy, z, act, dx, db=None, dy2=None, q8=None):
         if dy2 is not None or q8 is not None:
             raise NotImplementedError("NoNorm.bwd: dy2 / q8 are InstanceNorm-path features")
         if act == ACT_NONE and dx.t.data_ptr() == dy.t.data_ptr() and dx.off == dy.off:
@@ -529,15 +518,14 @@ class GeneratorEngine:
         ops.pad(x, xp, 1, "replicate")
         return xp
 
-    def _res_dgrad(self, g: Buffers, pc, dy: Feat, dx: Feat, accumulate, padbuf, inred=None):
-        """dx (+)= backward-data of a ResnetBlock conv for the padding type.  inred: see
-        ops.conv_dgrad; returns the IN partials per image it wrote (0: none)."""
+    def _res_dgrad(self, g: Buffers, pc, dy: Feat, dx: Feat, accumulate, padbuf):
+        """dx (+)= backward-data of a ResnetBlock conv for the padding type."""
         if self.padding_type != "replicate":
-            return ops.conv_dgrad(pc, dy, dx, accumulate=accumulate, pad_buf=padbuf, inred=inred) or 0
+            ops.conv_dgrad(pc, dy, dx, accumulate=accumulate, pad_buf=padbuf)
+            return
         dxp = Feat(g.get("res_dxp", (dx.N, dx.H + 2, dx.W + 2, dx.C), self.tdt))
         ops.conv_dgrad(pc, dy, dxp)
         ops.pad_fold(dxp, dx, 1, "replicate", accumulate=accumulate)
-        return 0
 
     def _bgrad(self, key):
         """Flat-buffer slice of parameter ``key``'s gradient, None when the layout has no
@@ -796,7 +784,6 @@ class GeneratorEngine:
         nb2 = 2 * self.n_blocks
         dy8 = Feat(g.get("dy8", (B, H2, W2, c2), torch.float8_e4m3fn)) if f8 else None
         k1, k2 = self.res_keys
-        nb_h = 0   # IN partials of dh for r{b}_2 written by block b + 1's conv1 backward-data
         for b in reversed(range(self.n_blocks)):
             p1, p2 = self.res[b]
             key = f"resblocks.{b}.conv_block."
@@ -809,32 +796,25 @@ class GeneratorEngine:
             xin2 = Feat(g.d[f"xp2_{b}"]) if self.padding_type == "replicate" else t2
             s2, s1 = nb2 + 2 * b, nb2 + 2 * b + 1
             self.norms[f"r{b}_2"].bwd(g, f"r{b}_2", dh, r2, ACT_NONE, dt_, db=self._bgrad(f"{key}{k2}.bias"),
-                                      q8=A.spec(s2, dy8) if f8 else None, part_nb=nb_h)
-            nb_r = 0
+                                      q8=A.spec(s2, dy8) if f8 else None)
             dr = Feat(g.get("dtmp2", (B, H2, W2, c2), T))
             if f8:
                 A.ensure(s2, dt_, dy8)
                 wg8(p2, f"{key}{k2}", Feat(g.d[f"x8_{2 * b + 1}"]), A.dqp_used(2 * b + 1), dy8, s2, xin2, dt_)
                 ops.conv_dgrad_fp8(p2, *self._w8(4 * b + 3), dy8, A.dqp(s2), dt_, dr)
             else:
-                n1 = self.norms[f"r{b}_1"]
-                nb_r = self._res_dgrad(g, p2, dt_, dr, False, padbuf,
-                                       inred=None if drop else n1.inred(g, f"r{b}_1", r1, ACT_RELU))
+                self._res_dgrad(g, p2, dt_, dr, False, padbuf)
                 wg(p2, f"{key}{k2}", xin2, dt_)
                 if drop:   # backward of the dropout: the same mask and scale on the gradient
                     ops.dropout(dr, dr, g.state["dropout_seed"] + 2 * b)
             self.norms[f"r{b}_1"].bwd(g, f"r{b}_1", dr, r1, ACT_RELU, dr, db=self._bgrad(f"{key}{k1}.bias"),
-                                      q8=A.spec(s1, dy8) if f8 else None, part_nb=nb_r)
-            nb_h = 0
+                                      q8=A.spec(s1, dy8) if f8 else None)
             if f8:
                 A.ensure(s1, dr, dy8)
                 wg8(p1, f"{key}{k1}", Feat(g.d[f"x8_{2 * b}"]), A.dqp_used(2 * b), dy8, s1, xin1, dr)
                 ops.conv_dgrad_fp8(p1, *self._w8(4 * b + 1), dy8, A.dqp(s1), dr, dh, accumulate=True)
             else:
-                inr = None
-                if b > 0:   # dh is the dy of block b - 1's second IN
-                    inr = self.norms[f"r{b - 1}_2"].inred(g, f"r{b - 1}_2", Feat(g.d[f"r2_{b - 1}"]), ACT_NONE)
-                nb_h = self._res_dgrad(g, p1, dr, dh, True, padbuf, inred=inr)
+                self._res_dgrad(g, p1, dr, dh, True, padbuf)
                 wg(p1, f"{key}{k1}", xin1, dr)
             ready(f"{key}{k1}.weight")
         if f8:

@@ -88,11 +88,6 @@ def set_ring_epi(on: bool) -> bool:
     return old
 
 
-# the ResnetBlock backward-data writes the following IN backward's partials in its store pass
-# (irgan_conv_dgrad_reflect_line_inred); IRGAN_NO_DGRAD_INRED=1 runs the separate reduce pass
-IN_DGRAD_REDUCE = [os.environ.get("IRGAN_NO_DGRAD_INRED") != "1"]
-
-
 def _ring(d, dy: "Feat", buf, p, dx: "Feat"):
     """The reflect-pad ring of a bf16 backward-data onto dx (after its interior): the line
     GEMM + fold on ResnetBlock shapes, else the general ring launch (the library decides)."""
@@ -375,22 +370,16 @@ def conv_fwd_stats(pc: PackedConv, x: Feat, y: Feat, part: torch.Tensor) -> int:
 
 
 def conv_dgrad(pc: PackedConv, dy: Feat, dx: Feat, accumulate=False, mask: Feat = None, mask_act=0,
-               pad_buf: torch.Tensor = None, bias=False, inred=None):
+               pad_buf: torch.Tensor = None, bias=False):
     """dx = d(conv)/dx^T dy.  Reflect-padded layers: interior straight into dx and the
     padded ring folded onto dx's border band -- bf16 ResnetBlock shapes: the ring's line
     GEMM, then the interior launch whose store pass adds the ring terms
     (irgan_conv_dgrad_reflect_line); other bf16 shapes: the interior launch, then the ring
     (irgan_reflect_dgrad_ring_ws); fp32: split-K ring partials in pad_buf (fp32 scratch)
     folded by irgan_reflect_ring_fold; stride-2 layers launch per phase (or all four
-    phases in one irgan_conv_dgrad_s2 launch).
-
-    inred = (z Feat, mr, act, work): dx feeds act(IN(z)) (a ResnetBlock IN); where the
-    line-ring launch takes the shape, its store pass also writes that IN's backward partials
-    into work (irgan_conv_dgrad_reflect_line_inred) and the call returns their count per
-    image for in_backward(part_nb=...); otherwise (and without inred) it returns 0."""
+    phases in one irgan_conv_dgrad_s2 launch)."""
     s = pc.spec
     assert dy.C == pc.cout_eff and dx.C == s.cin and dy.dt == pc.dtype
-    nbr = [0]
     if pc.reflect:
         # Backward-data over the reflect-padded domain g (Hp x Wp) folded back:
         # the interior u in [p, H+p) maps 1:1 onto dx and is written there
@@ -412,18 +401,6 @@ def conv_dgrad(pc: PackedConv, dy: Feat, dx: Feat, accumulate=False, mask: Feat 
             if ring_mfma and RING_LINE[0] and RING_EPI[0] and dx.dt == BF16:
                 # line GEMM, then the interior with the ring folded into its store pass
                 ws = _ring_ws(dx.t.device, dx.N * 4 * 68 * dx.C)
-                if inred is not None and IN_DGRAD_REDUCE[0]:
-                    z, mr, act, work = inred
-                    assert (z.N, z.H, z.W, z.C) == (dx.N, dx.H, dx.W, dx.C) and z.dt == BF16
-                    nb = ctypes.c_int32(0)
-                    rc = _lib.load().irgan_conv_dgrad_reflect_line_inred(
-                        ctypes.byref(d), dy.ptr, P(buf), p, dx.ptr, P(ws), ws.numel(), z.ptr, z.ld, z.off, P(mr),
-                        act, P(work), ctypes.byref(nb), stream())
-                    if rc == 0:
-                        nbr[0] = nb.value
-                        return
-                    if rc != IRGAN_EUNSUPPORTED:
-                        raise _lib.IrganError(f"irgan_conv_dgrad_reflect_line_inred failed with code {rc}")
                 rc = _lib.load().irgan_conv_dgrad_reflect_line(ctypes.byref(d), dy.ptr, P(buf), p, dx.ptr, P(ws),
                                                               ws.numel(), stream())
                 if rc == 0:
@@ -436,7 +413,7 @@ def conv_dgrad(pc: PackedConv, dy: Feat, dx: Feat, accumulate=False, mask: Feat 
 
         TIMER.wrap(conv_tag("dgrad", s, (H, W), dx.N), launch)
         if p == 0 or ring_mfma:
-            return nbr[0]
+            return
         # ring in split-K partials: rows[ks][N][2p][Wp][C], cols[ks][N][H][2p][C]
         rsz, csz = dx.N * 2 * p * Wp * s.cin, dx.N * H * 2 * p * s.cin
         nk = -(-(ay * ax * pc.cout_eff) // 64)
@@ -582,18 +559,10 @@ def in_bwd_parts(dy: Feat, x: Feat, act: int, mr, work, red, dx: Feat, db=None, 
     return reduce, apply
 
 
-def in_backward(dy: Feat, x: Feat, act: int, mr, work, red, dx: Feat, db=None, dy2: Feat = None, q8=None,
-                part_nb=0):
-    """dx = backward of act(IN(x)) applied to (dy [+ dy2]); x = PRE-norm input.
-    part_nb > 0: the reduce's partials of (dy, x) are already in work (part_nb per image,
-    written by conv_dgrad(inred=...)): only the finalize runs before the apply."""
+def in_backward(dy: Feat, x: Feat, act: int, mr, work, red, dx: Feat, db=None, dy2: Feat = None, q8=None):
+    """dx = backward of act(IN(x)) applied to (dy [+ dy2]); x = PRE-norm input."""
     reduce, apply = in_bwd_parts(dy, x, act, mr, work, red, dx, db, dy2, q8)
-    if part_nb:
-        assert dy2 is None
-        _timed("in_bwd_finalize", x, lambda: _lib.call("irgan_in_bwd_finalize", P(work), x.N, x.H * x.W, x.C,
-                                                       part_nb, P(red), stream()))
-    else:
-        _timed("in_bwd_reduce", x, reduce)
+    _timed("in_bwd_reduce", x, reduce)
     _timed("in_bwd_apply", x, apply)
 
 
