@@ -486,3 +486,49 @@ def test_fp8_step_config5_b32_finite():
         assert torch.isfinite(st.grad).all() and torch.isfinite(st.flat).all()
     assert all(np.isfinite(v) for v in l8.values())
     assert (t8.netG.engine.f8a.q > 0).all() and (t8.netG.engine.f8w.q > 0).all()
+
+
+@pytest.mark.parametrize("ngf,size,B,expect", [(32, 64, 2, (True, False)), (64, 576, 1, (True, False))])
+def test_fp8_step_beyond_fp8_kernel_limits(ngf, size, B, expect):
+    """compute_dtype "fp8" where a layer group is outside the fp8 kernels' limits
+    (GeneratorEngine.fp8_layers): ngf = 32 gives down2 Cin = 64 (the fp8 conv takes 128-channel
+    K chunks) and 576 x 576 gives 18 x 18 > IN_PARTS fused-statistics tiles at H/2 -- down2 /
+    up1_conv then run on the bf16 kernels while the ResnetBlocks stay on e4m3.  Two steps: no
+    IrganError, everything finite, step-1 losses within 5e-2 of the bf16 step's."""
+    import numpy as np
+    from oracle import step as O
+    from test_gpu_step import LOSS_KEYS
+    irc = pkg()
+
+    def trainer(dtype):
+        cfg = irc.Config()
+        cfg.device = DEV
+        cfg.compute_dtype = dtype
+        cfg.ngf = ngf
+        cfg.batch_size = B
+        cfg.img_size = size
+        tr = irc.GANTrainer(cfg)
+        tr.netG.store.load(O.seeded_params(O.g_param_shapes(ngf=ngf), 1, bias_std=0.02), strict=True)
+        tr.netD.store.load(O.seeded_params(O.d_param_shapes(), 2, bias_std=0.02), strict=True)
+        tr.vgg.store.load(O.seeded_params(O.vgg_param_shapes(), 3, kaiming=True), strict=True)
+        for m in (tr.netG, tr.netD, tr.vgg):
+            m.repack()
+        return tr
+
+    g = torch.Generator().manual_seed(47)
+    ir = (torch.rand(B, 1, size, size, generator=g) * 2 - 1).to(DEV)
+    rgb = (torch.rand(B, 3, size, size, generator=g) * 2 - 1).to(DEV)
+    t8 = trainer("fp8")
+    assert t8.netG.engine.fp8_layers(B, size, size) == expect
+    l8 = t8.losses(t8.step(ir, rgb))
+    tb = trainer("bf16")
+    lb = tb.losses(tb.step(ir, rgb))
+    del tb
+    for k in LOSS_KEYS:
+        assert np.isfinite(l8[k]), k
+        if k != "loss_G_TV":
+            assert abs(l8[k] - lb[k]) <= 5e-2 * max(1.0, abs(lb[k])), (k, l8[k], lb[k])
+    l8 = t8.losses(t8.step(ir, rgb))
+    assert all(np.isfinite(v) for v in l8.values())
+    for st in (t8.netG.store, t8.netD.store):
+        assert torch.isfinite(st.grad).all() and torch.isfinite(st.flat).all()
