@@ -84,6 +84,31 @@ def cpu_share():
     return max(1, n)
 
 
+def mfma_peak_measured(ops, reps=3, iters=1500):
+    """bf16 MFMA rate this box sustains on random operands (irgan_mfma_probe: every wave issues
+    back-to-back v_mfma_f32_16x16x32_bf16, no memory traffic), best of `reps` timed launches after
+    one warm-up, in TFLOP/s -- SURVEY.md 8d asks for the roofline's peak measured on the box; the
+    chip holds a lower clock under dense MFMA load than the 2.4 GHz the nominal 2.5 PF assumes."""
+    import torch
+    cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    blocks = 4 * cus   # 4 waves per block: 4 waves per SIMD
+    g = torch.Generator().manual_seed(11)
+    src = torch.randn(4096 * 8, generator=g).bfloat16().cuda()
+    out = torch.empty(blocks * 256, device="cuda")
+    flop = blocks * 4 * iters * 8 * 16384
+    best = 0.0
+    for r in range(reps + 1):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        ops._lib.call("irgan_mfma_probe", ops.P(src), ops.P(out), blocks, iters, ops.stream())
+        b.record()
+        torch.cuda.synchronize()
+        if r:
+            best = max(best, flop / (a.elapsed_time(b) * 1e-3) / 1e12)
+    assert bool(torch.isfinite(out).all())
+    return round(best, 1)
+
+
 def _time_oracle(O, G, D, V, ir, rgb, threads, budget_s, min_steps, max_steps, warmup=1, as_written=False):
     """Median seconds per oracle step on `threads` torch CPU threads."""
     import torch
@@ -279,6 +304,10 @@ def main():
         achieved = kern[dom]["tflops"] if dom else None
         peak = peak_of(dom) if dom else BF16_DENSE_PEAK_TFLOPS
         traffic = pmc_traffic(dom.split(":")[0]) if (dom and H == 256 and B == 16 and args.dtype == "bf16") else None
+        mp = mfma_peak_measured(ops) if args.dtype != "fp32" else None
+        # fp8 (block-scaled f8f6f4, 32x32x64): the cycles of the bf16 32x32x16 at 4x the K, i.e. 2x
+        # the bf16 rate per clock (MI355X_MICROARCH.md), so its measured peak is 2x the bf16 probe
+        mpeak = (2 * mp if (dom or "").split(":")[0].endswith("8") else mp) if mp else None
         step_tflops = value * min_gflop_per_img(H, W) / 1e3 / world
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "img/s", "n_gpus": world, "steps": args.steps,
@@ -293,6 +322,12 @@ def main():
                        "step_frac_of_bf16_peak": round(step_tflops / BF16_DENSE_PEAK_TFLOPS, 4)},
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4) if achieved else None, "traffic": traffic,
+                         "peak_measured": mpeak, "frac_of_measured_peak": round(achieved / mpeak, 4)
+                         if (achieved and mpeak) else None,
+                         "peak_measured_note": "irgan_mfma_probe: back-to-back bf16 16x16x32 MFMAs on random "
+                                               "operands, every SIMD 4 waves deep, no memory traffic (the rate the "
+                                               "box sustains under MFMA load); fp8: 2x that (f8f6f4 cycles per "
+                                               "FLOP); `peak` stays the nominal dense figure",
                          "traffic_unit": "HBM bytes per launch (rocprofv3 PMC: 2*FETCH_SIZE + WRITE_SIZE, "
                                          f"{os.path.relpath(pmc_file(), ROOT) if pmc_file() else 'none'})",
                          "flop_per_launch": res_flop, "per_kernel": kern,

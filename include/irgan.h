@@ -472,6 +472,12 @@ IRGAN_API int irgan_ssim_eval_u8(const void* pred, const void* gt, int32_t N, in
 IRGAN_API int irgan_dropout(const void* x, int32_t xdt, int32_t P, int32_t C, int32_t ldx, int32_t xoff, void* y,
                   int32_t ydt, int32_t ldy, int32_t yoff, uint64_t seed, float p, irgan_stream_t s);
 
+/* MFMA throughput probe (bench.py's measured MFMA peak): blocks x 256 threads,
+ * each wave iters x 8 back-to-back v_mfma_f32_16x16x32_bf16 (16384 FLOP each) on operands
+ * read once from src (>= 4096 x 16 bytes of random bf16); one float per thread to out
+ * (blocks * 256 floats).  FLOP = blocks * 4 * iters * 8 * 16384; time it with events. */
+IRGAN_API int irgan_mfma_probe(const void* src, float* out, int32_t blocks, int32_t iters, irgan_stream_t s);
+
 /* Version / capability probe (no GPU work). */
 IRGAN_API int irgan_version(void);
 

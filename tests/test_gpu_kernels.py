@@ -335,3 +335,13 @@ def test_conv_fwd_fused_in_stats(ops, case):
     torch.cuda.synchronize()
     assert torch.equal(y0.t, y1.t)
     torch.testing.assert_close(mr1, mr0, rtol=2e-5, atol=1e-6)
+
+
+def test_mfma_probe_rate_is_sane():
+    """irgan_mfma_probe (bench.py's measured MFMA peak): finite outputs, and a bf16 rate that is
+    positive and not above the nominal 2.5 PFLOP/s dense peak (a FLOP-accounting check)."""
+    import bench
+    ops = pkg().ops
+    tf = bench.mfma_peak_measured(ops, reps=2, iters=400)
+    print("measured bf16 MFMA rate", tf, "TFLOP/s")
+    assert 200.0 < tf <= bench.BF16_DENSE_PEAK_TFLOPS * 1.02, tf
