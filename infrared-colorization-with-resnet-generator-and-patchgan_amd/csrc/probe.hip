@@ -18,17 +18,26 @@ __global__ __launch_bounds__(256) void mfma_probe_kernel(const uint4* __restrict
     const uint4 b0 = src[(4 * tid + 2) % PROBE_SRC], b1 = src[(4 * tid + 3) % PROBE_SRC];
     const bf16x8_t A0 = __builtin_bit_cast(bf16x8_t, a0), A1 = __builtin_bit_cast(bf16x8_t, a1);
     const bf16x8_t B0 = __builtin_bit_cast(bf16x8_t, b0), B1 = __builtin_bit_cast(bf16x8_t, b1);
-    f32x4 acc[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // inline asm: each accumulator stays in its own registers across iterations (compiled
+    // from the builtin, the loop-carried accumulators are rotated through v_accvgpr_mov copies
+    // that wait on the MFMAs and halve the rate); a dependent MFMA is 8 issues (128 cycles) away
+    f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0, c3 = c0, c4 = c0, c5 = c0, c6 = c0, c7 = c0;
     for (int it = 0; it < iters; ++it) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-            acc[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k & 1 ? A1 : A0, k & 2 ? B1 : B0, acc[k], 0, 0, 0);
+        asm volatile(
+            "v_mfma_f32_16x16x32_bf16 %0, %8, %10, %0\n\t"
+            "v_mfma_f32_16x16x32_bf16 %1, %9, %10, %1\n\t"
+            "v_mfma_f32_16x16x32_bf16 %2, %8, %11, %2\n\t"
+            "v_mfma_f32_16x16x32_bf16 %3, %9, %11, %3\n\t"
+            "v_mfma_f32_16x16x32_bf16 %4, %8, %10, %4\n\t"
+            "v_mfma_f32_16x16x32_bf16 %5, %9, %10, %5\n\t"
+            "v_mfma_f32_16x16x32_bf16 %6, %8, %11, %6\n\t"
+            "v_mfma_f32_16x16x32_bf16 %7, %9, %11, %7"
+            : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(c4), "+v"(c5), "+v"(c6), "+v"(c7)
+            : "v"(A0), "v"(A1), "v"(B0), "v"(B1));
     }
-    float s = 0.f;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) s += acc[k][0] + acc[k][1] + acc[k][2] + acc[k][3];
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // MFMA results before the VALU reads them
+    const f32x4 t = ((c0 + c1) + (c2 + c3)) + ((c4 + c5) + (c6 + c7));
+    const float s = (t[0] + t[1]) + (t[2] + t[3]);
     out[tid] = s;
 }
 
