@@ -472,6 +472,18 @@ IRGAN_API int irgan_ssim_eval_u8(const void* pred, const void* gt, int32_t N, in
 IRGAN_API int irgan_dropout(const void* x, int32_t xdt, int32_t P, int32_t C, int32_t ldx, int32_t xoff, void* y,
                   int32_t ydt, int32_t ldy, int32_t yoff, uint64_t seed, float p, irgan_stream_t s);
 
+/* PatchGAN head: NLayerDiscriminator's last layer, Conv2d(C, 1, 4, stride 1, padding 1)
+ * (ir:625-627), on VALU kernels (bf16 products, fp32 sums, fixed order).  Forward: x bf16 NHWC
+ * [N][H][W] (ldx, xoff), w the forward pack row [16 taps][C] bf16 (tap = ky * 4 + kx), y fp32
+ * [N][H-1][W-1] = conv + bias[0] (bias may be NULL).  Backward-data: g = dL/dy fp32, pixel
+ * stride ldg floats; dx bf16 NHWC [N][H][W] (lddx, dxoff) is written (not accumulated).
+ * C must be 512 and ldx / xoff / lddx / dxoff multiples of 8, else IRGAN_EUNSUPPORTED
+ * (nothing launched). */
+IRGAN_API int irgan_patch_head_fwd(const void* x, int32_t N, int32_t H, int32_t W, int32_t C, int32_t ldx,
+                         int32_t xoff, const void* w, const float* bias, float* y, irgan_stream_t s);
+IRGAN_API int irgan_patch_head_dgrad(const float* g, int32_t ldg, const void* w, void* dx, int32_t N, int32_t H,
+                           int32_t W, int32_t C, int32_t lddx, int32_t dxoff, irgan_stream_t s);
+
 /* MFMA throughput probe (bench.py's measured MFMA peak): blocks x 256 threads,
  * each wave iters x 8 back-to-back v_mfma_f32_16x16x32_bf16 (16384 FLOP each) on operands
  * read once from src (>= 4096 x 16 bytes of random bf16); one float per thread to out

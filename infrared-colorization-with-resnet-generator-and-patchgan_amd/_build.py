@@ -24,7 +24,7 @@ OBJDIR = os.path.join(HERE, "build")
 SOURCES = ["conv.hip", "conv_glds.hip", "conv_halo.hip", "conv_pp.hip", "conv_res64.hip", "conv_wgrad_halo.hip",
            "conv_wgrad_pc.hip", "conv_wgrad_f8.hip", "conv_wgrad_narrow.hip", "conv_ring.hip", "conv_c8.hip",
            "conv_rowspan.hip", "conv_dgrad_s2.hip", "fp8.hip", "infer.hip", "data.hip", "norm.hip",
-           "resample.hip", "loss.hip", "probe.hip", "build_id.hip"]
+           "resample.hip", "loss.hip", "head.hip", "probe.hip", "build_id.hip"]
 ARCH = os.environ.get("IRGAN_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", INCLUDE, "-I", CSRC,
          "-Wno-unused-result", "-fvisibility=hidden"]

@@ -898,7 +898,8 @@ class DiscriminatorEngine:
             if i == 0:
                 ops.conv_fwd(pc, x, y, act=ACT_LRELU)
             elif last:
-                ops.conv_fwd(pc, x, y)
+                if not ops.patch_head_fwd(pc, x, y.t):
+                    ops.conv_fwd(pc, x, y)
             else:
                 z = Feat(g.get(f"{tag}z{i}", (x.N, Ho, Wo, pc.spec.cout), T))
                 self.norms[i].conv_fwd(g, f"{tag}n{i}", pc, x, z, y, ACT_LRELU)
@@ -948,7 +949,7 @@ class DiscriminatorEngine:
             dx = Feat(g.get(f"{tag}d{i}", (x.N, x.H, x.W, x.C), T))
             if i == 1:  # previous activation is LReLU without IN: fold its derivative in the epilogue
                 ops.conv_dgrad(pc, dy, dx, mask=x, mask_act=2)
-            else:
+            elif not (i == n - 1 and ops.patch_head_dgrad(pc, dout, dx)):   # the head from the fp32 dL/dlogits
                 ops.conv_dgrad(pc, dy, dx)
             dy = dx
         return None

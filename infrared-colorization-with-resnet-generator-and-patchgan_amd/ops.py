@@ -369,6 +369,49 @@ def conv_fwd_stats(pc: PackedConv, x: Feat, y: Feat, part: torch.Tensor) -> int:
 
 
 
+# D's last layer (4x4, stride 1, pad 1, one output channel) on the dedicated VALU kernels
+# (csrc/head.hip); IRGAN_NO_PATCH_HEAD=1 runs it on the generic conv kernels
+PATCH_HEAD = [os.environ.get("IRGAN_NO_PATCH_HEAD") != "1"]
+
+
+def _is_patch_head(pc: PackedConv, x: Feat) -> bool:
+    s = pc.spec
+    return (PATCH_HEAD[0] and pc.dtype == BF16 and x.dt == BF16 and s.cout == 1 and s.k == 4 and s.stride == 1
+            and s.pad == 1 and s.mode == PAD_ZERO and s.cin == x.C == 512)
+
+
+def patch_head_fwd(pc: PackedConv, x: Feat, y: torch.Tensor) -> bool:
+    """y (fp32 [N][H-1][W-1][1]) = the PatchGAN head conv of x + bias (irgan_patch_head_fwd);
+    False (nothing launched) where the dedicated kernel does not take the layer."""
+    if not _is_patch_head(pc, x):
+        return False
+    assert y.dtype == torch.float32 and tuple(y.shape) == (x.N, x.H - 1, x.W - 1, 1) and y.is_contiguous()
+
+    def launch():
+        rc = _lib.load().irgan_patch_head_fwd(x.ptr, x.N, x.H, x.W, x.C, x.ld, x.off, P(pc.fwd),
+                                              P(pc.bias) if pc.bias is not None else None, P(y), stream())
+        if rc not in (0, IRGAN_EUNSUPPORTED):
+            raise _lib.IrganError(f"irgan_patch_head_fwd failed with code {rc}")
+        return rc == 0
+    return TIMER.wrap(conv_tag("fwd", pc.spec, (x.H, x.W), x.N), launch)
+
+
+def patch_head_dgrad(pc: PackedConv, g: torch.Tensor, dx: Feat) -> bool:
+    """dx (bf16, written) = the PatchGAN head's backward-data of g = dL/dy (fp32 [N][H-1][W-1][1])
+    (irgan_patch_head_dgrad); False (nothing launched) where the kernel does not take the layer."""
+    if not _is_patch_head(pc, dx):
+        return False
+    assert g.dtype == torch.float32 and tuple(g.shape[:3]) == (dx.N, dx.H - 1, dx.W - 1) and g.is_contiguous()
+
+    def launch():
+        rc = _lib.load().irgan_patch_head_dgrad(P(g), g.shape[3], P(pc.fwd), dx.ptr, dx.N, dx.H, dx.W, dx.C, dx.ld,
+                                                dx.off, stream())
+        if rc not in (0, IRGAN_EUNSUPPORTED):
+            raise _lib.IrganError(f"irgan_patch_head_dgrad failed with code {rc}")
+        return rc == 0
+    return TIMER.wrap(conv_tag("dgrad", pc.spec, (dx.H, dx.W), dx.N), launch)
+
+
 def conv_dgrad(pc: PackedConv, dy: Feat, dx: Feat, accumulate=False, mask: Feat = None, mask_act=0,
                pad_buf: torch.Tensor = None, bias=False):
     """dx = d(conv)/dx^T dy.  Reflect-padded layers: interior straight into dx and the
