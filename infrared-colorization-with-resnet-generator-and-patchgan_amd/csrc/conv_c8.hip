@@ -247,11 +247,16 @@ struct C8R {
     static_assert(2 * LDS <= 160 * 1024, "two resident blocks per CU");
 };
 
-template <int KH, int KW, int S, int CR>
+// STATS (irgan_conv_fwd_stats, the G inc layer's reflect-pad 7x7 conv -> InstanceNorm, ir:458-463):
+// each patch also writes its per-channel (sum, sum of squares) of the stored bf16 outputs, one
+// float2 per (image, patch, channel) in finalize_kernel's layout (norm.hip) -- the separate
+// statistics pass over the 134 MB output is gone.
+template <int KH, int KW, int S, int CR, bool STATS = false>
 __global__ __launch_bounds__(256, 2) void conv_c8r_kernel(const irgan_conv_desc d, const bf16_t* __restrict__ x,
                                                           const bf16_t* __restrict__ w,
                                                           const float* __restrict__ bias, bf16_t* __restrict__ y,
-                                                          int tpx, int tpy, int npatch) {
+                                                          int tpx, int tpy, int npatch,
+                                                          float2* __restrict__ part = nullptr) {
     using G = C8R<KH, KW, S, CR>;
     constexpr int TAPS = G::TAPS, HWd = G::HWd, HPIX = G::HPIX, KR = G::KR, KP = G::KP, WS = G::WS, TS = G::TS;
     __shared__ __attribute__((aligned(16))) char smem[G::LDS];
@@ -395,31 +400,67 @@ __global__ __launch_bounds__(256, 2) void conv_c8r_kernel(const irgan_conv_desc 
         // whole pixel rows: 8 lanes x 16 B per pixel, 8 pixels per wave instruction
         {
             const int pxi = p % tpx, r0 = p / tpx, pyi = r0 % tpy, img = r0 / tpy;
+            float s1[8], s2[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.f;
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const int e = u * 256 + tid, px = e >> 3, ch = e & 7;
                 const int oy = pyi * PH + (px >> 4), ox = pxi * PW + (px & 15);
                 const long pix = ((long)img * d.OH + oy * d.omy + d.ooy) * d.OW + ox * d.omx + d.oox;
-                const int off = (oy < d.Ho && ox < d.Wo) ? (int)((pix * d.ldy + d.yoff + ch * 8) * 2) : (int)IRGAN_OOB;
+                const bool in = oy < d.Ho && ox < d.Wo;
+                const int off = in ? (int)((pix * d.ldy + d.yoff + ch * 8) * 2) : (int)IRGAN_OOB;
                 const uint4 o = *(const uint4*)(sT + px * TS + ch * 16);
                 __builtin_amdgcn_raw_buffer_store_b128(
                     __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, o), yr, off, 0, 0);
+                if constexpr (STATS) {
+                    if (in) {
+                        const uint32_t wv[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            const float lo = __uint_as_float(wv[k] << 16), hi = __uint_as_float(wv[k] & 0xffff0000u);
+                            s1[2 * k] += lo; s2[2 * k] += lo * lo;
+                            s1[2 * k + 1] += hi; s2[2 * k + 1] += hi * hi;
+                        }
+                    }
+                }
+            }
+            if constexpr (STATS) {
+                // this thread's channels (tid & 7) * 8 .. +7 over its 8 pixels; the 32 threads of a
+                // channel group add through LDS in a fixed order (the staging tile is free again)
+                __syncthreads();
+                float2* red = (float2*)sT;  // [32 pixel groups][64 channels]
+                const int ch8 = (tid & 7) * 8, grp = tid >> 3;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) red[grp * 64 + ch8 + k] = make_float2(s1[k], s2[k]);
+                __syncthreads();
+                if (tid < 64) {
+                    float a = 0.f, b = 0.f;
+                    for (int r = 0; r < 32; ++r) {
+                        const float2 v = red[r * 64 + tid];
+                        a += v.x;
+                        b += v.y;
+                    }
+                    part[((long)img * (tpx * tpy) + pyi * tpx + pxi) * 64 + tid] = make_float2(a, b);
+                }
             }
         }
     }
 }
 
-template <int KH, int KW, int S, int CR>
-void launch_c8r(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y, hipStream_t st) {
+template <int KH, int KW, int S, int CR, bool STATS = false>
+void launch_c8r(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y, hipStream_t st,
+                float2* part = nullptr) {
     static int occ = 0;  // resident blocks per CU (a property of the kernel on gfx950)
-    if (!occ && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv_c8r_kernel<KH, KW, S, CR>, 256, 0) != hipSuccess || occ < 1))
+    if (!occ && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv_c8r_kernel<KH, KW, S, CR, STATS>, 256, 0) !=
+                     hipSuccess || occ < 1))
         occ = 1;
     const int slots = occ * irgan_cu_count();
     const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH);
     const int npatch = d->N * tpx * tpy;
     const int grid = npatch < slots ? npatch : slots;
-    conv_c8r_kernel<KH, KW, S, CR><<<grid, 256, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias, (bf16_t*)y,
-                                                        tpx, tpy, npatch);
+    conv_c8r_kernel<KH, KW, S, CR, STATS><<<grid, 256, 0, st>>>(*d, (const bf16_t*)x, (const bf16_t*)w, bias,
+                                                               (bf16_t*)y, tpx, tpy, npatch, part);
 }
 
 // the dense-K launch for (KH, KW, S, cin_real); false: no instance (the caller runs conv_c8)
@@ -439,6 +480,23 @@ bool try_c8r(const irgan_conv_desc* d, const void* x, const void* w, const float
 }
 
 }  // namespace
+
+// conv_pp.hip's irgan_conv_fwd_stats for the 8-channel-input convs: the G inc layer (7x7,
+// stride 1, one real input channel, 64 outputs) with the InstanceNorm partials fused (STATS);
+// returns the partials per image, 0 when this kernel does not take the layer (nothing ran)
+int c8r_fwd_stats(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y, void* part,
+                  hipStream_t st) {
+    static const bool off = getenv("IRGAN_NO_C8R") != nullptr || getenv("IRGAN_NO_C8R_STATS") != nullptr;
+    if (off || d->dtype != IRGAN_BF16 || d->Cin != 8 || d->ldx % 8 || d->xoff % 8 || d->cin_real != 1 ||
+        d->KH != 7 || d->KW != 7 || d->sy != 1 || d->sx != 1 || d->Cout != 64 || d->out_dtype != IRGAN_BF16 ||
+        d->ldy % 8 || d->yoff % 8 || d->accumulate || d->act != IRGAN_ACT_NONE || d->Ho != d->OH || d->Wo != d->OW ||
+        d->omy != 1 || d->omx != 1 || d->ooy || d->oox)
+        return 0;
+    const int tpx = irgan_cdiv(d->Wo, PW), tpy = irgan_cdiv(d->Ho, PH);
+    if (tpx * tpy > IRGAN_IN_PARTS || (long)d->N * d->Ho * d->Wo <= 0) return 0;
+    launch_c8r<7, 7, 1, 1, true>(d, x, w, bias, y, st, (float2*)part);
+    return tpx * tpy;
+}
 
 // Preconditions: bf16 input and weights, Cin == 8, ldx % 8 == 0, xoff % 8 == 0,
 // sy = sx = 1 with (KH, KW) in {(7,7), (4,4), (3,3)} or sy = sx = 2 with 4x4 (D's first

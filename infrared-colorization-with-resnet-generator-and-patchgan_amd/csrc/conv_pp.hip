@@ -219,9 +219,20 @@ extern "C" int irgan_conv_dgrad_s2_pp(const irgan_conv_desc* dd, const void* dy,
 // them with irgan_in_finalize.  IRGAN_EUNSUPPORTED when the layer is not a plain
 // bf16 ping-pong conv with Cout % 64 == 0, Cout != 192 (the caller then runs conv +
 // in_stats).
+// conv_c8.hip: the 8-channel-input (G inc) conv with fused statistics; 0 = not taken
+int c8r_fwd_stats(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y, void* part,
+                  hipStream_t st);
+
 extern "C" int irgan_conv_fwd_stats(const irgan_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
                                     void* part, int32_t* nb, irgan_stream_t s) {
     if (!d || !x || !w || !y || !part || !nb) return IRGAN_EINVAL;
+    if (d->Cin == 8) {
+        const int n = c8r_fwd_stats(d, x, w, bias, y, part, (hipStream_t)s);
+        if (!n) return IRGAN_EUNSUPPORTED;
+        IRGAN_LAUNCH_CHECK();
+        *nb = n;
+        return 0;
+    }
     const bool k33 = d->KH == 3 && d->KW == 3, k44 = d->KH == 4 && d->KW == 4;
     const bool s2d = k44 && d->sy == 2 && d->sx == 2;  // as irgan_conv_fwd_pp
     if (d->dtype != IRGAN_BF16 || d->out_dtype != IRGAN_BF16 || d->accumulate || d->act != IRGAN_ACT_NONE ||

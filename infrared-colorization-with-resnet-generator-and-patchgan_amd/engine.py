@@ -588,8 +588,7 @@ class GeneratorEngine:
         dq_x1 = (A.dqp(self.s_x1) if calib else A.dqp(self.s_cat)) if ud else None
         # inc: reflect-pad 3, conv7x7, IN, ReLU  (ir:458-463)
         z0 = Feat(g.get("z0", (B, H, W, c0), T))
-        ops.conv_fwd(self.inc, ir_t, z0)
-        self.norms["inc"].fwd(g, "inc", z0, x0, ACT_RELU)
+        self.norms["inc"].conv_fwd(g, "inc", self.inc, ir_t, z0, x0, ACT_RELU)   # statistics fused where taken
         # down1 (+ blur-down)  (ir:469-474)
         if self.no_aa:
             z1 = Feat(g.get("z1", (B, H1, W1, c1), T))

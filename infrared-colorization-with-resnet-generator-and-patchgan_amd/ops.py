@@ -355,7 +355,7 @@ def conv_fwd_stats(pc: PackedConv, x: Feat, y: Feat, part: torch.Tensor) -> int:
     d = _desc(N=x.N, H=x.H, W=x.W, Cin=pc.cin_eff, ldx=x.ld, xoff=x.off, Ho=Ho, Wo=Wo, Cout=s.cout, ldy=y.ld,
               yoff=y.off, OH=Ho, OW=Wo, omy=1, ooy=0, omx=1, oox=0, KH=s.k, KW=s.k, sy=s.stride, sx=s.stride,
               c0y=-s.pad, c0x=-s.pad, pad_mode=s.mode, act=ACT_NONE, accumulate=0, dtype=pc.dtype,
-              out_dtype=y.dt, mask_act=0, ldm=0, moff=0)
+              out_dtype=y.dt, mask_act=0, ldm=0, moff=0, cin_real=s.cin if s.cin < pc.cin_eff else 0)
     nb = ctypes.c_int32(0)
     fn = getattr(_lib.load(), "irgan_conv_fwd_stats")
     rc = TIMER.wrap(conv_tag("fwd", s, (x.H, x.W), x.N), lambda: fn(
