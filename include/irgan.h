@@ -92,7 +92,8 @@ IRGAN_API int irgan_conv_fwd(const irgan_conv_desc* d, const void* x, const void
  * ResnetBlock and the encoder / D (ir:386-392, 405-411, 468-470, 606-624) -- as
  * float2 (sum, sum of squares) partials part[n][b][c], b < *nb (16x16 patches per
  * image, <= IRGAN_IN_PARTS; Cout % 64 == 0 except 192); irgan_in_finalize turns them
- * into {mean, rstd}.
+ * into {mean, rstd}.  Also the G inc layer (ir:458-463): 7x7 stride 1, Cin = 8 with
+ * cin_real = 1 (the zero-padded IR channel), Cout = 64.
  * Returns IRGAN_EUNSUPPORTED (nothing launched) for other layers. */
 IRGAN_API int irgan_conv_fwd_stats(const irgan_conv_desc* d, const void* x, const void* w,
                          const float* bias, void* y, void* part, int32_t* nb, irgan_stream_t s);
