@@ -620,6 +620,72 @@ __global__ __launch_bounds__(TPB) void maxpool_bwd_kernel(const void* __restrict
     }
 }
 
+// The bf16 form for C = 8 CL channels (CL = 8, 16, 32: the VGG pools, C = 64 / 128 / 256), laid
+// out for whole-row memory transactions: 2 CL lanes per pooled pixel, lane (b, chunk) reading
+// input column 2j + b of both rows as 16-byte pieces, so one wave instruction covers
+// 64 / (2 CL) pooled pixels' 2 C contiguous channels (maxpool_bwd_kernel's thread per pooled
+// pixel read every other 128-256 B segment).  The partner column's values come by lane
+// exchange; the argmax is taken in maxpool_bwd_kernel's order over the four window positions
+// (first maximum, NaN wins), so dx is bit-identical.
+template <int CL>
+IRGAN_HD uint32_t xchg(uint32_t v) {   // value of lane ^ CL
+    if constexpr (CL < 16) return (uint32_t)__float_as_int(dpp_xor16<CL>(__int_as_float((int)v)));
+    else return (uint32_t)__shfl_xor((int)v, CL, 64);
+}
+template <int CL>
+__global__ __launch_bounds__(TPB) void maxpool_bwd_rows_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
+                                                               int H, int W, bf16_t* __restrict__ dx, int relu_mask) {
+    constexpr int C = CL * 8, PPW = 64 / (2 * CL);  // pooled pixels per wave
+    const int Ho = H / 2, Wo = W / 2;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int n = blockIdx.y / Ho, i = blockIdx.y - n * Ho;
+    const int b = (lane / CL) & 1, ch = lane % CL;
+    const int j = (blockIdx.x * (TPB / 64) + wv) * PPW + lane / (2 * CL);
+    const bool on = j < Wo;   // whole pixel groups: the partner lane has the same j
+    const long r0 = ((long)n * H + 2 * i) * W + 2 * j + b, r1 = r0 + W;
+    uint4 x0 = make_uint4(0u, 0u, 0u, 0u), x1 = x0, g4 = x0;
+    if (on) {
+        x0 = *(const uint4*)(x + r0 * C + ch * 8);
+        x1 = *(const uint4*)(x + r1 * C + ch * 8);
+        g4 = *(const uint4*)(dy + (((long)n * Ho + i) * Wo + j) * C + ch * 8);
+    }
+    const uint32_t own0[4] = {x0.x, x0.y, x0.z, x0.w}, own1[4] = {x1.x, x1.y, x1.z, x1.w};
+    uint32_t oth0[4], oth1[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        oth0[k] = xchg<CL>(own0[k]);
+        oth1[k] = xchg<CL>(own1[k]);
+    }
+    if (!on) return;
+    const uint32_t gw[4] = {g4.x, g4.y, g4.z, g4.w};
+    uint32_t o0[4], o1[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        // window order q = 2a + b': (0,0), (0,1), (1,0), (1,1)
+        const uint32_t q[4] = {b ? oth0[k] : own0[k], b ? own0[k] : oth0[k], b ? oth1[k] : own1[k],
+                               b ? own1[k] : oth1[k]};
+        float r[2][2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            float m = -INFINITY;
+            int am = 0;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const float v = __uint_as_float(h ? q[t] & 0xffff0000u : q[t] << 16);
+                if (v > m || isnan(v)) { m = v; am = t; }
+            }
+            float gv = __uint_as_float(h ? gw[k] & 0xffff0000u : gw[k] << 16);
+            if (relu_mask && !(m > 0.f)) gv = 0.f;
+            r[0][h] = am == b ? gv : 0.f;        // row 2i, this lane's column
+            r[1][h] = am == 2 + b ? gv : 0.f;    // row 2i + 1
+        }
+        o0[k] = pk_bf16(r[0][0], r[0][1]);
+        o1[k] = pk_bf16(r[1][0], r[1][1]);
+    }
+    *(uint4*)(dx + r0 * C + ch * 8) = make_uint4(o0[0], o0[1], o0[2], o0[3]);
+    *(uint4*)(dx + r1 * C + ch * 8) = make_uint4(o1[0], o1[1], o1[2], o1[3]);
+}
+
 __global__ __launch_bounds__(TPB) void nchw_to_nhwc_kernel(const float* __restrict__ x, int C, int HW,
                                                            void* __restrict__ y, int dt, int ldy, int yoff,
                                                            const float* __restrict__ scale,
@@ -976,7 +1042,15 @@ extern "C" int irgan_maxpool_bwd(const void* x, const void* dy, int32_t dt, int3
     long total = (long)N * (H / 2) * (W / 2) * C;
     RS_CHECK(total);
     if ((long)N * (H / 2) > 65535) return IRGAN_EUNSUPPORTED;
-    if (C % 8 == 0) {
+    static const bool rows = !getenv("IRGAN_NO_POOL_ROWS");
+    if (rows && dt == IRGAN_BF16 && (C == 64 || C == 128 || C == 256)) {
+        const int ppb = (TPB / 64) * (64 / (2 * (C / 8)));   // pooled pixels per block
+        dim3 g(irgan_cdiv(W / 2, ppb), N * (H / 2));
+        const bf16_t *xp = (const bf16_t*)x, *gp = (const bf16_t*)dy;
+        if (C == 64) maxpool_bwd_rows_kernel<8><<<g, TPB, 0, (hipStream_t)s>>>(xp, gp, H, W, (bf16_t*)dx, relu_mask);
+        else if (C == 128) maxpool_bwd_rows_kernel<16><<<g, TPB, 0, (hipStream_t)s>>>(xp, gp, H, W, (bf16_t*)dx, relu_mask);
+        else maxpool_bwd_rows_kernel<32><<<g, TPB, 0, (hipStream_t)s>>>(xp, gp, H, W, (bf16_t*)dx, relu_mask);
+    } else if (C % 8 == 0) {
         dim3 g(irgan_cdiv((long)(W / 2) * (C / 8), TPB), N * (H / 2));
         maxpool_bwd_kernel<8><<<g, TPB, 0, (hipStream_t)s>>>(x, dy, dt, H, W, C, dx, relu_mask);
     } else {

@@ -345,3 +345,29 @@ def test_mfma_probe_rate_is_sane():
     tf = bench.mfma_peak_measured(ops, reps=2, iters=400)
     print("measured bf16 MFMA rate", tf, "TFLOP/s")
     assert 200.0 < tf <= bench.BF16_DENSE_PEAK_TFLOPS * 1.02, tf
+
+
+@pytest.mark.parametrize("N,H,W,C,mask", [(16, 256, 256, 64, True), (16, 128, 128, 128, True), (2, 64, 48, 256, False),
+                                          (3, 30, 34, 64, False), (2, 16, 16, 32, True)])
+def test_maxpool_bwd_first_max_exact(N, H, W, C, mask):
+    """MaxPool2d(2) backward (ir:664, VGG-16 features): dL/dy routed to the first maximum of each
+    2x2 window in row-major order, times the ReLU' of the pooled value when mask -- exact against
+    a torch restatement (the C = 64 / 128 / 256 bf16 layers run the row-coalesced kernel, C = 32
+    the per-pixel one); ties (many zeros after a ReLU) included."""
+    ops = pkg().ops
+    g = torch.Generator().manual_seed(N * H + C)
+    x = torch.relu(torch.randn(N, H, W, C, generator=g)).bfloat16()
+    x[:, ::3, ::5] = 0.5   # exact ties
+    dy = torch.randn(N, H // 2, W // 2, C, generator=g).bfloat16()
+    dx = torch.full((N, H, W, C), 7.0, dtype=torch.bfloat16, device=DEV)
+    ops.maxpool_bwd(ops.Feat(x.to(DEV)), ops.Feat(dy.to(DEV)), ops.Feat(dx), relu_mask=mask)
+    torch.cuda.synchronize()
+    xf = x.float()[:, : H // 2 * 2, : W // 2 * 2]
+    win = xf.view(N, H // 2, 2, W // 2, 2, C).permute(0, 1, 3, 5, 2, 4).reshape(N, H // 2, W // 2, C, 4)
+    am = win.argmax(-1)                                    # first maximum in (0,0), (0,1), (1,0), (1,1) order
+    gm = dy.float() * ((win.max(-1).values > 0).float() if mask else 1.0)
+    ref = torch.zeros(N, H // 2, W // 2, C, 4)
+    ref.scatter_(-1, am.unsqueeze(-1), gm.unsqueeze(-1))
+    ref = ref.view(N, H // 2, W // 2, C, 2, 2).permute(0, 1, 4, 2, 5, 3).reshape(N, H // 2 * 2, W // 2 * 2, C)
+    got = dx.float().cpu()[:, : H // 2 * 2, : W // 2 * 2]
+    assert torch.equal(got, ref.bfloat16().float())
