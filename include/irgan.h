@@ -474,16 +474,26 @@ IRGAN_API int irgan_dropout(const void* x, int32_t xdt, int32_t P, int32_t C, in
                   int32_t ydt, int32_t ldy, int32_t yoff, uint64_t seed, float p, irgan_stream_t s);
 
 /* PatchGAN head: NLayerDiscriminator's last layer, Conv2d(C, 1, 4, stride 1, padding 1)
- * (ir:625-627), on VALU kernels (bf16 products, fp32 sums, fixed order).  Forward: x bf16 NHWC
- * [N][H][W] (ldx, xoff), w the forward pack row [16 taps][C] bf16 (tap = ky * 4 + kx), y fp32
- * [N][H-1][W-1] = conv + bias[0] (bias may be NULL).  Backward-data: g = dL/dy fp32, pixel
- * stride ldg floats; dx bf16 NHWC [N][H][W] (lddx, dxoff) is written (not accumulated).
- * C must be 512 and ldx / xoff / lddx / dxoff multiples of 8, else IRGAN_EUNSUPPORTED
- * (nothing launched). */
+ * (ir:625-627), as GEMMs over the 16 taps on v_mfma_f32_16x16x32_bf16 (bf16 products, fp32
+ * sums, fixed order).  Forward: x bf16 NHWC [N][H][W] (ldx, xoff), w the forward pack row
+ * [16 taps][C] bf16 (tap = ky * 4 + kx), y fp32 [N][H-1][W-1] = conv + bias[0] (bias may be
+ * NULL); ws holds the per-pixel tap products (16 x N*H*W rounded up to 16 floats; smaller ->
+ * IRGAN_EUNSUPPORTED).  Backward-data: g = dL/dy fp32, pixel stride ldg floats (split into two
+ * bf16 parts, so not rounded to bf16); dx bf16 NHWC [N][H][W] (lddx, dxoff) is written (not
+ * accumulated).  C must be 512 and ldx / xoff / lddx / dxoff multiples of 8, else
+ * IRGAN_EUNSUPPORTED (nothing launched). */
 IRGAN_API int irgan_patch_head_fwd(const void* x, int32_t N, int32_t H, int32_t W, int32_t C, int32_t ldx,
-                         int32_t xoff, const void* w, const float* bias, float* y, irgan_stream_t s);
+                         int32_t xoff, const void* w, const float* bias, float* y, float* ws, int64_t ws_floats,
+                         irgan_stream_t s);
 IRGAN_API int irgan_patch_head_dgrad(const float* g, int32_t ldg, const void* w, void* dx, int32_t N, int32_t H,
                            int32_t W, int32_t C, int32_t lddx, int32_t dxoff, irgan_stream_t s);
+/* Weight gradient of the same layer (its Conv2d weight grad under loss_D.backward(),
+ * ir:1650): dw fp32 [16 taps][C] += sum over pixels of x * g (g = dL/dy fp32 as above, not
+ * rounded to bf16).  Block partials (<= 256) go to ws and one ordered pass adds them into dw
+ * (deterministic); ws_floats too small for the launch's partials -> IRGAN_EUNSUPPORTED. */
+IRGAN_API int irgan_patch_head_wgrad(const void* x, int32_t N, int32_t H, int32_t W, int32_t C, int32_t ldx,
+                           int32_t xoff, const float* g, int32_t ldg, float* dw, float* ws, int64_t ws_floats,
+                           irgan_stream_t s);
 
 /* MFMA throughput probe (bench.py's measured MFMA peak): blocks x 256 threads,
  * each wave iters x 8 back-to-back v_mfma_f32_16x16x32_bf16 (16384 FLOP each) on operands

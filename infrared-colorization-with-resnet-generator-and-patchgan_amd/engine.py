@@ -918,12 +918,16 @@ class DiscriminatorEngine:
         acts, pre = g.state[tag]
         G = S.grad
         n = len(self.packs)
-        dbuf = g.zeros(f"{tag}dout_t", tuple(dout.shape[:3]) + (8,), T)   # 1-ch logits grad, padded to 8
-        ops.axpby(Feat(dout), 1.0, Feat(dbuf, 0, dout.shape[3]))
-        dy = Feat(dbuf, 0, self.packs[-1].cout_eff)
+        def logits_grad():   # the generic kernels' bf16 copy of dL/dlogits, padded to 8 channels
+            dbuf = g.zeros(f"{tag}dout_t", tuple(dout.shape[:3]) + (8,), T)
+            ops.axpby(Feat(dout), 1.0, Feat(dbuf, 0, dout.shape[3]))
+            return Feat(dbuf, 0, self.packs[-1].cout_eff)
+        dy = None   # the PatchGAN head kernels read the fp32 dout itself
         for i in reversed(range(n)):
             pc, key = self.packs[i], self.LAYERS[i][0]
             x = acts[i]
+            if dy is None and not (i == n - 1 and ops.is_patch_head(pc, x)):
+                dy = logits_grad()
             bias_sum = None
             if i == n - 1:
                 if want_wgrad:
@@ -936,20 +940,23 @@ class DiscriminatorEngine:
             if want_wgrad:
                 if bias_sum is not None:
                     ops.channel_sum(bias_sum, S.krsc(key + ".bias", G))
-                ops.conv_wgrad(pc.spec, x, Feat(dy.t, dy.off, pc.spec.cout), S.krsc(key + ".weight", G), self.dtype)
+                dw = S.krsc(key + ".weight", G)
+                if dy is not None or not ops.patch_head_wgrad(pc, x, dout, dw):
+                    dy = dy or logits_grad()
+                    ops.conv_wgrad(pc.spec, x, Feat(dy.t, dy.off, pc.spec.cout), dw, self.dtype)
                 if ready is not None:
                     ready(key + ".weight")
             if i == 0:
                 if not want_dinput:
                     return None
                 dx = Feat(g.get(f"{tag}dinput", (x.N, x.H, x.W, pc.spec.cin), torch.float32))
-                ops.conv_dgrad(pc, dy, dx)
+                ops.conv_dgrad(pc, dy or logits_grad(), dx)
                 return dx
             dx = Feat(g.get(f"{tag}d{i}", (x.N, x.H, x.W, x.C), T))
             if i == 1:  # previous activation is LReLU without IN: fold its derivative in the epilogue
                 ops.conv_dgrad(pc, dy, dx, mask=x, mask_act=2)
-            elif not (i == n - 1 and ops.patch_head_dgrad(pc, dout, dx)):   # the head from the fp32 dL/dlogits
-                ops.conv_dgrad(pc, dy, dx)
+            elif not (dy is None and ops.patch_head_dgrad(pc, dout, dx)):   # the head from the fp32 dL/dlogits
+                ops.conv_dgrad(pc, dy or logits_grad(), dx)
             dy = dx
         return None
 

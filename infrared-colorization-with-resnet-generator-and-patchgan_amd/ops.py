@@ -374,7 +374,7 @@ def conv_fwd_stats(pc: PackedConv, x: Feat, y: Feat, part: torch.Tensor) -> int:
 PATCH_HEAD = [os.environ.get("IRGAN_NO_PATCH_HEAD") != "1"]
 
 
-def _is_patch_head(pc: PackedConv, x: Feat) -> bool:
+def is_patch_head(pc: PackedConv, x: Feat) -> bool:
     s = pc.spec
     return (PATCH_HEAD[0] and pc.dtype == BF16 and x.dt == BF16 and s.cout == 1 and s.k == 4 and s.stride == 1
             and s.pad == 1 and s.mode == PAD_ZERO and s.cin == x.C == 512)
@@ -383,13 +383,16 @@ def _is_patch_head(pc: PackedConv, x: Feat) -> bool:
 def patch_head_fwd(pc: PackedConv, x: Feat, y: torch.Tensor) -> bool:
     """y (fp32 [N][H-1][W-1][1]) = the PatchGAN head conv of x + bias (irgan_patch_head_fwd);
     False (nothing launched) where the dedicated kernel does not take the layer."""
-    if not _is_patch_head(pc, x):
+    if not is_patch_head(pc, x):
         return False
     assert y.dtype == torch.float32 and tuple(y.shape) == (x.N, x.H - 1, x.W - 1, 1) and y.is_contiguous()
 
+    ws = _wgrad_ws(y.device)   # the per-pixel tap products; consumed by the same stream's next launch
+
     def launch():
         rc = _lib.load().irgan_patch_head_fwd(x.ptr, x.N, x.H, x.W, x.C, x.ld, x.off, P(pc.fwd),
-                                              P(pc.bias) if pc.bias is not None else None, P(y), stream())
+                                              P(pc.bias) if pc.bias is not None else None, P(y), P(ws),
+                                              ws.numel(), stream())
         if rc not in (0, IRGAN_EUNSUPPORTED):
             raise _lib.IrganError(f"irgan_patch_head_fwd failed with code {rc}")
         return rc == 0
@@ -399,7 +402,7 @@ def patch_head_fwd(pc: PackedConv, x: Feat, y: torch.Tensor) -> bool:
 def patch_head_dgrad(pc: PackedConv, g: torch.Tensor, dx: Feat) -> bool:
     """dx (bf16, written) = the PatchGAN head's backward-data of g = dL/dy (fp32 [N][H-1][W-1][1])
     (irgan_patch_head_dgrad); False (nothing launched) where the kernel does not take the layer."""
-    if not _is_patch_head(pc, dx):
+    if not is_patch_head(pc, dx):
         return False
     assert g.dtype == torch.float32 and tuple(g.shape[:3]) == (dx.N, dx.H - 1, dx.W - 1) and g.is_contiguous()
 
@@ -410,6 +413,25 @@ def patch_head_dgrad(pc: PackedConv, g: torch.Tensor, dx: Feat) -> bool:
             raise _lib.IrganError(f"irgan_patch_head_dgrad failed with code {rc}")
         return rc == 0
     return TIMER.wrap(conv_tag("dgrad", pc.spec, (dx.H, dx.W), dx.N), launch)
+
+
+def patch_head_wgrad(pc: PackedConv, x: Feat, g: torch.Tensor, dw: torch.Tensor) -> bool:
+    """dw (fp32 KRSC view, accumulated) += the PatchGAN head's weight gradient from x and
+    g = dL/dy (fp32 [N][H-1][W-1][1]) (irgan_patch_head_wgrad: block partials in the wgrad
+    workspace, ordered reduce); False (nothing launched) where the kernel does not take it."""
+    if not is_patch_head(pc, x):
+        return False
+    assert g.dtype == torch.float32 and tuple(g.shape[:3]) == (x.N, x.H - 1, x.W - 1) and g.is_contiguous()
+    assert dw.dtype == torch.float32 and dw.is_contiguous() and dw.numel() == 16 * x.C
+    ws = _wgrad_ws(dw.device)
+
+    def launch():
+        rc = _lib.load().irgan_patch_head_wgrad(x.ptr, x.N, x.H, x.W, x.C, x.ld, x.off, P(g), g.shape[3], P(dw),
+                                                P(ws), ws.numel(), stream())
+        if rc not in (0, IRGAN_EUNSUPPORTED):
+            raise _lib.IrganError(f"irgan_patch_head_wgrad failed with code {rc}")
+        return rc == 0
+    return TIMER.wrap(conv_tag("wgrad", pc.spec, (x.H, x.W), x.N), launch)
 
 
 def conv_dgrad(pc: PackedConv, dy: Feat, dx: Feat, accumulate=False, mask: Feat = None, mask_act=0,
