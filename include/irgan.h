@@ -488,8 +488,8 @@ IRGAN_API int irgan_patch_head_fwd(const void* x, int32_t N, int32_t H, int32_t 
 IRGAN_API int irgan_patch_head_dgrad(const float* g, int32_t ldg, const void* w, void* dx, int32_t N, int32_t H,
                            int32_t W, int32_t C, int32_t lddx, int32_t dxoff, irgan_stream_t s);
 /* Weight gradient of the same layer (its Conv2d weight grad under loss_D.backward(),
- * ir:1650): dw fp32 [16 taps][C] += sum over pixels of x * g (g = dL/dy fp32 as above, not
- * rounded to bf16).  Block partials (<= 256) go to ws and one ordered pass adds them into dw
+ * ir:1650): dw fp32 [16 taps][C] += sum over pixels of x * g (g = dL/dy fp32 as above, split
+ * into bf16 hi + lo).  Block partials (<= 256) go to ws and one ordered pass adds them into dw
  * (deterministic); ws_floats too small for the launch's partials -> IRGAN_EUNSUPPORTED. */
 IRGAN_API int irgan_patch_head_wgrad(const void* x, int32_t N, int32_t H, int32_t W, int32_t C, int32_t ldx,
                            int32_t xoff, const float* g, int32_t ldg, float* dw, float* ws, int64_t ws_floats,

@@ -9,19 +9,17 @@
 //  * backward-data: dx[pixel] = sum_tap G[pixel][tap] w[tap] with G the 16 shifted dL/dy
 //    values of the pixel (K = 16 taps, run as K = 32 with dL/dy split into bf16 hi + lo, so
 //    the fp32 gradient is not rounded to bf16), 16-byte bf16 stores;
-//  * weight gradient: VALU (the reduction runs over pixels, x's non-contiguous axis): x in
-//    registers, dL/dy broadcast by v_readlane into packed fp32 FMAs, block partials summed
-//    in a fixed order by one reduce pass.
+//  * weight gradient: dW = G^T x (M = 16 taps, K = pixels): x staged in LDS and read
+//    column-wise by ds_read_b64_tr_b16 (pixels are x's non-contiguous axis), G split hi + lo
+//    as above; one partial per block, summed in a fixed order by one reduce pass.
 //
 // Deterministic (fixed summation order, no atomics).  C = 512 channels.
 #include "common.h"
 
 namespace {
 
-constexpr int HC = 512, HS = 8;  // channels; input columns per wave (weight gradient)
+constexpr int HC = 512;  // channels
 
-typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 IRGAN_HD f32x4 mfma(const uint4 a, const uint4 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
@@ -144,122 +142,110 @@ __global__ __launch_bounds__(256) void head_dgrad_kernel(const float* __restrict
     }
 }
 
-// dw[ky * 4 + kx][c] += sum_{n, iy, ix} x[n][iy][ix][c] * g[n][iy + 1 - ky][ix + 1 - kx] (g = dL/dy,
-// fp32 [N][Ho][Wo], pixel stride ldg; terms outside the output are zero).  The transpose of the
-// backward-data product: a wave owns HS input columns of hr input rows, a lane 8 channels and
-// the 16 taps' fp32 sums of them (128 registers); per input row the 4 x (HS + 3) dL/dy window
-// is loaded one per lane and broadcast by v_readlane into packed fp32 FMAs.  The block's four
-// wave sums are added in LDS in wave order and stored as one partial [16][512]; one ordered
-// pass (head_wgrad_reduce) adds the partials into dw -- deterministic, no atomics.
-// grid (ceil(nstrip / 4), ceil(H / hr), N)
-__global__ __launch_bounds__(256) void head_wgrad_kernel(const bf16_t* __restrict__ x, int H, int W, int ldx, int xoff,
-                                                         const float* __restrict__ g, int ldg, int hr, int nstrip,
-                                                         float* __restrict__ part) {
-    constexpr int GC = HS + 3;
-    __shared__ float4 red[16 * HC / 4];   // 32 KB: [tap][channel]
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int strip = blockIdx.x * 4 + wv;
-    const int iy0 = blockIdx.y * hr, n = blockIdx.z;
-    const int Ho = H - 1, Wo = W - 1, ix0 = strip * HS;
-    f32x2 a[16][4];
+// Weight gradient on MFMA: dW[tap][c] = sum_p G[p][tap] x[p][c], a GEMM of M = 16 taps, N = 512
+// channels, K = pixels.  Per 32-pixel chunk the block stages x[32][512] in LDS (one 16-byte
+// load per thread and piece, coalesced) and each wave reads its B operands (x, K = pixels x
+// 16 channels) column-wise with ds_read_b64_tr_b16 -- the reduction axis is x's non-contiguous
+// one; A = G^T (16 taps x 32 pixels) is gathered from the fp32 dL/dy and split into bf16 hi +
+// lo (two MFMAs per tile), so dL/dy keeps ~16 bits.  Wave = 128 channels (8 tiles of 16);
+// block = chunks blockIdx.x, + gridDim.x, ...; one partial [16][512] per block.
+constexpr int WG_PIT = HC * 2 + 32;   // bytes per staged pixel row (pad: rows 8 apart share no banks)
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4_t lds_bf16x4_t;
+__global__ __launch_bounds__(256) void head_wgrad_mfma_kernel(const bf16_t* __restrict__ x, int N, int H, int W,
+                                                              int ldx, int xoff, const float* __restrict__ g, int ldg,
+                                                              int nchunk, float* __restrict__ part) {
+    __shared__ __attribute__((aligned(16))) unsigned char sx[32 * WG_PIT];
+    const int tid = threadIdx.x, lane = tid & 63, q = lane >> 4, r = lane & 15, wv = tid >> 6;
+    const int Ho = H - 1, Wo = W - 1, P = N * H * W;
+    f32x4 acc[8];
 #pragma unroll
-    for (int t = 0; t < 16; ++t)
+    for (int nt = 0; nt < 8; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // chunk ch's x pieces and dL/dy gathers; the next chunk's are in flight during this one's MFMAs
+    uint4 v[8];   // x[pc0 + row][16-byte piece]: row = e >> 6, piece = e & 63, e = tid + 256 k
+    float gv[8];  // A = G^T: lane (tap r, quarter q) holds G[pc0 + 8q + j][r], j = 0..7
+    auto load = [&](int ch) {
+        const int pc0 = ch * 32;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) a[t][k] = f32x2{0.f, 0.f};
-    if (strip < nstrip) {   // wave-uniform; idle waves still take part in the block sum below
-        const int iy1 = min(H, iy0 + hr);
-        // per input row: lane r * GC + c holds g[n][iy + 1 - r][ix0 - 2 + c] (0 outside the
-        // output), r = ky, and xv the row's HS pixels; the next row's load while this one sums
-        auto load_row = [&](int iy, float& gl, uint4* xv) {
-            gl = 0.f;
-            if (lane < 4 * GC) {
-                const int r = lane / GC, c = lane - r * GC;
-                const int oy = iy + 1 - r, ox = ix0 - 2 + c;
-                if ((unsigned)oy < (unsigned)Ho && (unsigned)ox < (unsigned)Wo)
-                    gl = g[(((long)n * Ho + oy) * Wo + ox) * ldg];
-            }
-            const bf16_t* row = x + (long)(n * H + iy) * W * ldx + xoff + lane * 8;
-#pragma unroll
-            for (int p = 0; p < HS; ++p)
-                xv[p] = ix0 + p < W ? *(const uint4*)(row + (long)(ix0 + p) * ldx) : make_uint4(0u, 0u, 0u, 0u);
-        };
-        float gl, gn = 0.f;
-        uint4 xv[HS], xn[HS];
-        load_row(iy0, gl, xv);
-#pragma unroll 1
-        for (int iy = iy0; iy < iy1; ++iy) {
-            if (iy + 1 < iy1) load_row(iy + 1, gn, xn);
-#pragma unroll
-            for (int p = 0; p < HS; ++p) {
-                const uint32_t u[4] = {xv[p].x, xv[p].y, xv[p].z, xv[p].w};
-                f32x2 xf[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) xf[k] = f32x2{__uint_as_float(u[k] << 16), __uint_as_float(u[k] & 0xffff0000u)};
-#pragma unroll
-                for (int ky = 0; ky < 4; ++ky)
-#pragma unroll
-                    for (int kx = 0; kx < 4; ++kx) {
-                        const float gv =
-                            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gl), ky * GC + p + 3 - kx));
-                        const f32x2 g2 = f32x2{gv, gv};
-#pragma unroll
-                        for (int k = 0; k < 4; ++k) a[ky * 4 + kx][k] = __builtin_elementwise_fma(xf[k], g2, a[ky * 4 + kx][k]);
-                    }
-            }
-            gl = gn;
-#pragma unroll
-            for (int p = 0; p < HS; ++p) xv[p] = xn[p];
+        for (int k = 0; k < 8; ++k) {
+            const int e = tid + 256 * k, p = pc0 + (e >> 6);
+            v[k] = p < P ? *(const uint4*)(x + (long)p * ldx + xoff + (e & 63) * 8) : make_uint4(0u, 0u, 0u, 0u);
         }
-    }
-    for (int w = 0; w < 4; ++w) {   // block sum in wave order
-        if (wv == w) {
 #pragma unroll
-            for (int t = 0; t < 16; ++t)
+        for (int j = 0; j < 8; ++j) {
+            const int p = min(pc0 + 8 * q + j, P - 1);
+            const int ix = p % W, iy = (p / W) % H, n = p / (W * H);
+            const int oy = iy + 1 - (r >> 2), ox = ix + 1 - (r & 3);
+            gv[j] = g[(((long)n * Ho + min(max(oy, 0), Ho - 1)) * Wo + min(max(ox, 0), Wo - 1)) * ldg];
+            if (pc0 + 8 * q + j >= P || (unsigned)oy >= (unsigned)Ho || (unsigned)ox >= (unsigned)Wo) gv[j] = 0.f;
+        }
+    };
+    if (blockIdx.x < nchunk) load(blockIdx.x);
+    for (int ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {   // block-uniform
+        uint32_t hw[4], lw[4];
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    float4& r = red[t * (HC / 4) + lane * 2 + h];
-                    const f32x2 lo = a[t][2 * h], hi = a[t][2 * h + 1];
-                    if (w == 0) r = make_float4(lo.x, lo.y, hi.x, hi.y);
-                    else {
-                        float4 v = r;
-                        v.x += lo.x; v.y += lo.y; v.z += hi.x; v.w += hi.y;
-                        r = v;
-                    }
-                }
+        for (int j = 0; j < 4; ++j) {
+            hw[j] = pk_bf16(gv[2 * j], gv[2 * j + 1]);
+            lw[j] = pk_bf16(gv[2 * j] - __uint_as_float(hw[j] << 16), gv[2 * j + 1] - __uint_as_float(hw[j] & 0xffff0000u));
+        }
+        const uint4 ahi = make_uint4(hw[0], hw[1], hw[2], hw[3]), alo = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+        __syncthreads();   // the previous chunk's reads are done
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int e = tid + 256 * k;
+            *(uint4*)(sx + (e >> 6) * WG_PIT + (e & 63) * 16) = v[k];
         }
         __syncthreads();
+        if (ch + (int)gridDim.x < nchunk) load(ch + gridDim.x);
+        // B = x (K = 32 pixels x 16 channels): group q reads rows 8q .. 8q + 7 of the tile's 16
+        // channels in two 4-row transposed reads; lane 4q' + p' addresses row 8q + q',
+        // channels c0 + 4p' .. + 3, and receives its column (channel c0 + r) of the 4 rows
+        const unsigned char* b1 = sx + (8 * q + (r >> 2)) * WG_PIT + (wv * 128 + 4 * (r & 3)) * 2;
+#pragma unroll
+        for (int nt = 0; nt < 8; ++nt) {
+            const bf16x4_t t0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(b1 + nt * 32));
+            const bf16x4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(b1 + nt * 32 + 4 * WG_PIT));
+            const uint2 u0 = __builtin_bit_cast(uint2, t0), u1 = __builtin_bit_cast(uint2, t1);
+            const uint4 bop = make_uint4(u0.x, u0.y, u1.x, u1.y);
+            acc[nt] = mfma(ahi, bop, acc[nt]);
+            acc[nt] = mfma(alo, bop, acc[nt]);
+        }
     }
-    const long b = ((long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-    float4* dst = (float4*)(part + b * 16 * HC);
-    for (int e = threadIdx.x; e < 16 * HC / 4; e += 256) dst[e] = red[e];
+    // D[tap 4q + e][channel wv * 128 + nt * 16 + r]
+    float* dst = part + (long)blockIdx.x * 16 * HC + wv * 128 + r;
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dst[(4 * q + e) * HC + nt * 16] = acc[nt][e];
 }
 
-// Ordered sum of the nb block partials (16 * 512 floats each) into dw in one pass: block =
-// 64 float4 outputs x 8 waves, wave w adds partials [w * per, (w + 1) * per) with all its loads
-// in flight (per <= 32), then wave 0 adds the 8 wave sums in order onto dw.
-constexpr int HW_N = 16 * HC, HW_WAVES = 8, HW_PER = 32;
-__global__ __launch_bounds__(64 * HW_WAVES) void head_wgrad_reduce(const float4* __restrict__ part, int nb,
-                                                                   float4* __restrict__ dw) {
-    __shared__ float4 sums[HW_WAVES][64];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int i = blockIdx.x * 64 + lane;   // float4 index in [0, HW_N / 4)
-    const int per = (nb + HW_WAVES - 1) / HW_WAVES, b0 = wv * per;
-    float4 v[HW_PER];
+// Ordered sum of the nb (<= 256) block partials (16 * 512 floats each) into dw: block = 16
+// float4 outputs x 16 partial groups; thread (column c, group k) adds partials k, k + 16, ...
+// with all its loads in flight, then the 16 group sums are added in order onto dw.
+constexpr int HW_N = 16 * HC, HW_MAXB = 256;
+__global__ __launch_bounds__(256) void head_wgrad_reduce(const float4* __restrict__ part, int nb,
+                                                         float4* __restrict__ dw) {
+    __shared__ float4 sums[16][16];
+    const int c = threadIdx.x & 15, k = threadIdx.x >> 4;
+    const int i = blockIdx.x * 16 + c;   // float4 index in [0, HW_N / 4)
+    float4 v[HW_MAXB / 16];
 #pragma unroll
-    for (int k = 0; k < HW_PER; ++k)
-        v[k] = k < per && b0 + k < nb ? part[(long)(b0 + k) * (HW_N / 4) + i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int m = 0; m < HW_MAXB / 16; ++m) {
+        const int b = k + 16 * m;
+        v[m] = b < nb ? part[(long)b * (HW_N / 4) + i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     float4 a = v[0];
 #pragma unroll
-    for (int k = 1; k < HW_PER; ++k) {
-        a.x += v[k].x; a.y += v[k].y; a.z += v[k].z; a.w += v[k].w;
+    for (int m = 1; m < HW_MAXB / 16; ++m) {
+        a.x += v[m].x; a.y += v[m].y; a.z += v[m].z; a.w += v[m].w;
     }
-    sums[wv][lane] = a;
+    sums[k][c] = a;
     __syncthreads();
-    if (wv == 0) {
+    if (k == 0) {
         float4 r = dw[i];
 #pragma unroll
-        for (int w = 0; w < HW_WAVES; ++w) {
-            r.x += sums[w][lane].x; r.y += sums[w][lane].y; r.z += sums[w][lane].z; r.w += sums[w][lane].w;
+        for (int m = 0; m < 16; ++m) {
+            r.x += sums[m][c].x; r.y += sums[m][c].y; r.z += sums[m][c].z; r.w += sums[m][c].w;
         }
         dw[i] = r;
     }
@@ -302,21 +288,13 @@ extern "C" int irgan_patch_head_wgrad(const void* x, int32_t N, int32_t H, int32
     if (!x || !g || !dw || ldg < 1) return IRGAN_EINVAL;
     if (N <= 0 || H < 2 || W < 2) return 0;
     static const bool off = getenv("IRGAN_NO_HEAD_WGRAD") != nullptr;   // A/B: the generic wgrad
-    if (off || C != HC || ldx % 8 || xoff % 8 || N > 65535 || H > 65535 || (long)N * H * W * ldx >= (1L << 31))
-        return IRGAN_EUNSUPPORTED;
-    const int nstrip = irgan_cdiv(W, HS);
-    // rows per wave: the most (<= 8) that still launch >= 1024 waves, then more until the block
-    // partials fit the reduce (<= 256)
-    auto blocks = [&](int r) { return (long)irgan_cdiv(nstrip, 4) * irgan_cdiv(H, r) * N; };
-    int hr = 8;
-    while (hr > 1 && 4 * blocks(hr) < 1024) hr >>= 1;
-    while (blocks(hr) > HW_WAVES * HW_PER) hr *= 2;
-    const dim3 grid(irgan_cdiv(nstrip, 4), irgan_cdiv(H, hr), N);
-    const int nb = grid.x * grid.y * grid.z;
-    if (!ws || nb > HW_WAVES * HW_PER || (long)nb * HW_N > ws_cap) return IRGAN_EUNSUPPORTED;
-    head_wgrad_kernel<<<grid, 256, 0, (hipStream_t)s>>>((const bf16_t*)x, H, W, ldx, xoff, g, ldg, hr, nstrip, ws);
+    const long P = (long)N * H * W;
+    if (off || C != HC || ldx % 8 || xoff % 8 || P * ldx >= (1L << 31)) return IRGAN_EUNSUPPORTED;
+    const int nchunk = irgan_cdiv(P, 32), nb = min(nchunk, HW_MAXB);
+    if (!ws || (long)nb * HW_N > ws_cap) return IRGAN_EUNSUPPORTED;
+    head_wgrad_mfma_kernel<<<nb, 256, 0, (hipStream_t)s>>>((const bf16_t*)x, N, H, W, ldx, xoff, g, ldg, nchunk, ws);
     IRGAN_LAUNCH_CHECK();
-    head_wgrad_reduce<<<HW_N / 4 / 64, 64 * HW_WAVES, 0, (hipStream_t)s>>>((const float4*)ws, nb, (float4*)dw);
+    head_wgrad_reduce<<<HW_N / 4 / 16, 256, 0, (hipStream_t)s>>>((const float4*)ws, nb, (float4*)dw);
     IRGAN_LAUNCH_CHECK();
     return 0;
 }
