@@ -75,51 +75,6 @@ __global__ __launch_bounds__(256) void head_fwd_sum_kernel(const float* __restri
     y[i] = a;
 }
 
-// Forward in one launch: block = (image, hr output rows); its waves compute Z for the hr + 3
-// input rows those rows read (as head_fwd_z_kernel, same K order) into LDS, then the block sums
-// the shifted taps -- bit-identical to the two-launch path, without Z's round trip through
-// memory and the second launch.  The halo rows' products are computed twice (3 / hr extra).
-__global__ __launch_bounds__(256) void head_fwd_fused_kernel(const bf16_t* __restrict__ x, int H, int W, int ldx,
-                                                             int xoff, const bf16_t* __restrict__ w,
-                                                             const float* __restrict__ bias, float* __restrict__ y,
-                                                             int hr, int zp) {
-    extern __shared__ __attribute__((aligned(16))) float zs[];   // [16][zp]
-    const int lane = threadIdx.x & 63, q = lane >> 4, r = lane & 15, wv = threadIdx.x >> 6;
-    const int n = blockIdx.y, oy0 = blockIdx.x * hr, Ho = H - 1, Wo = W - 1;
-    const int nrow = min(hr, Ho - oy0);
-    const int ir0 = max(oy0 - 1, 0), ir1 = min(oy0 + nrow + 2, H);   // input rows [ir0, ir1)
-    const int npx = (ir1 - ir0) * W;
-    const bf16_t* xi = x + ((long)n * H + ir0) * W * ldx + xoff + q * 8;
-    uint4 wb[16];
-    const bf16_t* wr = w + r * HC + q * 8;
-#pragma unroll
-    for (int kk = 0; kk < 16; ++kk) wb[kk] = *(const uint4*)(wr + kk * 32);
-    for (int t = wv; t * 16 < npx; t += 4) {   // wave-uniform
-        uint4 xa[16];
-        const bf16_t* xr = xi + (long)min(t * 16 + r, npx - 1) * ldx;
-#pragma unroll
-        for (int kk = 0; kk < 16; ++kk) xa[kk] = *(const uint4*)(xr + kk * 32);
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kk = 0; kk < 16; ++kk) acc = mfma(xa[kk], wb[kk], acc);
-        *(f32x4*)(zs + r * zp + t * 16 + 4 * q) = acc;
-    }
-    __syncthreads();
-    const float b = bias ? bias[0] : 0.f;
-    for (int o = threadIdx.x; o < nrow * Wo; o += 256) {
-        const int oy = oy0 + o / Wo, ox = o % Wo;
-        float a = b;
-#pragma unroll
-        for (int t = 0; t < 16; ++t) {
-            const int iy = oy + (t >> 2) - 1, ix = ox + (t & 3) - 1;
-            const bool in = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
-            const float v = zs[t * zp + (in ? (iy - ir0) * W + ix : 0)];
-            a += in ? v : 0.f;
-        }
-        y[((long)n * Ho + oy) * Wo + ox] = a;
-    }
-}
-
 // Backward-data: dx[p][c] = sum_tap G[p][tap] * w[tap][c], G[p][ky * 4 + kx] = g[n][iy + 1 - ky]
 // [ix + 1 - kx] (0 outside the output) -- a GEMM of K = 16 taps, run transposed on
 // v_mfma_f32_16x16x32_bf16 (A = w^T: 16 channels x K, B = G^T: K x 16 pixels) with K = 32 =
@@ -304,19 +259,8 @@ extern "C" int irgan_patch_head_fwd(const void* x, int32_t N, int32_t H, int32_t
     if (!x || !w || !y) return IRGAN_EINVAL;
     if (N <= 0 || H < 2 || W < 2) return 0;
     const long P = (long)N * H * W, Pp = (P + 15) / 16 * 16;
-    if (C != HC || ldx % 8 || xoff % 8 || P * ldx >= (1L << 31)) return IRGAN_EUNSUPPORTED;
-    // one launch: hr output rows per block, the most (<= 4) that still give >= 240 blocks
-    int hr = 4;
-    while (hr > 1 && (long)irgan_cdiv(H - 1, hr) * N < 240) hr >>= 1;
-    const int zp = ((hr + 3) * W + 15) / 16 * 16;
-    static const bool fused = getenv("IRGAN_HEAD_FWD_FUSED") != nullptr;   // A/B: one launch
-    if (fused && 16L * zp * 4 <= 64 * 1024 && N <= 65535) {
-        head_fwd_fused_kernel<<<dim3(irgan_cdiv(H - 1, hr), N), 256, 16 * zp * 4, (hipStream_t)s>>>(
-            (const bf16_t*)x, H, W, ldx, xoff, (const bf16_t*)w, bias, y, hr, zp);
-        IRGAN_LAUNCH_CHECK();
-        return 0;
-    }
-    if (!ws || 16 * Pp > ws_floats) return IRGAN_EUNSUPPORTED;
+    if (C != HC || ldx % 8 || xoff % 8 || P * ldx >= (1L << 31) || !ws || 16 * Pp > ws_floats)
+        return IRGAN_EUNSUPPORTED;
     head_fwd_z_kernel<<<irgan_cdiv(P, 64), 256, 0, (hipStream_t)s>>>((const bf16_t*)x, P, Pp, ldx, xoff,
                                                                      (const bf16_t*)w, ws);
     IRGAN_LAUNCH_CHECK();
